@@ -1,0 +1,221 @@
+"""Headline benchmark: SCORE throughput (BASELINE.json metric, config 2).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (config 2 of BASELINE.json): 10M synthetic 256-byte documents per GPU,
+20 languages, gram lengths 1-5, scored against a K=500 profile table that this
+script first FITs on the GPU from a synthetic training corpus.  A step = one
+pass of the SCORE kernel over the GPU's 10M resident documents (inputs already
+in HBM).  Documents shard across ranks with no collective (weak scaling);
+value = documents scored by all ranks / max-over-ranks time.
+
+Also reported: the SCORE kernel's roofline position (algorithmic bytes / HIP
+event time on the launch stream) and a CPU baseline (the oracle's C
+restatement, multithreaded, on a bounded sample; kind "port" -- the Scala
+reference cannot run without a JVM).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spark-languagedetector_amd"))
+
+from languagedetection import synth  # noqa: E402
+from languagedetection.runtime import DeviceCounts, DeviceModel  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "documents/sec scored (whole node, 1/2/4/8 GPU) + achieved HBM GB/s vs roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs", type=int, default=10_000_000, help="documents per GPU")
+    ap.add_argument("--doc-bytes", type=int, default=256)
+    ap.add_argument("--langs", type=int, default=20)
+    ap.add_argument("--grams", type=str, default="1,2,3,4,5")
+    ap.add_argument("--profile-size", type=int, default=500)
+    ap.add_argument("--pool", type=int, default=250_000, help="distinct generated docs, tiled to --docs")
+    ap.add_argument("--train-docs", type=int, default=1000, help="training docs per language for the table")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--empty-table", action="store_true", help="calibration: table with no keys")
+    ap.add_argument("--json-out", type=str, default="")
+    return ap.parse_args()
+
+
+def build_table(args, ls, device):
+    """FIT on the GPU (the reference's LanguageDetector.fit path) -> profile table."""
+    grams = [int(x) for x in args.grams.split(",")]
+    lang = np.repeat(np.arange(args.langs, dtype=np.int32), args.train_docs)
+    data, off, lang = synth.generate(ls, len(lang), 200, 2000, seed=synth.SEED_BASE + 100, doc_lang=lang)
+    t0 = time.perf_counter()
+    counts = DeviceCounts(args.langs, grams, capacity_hint=1 << 20, device=device)
+    counts.count(data, off, lang)
+    n_distinct = counts.size()
+    table = counts.fit_table(args.profile_size)
+    fit_s = time.perf_counter() - t0
+    counts.close()
+    fit_info = {"train_docs": int(len(lang)), "train_bytes": int(off[-1]), "distinct_grams": int(n_distinct),
+                "table_rows": len(table), "host_wall_s": round(fit_s, 3)}
+    return table, grams, fit_info
+
+
+def cpu_baseline(args, table, grams, data, off):
+    """The oracle's C restatement (kind 'port'), on rank 0, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ldoracle_c as OC
+    threads = int(min(16, os.cpu_count() or 1))
+    t = OC.Table(table, args.langs)
+    probe = min(20_000, len(off) - 1)
+    t0 = time.perf_counter()
+    t.score(grams, data, off[:probe + 1], nthreads=threads)
+    rate = probe / max(time.perf_counter() - t0, 1e-9)
+    n = int(min(len(off) - 1, max(probe, rate * args.cpu_seconds)))
+    t0 = time.perf_counter()
+    t.score(grams, data, off[:n + 1], nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "docs/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} of the GPU's documents ({args.doc_bytes} B each), same table, "
+                      f"{threads} pthreads, {dt:.1f} s"}
+
+
+def traffic_from_profiles(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes, if they
+    were collected for this exact workload (tools/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None
+    if d.get("workload_key") != workload_key:
+        return None
+    return d.get("traffic_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    ls = synth.make_languages(args.langs)
+    if args.empty_table:
+        table, grams, fit_info = {}, [int(x) for x in args.grams.split(",")], {}
+    else:
+        table, grams, fit_info = build_table(args, ls, local)
+    model = DeviceModel(table, args.langs, grams, device=local)
+
+    # this rank's documents: a generated pool tiled to --docs, resident in HBM
+    pool = min(args.pool, args.docs)
+    pdata, poff, plang = synth.generate(ls, pool, args.doc_bytes, args.doc_bytes,
+                                        seed=synth.SEED_BASE + 2 + 1000 * rank)
+    data, off, _ = synth.tile(pdata, poff, plang, args.docs)
+    n_docs = len(off) - 1
+    n_bytes = int(off[-1])
+    d_bytes = torch.empty(((n_bytes + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n_bytes].copy_(torch.from_numpy(data))
+    d_off = torch.from_numpy(off).to(dev)
+    d_lab = torch.empty(n_docs, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        model.score_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), n_docs, d_lab.data_ptr(), 0,
+                           stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # labels sanity (synthetic docs carry their generating language)
+    acc = float((d_lab[:pool].cpu().numpy() == plang[:n_docs][:pool]).mean()) if table else None
+
+    info = model.info()
+    doc_b = args.doc_bytes
+    algo_per_doc = doc_b + 8 + 4                          # bytes + int64 offset + int32 label
+    table_bytes = info["device_bytes"]                    # read once per launch (amortised)
+    algo_per_launch = n_docs * algo_per_doc + table_bytes
+    achieved = algo_per_launch / (kernel_ms * 1e-3) / 1e9
+    workload_key = f"score:docs={n_docs}:bytes={doc_b}:L={args.langs}:G={args.grams}:K={args.profile_size}"
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(workload_key),
+                "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo_per_launch),
+                "lookups_per_s": round(n_docs * sum(max(doc_b - n + 1, 1) for n in grams) / (kernel_ms * 1e-3), 1)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and table:
+        cpu = cpu_baseline(args, table, grams, data, off)
+
+    total_docs = n_docs * world * args.steps
+    line = {
+        "metric": METRIC,
+        "value": round(total_docs / elapsed, 1),
+        "unit": "docs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Markov-chain text per language, SURVEY.md §8d generator; table FIT on the GPU)",
+        "config": {"workload": f"config2: score {n_docs} x {doc_b} B docs per GPU, {args.langs} languages, "
+                               f"grams {args.grams}, profile size {args.profile_size}",
+                   "docs_per_gpu": n_docs, "doc_bytes": doc_b, "languages": args.langs, "gram_lengths": grams,
+                   "profile_size": args.profile_size, "table_rows": info["n_keys"],
+                   "table_mode": "mask" if info["mode"] == 0 else "dense",
+                   "parallelism": f"dp{world} (documents sharded, no collective)"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "fit_setup": fit_info,
+        "label_accuracy_vs_generator": acc,
+    }
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(s + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/* ldgpu.h -- C ABI of libldgpu.so, the MI355X (gfx950) hot path of
+ * spark-languagedetector: FIT byte n-gram counting into per-language gram
+ * probability tables, and SCORE (window scan, gram->row lookup, fp64
+ * accumulation, argmax).
+ *
+ * Plain C, POD arguments only.  Every entry point returns an int status
+ * (LDGPU_OK = 0) and leaves a thread-local message for ldgpu_last_error().
+ * All entry points are thread-safe; calls on one ldgpu_ctx are serialised on
+ * that context's HIP stream.
+ *
+ * Reference interfaces replaced (Scala, /root/reference/src/main/scala/org/
+ * apache/spark/ml/feature/languagedetection/):
+ *   ldgpu_model_create  -- new LanguageDetectorModel(gramProbabilities,
+ *                          gramLengths, languages)  LanguageDetectorModel.scala:178-198
+ *                          + the table broadcast of transform  :222
+ *   ldgpu_score[_device]-- LanguageDetectorModel.detect(Array[Byte], map, langs,
+ *                          grams) :131-156, batched over documents (the per-row
+ *                          map of transform :225-238)
+ *   ldgpu_count[_device]-- LanguageDetector computeGrams + reduceGrams
+ *                          LanguageDetector.scala:25-66
+ *   ldgpu_fit_table_*   -- computeProbabilities + filterTopGrams + collect.toMap
+ *                          LanguageDetector.scala:75-132, :252-254
+ *
+ * Encodings are the caller's job (as in the reference): FIT documents are
+ * UTF-8 bytes (String.getBytes(UTF-8), LanguageDetector.scala:37); SCORE
+ * documents are the low byte of every UTF-16 code unit
+ * (text.toCharArray.map(_.toByte), LanguageDetectorModel.scala:161).
+ *
+ * Documents are packed: bytes[offsets[d] .. offsets[d+1]) is document d;
+ * offsets has n_docs + 1 non-decreasing entries.
+ */
+#ifndef LDGPU_H
+#define LDGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ldgpu_status {
+    LDGPU_OK = 0,
+    LDGPU_EINVAL = 1,        /* bad argument: gram length <= 0, bad offsets, null pointer, L < 1 */
+    LDGPU_EROWLEN = 2,       /* a scored window hit a row whose length != #languages
+                                (BLAS.axpy require, LanguageDetectorModel.scala:149) */
+    LDGPU_ENOMEM = 3,        /* device or host allocation failed / count table full */
+    LDGPU_EDEVICE = 4,       /* HIP runtime error */
+    LDGPU_EUNSUPPORTED = 5,  /* outside the device path's limits (see below) */
+    LDGPU_ENODEV = 6         /* no HIP device */
+};
+
+/* Device-path limits: gram lengths 1..LDGPU_MAX_GRAM (a key packs into one
+ * u64: 7 payload bytes + a length byte), 1..LDGPU_MAX_LANGS languages. */
+#define LDGPU_MAX_GRAM 7
+#define LDGPU_MAX_LANGS 256
+#define LDGPU_MAX_GRAM_LENGTHS 32
+
+const char* ldgpu_version(void);
+const char* ldgpu_last_error(void);          /* thread-local, never NULL */
+int ldgpu_device_count(int32_t* out_count);
+
+/* ---------------------------------------------------------------- context */
+typedef struct ldgpu_ctx ldgpu_ctx;
+int ldgpu_ctx_create(int32_t device, ldgpu_ctx** out);
+int ldgpu_ctx_destroy(ldgpu_ctx* ctx);
+int ldgpu_ctx_synchronize(ldgpu_ctx* ctx);
+void* ldgpu_ctx_stream(ldgpu_ctx* ctx);      /* the context's hipStream_t */
+
+/* ------------------------------------------------------------------ SCORE */
+typedef struct ldgpu_model ldgpu_model;
+
+/* The gram -> probability-row map.  Key i is key_bytes[key_offsets[i] ..
+ * key_offsets[i+1]); its row is rows[i*n_langs .. (i+1)*n_langs) in
+ * supported-language order.  row_ok (nullable) marks rows whose length in the
+ * caller's map differs from n_langs: scoring a document that hits such a row
+ * fails with LDGPU_EROWLEN, as BLAS.axpy does in the reference.  A later
+ * duplicate key replaces an earlier one (Scala toMap).  gram_lengths is kept
+ * in order, duplicates included (each repeat scans the document again). */
+int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                       const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
+                       int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                       ldgpu_model** out);
+int ldgpu_model_destroy(ldgpu_model* model);
+
+/* mode: 0 = every row is one value times a language bitmask (fit-produced
+ * tables), 1 = dense fp64 rows.  n_keys: keys resident on the device. */
+int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
+                     int64_t* table_slots, int64_t* filter_bits, int64_t* device_bytes);
+
+/* Host buffers in, host buffers out; synchronous.  out_scores is nullable
+ * ([n_docs][n_langs] fp64).  out_labels[d] is the index into the supported
+ * languages of argmax(scores of d): first maximum, all-zero -> 0. */
+int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets,
+                int64_t n_docs, int32_t* out_labels, double* out_scores);
+
+/* Device-resident variant, asynchronous on `stream` (NULL = the context's
+ * stream).  d_bytes must be 4-byte aligned and n_bytes >= d_offsets[n_docs].
+ * d_scores is nullable.  Offsets are trusted (validate with the host API). */
+int ldgpu_score_device(ldgpu_model* model, const uint8_t* d_bytes, int64_t n_bytes,
+                       const int64_t* d_offsets, int64_t n_docs, int32_t* d_labels,
+                       double* d_scores, void* stream);
+
+/* -------------------------------------------------------------------- FIT */
+typedef struct ldgpu_counts ldgpu_counts;
+
+/* A device count table for n_langs languages and the given gram lengths.
+ * capacity_hint: expected distinct grams (0 = default); the table grows when
+ * it passes half full between batches. */
+int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths,
+                        int32_t n_grams, int64_t capacity_hint, ldgpu_counts** out);
+int ldgpu_counts_destroy(ldgpu_counts* counts);
+
+/* Accumulate one batch of documents: every window of every gram length is
+ * counted for doc_lang[d] (documents whose doc_lang is outside [0, n_langs)
+ * are skipped, as reduceGrams filters unsupported languages). */
+int ldgpu_count(ldgpu_counts* counts, const uint8_t* bytes, const int64_t* offsets,
+                const int32_t* doc_lang, int64_t n_docs);
+int ldgpu_count_device(ldgpu_counts* counts, const uint8_t* d_bytes, int64_t n_bytes,
+                       const int64_t* d_offsets, const int32_t* d_doc_lang, int64_t n_docs,
+                       void* stream);
+
+/* Distinct grams and their total key bytes. */
+int ldgpu_counts_size(ldgpu_counts* counts, int64_t* n_grams, int64_t* key_bytes);
+/* Export sorted by (length, unsigned bytes): key_bytes, key_offsets[n+1],
+ * counts[n][n_langs] (raw int64 sums; the JVM sums wrap at 2^31). */
+int ldgpu_counts_export(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
+                        int64_t* counts_out);
+
+/* Merge a dense (keys, counts[n][n_langs]) block into the table (used by the
+ * multi-GPU merge after an all-reduce over a common key list).  Keys are
+ * given packed as in ldgpu_counts_export. */
+int ldgpu_counts_add(ldgpu_counts* counts, int64_t n, const uint8_t* key_bytes,
+                     const int64_t* key_offsets, const int64_t* counts_in);
+
+/* computeProbabilities + filterTopGrams: v_l = log(1 + [g in l] / k_g);
+ * per language the profile_size largest v_l (ties: ascending (length, bytes));
+ * the union of the chosen grams with their full rows.  Two calls: _size
+ * computes and caches the table, _export copies it (sorted by (length, bytes)). */
+int ldgpu_fit_table_size(ldgpu_counts* counts, int32_t profile_size, int64_t* n_rows,
+                         int64_t* key_bytes);
+int ldgpu_fit_table_export(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
+                           double* rows);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LDGPU_H */

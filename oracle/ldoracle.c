@@ -1,0 +1,246 @@
+/* ldoracle.c -- C restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Used by tests/ (parity at sizes the Python oracle is too slow for) and by
+ * bench.py's cpu_baseline leg (kind "port").  Never linked into libldgpu.so.
+ *
+ * Follows, rule by rule (same rules as oracle/ldoracle.py):
+ *   ldo_score  -- LanguageDetectorModel.detect(Array[Byte], ...)
+ *                 LanguageDetectorModel.scala:131-156: for n in gramLengths (order,
+ *                 duplicates repeat), for every window of the Scala sliding(n)
+ *                 (partial rule: 0<len<n -> one window = whole text), a map hit does
+ *                 s[l] = s[l] + row[l] (F2J daxpy, a = 1.0), then breeze argmax
+ *                 (first max, strict >).
+ *   ldo_count  -- computeGrams + reduceGrams, LanguageDetector.scala:25-66: per doc,
+ *                 per n, every window counted; summed per (lang, gram).  Raw int64
+ *                 sums are exported; the JVM Int wrap is applied by the caller.
+ *
+ * Keys are arbitrary-length byte strings compared with memcmp: deliberately a
+ * different representation from the device's packed u64 keys.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ hashing */
+static uint64_t hbytes(const uint8_t* p, int64_t n) {
+    uint64_t h = 1469598103934665603ull; /* FNV-1a 64 */
+    for (int64_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
+    h ^= h >> 29; h *= 0xbf58476d1ce4e5b9ull; h ^= h >> 32;
+    return h;
+}
+
+typedef struct { uint64_t h; const uint8_t* p; int64_t len; int64_t idx; } entry;
+
+typedef struct {
+    entry* e; int64_t cap; int64_t n;
+} hmap;
+
+static void hm_init(hmap* m, int64_t want) {
+    int64_t cap = 16;
+    while (cap < 2 * want) cap <<= 1;
+    m->e = (entry*)calloc((size_t)cap, sizeof(entry));
+    m->cap = cap; m->n = 0;
+    for (int64_t i = 0; i < cap; ++i) m->e[i].idx = -1;
+}
+
+static int64_t hm_find(const hmap* m, const uint8_t* p, int64_t len, uint64_t h) {
+    int64_t mask = m->cap - 1, s = (int64_t)(h & (uint64_t)mask);
+    for (;;) {
+        const entry* e = &m->e[s];
+        if (e->idx < 0) return -1;
+        if (e->h == h && e->len == len && memcmp(e->p, p, (size_t)len) == 0) return e->idx;
+        s = (s + 1) & mask;
+    }
+}
+
+static void hm_grow(hmap* m);
+
+/* insert if absent; returns the entry's idx (new idx = next_idx when inserted) */
+static int64_t hm_upsert(hmap* m, const uint8_t* p, int64_t len, uint64_t h, int64_t next_idx, int* inserted) {
+    if (2 * (m->n + 1) > m->cap) hm_grow(m);
+    int64_t mask = m->cap - 1, s = (int64_t)(h & (uint64_t)mask);
+    for (;;) {
+        entry* e = &m->e[s];
+        if (e->idx < 0) {
+            e->h = h; e->p = p; e->len = len; e->idx = next_idx; m->n++;
+            *inserted = 1; return next_idx;
+        }
+        if (e->h == h && e->len == len && memcmp(e->p, p, (size_t)len) == 0) { *inserted = 0; return e->idx; }
+        s = (s + 1) & mask;
+    }
+}
+
+static void hm_grow(hmap* m) {
+    hmap n2; hm_init(&n2, m->cap);
+    for (int64_t i = 0; i < m->cap; ++i) {
+        if (m->e[i].idx < 0) continue;
+        int64_t mask = n2.cap - 1, s = (int64_t)(m->e[i].h & (uint64_t)mask);
+        while (n2.e[s].idx >= 0) s = (s + 1) & mask;
+        n2.e[s] = m->e[i]; n2.n++;
+    }
+    free(m->e); *m = n2;
+}
+
+/* -------------------------------------------------------------------- score */
+typedef struct {
+    hmap m; int32_t L; const double* rows; uint8_t* blob;
+} ldo_table;
+
+ldo_table* ldo_table_create(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets,
+                            const double* rows, int32_t L) {
+    ldo_table* t = (ldo_table*)calloc(1, sizeof(ldo_table));
+    int64_t nb = key_offsets[n_rows] - key_offsets[0];
+    t->blob = (uint8_t*)malloc((size_t)(nb > 0 ? nb : 1));
+    memcpy(t->blob, key_bytes + key_offsets[0], (size_t)nb);
+    double* r = (double*)malloc(sizeof(double) * (size_t)(n_rows * L > 0 ? n_rows * L : 1));
+    memcpy(r, rows, sizeof(double) * (size_t)(n_rows * L));
+    t->rows = r; t->L = L;
+    hm_init(&t->m, n_rows);
+    for (int64_t i = 0; i < n_rows; ++i) {
+        const uint8_t* p = t->blob + (key_offsets[i] - key_offsets[0]);
+        int64_t len = key_offsets[i + 1] - key_offsets[i];
+        uint64_t h = hbytes(p, len);
+        int ins;
+        int64_t idx = hm_upsert(&t->m, p, len, h, i, &ins);
+        if (!ins) { /* Scala toMap: a later duplicate key overwrites */
+            int64_t mask = t->m.cap - 1, s = (int64_t)(h & (uint64_t)mask);
+            while (t->m.e[s].idx != idx) s = (s + 1) & mask;
+            t->m.e[s].idx = i; t->m.e[s].p = p;
+        }
+    }
+    return t;
+}
+
+void ldo_table_destroy(ldo_table* t) {
+    if (!t) return;
+    free(t->m.e); free((void*)t->rows); free(t->blob); free(t);
+}
+
+static int32_t score_one(const ldo_table* t, const int32_t* G, int32_t nG, const uint8_t* d, int64_t len,
+                         double* s) {
+    const int32_t L = t->L;
+    for (int32_t l = 0; l < L; ++l) s[l] = 0.0;
+    for (int32_t gi = 0; gi < nG; ++gi) {
+        int64_t n = G[gi];
+        int64_t nw = len == 0 ? 0 : (len < n ? 1 : len - n + 1);
+        int64_t wl = len < n ? len : n;
+        for (int64_t p = 0; p < nw; ++p) {
+            int64_t r = hm_find(&t->m, d + p, wl, hbytes(d + p, wl));
+            if (r < 0) continue;
+            const double* row = t->rows + r * L;
+            for (int32_t l = 0; l < L; ++l) s[l] = s[l] + 1.0 * row[l];
+        }
+    }
+    int32_t bi = 0; double best = s[0];
+    for (int32_t l = 1; l < L; ++l) if (s[l] > best) { best = s[l]; bi = l; }
+    return bi;
+}
+
+typedef struct {
+    const ldo_table* t; const int32_t* G; int32_t nG; const uint8_t* bytes; const int64_t* off;
+    int64_t d0, d1; int32_t* labels; double* scores;
+} score_job;
+
+static void* score_worker(void* arg) {
+    score_job* j = (score_job*)arg;
+    const int32_t L = j->t->L;
+    double* tmp = (double*)malloc(sizeof(double) * (size_t)L);
+    for (int64_t d = j->d0; d < j->d1; ++d) {
+        double* s = j->scores ? j->scores + d * L : tmp;
+        j->labels[d] = score_one(j->t, j->G, j->nG, j->bytes + j->off[d], j->off[d + 1] - j->off[d], s);
+    }
+    free(tmp);
+    return NULL;
+}
+
+/* labels[n_docs]; scores nullable [n_docs][L]; nthreads >= 1 */
+int ldo_score(const ldo_table* t, const int32_t* G, int32_t nG, const uint8_t* bytes, const int64_t* offsets,
+              int64_t n_docs, int32_t* labels, double* scores, int32_t nthreads) {
+    if (t->L < 1) return 1;
+    for (int32_t i = 0; i < nG; ++i) if (G[i] <= 0) return 1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256]; score_job jobs[256];
+    for (int32_t i = 0; i < nthreads; ++i) {
+        jobs[i] = (score_job){t, G, nG, bytes, offsets, n_docs * i / nthreads, n_docs * (i + 1) / nthreads, labels, scores};
+        if (nthreads == 1) score_worker(&jobs[i]);
+        else pthread_create(&th[i], NULL, score_worker, &jobs[i]);
+    }
+    if (nthreads > 1) for (int32_t i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    return 0;
+}
+
+/* -------------------------------------------------------------------- count */
+typedef struct {
+    hmap m; int32_t L; int64_t n; int64_t cap_rows; int64_t* counts;
+} ldo_counts;
+
+ldo_counts* ldo_count(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, int64_t n_docs,
+                      int32_t L, const int32_t* G, int32_t nG) {
+    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
+    c->L = L; c->cap_rows = 1024;
+    c->counts = (int64_t*)calloc((size_t)(c->cap_rows * L), sizeof(int64_t));
+    hm_init(&c->m, 1024);
+    for (int64_t d = 0; d < n_docs; ++d) {
+        const uint8_t* p = bytes + offsets[d];
+        int64_t len = offsets[d + 1] - offsets[d];
+        int32_t lang = doc_lang[d];
+        if (lang < 0 || lang >= L) continue;
+        for (int32_t gi = 0; gi < nG; ++gi) {
+            int64_t n = G[gi];
+            int64_t nw = len == 0 ? 0 : (len < n ? 1 : len - n + 1);
+            int64_t wl = len < n ? len : n;
+            for (int64_t i = 0; i < nw; ++i) {
+                int ins;
+                int64_t idx = hm_upsert(&c->m, p + i, wl, hbytes(p + i, wl), c->n, &ins);
+                if (ins) {
+                    if (c->n + 1 > c->cap_rows) {
+                        int64_t nc = c->cap_rows * 2;
+                        c->counts = (int64_t*)realloc(c->counts, sizeof(int64_t) * (size_t)(nc * L));
+                        memset(c->counts + c->cap_rows * L, 0, sizeof(int64_t) * (size_t)((nc - c->cap_rows) * L));
+                        c->cap_rows = nc;
+                    }
+                    c->n++;
+                }
+                c->counts[idx * L + lang] += 1;
+            }
+        }
+    }
+    return c;
+}
+
+int64_t ldo_counts_size(const ldo_counts* c) { return c->n; }
+
+int64_t ldo_counts_key_bytes(const ldo_counts* c) {
+    int64_t s = 0;
+    for (int64_t i = 0; i < c->m.cap; ++i) if (c->m.e[i].idx >= 0) s += c->m.e[i].len;
+    return s;
+}
+
+static int cmp_entry(const void* a, const void* b) {
+    const entry* x = *(const entry* const*)a; const entry* y = *(const entry* const*)b;
+    if (x->len != y->len) return x->len < y->len ? -1 : 1;
+    return memcmp(x->p, y->p, (size_t)x->len);
+}
+
+/* export sorted by (length, unsigned bytes): key_bytes, key_offsets[n+1], counts[n][L] */
+void ldo_counts_export(const ldo_counts* c, uint8_t* key_bytes, int64_t* key_offsets, int64_t* counts) {
+    const entry** v = (const entry**)malloc(sizeof(entry*) * (size_t)(c->n > 0 ? c->n : 1));
+    int64_t k = 0;
+    for (int64_t i = 0; i < c->m.cap; ++i) if (c->m.e[i].idx >= 0) v[k++] = &c->m.e[i];
+    qsort(v, (size_t)k, sizeof(entry*), cmp_entry);
+    int64_t o = 0;
+    key_offsets[0] = 0;
+    for (int64_t i = 0; i < k; ++i) {
+        memcpy(key_bytes + o, v[i]->p, (size_t)v[i]->len);
+        o += v[i]->len; key_offsets[i + 1] = o;
+        memcpy(counts + i * c->L, c->counts + v[i]->idx * c->L, sizeof(int64_t) * (size_t)c->L);
+    }
+    free(v);
+}
+
+void ldo_counts_destroy(ldo_counts* c) {
+    if (!c) return;
+    free(c->m.e); free(c->counts); free(c);
+}

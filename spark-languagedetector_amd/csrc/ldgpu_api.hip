@@ -1,0 +1,883 @@
+// ldgpu_api.hip -- host runtime of libldgpu.so: the C ABI declared in
+// include/ldgpu.h (contexts, device tables, H2D/D2H staging, count-table
+// growth, probability / top-K table build).
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ldgpu.h"
+#include "ldgpu_internal.h"
+
+using namespace ldgpu;
+
+// ------------------------------------------------------------------- errors
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int ok() {
+    g_err.clear();
+    return LDGPU_OK;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return fail(LDGPU_EDEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int log2u(uint64_t p) {
+    int l = 0;
+    while ((1ull << l) < p) ++l;
+    return l;
+}
+
+// device buffer that only grows
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1 << 20);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+int check_grams(const int32_t* G, int32_t nG) {
+    if (nG < 0 || nG > LDGPU_MAX_GRAM_LENGTHS)
+        return fail(LDGPU_EINVAL, "number of gram lengths %d outside [0, %d]", nG, LDGPU_MAX_GRAM_LENGTHS);
+    if (nG > 0 && !G) return fail(LDGPU_EINVAL, "gram_lengths is NULL");
+    for (int i = 0; i < nG; ++i) {
+        if (G[i] <= 0)
+            return fail(LDGPU_EINVAL, "requirement failed: size=%d and step=1, but both must be positive", G[i]);
+        if (G[i] > LDGPU_MAX_GRAM)
+            return fail(LDGPU_EUNSUPPORTED, "gram length %d exceeds the device path's limit of %d bytes", G[i],
+                        LDGPU_MAX_GRAM);
+    }
+    return LDGPU_OK;
+}
+
+int check_offsets(const int64_t* off, int64_t n_docs) {
+    if (n_docs < 0) return fail(LDGPU_EINVAL, "n_docs < 0");
+    if (!off) return fail(LDGPU_EINVAL, "offsets is NULL");
+    if (off[0] < 0) return fail(LDGPU_EINVAL, "offsets[0] < 0");
+    for (int64_t d = 0; d < n_docs; ++d)
+        if (off[d + 1] < off[d]) return fail(LDGPU_EINVAL, "offsets decrease at document %lld", (long long)d);
+    return LDGPU_OK;
+}
+
+// (length, unsigned bytes) order of a packed key
+inline uint64_t sort_key(uint64_t key) {
+    const int len = key_len(key);
+    uint64_t s = (uint64_t)len << 56;
+    for (int i = 0; i < len; ++i) s |= ((key >> (8 * i)) & 0xffull) << (48 - 8 * i);
+    return s;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ context
+struct ldgpu_ctx {
+    int device = 0;
+    int cus = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf bytes, offsets, labels, scores, langs;
+};
+
+extern "C" const char* ldgpu_version(void) { return "ldgpu 0.1.0 (gfx950)"; }
+extern "C" const char* ldgpu_last_error(void) { return g_err.c_str(); }
+
+extern "C" int ldgpu_device_count(int32_t* out) {
+    if (!out) return fail(LDGPU_EINVAL, "out is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return ok();
+}
+
+extern "C" int ldgpu_ctx_create(int32_t device, ldgpu_ctx** out) {
+    if (!out) return fail(LDGPU_EINVAL, "out is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(LDGPU_ENODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(LDGPU_EINVAL, "device %d outside [0, %d)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    auto* c = new ldgpu_ctx();
+    c->device = device;
+    c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(LDGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return ok();
+}
+
+extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
+    if (!c) return ok();
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->bytes.release();
+    c->offsets.release();
+    c->labels.release();
+    c->scores.release();
+    c->langs.release();
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return ok();
+}
+
+extern "C" int ldgpu_ctx_synchronize(ldgpu_ctx* c) {
+    if (!c) return fail(LDGPU_EINVAL, "ctx is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ok();
+}
+
+extern "C" void* ldgpu_ctx_stream(ldgpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// -------------------------------------------------------------------- model
+struct ldgpu_model {
+    ldgpu_ctx* ctx = nullptr;
+    int32_t L = 0, nG = 0;
+    int32_t G[kMaxGramLengths] = {};
+    int slices = 1;
+    bool dense = false;
+    bool lds_filter = true;
+    bool has_bad = false;
+    int64_t n_keys = 0;
+    uint64_t slot_cap = 0;
+    int filter_log2 = 10;
+    size_t lds_bytes = 0;
+    int wg_per_cu = 1;
+    size_t device_bytes = 0;
+    Slot* d_slots = nullptr;
+    uint32_t* d_filter = nullptr;
+    uint64_t* d_masks = nullptr;
+    double* d_vals = nullptr;
+    double* d_rows = nullptr;
+    int32_t* d_err = nullptr;
+};
+
+namespace {
+void model_free(ldgpu_model* m) {
+    if (!m) return;
+    if (m->ctx) (void)hipSetDevice(m->ctx->device);
+    for (void* p : {(void*)m->d_slots, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
+                    (void*)m->d_err})
+        if (p) (void)hipFree(p);
+    delete m;
+}
+
+template <typename T>
+hipError_t upload(T** dst, const std::vector<T>& src, size_t* total) {
+    const size_t n = std::max<size_t>(src.size(), 1) * sizeof(T);
+    hipError_t e = hipMalloc((void**)dst, n);
+    if (e != hipSuccess) return e;
+    *total += n;
+    if (src.empty()) return hipMemset(*dst, 0, n);
+    return hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+}  // namespace
+
+extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                                  const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
+                                  int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                                  ldgpu_model** out) {
+    if (!ctx || !out) return fail(LDGPU_EINVAL, "ctx/out is NULL");
+    if (n_langs < 1) return fail(LDGPU_EINVAL, "No values in array: the model has no supported languages");
+    if (n_langs > LDGPU_MAX_LANGS)
+        return fail(LDGPU_EUNSUPPORTED, "%d languages exceed the device path's limit of %d", n_langs,
+                    LDGPU_MAX_LANGS);
+    if (n_rows < 0) return fail(LDGPU_EINVAL, "n_rows < 0");
+    if (n_rows > 0 && (!key_bytes || !key_offsets || !rows)) return fail(LDGPU_EINVAL, "table pointer is NULL");
+    if (int rc = check_grams(gram_lengths, n_grams)) return rc;
+    int maxg = 0;
+    for (int i = 0; i < n_grams; ++i) maxg = std::max(maxg, gram_lengths[i]);
+
+    // host map, Scala toMap semantics (a later duplicate key wins); keys longer
+    // than every window (> max gram length) can never be hit and stay host-side.
+    std::unordered_map<uint64_t, int64_t> idx;
+    idx.reserve((size_t)n_rows * 2 + 1);
+    std::vector<uint64_t> keys;
+    std::vector<int64_t> src_row;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t len = key_offsets[r + 1] - key_offsets[r];
+        if (len < 0) return fail(LDGPU_EINVAL, "key_offsets decrease at row %lld", (long long)r);
+        if (len == 0 || len > maxg) continue;
+        const uint64_t k = pack_key_host(key_bytes + key_offsets[r], (int)len);
+        auto it = idx.find(k);
+        if (it == idx.end()) {
+            idx.emplace(k, (int64_t)keys.size());
+            keys.push_back(k);
+            src_row.push_back(r);
+        } else {
+            src_row[it->second] = r;
+        }
+    }
+    const int64_t nk = (int64_t)keys.size();
+    const int S = (n_langs + 63) / 64;
+
+    // mask form: every nonzero entry of every row bitwise equal within the row
+    bool dense = false;
+    for (int64_t i = 0; i < nk && !dense; ++i) {
+        const double* rw = rows + src_row[i] * (int64_t)n_langs;
+        uint64_t v = 0;
+        bool have = false;
+        for (int l = 0; l < n_langs; ++l) {
+            if (rw[l] == 0.0) continue;
+            uint64_t b;
+            memcpy(&b, &rw[l], 8);
+            if (!have) {
+                v = b;
+                have = true;
+            } else if (b != v) {
+                dense = true;
+                break;
+            }
+        }
+    }
+
+    auto* m = new ldgpu_model();
+    m->ctx = ctx;
+    m->L = n_langs;
+    m->nG = n_grams;
+    for (int i = 0; i < n_grams; ++i) m->G[i] = gram_lengths[i];
+    m->slices = S;
+    m->dense = dense;
+    m->n_keys = nk;
+
+    std::vector<uint64_t> masks;
+    std::vector<double> vals, drows;
+    if (!dense) {
+        masks.assign((size_t)nk * S, 0);
+        vals.assign((size_t)nk, 0.0);
+        for (int64_t i = 0; i < nk; ++i) {
+            const double* rw = rows + src_row[i] * (int64_t)n_langs;
+            for (int l = 0; l < n_langs; ++l) {
+                if (rw[l] == 0.0) continue;
+                masks[(size_t)i * S + l / 64] |= 1ull << (l % 64);
+                vals[i] = rw[l];
+            }
+        }
+    } else {
+        drows.resize((size_t)nk * n_langs);
+        for (int64_t i = 0; i < nk; ++i)
+            memcpy(&drows[(size_t)i * n_langs], rows + src_row[i] * (int64_t)n_langs, sizeof(double) * n_langs);
+    }
+
+    // key -> row slots
+    m->slot_cap = next_pow2(std::max<uint64_t>(16, 2 * (uint64_t)nk));
+    const int slog = log2u(m->slot_cap);
+    std::vector<Slot> slots(m->slot_cap, Slot{kEmpty, 0, 0});
+    for (int64_t i = 0; i < nk; ++i) {
+        uint64_t s = mix64(keys[i]) >> (64 - slog);
+        while (slots[s].key != kEmpty) s = (s + 1) & (m->slot_cap - 1);
+        slots[s].key = keys[i];
+        slots[s].row = (uint32_t)i;
+        if (row_ok && !row_ok[src_row[i]]) {
+            slots[s].row |= kBadRow;
+            m->has_bad = true;
+        }
+    }
+
+    // bit filter: >= 32 bits per key while it fits LDS (<= 64 KiB), else a
+    // global (L2 / Infinity-Cache resident) filter at 16 bits per key
+    uint64_t fbits = next_pow2(std::max<uint64_t>(1024, 32 * (uint64_t)nk));
+    m->lds_filter = fbits <= (1ull << kMaxLdsFilterLog2);
+    if (!m->lds_filter) fbits = std::min<uint64_t>(next_pow2(16 * (uint64_t)nk), 1ull << 31);
+    m->filter_log2 = log2u(fbits);
+    std::vector<uint32_t> filter(fbits / 32, 0u);
+    for (int64_t i = 0; i < nk; ++i) {
+        const uint32_t bit = filter_hash_key(keys[i]) >> (32 - m->filter_log2);
+        filter[bit >> 5] |= 1u << (bit & 31);
+    }
+
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = upload(&m->d_slots, slots, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_filter, filter, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_masks, masks, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_vals, vals, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_rows, drows, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
+    m->lds_bytes = (m->lds_filter ? (size_t)(fbits / 8) : 0) + (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
+    m->wg_per_cu = std::max<int>(1, std::min<int>(2, (int)(163840 / m->lds_bytes)));
+    if (e == hipSuccess) e = score_prepare(S, dense, m->lds_filter, m->lds_bytes);
+    if (e != hipSuccess) {
+        model_free(m);
+        return fail(e == hipErrorOutOfMemory ? LDGPU_ENOMEM : LDGPU_EDEVICE, "model upload: %s",
+                    hipGetErrorString(e));
+    }
+    *out = m;
+    return ok();
+}
+
+extern "C" int ldgpu_model_destroy(ldgpu_model* m) {
+    model_free(m);
+    return ok();
+}
+
+extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_keys, int64_t* table_slots,
+                                int64_t* filter_bits, int64_t* device_bytes) {
+    if (!m) return fail(LDGPU_EINVAL, "model is NULL");
+    if (mode) *mode = m->dense ? 1 : 0;
+    if (n_keys) *n_keys = m->n_keys;
+    if (table_slots) *table_slots = (int64_t)m->slot_cap;
+    if (filter_bits) *filter_bits = (int64_t)1 << m->filter_log2;
+    if (device_bytes) *device_bytes = (int64_t)m->device_bytes;
+    return ok();
+}
+
+namespace {
+int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
+                 int32_t* d_labels, double* d_scores, hipStream_t st) {
+    if (n_docs == 0) return LDGPU_OK;
+    ScoreParams p{};
+    p.bytes = d_bytes;
+    p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+    p.offsets = d_offsets;
+    p.n_docs = n_docs;
+    p.labels = d_labels;
+    p.scores = d_scores;
+    p.slots = m->d_slots;
+    const int slog = log2u(m->slot_cap);
+    p.slot_shift = (uint32_t)(64 - slog);
+    p.slot_mask = m->slot_cap - 1;
+    p.filter = m->d_filter;
+    p.filter_shift = (uint32_t)(32 - m->filter_log2);
+    p.filter_words = (uint32_t)(((uint64_t)1 << m->filter_log2) / 32);
+    p.masks = m->d_masks;
+    p.vals = m->d_vals;
+    p.rows = m->d_rows;
+    p.err = m->d_err;
+    p.L = m->L;
+    p.nG = m->nG;
+    for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
+    const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
+    HIP_TRY(launch_score(p, m->slices, m->dense, m->lds_filter, grid, st));
+    return LDGPU_OK;
+}
+
+int check_row_error(ldgpu_model* m, hipStream_t st) {
+    int32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, m->d_err, sizeof err, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (err) {
+        int32_t z = 0;
+        HIP_TRY(hipMemcpy(m->d_err, &z, sizeof z, hipMemcpyHostToDevice));
+        return fail(LDGPU_EROWLEN, "requirement failed: BLAS.axpy size mismatch (a hit gram's row length != %d)",
+                    m->L);
+    }
+    return LDGPU_OK;
+}
+}  // namespace
+
+extern "C" int ldgpu_score_device(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                                  int64_t n_docs, int32_t* d_labels, double* d_scores, void* stream) {
+    if (!m) return fail(LDGPU_EINVAL, "model is NULL");
+    if (n_docs < 0) return fail(LDGPU_EINVAL, "n_docs < 0");
+    if (n_docs > 0 && (!d_offsets || !d_labels || (n_bytes > 0 && !d_bytes)))
+        return fail(LDGPU_EINVAL, "device pointer is NULL");
+    if (((uintptr_t)d_bytes & 3) != 0) return fail(LDGPU_EINVAL, "d_bytes must be 4-byte aligned");
+    hipStream_t st = stream ? (hipStream_t)stream : m->ctx->stream;
+    HIP_TRY(hipSetDevice(m->ctx->device));
+    if (int rc = score_launch(m, d_bytes, n_bytes, d_offsets, n_docs, d_labels, d_scores, st)) return rc;
+    if (m->has_bad) {
+        if (int rc = check_row_error(m, st)) return rc;
+    }
+    return ok();
+}
+
+extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* offsets, int64_t n_docs,
+                           int32_t* out_labels, double* out_scores) {
+    if (!m) return fail(LDGPU_EINVAL, "model is NULL");
+    if (int rc = check_offsets(offsets, n_docs)) return rc;
+    if (n_docs == 0) return ok();
+    if (!out_labels) return fail(LDGPU_EINVAL, "out_labels is NULL");
+    if (!bytes && offsets[n_docs] > offsets[0]) return fail(LDGPU_EINVAL, "bytes is NULL");
+    ldgpu_ctx* c = m->ctx;
+    std::lock_guard<std::mutex> lock(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t kChunkBytes = 256ll << 20, kChunkDocs = 8ll << 20;
+    std::vector<int64_t> off;
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0 + 1;
+        while (d1 < n_docs && d1 - d0 < kChunkDocs && offsets[d1 + 1] - offsets[d0] <= kChunkBytes) ++d1;
+        const int64_t nd = d1 - d0, b0 = offsets[d0], nb = offsets[d1] - b0;
+        off.resize(nd + 1);
+        for (int64_t i = 0; i <= nd; ++i) off[i] = offsets[d0 + i] - b0;
+        HIP_TRY(c->bytes.ensure((size_t)nb + 16));
+        HIP_TRY(c->offsets.ensure(sizeof(int64_t) * (nd + 1)));
+        HIP_TRY(c->labels.ensure(sizeof(int32_t) * nd));
+        if (out_scores) HIP_TRY(c->scores.ensure(sizeof(double) * nd * m->L));
+        if (nb) HIP_TRY(hipMemcpyAsync(c->bytes.p, bytes + b0, nb, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->offsets.p, off.data(), sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice,
+                               c->stream));
+        if (int rc = score_launch(m, (const uint8_t*)c->bytes.p, nb, (const int64_t*)c->offsets.p, nd,
+                                  (int32_t*)c->labels.p, out_scores ? (double*)c->scores.p : nullptr, c->stream))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(out_labels + d0, c->labels.p, sizeof(int32_t) * nd, hipMemcpyDeviceToHost,
+                               c->stream));
+        if (out_scores)
+            HIP_TRY(hipMemcpyAsync(out_scores + d0 * m->L, c->scores.p, sizeof(double) * nd * m->L,
+                                   hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        d0 = d1;
+    }
+    if (m->has_bad) {
+        if (int rc = check_row_error(m, c->stream)) return rc;
+    }
+    return ok();
+}
+
+// ---------------------------------------------------------------------- FIT
+struct ldgpu_counts {
+    ldgpu_ctx* ctx = nullptr;
+    int32_t L = 0, nG = 0;
+    int32_t G[kMaxGramLengths] = {};
+    uint64_t cap = 0;
+    uint64_t* d_keys = nullptr;
+    unsigned long long* d_counts = nullptr;
+    unsigned long long* d_size = nullptr;
+    uint64_t* d_ovf_keys = nullptr;
+    int32_t* d_ovf_lang = nullptr;
+    unsigned int* d_ovf_n = nullptr;
+    uint32_t ovf_cap = 1u << 22;
+    uint64_t size = 0;
+    // cached fit table (ldgpu_fit_table_size -> _export)
+    bool tbl_valid = false;
+    std::vector<uint8_t> tbl_bytes;
+    std::vector<int64_t> tbl_off;
+    std::vector<double> tbl_rows;
+};
+
+namespace {
+CountParams count_params(const ldgpu_counts* c) {
+    CountParams p{};
+    p.keys = c->d_keys;
+    p.counts = c->d_counts;
+    p.shift = (uint32_t)(64 - log2u(c->cap));
+    p.mask = c->cap - 1;
+    p.size = c->d_size;
+    p.ovf_keys = c->d_ovf_keys;
+    p.ovf_lang = c->d_ovf_lang;
+    p.ovf_n = c->d_ovf_n;
+    p.ovf_cap = c->ovf_cap;
+    p.L = c->L;
+    p.nG = c->nG;
+    for (int i = 0; i < c->nG; ++i) p.G[i] = c->G[i];
+    return p;
+}
+
+void counts_free(ldgpu_counts* c) {
+    if (!c) return;
+    if (c->ctx) (void)hipSetDevice(c->ctx->device);
+    for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_size, (void*)c->d_ovf_keys,
+                    (void*)c->d_ovf_lang, (void*)c->d_ovf_n})
+        if (p) (void)hipFree(p);
+    delete c;
+}
+
+int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, unsigned long long** counts) {
+    HIP_TRY(hipMalloc((void**)keys, cap * sizeof(uint64_t)));
+    hipError_t e = hipMalloc((void**)counts, cap * (size_t)c->L * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        (void)hipFree(*keys);
+        *keys = nullptr;
+        return fail(LDGPU_ENOMEM, "count table of %llu slots: %s", (unsigned long long)cap, hipGetErrorString(e));
+    }
+    HIP_TRY(hipMemsetAsync(*keys, 0, cap * sizeof(uint64_t), c->ctx->stream));
+    HIP_TRY(hipMemsetAsync(*counts, 0, cap * (size_t)c->L * sizeof(unsigned long long), c->ctx->stream));
+    return LDGPU_OK;
+}
+
+// grow to new_cap (power of two) by rehashing on the device
+int grow(ldgpu_counts* c, uint64_t new_cap) {
+    if (new_cap <= c->cap) return LDGPU_OK;
+    uint64_t* nk = nullptr;
+    unsigned long long* nc = nullptr;
+    if (int rc = alloc_table(c, new_cap, &nk, &nc)) return rc;
+    CountParams from = count_params(c);
+    ldgpu_counts tmp;
+    tmp.L = c->L;
+    tmp.cap = new_cap;
+    tmp.d_keys = nk;
+    tmp.d_counts = nc;
+    CountParams to = count_params(&tmp);
+    HIP_TRY(launch_rehash(from, to, c->cap, c->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    (void)hipFree(c->d_keys);
+    (void)hipFree(c->d_counts);
+    c->d_keys = nk;
+    c->d_counts = nc;
+    c->cap = new_cap;
+    return LDGPU_OK;
+}
+
+// after a batch: read size / overflow, grow, re-insert overflow entries
+int after_batch(ldgpu_counts* c) {
+    unsigned long long size = 0;
+    unsigned int novf = 0;
+    HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&novf, c->d_ovf_n, sizeof novf, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    if (novf > c->ovf_cap)
+        return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost): pass a larger capacity_hint", novf);
+    c->size = size;
+    if (2 * (size + novf) > c->cap || novf > 0) {
+        if (int rc = grow(c, next_pow2(4 * (size + novf) + 16))) return rc;
+    }
+    if (novf > 0) {
+        CountParams p = count_params(c);
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream));
+        HIP_TRY(launch_counts_add(p, c->d_ovf_keys, nullptr, c->d_ovf_lang, novf, c->ctx->stream));
+        unsigned int again = 0;
+        HIP_TRY(hipMemcpyAsync(&again, c->d_ovf_n, sizeof again, hipMemcpyDeviceToHost, c->ctx->stream));
+        HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
+        HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+        if (again) return fail(LDGPU_ENOMEM, "count table overflow after growing");
+        c->size = size;
+    }
+    c->tbl_valid = false;
+    return LDGPU_OK;
+}
+
+int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                 const int32_t* d_lang, int64_t n_docs, hipStream_t st) {
+    if (n_docs == 0) return LDGPU_OK;
+    CountParams p = count_params(c);
+    p.bytes = d_bytes;
+    p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+    p.offsets = d_offsets;
+    p.doc_lang = d_lang;
+    p.n_docs = n_docs;
+    const int64_t want = (n_docs + kCountWaves - 1) / kCountWaves;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->ctx->cus * 2));
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+    HIP_TRY(launch_count(p, grid, st));
+    if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));
+    return after_batch(c);
+}
+}  // namespace
+
+extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                                   int64_t capacity_hint, ldgpu_counts** out) {
+    if (!ctx || !out) return fail(LDGPU_EINVAL, "ctx/out is NULL");
+    if (n_langs < 1 || n_langs > LDGPU_MAX_LANGS)
+        return fail(n_langs < 1 ? LDGPU_EINVAL : LDGPU_EUNSUPPORTED, "n_langs %d outside [1, %d]", n_langs,
+                    LDGPU_MAX_LANGS);
+    if (int rc = check_grams(gram_lengths, n_grams)) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto* c = new ldgpu_counts();
+    c->ctx = ctx;
+    c->L = n_langs;
+    c->nG = n_grams;
+    for (int i = 0; i < n_grams; ++i) c->G[i] = gram_lengths[i];
+    c->cap = next_pow2(std::max<int64_t>(1 << 12, 2 * std::max<int64_t>(capacity_hint, 0)));
+    int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
+    hipError_t e = hipSuccess;
+    if (!rc) e = hipMalloc((void**)&c->d_size, sizeof(unsigned long long));
+    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
+    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
+    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_n, sizeof(unsigned int));
+    if (!rc && e == hipSuccess) e = hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), ctx->stream);
+    if (!rc && e == hipSuccess) e = hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), ctx->stream);
+    if (!rc && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (rc || e != hipSuccess) {
+        counts_free(c);
+        return rc ? rc : fail(LDGPU_ENOMEM, "count table: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return ok();
+}
+
+extern "C" int ldgpu_counts_destroy(ldgpu_counts* c) {
+    counts_free(c);
+    return ok();
+}
+
+extern "C" int ldgpu_count_device(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                                  const int32_t* d_doc_lang, int64_t n_docs, void* stream) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (n_docs < 0) return fail(LDGPU_EINVAL, "n_docs < 0");
+    if (n_docs > 0 && (!d_offsets || !d_doc_lang || (n_bytes > 0 && !d_bytes)))
+        return fail(LDGPU_EINVAL, "device pointer is NULL");
+    if (((uintptr_t)d_bytes & 3) != 0) return fail(LDGPU_EINVAL, "d_bytes must be 4-byte aligned");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->ctx->stream;
+    if (int rc = count_launch(c, d_bytes, n_bytes, d_offsets, d_doc_lang, n_docs, st)) return rc;
+    return ok();
+}
+
+extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang,
+                           int64_t n_docs) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (int rc = check_offsets(offsets, n_docs)) return rc;
+    if (n_docs == 0) return ok();
+    if (!doc_lang) return fail(LDGPU_EINVAL, "doc_lang is NULL");
+    if (!bytes && offsets[n_docs] > offsets[0]) return fail(LDGPU_EINVAL, "bytes is NULL");
+    ldgpu_ctx* x = c->ctx;
+    std::lock_guard<std::mutex> lock(x->mu);
+    HIP_TRY(hipSetDevice(x->device));
+    const int64_t kChunkBytes = 64ll << 20, kChunkDocs = 4ll << 20;
+    std::vector<int64_t> off;
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0 + 1;
+        while (d1 < n_docs && d1 - d0 < kChunkDocs && offsets[d1 + 1] - offsets[d0] <= kChunkBytes) ++d1;
+        const int64_t nd = d1 - d0, b0 = offsets[d0], nb = offsets[d1] - b0;
+        off.resize(nd + 1);
+        for (int64_t i = 0; i <= nd; ++i) off[i] = offsets[d0 + i] - b0;
+        HIP_TRY(x->bytes.ensure((size_t)nb + 16));
+        HIP_TRY(x->offsets.ensure(sizeof(int64_t) * (nd + 1)));
+        HIP_TRY(x->langs.ensure(sizeof(int32_t) * nd));
+        if (nb) HIP_TRY(hipMemcpyAsync(x->bytes.p, bytes + b0, nb, hipMemcpyHostToDevice, x->stream));
+        HIP_TRY(hipMemcpyAsync(x->offsets.p, off.data(), sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice,
+                               x->stream));
+        HIP_TRY(hipMemcpyAsync(x->langs.p, doc_lang + d0, sizeof(int32_t) * nd, hipMemcpyHostToDevice, x->stream));
+        if (int rc = count_launch(c, (const uint8_t*)x->bytes.p, nb, (const int64_t*)x->offsets.p,
+                                  (const int32_t*)x->langs.p, nd, x->stream))
+            return rc;
+        d0 = d1;
+    }
+    return ok();
+}
+
+namespace {
+// compacted host copy: keys + counts rows, sorted by (length, bytes)
+int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsigned long long>& cnt) {
+    const uint64_t n = c->size;
+    uint64_t* d_k = nullptr;
+    unsigned long long *d_c = nullptr, *d_n = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_k, std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
+    hipError_t e = hipMalloc((void**)&d_c, std::max<uint64_t>(n, 1) * c->L * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_n, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(d_n, 0, sizeof(unsigned long long), c->ctx->stream);
+    if (e == hipSuccess) e = launch_compact(count_params(c), c->cap, d_k, d_c, d_n, c->ctx->stream);
+    unsigned long long got = 0;
+    std::vector<uint64_t> k(n);
+    std::vector<unsigned long long> cc((size_t)n * c->L);
+    if (e == hipSuccess) e = hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, c->ctx->stream);
+    if (e == hipSuccess && n)
+        e = hipMemcpyAsync(k.data(), d_k, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->ctx->stream);
+    if (e == hipSuccess && n)
+        e = hipMemcpyAsync(cc.data(), d_c, n * c->L * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
+    for (void* p : {(void*)d_k, (void*)d_c, (void*)d_n})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "count export: %s", hipGetErrorString(e));
+    if (got != n) return fail(LDGPU_EDEVICE, "count export: %llu slots occupied, %llu expected", got,
+                              (unsigned long long)n);
+    std::vector<uint64_t> order(n);
+    std::vector<std::pair<uint64_t, uint64_t>> sk(n);
+    for (uint64_t i = 0; i < n; ++i) sk[i] = {sort_key(k[i]), i};
+    std::sort(sk.begin(), sk.end());
+    keys.resize(n);
+    cnt.resize((size_t)n * c->L);
+    for (uint64_t i = 0; i < n; ++i) {
+        keys[i] = k[sk[i].second];
+        memcpy(&cnt[(size_t)i * c->L], &cc[(size_t)sk[i].second * c->L], sizeof(unsigned long long) * c->L);
+    }
+    return LDGPU_OK;
+}
+
+void write_keys(const std::vector<uint64_t>& keys, uint8_t* key_bytes, int64_t* key_offsets) {
+    int64_t o = 0;
+    key_offsets[0] = 0;
+    for (size_t i = 0; i < keys.size(); ++i) {
+        const int len = key_len(keys[i]);
+        for (int j = 0; j < len; ++j) key_bytes[o + j] = (uint8_t)(keys[i] >> (8 * j));
+        o += len;
+        key_offsets[i + 1] = o;
+    }
+}
+}  // namespace
+
+extern "C" int ldgpu_counts_size(ldgpu_counts* c, int64_t* n_grams, int64_t* key_bytes) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    if (n_grams) *n_grams = (int64_t)c->size;
+    if (key_bytes) {
+        std::vector<uint64_t> k;
+        std::vector<unsigned long long> cc;
+        if (int rc = counts_pull(c, k, cc)) return rc;
+        int64_t s = 0;
+        for (uint64_t x : k) s += key_len(x);
+        *key_bytes = s;
+    }
+    return ok();
+}
+
+extern "C" int ldgpu_counts_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t* key_offsets, int64_t* counts_out) {
+    if (!c || !key_offsets || !counts_out) return fail(LDGPU_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    std::vector<uint64_t> k;
+    std::vector<unsigned long long> cc;
+    if (int rc = counts_pull(c, k, cc)) return rc;
+    write_keys(k, key_bytes, key_offsets);
+    for (size_t i = 0; i < cc.size(); ++i) counts_out[i] = (int64_t)cc[i];
+    return ok();
+}
+
+extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_bytes, const int64_t* key_offsets,
+                                const int64_t* counts_in) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
+    if (n == 0) return ok();
+    if (!key_bytes || !key_offsets || !counts_in) return fail(LDGPU_EINVAL, "NULL argument");
+    std::vector<uint64_t> keys(n);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = key_offsets[i + 1] - key_offsets[i];
+        if (len < 1 || len > LDGPU_MAX_GRAM)
+            return fail(LDGPU_EINVAL, "key %lld has length %lld outside [1, %d]", (long long)i, (long long)len,
+                        LDGPU_MAX_GRAM);
+        keys[i] = pack_key_host(key_bytes + key_offsets[i], (int)len);
+    }
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    if (2 * (c->size + (uint64_t)n) > c->cap) {
+        if (int rc = grow(c, next_pow2(4 * (c->size + n) + 16))) return rc;
+    }
+    uint64_t* d_k = nullptr;
+    unsigned long long* d_c = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_k, n * sizeof(uint64_t)));
+    hipError_t e = hipMalloc((void**)&d_c, (size_t)n * c->L * sizeof(unsigned long long));
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_k, keys.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, c->ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_c, counts_in, (size_t)n * c->L * sizeof(int64_t), hipMemcpyHostToDevice, c->ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream);
+    if (e == hipSuccess) e = launch_counts_add(count_params(c), d_k, d_c, nullptr, n, c->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
+    (void)hipFree(d_k);
+    if (d_c) (void)hipFree(d_c);
+    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "counts_add: %s", hipGetErrorString(e));
+    if (int rc = after_batch(c)) return rc;
+    return ok();
+}
+
+// computeProbabilities + filterTopGrams (LanguageDetector.scala:75-132).
+extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    std::vector<uint64_t> keys;
+    std::vector<unsigned long long> cnt;
+    if (int rc = counts_pull(c, keys, cnt)) return rc;
+    const int L = c->L;
+    const size_t n = keys.size();
+    // presence class k_g = #languages with the gram; v_l = log(1 + [l]/k)
+    std::vector<int> kg(n, 0);
+    for (size_t i = 0; i < n; ++i)
+        for (int l = 0; l < L; ++l) kg[i] += cnt[i * L + l] > 0;
+    std::vector<double> w(L + 1, 0.0);
+    for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
+    // per language: count per class, then the threshold class and how many of
+    // it to take (keys are already in (length, bytes) order = the tie-break)
+    std::vector<uint8_t> chosen(n, 0);
+    if (K > 0) {
+        std::vector<int64_t> per((size_t)L * (L + 1), 0);
+        for (size_t i = 0; i < n; ++i)
+            for (int l = 0; l < L; ++l)
+                if (cnt[i * L + l]) per[(size_t)l * (L + 1) + kg[i]]++;
+        std::vector<int> kstar(L, L + 1);
+        std::vector<int64_t> need(L, 0), absent_need(L, 0);
+        for (int l = 0; l < L; ++l) {
+            int64_t acc = 0;
+            for (int k = 1; k <= L; ++k) {
+                const int64_t c_k = per[(size_t)l * (L + 1) + k];
+                if (acc + c_k >= K) {
+                    kstar[l] = k;
+                    need[l] = K - acc;
+                    break;
+                }
+                acc += c_k;
+            }
+            if (kstar[l] == L + 1) absent_need[l] = K - acc;  // every present gram + zeros
+        }
+        std::vector<int64_t> taken(L, 0), absent_taken(L, 0);
+        for (size_t i = 0; i < n; ++i) {
+            for (int l = 0; l < L; ++l) {
+                if (cnt[i * L + l]) {
+                    if (kg[i] < kstar[l]) {
+                        chosen[i] = 1;
+                    } else if (kg[i] == kstar[l] && taken[l] < need[l]) {
+                        taken[l]++;
+                        chosen[i] = 1;
+                    }
+                } else if (absent_taken[l] < absent_need[l]) {
+                    absent_taken[l]++;
+                    chosen[i] = 1;
+                }
+            }
+        }
+    }
+    std::vector<uint64_t> out_keys;
+    c->tbl_rows.clear();
+    for (size_t i = 0; i < n; ++i) {
+        if (!chosen[i]) continue;
+        out_keys.push_back(keys[i]);
+        for (int l = 0; l < L; ++l) c->tbl_rows.push_back(cnt[i * L + l] ? w[kg[i]] : 0.0);
+    }
+    int64_t nb = 0;
+    for (uint64_t k : out_keys) nb += key_len(k);
+    c->tbl_bytes.assign((size_t)std::max<int64_t>(nb, 1), 0);
+    c->tbl_off.assign(out_keys.size() + 1, 0);
+    write_keys(out_keys, c->tbl_bytes.data(), c->tbl_off.data());
+    c->tbl_valid = true;
+    if (n_rows) *n_rows = (int64_t)out_keys.size();
+    if (key_bytes) *key_bytes = nb;
+    return ok();
+}
+
+extern "C" int ldgpu_fit_table_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t* key_offsets, double* rows) {
+    if (!c || !key_offsets || !rows) return fail(LDGPU_EINVAL, "NULL argument");
+    if (!c->tbl_valid) return fail(LDGPU_EINVAL, "call ldgpu_fit_table_size first");
+    const size_t n = c->tbl_off.size() - 1;
+    if (c->tbl_off[n] && !key_bytes) return fail(LDGPU_EINVAL, "key_bytes is NULL");
+    if (c->tbl_off[n]) memcpy(key_bytes, c->tbl_bytes.data(), (size_t)c->tbl_off[n]);
+    memcpy(key_offsets, c->tbl_off.data(), sizeof(int64_t) * (n + 1));
+    if (!c->tbl_rows.empty()) memcpy(rows, c->tbl_rows.data(), sizeof(double) * c->tbl_rows.size());
+    return ok();
+}

@@ -1,0 +1,207 @@
+// ldgpu_fit.hip -- FIT counting kernels for gfx950.
+//
+// Semantic target: computeGrams + reduceGrams (LanguageDetector.scala:25-66):
+// for every training document (lang, text), for every n in gramLengths (order,
+// duplicates included), every window of the Scala sliding(n) over the UTF-8
+// bytes (0 < len < n -> the whole text) adds 1 to count(lang, window).
+//
+// Table: one open-addressed hash table keyed by the packed gram key with a
+// row of L u64 counters per slot (keys[cap], counts[cap][L]).  Integer atomics
+// are order-independent, so the counts are bit-exact whatever the schedule.
+//
+// Kernel structure (one wave per document, persistent grid): lanes = 64
+// consecutive window positions of one gram length.  1-gram windows (the
+// hottest keys: every document hits ' ', 'e', ...) are first aggregated in a
+// per-wave 256-bin LDS histogram and flushed once per document, so the global
+// atomics on those rows drop from one per byte to one per distinct byte per
+// document.  Longer keys insert straight into the global table: find-or-CAS
+// the key (relaxed agent-scope loads, device-scope CAS), then one u64 atomic
+// add on the (slot, lang) counter.  An insert that exceeds kMaxProbe probes
+// appends (key, lang) to an overflow list that the host re-inserts after
+// growing the table.
+#include "ldgpu_internal.h"
+
+namespace ldgpu {
+
+namespace {
+
+__device__ __forceinline__ uint32_t ld_dw(const uint32_t* w, int64_t i, int64_t last) {
+    return w[i < last ? i : last];
+}
+
+// find-or-insert; returns the slot or -1 when the probe limit is reached
+__device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key) {
+    uint64_t s = mix64(key) >> p.shift;
+    for (int probe = 0; probe < kMaxProbe; ++probe) {
+        uint64_t k = __hip_atomic_load(&p.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key) return (int64_t)s;
+        if (k == kEmpty) {
+            const unsigned long long old =
+                atomicCAS(reinterpret_cast<unsigned long long*>(&p.keys[s]), 0ull, (unsigned long long)key);
+            if (old == 0ull) {
+                atomicAdd(p.size, 1ull);
+                return (int64_t)s;
+            }
+            if (old == key) return (int64_t)s;
+        }
+        s = (s + 1) & p.mask;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
+    const int64_t s = find_or_insert(p, key);
+    if (s >= 0) {
+        atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
+    } else {
+        // overflow: one entry per unit count (c == 1 on this path except for
+        // the 1-gram histogram flush, which repeats the entry c times)
+        for (unsigned long long r = 0; r < c; ++r) {
+            const unsigned int at = atomicAdd(p.ovf_n, 1u);
+            if (at < p.ovf_cap) {
+                p.ovf_keys[at] = key;
+                p.ovf_lang[at] = lang;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountParams p) {
+    __shared__ unsigned int hist[kCountWaves][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned int* h1 = hist[wave];
+    for (int i = lane; i < 256; i += 64) h1[i] = 0u;
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+    const int64_t stride = (int64_t)gridDim.x * kCountWaves;
+    for (int64_t doc = (int64_t)blockIdx.x * kCountWaves + wave; doc < p.n_docs; doc += stride) {
+        const int lang = p.doc_lang[doc];
+        if (lang < 0 || lang >= p.L) continue;
+        const int64_t b = p.offsets[doc];
+        const int64_t len = p.offsets[doc + 1] - b;
+        bool used_hist = false;
+        for (int gi = 0; gi < p.nG; ++gi) {
+            const int n = p.G[gi];
+            const int64_t nwin = n_windows(len, n);
+            const int klen = len < n ? (int)len : n;
+            const uint32_t lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
+            const uint32_t himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
+            const uint32_t hitag = (uint32_t)klen << 24;
+            for (int64_t p0 = 0; p0 < nwin; p0 += 64) {
+                const int64_t pos = p0 + lane;
+                if (pos >= nwin) continue;
+                const int64_t a = b + pos;
+                const int64_t i = a >> 2;
+                const uint32_t sh = (uint32_t)(a & 3);
+                const uint32_t w0 = ld_dw(W, i, p.last_dword);
+                const uint32_t w1 = ld_dw(W, i + 1, p.last_dword);
+                const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh) & lomask;
+                if (klen == 1) {
+                    atomicAdd(&h1[lo], 1u);
+                    used_hist = true;
+                    continue;
+                }
+                uint32_t hi = hitag;
+                if (klen > 4) {
+                    const uint32_t w2 = ld_dw(W, i + 2, p.last_dword);
+                    hi |= __builtin_amdgcn_alignbyte(w2, w1, sh) & himask;
+                }
+                add_count(p, ((uint64_t)hi << 32) | lo, lang, 1ull);
+            }
+        }
+        if (__ballot(used_hist)) {
+            __builtin_amdgcn_wave_barrier();
+            for (int i = lane; i < 256; i += 64) {
+                const unsigned int c = h1[i];
+                if (c) {
+                    h1[i] = 0u;
+                    add_count(p, ((uint64_t)1 << 56) | (uint64_t)i, lang, (unsigned long long)c);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+__global__ void counts_add_kernel(const CountParams p, const uint64_t* keys, const unsigned long long* rows,
+                                  const int32_t* lang_of, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t s = find_or_insert(p, keys[i]);
+    if (s < 0) {
+        atomicAdd(p.ovf_n, 1u);  // cannot happen after a grow; reported as table full
+        return;
+    }
+    if (lang_of) {
+        atomicAdd(&p.counts[(size_t)s * p.L + lang_of[i]], 1ull);
+    } else {
+        for (int l = 0; l < p.L; ++l) {
+            const unsigned long long c = rows[(size_t)i * p.L + l];
+            if (c) atomicAdd(&p.counts[(size_t)s * p.L + l], c);
+        }
+    }
+}
+
+__global__ void rehash_kernel(const CountParams from, const CountParams to, uint64_t from_cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= from_cap) return;
+    const uint64_t key = from.keys[i];
+    if (key == kEmpty) return;
+    uint64_t s = mix64(key) >> to.shift;
+    for (;;) {
+        const unsigned long long old =
+            atomicCAS(reinterpret_cast<unsigned long long*>(&to.keys[s]), 0ull, (unsigned long long)key);
+        if (old == 0ull) break;
+        s = (s + 1) & to.mask;
+    }
+    for (int l = 0; l < from.L; ++l) to.counts[(size_t)s * to.L + l] = from.counts[(size_t)i * from.L + l];
+}
+
+__global__ void compact_kernel(const CountParams p, uint64_t cap, uint64_t* out_keys,
+                               unsigned long long* out_counts, unsigned long long* out_n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool occ = i < cap && p.keys[i] != kEmpty;
+    const uint64_t m = __ballot(occ);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    const int leader = __builtin_ctzll(m);
+    if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (!occ) return;
+    const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const unsigned long long o = base + off;
+    out_keys[o] = p.keys[i];
+    for (int l = 0; l < p.L; ++l) out_counts[o * p.L + l] = p.counts[i * p.L + l];
+}
+
+}  // namespace
+
+hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(count_kernel, dim3(grid), dim3(kCountWaves * 64), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const unsigned long long* rows,
+                             const int32_t* lang_of, int64_t n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(counts_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, p, keys, rows,
+                       lang_of, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap, hipStream_t stream) {
+    hipLaunchKernelGGL(rehash_kernel, dim3((unsigned)((from_cap + 255) / 256)), dim3(256), 0, stream, from, to,
+                       from_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys, unsigned long long* out_counts,
+                          unsigned long long* out_n, hipStream_t stream) {
+    hipLaunchKernelGGL(compact_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out_keys,
+                       out_counts, out_n);
+    return hipGetLastError();
+}
+
+}  // namespace ldgpu

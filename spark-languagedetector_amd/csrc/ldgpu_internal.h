@@ -1,0 +1,78 @@
+// ldgpu_internal.h -- kernel parameter blocks and launchers shared between the
+// kernels (ldgpu_score.hip, ldgpu_fit.hip) and the host runtime (ldgpu_api.hip).
+#pragma once
+
+#include "ldgpu_common.h"
+
+namespace ldgpu {
+
+// ------------------------------------------------------------------ SCORE
+struct ScoreParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    int64_t last_dword;         // index of the last readable dword of bytes (-1: none)
+    const int64_t* offsets;     // [n_docs + 1]
+    int64_t n_docs;
+    int32_t* labels;            // [n_docs]
+    double* scores;             // nullable [n_docs][L]
+    const Slot* slots;          // open-addressed key -> row table
+    uint32_t slot_shift;        // slot = mix64(key) >> slot_shift
+    uint64_t slot_mask;
+    const uint32_t* filter;     // bit filter over filter_hash(key)
+    uint32_t filter_shift;      // bit index = hash >> filter_shift
+    uint32_t filter_words;
+    const uint64_t* masks;      // mask mode: [rows][S] language bitmasks
+    const double* vals;         // mask mode: [rows] the row's one nonzero value
+    const double* rows;         // dense mode: [rows][L]
+    int32_t* err;               // set to 1 when a window hits a wrong-length row
+    int32_t L;
+    int32_t nG;
+    int32_t G[kMaxGramLengths];
+};
+
+// Launch configuration of the score kernel.
+constexpr int kScoreWaves = 16;            // waves per workgroup (1024 threads)
+constexpr int kQueueCap = 128;             // candidate keys per wave in LDS
+constexpr int kMaxLdsFilterLog2 = 19;      // 64 KiB bit filter in LDS
+
+// slices = ceil(L / 64); dense = general fp64 rows; lds_filter = filter staged in LDS
+hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_filter, int grid,
+                        hipStream_t stream);
+hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes);
+
+// -------------------------------------------------------------------- FIT
+struct CountParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    int64_t last_dword;
+    const int64_t* offsets;
+    const int32_t* doc_lang;
+    int64_t n_docs;
+    uint64_t* keys;             // [cap] gram keys (0 = empty)
+    unsigned long long* counts; // [cap][L]
+    uint32_t shift;             // slot = mix64(key) >> shift
+    uint64_t mask;              // cap - 1
+    unsigned long long* size;   // distinct keys inserted
+    uint64_t* ovf_keys;         // overflow (probe limit reached): key, lang
+    int32_t* ovf_lang;
+    unsigned int* ovf_n;
+    uint32_t ovf_cap;
+    int32_t L;
+    int32_t nG;
+    int32_t G[kMaxGramLengths];
+};
+
+constexpr int kCountWaves = 16;
+constexpr int kMaxProbe = 128;
+
+hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream);
+// insert keys[i] with counts rows[i][L] (add) into the table; n entries
+hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const unsigned long long* rows,
+                             const int32_t* lang_of /*nullable: row is one count 1 at lang_of[i]*/,
+                             int64_t n, hipStream_t stream);
+// rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
+hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
+                         hipStream_t stream);
+// compact occupied slots: out_keys[i], out_counts[i][L]; *out_n = number written
+hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys,
+                          unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
+
+}  // namespace ldgpu

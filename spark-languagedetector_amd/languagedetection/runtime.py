@@ -1,0 +1,145 @@
+"""Thin owners of libldgpu.so handles: device gram tables (SCORE) and device
+count tables (FIT).  Everything here calls straight into the HIP library."""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .encoding import pack, pack_table
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _grams(gram_lengths: Sequence[int]) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(list(gram_lengths), dtype=np.int32))
+
+
+class DeviceModel:
+    """A gram -> probability-row table resident on one GPU
+    (LanguageDetectorModel's broadcast table, LanguageDetectorModel.scala:222)."""
+
+    def __init__(self, table: Dict, n_langs: int, gram_lengths: Sequence[int], device: Optional[int] = None):
+        self.lib = _lib.load()
+        self.ctx = _lib.context(device)
+        self.L = int(n_langs)
+        self.gram_lengths = list(gram_lengths)
+        kb, ko, rows, ok = pack_table(table, self.L)
+        g = _grams(gram_lengths)
+        out = ctypes.c_void_p()
+        _lib.check(self.lib.ldgpu_model_create(self.ctx, len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(rows), _ptr(ok),
+                                               self.L, _ptr(g), len(g), ctypes.byref(out)))
+        self.h = out.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ldgpu_model_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> Dict[str, int]:
+        mode = ctypes.c_int32()
+        vals = [ctypes.c_int64() for _ in range(4)]
+        _lib.check(self.lib.ldgpu_model_info(self.h, ctypes.byref(mode), *[ctypes.byref(v) for v in vals]))
+        return {"mode": mode.value, "n_keys": vals[0].value, "table_slots": vals[1].value,
+                "filter_bits": vals[2].value, "device_bytes": vals[3].value}
+
+    def score(self, data: np.ndarray, offsets: np.ndarray, want_scores: bool = False
+              ) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """Host buffers -> (labels int32[n], scores fp64[n, L] or None)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(offsets) - 1
+        labels = np.zeros(max(n, 0), dtype=np.int32)
+        scores = np.zeros((max(n, 0), self.L), dtype=np.float64) if want_scores else None
+        _lib.check(self.lib.ldgpu_score(self.h, _ptr(data), _ptr(offsets), n, _ptr(labels), _ptr(scores)))
+        return labels, scores
+
+    def score_device(self, d_bytes: int, n_bytes: int, d_offsets: int, n_docs: int, d_labels: int,
+                     d_scores: int = 0, stream: int = 0) -> None:
+        """Device pointers (e.g. torch tensors' data_ptr()) -> labels in place, async on `stream`."""
+        _lib.check(self.lib.ldgpu_score_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
+                                               n_docs, ctypes.c_void_p(d_labels),
+                                               ctypes.c_void_p(d_scores) if d_scores else None,
+                                               ctypes.c_void_p(stream) if stream else None))
+
+
+class DeviceCounts:
+    """A (gram, language) -> count table on one GPU (computeGrams + reduceGrams)."""
+
+    def __init__(self, n_langs: int, gram_lengths: Sequence[int], capacity_hint: int = 0,
+                 device: Optional[int] = None):
+        self.lib = _lib.load()
+        self.ctx = _lib.context(device)
+        self.L = int(n_langs)
+        g = _grams(gram_lengths)
+        out = ctypes.c_void_p()
+        _lib.check(self.lib.ldgpu_counts_create(self.ctx, self.L, _ptr(g), len(g), int(capacity_hint),
+                                                ctypes.byref(out)))
+        self.h = out.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ldgpu_counts_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def count(self, data: np.ndarray, offsets: np.ndarray, doc_lang: np.ndarray) -> None:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        doc_lang = np.ascontiguousarray(doc_lang, dtype=np.int32)
+        _lib.check(self.lib.ldgpu_count(self.h, _ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1))
+
+    def count_device(self, d_bytes: int, n_bytes: int, d_offsets: int, d_doc_lang: int, n_docs: int,
+                     stream: int = 0) -> None:
+        _lib.check(self.lib.ldgpu_count_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
+                                               ctypes.c_void_p(d_doc_lang), n_docs,
+                                               ctypes.c_void_p(stream) if stream else None))
+
+    def size(self) -> int:
+        n = ctypes.c_int64()
+        _lib.check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), None))
+        return n.value
+
+    def export(self) -> Tuple[List[bytes], np.ndarray]:
+        """Distinct grams sorted by (length, bytes) and int64 counts [n, L]."""
+        n = ctypes.c_int64()
+        nb = ctypes.c_int64()
+        _lib.check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), ctypes.byref(nb)))
+        kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        ko = np.zeros(n.value + 1, dtype=np.int64)
+        cnt = np.zeros((n.value, self.L), dtype=np.int64)
+        _lib.check(self.lib.ldgpu_counts_export(self.h, _ptr(kb), _ptr(ko), _ptr(cnt)))
+        b = kb.tobytes()
+        return [b[ko[i]:ko[i + 1]] for i in range(n.value)], cnt
+
+    def add(self, keys: Sequence[bytes], counts: np.ndarray) -> None:
+        counts = np.ascontiguousarray(counts, dtype=np.int64).reshape(len(keys), self.L)
+        kb, ko = pack(list(keys))
+        _lib.check(self.lib.ldgpu_counts_add(self.h, len(keys), _ptr(kb), _ptr(ko), _ptr(counts)))
+
+    def fit_table(self, profile_size: int) -> Dict[bytes, List[float]]:
+        """computeProbabilities + filterTopGrams -> {gram: row}."""
+        n = ctypes.c_int64()
+        nb = ctypes.c_int64()
+        _lib.check(self.lib.ldgpu_fit_table_size(self.h, int(profile_size), ctypes.byref(n), ctypes.byref(nb)))
+        kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        ko = np.zeros(n.value + 1, dtype=np.int64)
+        rows = np.zeros((n.value, self.L), dtype=np.float64)
+        _lib.check(self.lib.ldgpu_fit_table_export(self.h, _ptr(kb), _ptr(ko), _ptr(rows)))
+        b = kb.tobytes()
+        return {b[ko[i]:ko[i + 1]]: rows[i].tolist() for i in range(n.value)}

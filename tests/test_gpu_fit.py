@@ -1,0 +1,138 @@
+"""GPU parity of FIT (LanguageDetector.scala:25-132): counts bit-exact, the
+probability rows and the deterministic top-K table equal to the oracle's."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import ldoracle as O
+import ldoracle_c as OC
+from conftest import GOLDEN
+from languagedetection import LanguageDetector, LanguageDetectorModel, encoding, synth
+from languagedetection.runtime import DeviceCounts
+
+pytestmark = pytest.mark.gpu
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def dec_table(enc):
+    return {bytes.fromhex(k): [float.fromhex(v) for v in row] for k, row in enc}
+
+
+@pytest.mark.parametrize("case", load("fit_cases.json"), ids=lambda c: c["name"])
+def test_golden_fit_cases(case):
+    rows = [tuple(r) for r in case["rows"]]
+    langs = case["languages"]
+    counts = LanguageDetector.count_grams(rows, case["gram_lengths"], langs)
+    keys, cnt = counts.export()
+    got = {}
+    for i, k in enumerate(keys):
+        for l, lang in enumerate(langs):
+            if cnt[i, l]:
+                got.setdefault(k.hex(), {})[lang] = int(O.int32_wrap(int(cnt[i, l])))
+    assert got == case["counts"]
+    table = counts.fit_table(case["profile_size"])
+    assert table == dec_table(case["table"])
+
+
+def test_reference_fit_kat():
+    """LanguageDetectorSpecs.scala:15-40 through the Estimator API."""
+    import pandas as pd
+    k = load("reference_kats.json")["fit_kat"]
+    df = pd.DataFrame(k["rows"], columns=["lang", "fulltext"])
+    det = LanguageDetector(supportedLanguages=k["languages"], gramLengths=k["gram_lengths"],
+                           languageProfileSize=k["profile_size"])
+    model = det.fit(df)
+    assert len(model.gramProbabilities) == k["expect_table_size"]
+    assert all(len(r) == k["expect_row_length"] for r in model.gramProbabilities.values())
+    probs = O.fit_probabilities([tuple(r) for r in k["rows"]], k["languages"], k["gram_lengths"])
+    assert O.topk_contract_violations(model.gramProbabilities, probs, k["languages"], k["profile_size"]) == []
+
+
+def test_validation_order_kat():
+    import pandas as pd
+    k = load("reference_kats.json")["validation_kat"]
+    det = LanguageDetector(k["languages"], k["gram_lengths"], k["profile_size"])
+    with pytest.raises(Exception) as e:
+        det.fit(pd.DataFrame(k["rows"], columns=["lang", "fulltext"]))
+    assert str(e.value) == k["code_order_raises"]
+
+
+@pytest.mark.parametrize("L,grams,n_docs", [(3, [1, 2, 3], 300), (20, [1, 2, 3, 4, 5], 2000),
+                                            (70, [7, 1, 4, 4], 1500), (200, [1, 2, 3], 1200)])
+def test_counts_match_c_oracle(L, grams, n_docs):
+    ls = synth.make_languages(L, seed=L)
+    data, off, lang = synth.generate(ls, n_docs, 0, 700, seed=L + 1)
+    counts = DeviceCounts(L, grams)
+    counts.count(data, off, lang)
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(data, off, lang, L, grams)
+    assert keys == okeys
+    assert np.array_equal(cnt, ocnt)
+
+
+def test_counts_growth_and_overflow_path():
+    """A tiny capacity hint forces overflow entries and device re-hashing."""
+    rng = np.random.default_rng(4)
+    docs = [bytes(rng.integers(0, 256, size=int(n), dtype=np.uint8)) for n in rng.integers(0, 2000, size=400)]
+    data, off = encoding.pack(docs)
+    lang = rng.integers(0, 4, size=len(docs)).astype(np.int32)
+    lang[::37] = -1   # unsupported labels are skipped (reduceGrams filter)
+    counts = DeviceCounts(4, [3, 5, 2], capacity_hint=16)
+    counts.count(data, off, lang)
+    counts.count(data, off, lang)  # second batch accumulates
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(data, off, lang, 4, [3, 5, 2])
+    assert keys == okeys
+    assert np.array_equal(cnt, 2 * ocnt)
+
+
+def test_counts_add_merges_blocks():
+    ls = synth.make_languages(5, seed=3)
+    data, off, lang = synth.generate(ls, 400, 10, 300, seed=4)
+    a = DeviceCounts(5, [1, 2, 3])
+    a.count(data, off, lang)
+    keys, cnt = a.export()
+    b = DeviceCounts(5, [1, 2, 3])
+    b.add(keys[::2], cnt[::2])
+    b.add(keys, cnt)
+    k2, c2 = b.export()
+    assert k2 == keys
+    extra = np.zeros_like(cnt)
+    extra[::2] = cnt[::2]
+    assert np.array_equal(c2, cnt + extra)
+
+
+@pytest.mark.parametrize("L,grams,K", [(3, [1, 2, 3], 50), (20, [1, 2, 3, 4, 5], 500), (8, [2, 3], 100000),
+                                       (5, [3], 0)])
+def test_fit_table_matches_oracle(L, grams, K):
+    ls = synth.make_languages(L, seed=100 + L)
+    data, off, lang = synth.generate(ls, 60 * L, 20, 200, seed=L)
+    rows = list(zip([ls.names[i] for i in lang], synth.texts(data, off)))
+    table = LanguageDetector.computeGramProbabilities(rows, grams, K, ls.names)
+    probs = O.fit_probabilities(rows, ls.names, grams)
+    expect = O.filter_top_grams(probs, ls.names, K)
+    assert table.keys() == expect.keys()
+    for g in expect:
+        assert table[g] == expect[g]  # log(1+1/k) computed by the same libm formula
+    assert O.topk_contract_violations(table, probs, ls.names, K) == []
+
+
+def test_fit_then_transform_end_to_end():
+    import pandas as pd
+    ls = synth.make_languages(6, seed=9)
+    tdata, toff, tlang = synth.generate(ls, 600, 100, 400, seed=10)
+    df = pd.DataFrame({"lang": [ls.names[i] for i in tlang], "fulltext": synth.texts(tdata, toff)})
+    model = LanguageDetector(ls.names, [1, 2, 3], 200).fit(df)
+    data, off, lang = synth.generate(ls, 500, 50, 300, seed=11)
+    texts = synth.texts(data, off)
+    out = model.transform(pd.DataFrame({"fulltext": texts}))
+    expect = O.transform(texts, model.gramProbabilities, ls.names, [1, 2, 3])
+    assert list(out["lang"]) == expect
+    acc = np.mean([ls.names[l] == p for l, p in zip(lang, out["lang"])])
+    assert acc > 0.9

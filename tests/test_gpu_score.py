@@ -1,0 +1,207 @@
+"""GPU parity of SCORE (LanguageDetectorModel.detect, LanguageDetectorModel.scala:131-156)
+through the C ABI: labels AND fp64 scores bit-identical to the oracle."""
+import ctypes
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import ldoracle as O
+import ldoracle_c as OC
+from conftest import GOLDEN
+from languagedetection import LanguageDetectorModel, _lib, encoding, synth
+from languagedetection.runtime import DeviceModel
+
+pytestmark = pytest.mark.gpu
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def dec_table(enc):
+    return {bytes.fromhex(k): [float.fromhex(v) for v in row] for k, row in enc}
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def oracle_c(table, L, grams, data, off, scores=True):
+    t = OC.Table(table, L)
+    return t.score(grams, data, off, want_scores=scores, nthreads=8)
+
+
+def check_parity(table, L, grams, data, off):
+    m = DeviceModel(table, L, grams)
+    labels, scores = m.score(data, off, want_scores=True)
+    ol, os_ = oracle_c(table, L, grams, data, off)
+    assert np.array_equal(labels, ol), np.nonzero(labels != ol)[0][:10]
+    assert np.array_equal(bits(scores), bits(os_))
+    return m
+
+
+def test_reference_score_kat_transform():
+    """LanguageDetectorModelSpecs.scala:15-44 through the Model API."""
+    import pandas as pd
+    k = load("reference_kats.json")["score_kat"]
+    model = LanguageDetectorModel(gramProbabilities=k["table"], gramLengths=k["gram_lengths"],
+                                  languages=k["languages"])
+    out = model.transform(pd.DataFrame({"fulltext": k["docs"]}))
+    labels = list(out["lang"])
+    assert len(out) == k["expect_rows"]
+    for lang, n in k["expect_count"].items():
+        assert labels.count(lang) == n
+    assert labels == ["de", "de", "en", "en"]
+    assert list(out.columns) == ["fulltext", "lang"]
+
+
+@pytest.mark.parametrize("case", load("score_cases.json"), ids=lambda c: c["name"])
+def test_golden_score_cases(case):
+    table = dec_table(case["table"])
+    docs = [bytes.fromhex(h) for h in case["docs_hex"]]
+    data, off = encoding.pack(docs)
+    m = DeviceModel(table, len(case["languages"]), case["gram_lengths"])
+    labels, scores = m.score(data, off, want_scores=True)
+    assert labels.tolist() == case["labels"]
+    assert [[v.hex() for v in row] for row in scores.tolist()] == case["scores"]
+
+
+def test_detect_static_string_and_bytes():
+    table = {"Die": [1.0, 0.0], "Thi": [0.0, 1.0]}
+    assert LanguageDetectorModel.detect("Dies ist", table, ["de", "en"], [3]) == "de"
+    assert LanguageDetectorModel.detect(b"This", table, ["de", "en"], [3]) == "en"
+    assert LanguageDetectorModel.detect("", table, ["de", "en"], [3]) == "de"  # no hit -> index 0
+
+
+def _random_table(rng, L, n_keys, grams, alphabet, mask_form):
+    table = {}
+    for _ in range(n_keys):
+        n = int(rng.choice(grams))
+        k = bytes(rng.choice(alphabet, size=n))
+        if mask_form:
+            m = rng.random(L) < rng.uniform(0.02, 0.6)
+            if not m.any():
+                m[int(rng.integers(0, L))] = True
+            v = math.log(1.0 + 1.0 / int(m.sum()))
+            table[k] = [v if b else 0.0 for b in m]
+        else:
+            table[k] = rng.normal(size=L).tolist()
+    return table
+
+
+@pytest.mark.parametrize("L,grams,mask_form", [
+    (3, [1, 2, 3], True), (20, [1, 2, 3, 4, 5], True), (64, [2, 3], True), (65, [3, 1], True),
+    (130, [1, 2, 3, 4, 5, 6, 7], True), (200, [5, 5, 2], True), (256, [4], True),
+    (3, [3], False), (20, [1, 2, 3, 4, 5], False), (100, [2, 7], False), (256, [1, 3], False),
+])
+def test_random_parity(L, grams, mask_form):
+    rng = np.random.default_rng(L * 7 + len(grams) + int(mask_form))
+    alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+    table = _random_table(rng, L, 400, grams, alphabet, mask_form)
+    lens = rng.integers(0, 300, size=600)
+    lens[:8] = [0, 1, 2, 3, 6, 7, 64, 65]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, grams, data, off)
+    assert m.info()["mode"] == (0 if mask_form else 1)
+
+
+def test_long_documents_and_hot_keys():
+    """Every 1-gram in the table: every window hits, so the per-wave candidate
+    queue flushes many times per document (order must survive the flushes)."""
+    rng = np.random.default_rng(5)
+    L = 9
+    table = {bytes([c]): rng.normal(size=L).tolist() for c in range(256)}
+    table.update({bytes(rng.integers(0, 256, size=3)): rng.normal(size=L).tolist() for _ in range(500)})
+    lens = [0, 1, 5000, 12345, 70000, 3]
+    docs = [bytes(rng.integers(0, 256, size=n, dtype=np.uint8)) for n in lens]
+    data, off = encoding.pack(docs)
+    check_parity(table, L, [1, 3, 2, 1], data, off)
+
+
+def test_unaligned_offsets_and_nonzero_start():
+    rng = np.random.default_rng(9)
+    alphabet = np.frombuffer(b"xyz", dtype=np.uint8)
+    table = _random_table(rng, 5, 50, [1, 2, 3], alphabet, True)
+    raw = bytes(rng.choice(alphabet, size=1001))
+    # offsets start at 3 and use odd boundaries
+    off = np.array([3, 4, 9, 9, 10, 500, 777, 1001], dtype=np.int64)
+    data = np.frombuffer(raw + b"\0" * 7, dtype=np.uint8)
+    m = DeviceModel(table, 5, [1, 2, 3])
+    labels, scores = m.score(data, off, want_scores=True)
+    docs = [raw[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+    for i, d in enumerate(docs):
+        s = O.detect_scores(d, table, 5, [1, 2, 3])
+        assert scores[i].tolist() == s
+        assert labels[i] == O.argmax_first(s)
+
+
+def test_wrong_length_row_raises_only_when_hit():
+    m = LanguageDetectorModel({"ab": [1.0, 0.0], "zz": [1.0]}, [2], ["a", "b"])
+    assert m.predict_indices(["abab"])[0].tolist() == [0]
+    with pytest.raises(ValueError, match="requirement failed"):
+        m.predict_indices(["xzz"])
+
+
+def test_duplicate_keys_last_wins():
+    lib = _lib.load()
+    ctx = _lib.context()
+    kb, ko = encoding.pack([b"ab", b"ab"])
+    rows = np.array([[1.0, 0.0], [0.0, 1.0]])
+    g = np.array([2], dtype=np.int32)
+    h = ctypes.c_void_p()
+    _lib.check(lib.ldgpu_model_create(ctx, 2, kb.ctypes.data, ko.ctypes.data, rows.ctypes.data, None, 2,
+                                      g.ctypes.data, 1, ctypes.byref(h)))
+    data, off = encoding.pack([b"xab"])
+    labels = np.zeros(1, dtype=np.int32)
+    _lib.check(lib.ldgpu_score(h.value, data.ctypes.data, off.ctypes.data, 1, labels.ctypes.data, None))
+    lib.ldgpu_model_destroy(h.value)
+    assert labels.tolist() == [1]
+
+
+def test_invalid_arguments():
+    with pytest.raises(ValueError, match="both must be positive"):
+        DeviceModel({b"a": [1.0]}, 1, [0])
+    with pytest.raises(NotImplementedError):
+        DeviceModel({b"a": [1.0]}, 1, [8])
+    m = DeviceModel({b"a": [1.0]}, 1, [1])
+    with pytest.raises(ValueError, match="offsets decrease"):
+        m.score(np.zeros(8, dtype=np.uint8), np.array([0, 4, 2], dtype=np.int64))
+
+
+def test_device_pointer_api_with_torch():
+    import torch
+    ls = synth.make_languages(20, seed=1)
+    data, off, _ = synth.generate(ls, 3000, 256, 256, seed=2)
+    rng = np.random.default_rng(3)
+    table = _random_table(rng, 20, 2000, [1, 2, 3, 4, 5], np.frombuffer(b"abcdefghijklmnopqrstuvwxyz '", np.uint8),
+                          True)
+    m = DeviceModel(table, 20, [1, 2, 3, 4, 5])
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(np.concatenate([data, np.zeros(8, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_lab = torch.empty(len(off) - 1, dtype=torch.int32, device=dev)
+    d_sc = torch.empty((len(off) - 1, 20), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    m.score_device(d_bytes.data_ptr(), int(len(data)), d_off.data_ptr(), len(off) - 1, d_lab.data_ptr(),
+                   d_sc.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ol, os_ = oracle_c(table, 20, [1, 2, 3, 4, 5], data, off)
+    assert np.array_equal(d_lab.cpu().numpy(), ol)
+    assert np.array_equal(bits(d_sc.cpu().numpy()), bits(os_))
+
+
+def test_bench_shape_parity_sample():
+    """The headline configuration's shape (L=20, grams 1-5, 256-byte docs) on a
+    fit-produced table, 20k documents, against the C restatement."""
+    from languagedetection.api import LanguageDetector
+    ls = synth.make_languages(20)
+    tdata, toff, tlang = synth.generate(ls, 2000, 200, 600, seed=synth.SEED_BASE + 100)
+    rows = list(zip([ls.names[i] for i in tlang], synth.texts(tdata, toff)))
+    table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3, 4, 5], 500, ls.names)
+    data, off, _ = synth.generate(ls, 20000, 256, 256, seed=synth.SEED_BASE + 2)
+    check_parity(table, 20, [1, 2, 3, 4, 5], data, off)

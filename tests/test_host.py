@@ -1,0 +1,114 @@
+"""CPU: host logic of the drop-in (encodings, packing, validation, params) and
+the C-ABI library: it loads and exports every symbol include/ldgpu.h declares.
+No compute call is made here (no GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import ldoracle as O
+from conftest import ROOT
+from languagedetection import _lib, encoding, synth
+from languagedetection.api import FitValidationError, LanguageDetector, LanguageDetectorModel
+
+HEADER = os.path.join(ROOT, "include", "ldgpu.h")
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(ldgpu_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(_lib.exported_symbols()) == syms
+    assert lib.ldgpu_version().decode().startswith("ldgpu")
+
+
+def test_library_is_gfx950_code_object():
+    so = _lib.LIB_PATH
+    blob = open(so, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_encodings_match_oracle():
+    texts = ["plain ascii", "schön", "日本語", "😀 x", "\ud800 lone", "\udfff", "", "Ärger über Öl"]
+    for t in texts:
+        assert encoding.fit_bytes(t) == O.fit_encode(t), t
+        assert encoding.score_bytes(t) == O.score_encode(t), t
+
+
+def test_pack_padding_and_offsets():
+    data, off = encoding.pack([b"ab", b"", b"cde"])
+    assert off.tolist() == [0, 2, 2, 5]
+    assert len(data) % 4 == 0 and len(data) >= 5 + 4
+    assert data[:5].tobytes() == b"abcde"
+
+
+def test_gram_key_forms():
+    assert encoding.gram_key("Die") == b"Die"
+    assert encoding.gram_key([-61, -74]) == b"\xc3\xb6"   # Scala signed bytes
+    assert encoding.gram_key(b"x") == b"x"
+
+
+def test_pack_table_marks_wrong_length_rows():
+    kb, ko, rows, ok = encoding.pack_table({b"a": [1.0, 2.0], b"b": [1.0]}, 2)
+    assert ok.tolist() == [1, 0]
+    assert rows[0].tolist() == [1.0, 2.0]
+
+
+def test_fit_validation_messages_follow_code_order():
+    with pytest.raises(FitValidationError) as e:
+        LanguageDetector.validate(["de", "de", "es"], ["de", "en"])
+    assert str(e.value) == "Input data contians es, but it is not in the list of supported languages"
+    with pytest.raises(FitValidationError) as e:
+        LanguageDetector.validate(["de"], ["de", "en"])
+    assert str(e.value) == "No training examples found for language en. Provide examples for each language"
+    LanguageDetector.validate(["en", "de"], ["de", "en"])
+
+
+def test_params_defaults_and_setters():
+    d = LanguageDetector(["de", "en"], [3], 5)
+    assert d.getInputCol() == "fulltext" and d.getLabelCol() == "lang"
+    assert d.uid.startswith("LanguageDetector_")
+    d.setInputCol("text").setLabelCol("label")
+    assert d.getInputCol() == "text" and d.getLabelCol() == "label"
+    m = LanguageDetectorModel({"Die": [1.0, 0.0]}, [3], ["de", "en"])
+    assert m.getInputCol() == "fulltext" and m.getOutputCol() == "lang"
+    assert m.gramLenghts == [3] and m.supportedLanguages == ["de", "en"]
+    assert m.gramProbabilities == {b"Die": [1.0, 0.0]}
+
+
+def test_transform_schema_rules():
+    m = LanguageDetectorModel({}, [3], ["de"])
+    assert m.transformSchema({"fulltext": "string"}) == {"fulltext": "string", "lang": "string"}
+    with pytest.raises(ValueError, match="Input type must be StringType"):
+        m.transformSchema({"fulltext": "int64"})
+    with pytest.raises(ValueError, match="Column lang already exists"):
+        m.transformSchema({"fulltext": "string", "lang": "string"})
+
+
+def test_synth_is_deterministic_ascii():
+    ls = synth.make_languages(5, seed=11)
+    a = synth.generate(ls, 50, 10, 40, seed=3)
+    b = synth.generate(synth.make_languages(5, seed=11), 50, 10, 40, seed=3)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    data, off, lang = a
+    assert data.max() < 128 and len(off) == 51 and off[-1] == len(data)
+    assert synth.language_names(3) == ["en", "de", "fr"]
+    assert len(set(synth.language_names(200))) == 200
+
+
+def test_no_gpu_fails_loudly():
+    """Without a visible GPU the product path raises; there is no fallback."""
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(Exception):
+        _lib.context(0)
