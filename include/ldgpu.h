@@ -93,8 +93,9 @@ int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
 int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets,
                 int64_t n_docs, int32_t* out_labels, double* out_scores);
 
-/* Device-resident variant, asynchronous on `stream` (NULL = the context's
- * stream).  d_bytes must be 4-byte aligned and n_bytes >= d_offsets[n_docs].
+/* Device-resident variant, asynchronous on `stream` (a hipStream_t used as
+ * given: NULL is HIP's null stream; ldgpu_ctx_stream() gives the context's).
+ * d_bytes must be 4-byte aligned and n_bytes >= d_offsets[n_docs].
  * d_scores is nullable.  Offsets are trusted (validate with the host API). */
 int ldgpu_score_device(ldgpu_model* model, const uint8_t* d_bytes, int64_t n_bytes,
                        const int64_t* d_offsets, int64_t n_docs, int32_t* d_labels,

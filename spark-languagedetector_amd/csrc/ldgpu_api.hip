@@ -387,7 +387,11 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.err = m->d_err;
     p.L = m->L;
     p.nG = m->nG;
-    for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
+    p.max_gram = 0;
+    for (int i = 0; i < m->nG; ++i) {
+        p.G[i] = m->G[i];
+        p.max_gram = std::max(p.max_gram, m->G[i]);
+    }
     const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
     HIP_TRY(launch_score(p, m->slices, m->dense, m->lds_filter, grid, st));
@@ -415,7 +419,7 @@ extern "C" int ldgpu_score_device(ldgpu_model* m, const uint8_t* d_bytes, int64_
     if (n_docs > 0 && (!d_offsets || !d_labels || (n_bytes > 0 && !d_bytes)))
         return fail(LDGPU_EINVAL, "device pointer is NULL");
     if (((uintptr_t)d_bytes & 3) != 0) return fail(LDGPU_EINVAL, "d_bytes must be 4-byte aligned");
-    hipStream_t st = stream ? (hipStream_t)stream : m->ctx->stream;
+    hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(m->ctx->device));
     if (int rc = score_launch(m, d_bytes, n_bytes, d_offsets, n_docs, d_labels, d_scores, st)) return rc;
     if (m->has_bad) {
@@ -479,7 +483,7 @@ struct ldgpu_counts {
     uint64_t* d_ovf_keys = nullptr;
     int32_t* d_ovf_lang = nullptr;
     unsigned int* d_ovf_n = nullptr;
-    uint32_t ovf_cap = 1u << 22;
+    uint32_t ovf_cap = 1u << 24;  // windows per sub-launch
     uint64_t size = 0;
     // cached fit table (ldgpu_fit_table_size -> _export)
     bool tbl_valid = false;
@@ -558,8 +562,8 @@ int after_batch(ldgpu_counts* c) {
     HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
     HIP_TRY(hipMemcpyAsync(&novf, c->d_ovf_n, sizeof novf, hipMemcpyDeviceToHost, c->ctx->stream));
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
-    if (novf > c->ovf_cap)
-        return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost): pass a larger capacity_hint", novf);
+    if (novf > c->ovf_cap)  // cannot happen: sub-launches hold <= ovf_cap windows
+        return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost)", novf);
     c->size = size;
     if (2 * (size + novf) > c->cap || novf > 0) {
         if (int rc = grow(c, next_pow2(4 * (size + novf) + 16))) return rc;
@@ -579,21 +583,46 @@ int after_batch(ldgpu_counts* c) {
     return LDGPU_OK;
 }
 
+// windows the count kernel visits for a document of len bytes
+int64_t doc_windows(const ldgpu_counts* c, int64_t len) {
+    int64_t w = 0;
+    for (int i = 0; i < c->nG; ++i) w += n_windows(len, c->G[i]);
+    return w;
+}
+
+// Count documents [0, n_docs) of d_offsets / d_lang (h_off: the same offsets on
+// the host, used to plan sub-launches of at most ovf_cap windows each, so the
+// overflow list can never lose an entry).
 int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
-                 const int32_t* d_lang, int64_t n_docs, hipStream_t st) {
-    if (n_docs == 0) return LDGPU_OK;
-    CountParams p = count_params(c);
-    p.bytes = d_bytes;
-    p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
-    p.offsets = d_offsets;
-    p.doc_lang = d_lang;
-    p.n_docs = n_docs;
-    const int64_t want = (n_docs + kCountWaves - 1) / kCountWaves;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->ctx->cus * 2));
-    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-    HIP_TRY(launch_count(p, grid, st));
-    if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));
-    return after_batch(c);
+                 const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0, win = 0;
+        while (d1 < n_docs) {
+            const int64_t w = doc_windows(c, h_off[d1 + 1] - h_off[d1]);
+            if (d1 > d0 && win + w > (int64_t)c->ovf_cap) break;
+            win += w;
+            ++d1;
+        }
+        // a single document larger than the overflow list: make room up front
+        if (win > (int64_t)c->ovf_cap) {
+            if (int rc = grow(c, next_pow2(4 * (c->size + (uint64_t)win) + 16))) return rc;
+        }
+        CountParams p = count_params(c);
+        p.bytes = d_bytes;
+        p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+        p.offsets = d_offsets + d0;
+        p.doc_lang = d_lang + d0;
+        p.n_docs = d1 - d0;
+        const int64_t want = (p.n_docs + kCountWaves - 1) / kCountWaves;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->ctx->cus * 2));
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+        HIP_TRY(launch_count(p, grid, st));
+        if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = after_batch(c)) return rc;
+        d0 = d1;
+    }
+    return LDGPU_OK;
 }
 }  // namespace
 
@@ -642,8 +671,12 @@ extern "C" int ldgpu_count_device(ldgpu_counts* c, const uint8_t* d_bytes, int64
     if (((uintptr_t)d_bytes & 3) != 0) return fail(LDGPU_EINVAL, "d_bytes must be 4-byte aligned");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->ctx->stream;
-    if (int rc = count_launch(c, d_bytes, n_bytes, d_offsets, d_doc_lang, n_docs, st)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    if (n_docs == 0) return ok();
+    std::vector<int64_t> h_off(n_docs + 1);
+    HIP_TRY(hipMemcpyAsync(h_off.data(), d_offsets, sizeof(int64_t) * (n_docs + 1), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = count_launch(c, d_bytes, n_bytes, d_offsets, d_doc_lang, n_docs, h_off.data(), st)) return rc;
     return ok();
 }
 
@@ -674,7 +707,7 @@ extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t*
                                x->stream));
         HIP_TRY(hipMemcpyAsync(x->langs.p, doc_lang + d0, sizeof(int32_t) * nd, hipMemcpyHostToDevice, x->stream));
         if (int rc = count_launch(c, (const uint8_t*)x->bytes.p, nb, (const int64_t*)x->offsets.p,
-                                  (const int32_t*)x->langs.p, nd, x->stream))
+                                  (const int32_t*)x->langs.p, nd, off.data(), x->stream))
             return rc;
         d0 = d1;
     }

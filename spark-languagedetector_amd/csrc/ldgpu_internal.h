@@ -25,6 +25,7 @@ struct ScoreParams {
     const double* rows;         // dense mode: [rows][L]
     int32_t* err;               // set to 1 when a window hits a wrong-length row
     int32_t L;
+    int32_t max_gram;           // max of G (windows need a high key word when > 4)
     int32_t nG;
     int32_t G[kMaxGramLengths];
 };

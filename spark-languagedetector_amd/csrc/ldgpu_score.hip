@@ -108,6 +108,66 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queu
     }
 }
 
+constexpr int kSub = 4;  // 64-position sub-blocks per superblock (loads issued together)
+
+// Window bytes of one position: lo = bytes[a..a+4), hi = bytes[a+4..a+8)
+// (dword loads + v_alignbyte; clamped at the last readable dword).
+__device__ __forceinline__ void load_window(const uint32_t* W, int64_t a, int64_t last, bool need_hi, uint32_t& lo,
+                                            uint32_t& hi) {
+    const int64_t i = a >> 2;
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t w0 = ld_dw(W, i, last);
+    const uint32_t w1 = ld_dw(W, i + 1, last);
+    lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    hi = 0;
+    if (need_hi) hi = __builtin_amdgcn_alignbyte(ld_dw(W, i + 2, last), w1, sh);
+}
+
+struct GramCtx {
+    int64_t nwin;
+    uint32_t lomask, himask, hitag, himix_c;
+    bool big;  // klen > 4
+};
+
+__device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
+    GramCtx g;
+    g.nwin = n_windows(len, n);
+    const int klen = len < n ? (int)len : n;
+    g.lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
+    g.himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
+    g.hitag = (uint32_t)klen << 24;
+    g.himix_c = hi_mix(g.hitag);
+    g.big = klen > 4;
+    return g;
+}
+
+// Filter-test 64 windows (one per lane) and append the candidates to the
+// wave's queue in lane (= position) order; flush when the queue is nearly full.
+template <int S, bool DENSE>
+__device__ __forceinline__ void probe_block(const ScoreParams& p, const uint32_t* filt, uint64_t* queue, int& qn,
+                                            double (&acc)[S], int lane, const GramCtx& g, uint32_t xlo, uint32_t xhi,
+                                            bool valid) {
+    const uint32_t lo = xlo & g.lomask;
+    uint32_t hi = g.hitag;
+    uint32_t himix = g.himix_c;
+    if (g.big) {
+        hi |= xhi & g.himask;
+        himix = hi_mix(hi);
+    }
+    const uint32_t bit = filter_hash(lo, himix) >> p.filter_shift;
+    const bool cand = valid && ((filt[bit >> 5] >> (bit & 31)) & 1u);
+    const uint64_t m = __ballot(cand);
+    if (m) {
+        const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (cand) queue[qn + off] = ((uint64_t)hi << 32) | lo;
+        qn += __popcll(m);
+        if (qn > kQueueCap - 64) {
+            flush<S, DENSE>(p, queue, qn, acc, lane);
+            qn = 0;
+        }
+    }
+}
+
 template <int S, bool DENSE, bool FLDS>
 __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -125,6 +185,7 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
         filt = lds;
     }
     const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+    const bool need_hi = p.max_gram > 4;
     const int64_t stride = (int64_t)gridDim.x * kScoreWaves;
     for (int64_t doc = (int64_t)blockIdx.x * kScoreWaves + wave; doc < p.n_docs; doc += stride) {
         const int64_t b = p.offsets[doc];
@@ -133,41 +194,34 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
 #pragma unroll
         for (int s = 0; s < S; ++s) acc[s] = 0.0;
         int qn = 0;
-        for (int gi = 0; gi < p.nG; ++gi) {
-            const int n = p.G[gi];
-            const int64_t nwin = n_windows(len, n);
-            const int klen = len < n ? (int)len : n;
-            const uint32_t lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
-            const uint32_t himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
-            const uint32_t hitag = (uint32_t)klen << 24;
-            const uint32_t himix_c = hi_mix(hitag);
-            for (int64_t p0 = 0; p0 < nwin; p0 += 64) {
-                const int64_t pos = p0 + lane;
-                const bool valid = pos < nwin;
-                const int64_t a = b + pos;
-                const int64_t i = a >> 2;
-                const uint32_t sh = (uint32_t)(a & 3);
-                const uint32_t w0 = ld_dw(W, i, p.last_dword);
-                const uint32_t w1 = ld_dw(W, i + 1, p.last_dword);
-                uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh) & lomask;
-                uint32_t hi = hitag;
-                uint32_t himix = himix_c;
-                if (klen > 4) {
-                    const uint32_t w2 = ld_dw(W, i + 2, p.last_dword);
-                    hi |= __builtin_amdgcn_alignbyte(w2, w1, sh) & himask;
-                    himix = hi_mix(hi);
+        if (len <= 64 * kSub) {
+            // one superblock: every gram length reuses the same window bytes
+            uint32_t xlo[kSub], xhi[kSub];
+#pragma unroll
+            for (int k = 0; k < kSub; ++k) load_window(W, b + 64 * k + lane, p.last_dword, need_hi, xlo[k], xhi[k]);
+            for (int gi = 0; gi < p.nG; ++gi) {
+                const GramCtx g = gram_ctx(len, p.G[gi]);
+#pragma unroll
+                for (int k = 0; k < kSub; ++k) {
+                    if (64 * k < g.nwin)
+                        probe_block<S, DENSE>(p, filt, queue, qn, acc, lane, g, xlo[k], xhi[k],
+                                              64 * k + lane < g.nwin);
                 }
-                const uint32_t bit = filter_hash(lo, himix) >> p.filter_shift;
-                const bool cand = valid && ((filt[bit >> 5] >> (bit & 31)) & 1u);
-                const uint64_t m = __ballot(cand);
-                if (m) {
-                    const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (cand) queue[qn + off] = ((uint64_t)hi << 32) | lo;
-                    qn += __popcll(m);
-                    if (qn > kQueueCap - 64) {
-                        flush<S, DENSE>(p, queue, qn, acc, lane);
-                        qn = 0;
+            }
+        } else {
+            // long documents: n outer (reference order), superblocks inner
+            for (int gi = 0; gi < p.nG; ++gi) {
+                const GramCtx g = gram_ctx(len, p.G[gi]);
+                for (int64_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
+                    uint32_t xlo[kSub], xhi[kSub];
+#pragma unroll
+                    for (int k = 0; k < kSub; ++k)
+                        load_window(W, b + p0 + 64 * k + lane, p.last_dword, g.big, xlo[k], xhi[k]);
+#pragma unroll
+                    for (int k = 0; k < kSub; ++k) {
+                        if (p0 + 64 * k < g.nwin)
+                            probe_block<S, DENSE>(p, filt, queue, qn, acc, lane, g, xlo[k], xhi[k],
+                                                  p0 + 64 * k + lane < g.nwin);
                     }
                 }
             }

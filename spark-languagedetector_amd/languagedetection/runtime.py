@@ -64,13 +64,20 @@ class DeviceModel:
         _lib.check(self.lib.ldgpu_score(self.h, _ptr(data), _ptr(offsets), n, _ptr(labels), _ptr(scores)))
         return labels, scores
 
+    def stream(self) -> int:
+        """The context's hipStream_t."""
+        return self.lib.ldgpu_ctx_stream(self.ctx) or 0
+
     def score_device(self, d_bytes: int, n_bytes: int, d_offsets: int, n_docs: int, d_labels: int,
-                     d_scores: int = 0, stream: int = 0) -> None:
-        """Device pointers (e.g. torch tensors' data_ptr()) -> labels in place, async on `stream`."""
+                     d_scores: int = 0, stream: Optional[int] = None) -> None:
+        """Device pointers (e.g. torch tensors' data_ptr()) -> labels in place,
+        async on `stream` (a hipStream_t; 0 = the null stream, None = the
+        context's stream)."""
+        st = self.stream() if stream is None else stream
         _lib.check(self.lib.ldgpu_score_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
                                                n_docs, ctypes.c_void_p(d_labels),
                                                ctypes.c_void_p(d_scores) if d_scores else None,
-                                               ctypes.c_void_p(stream) if stream else None))
+                                               ctypes.c_void_p(st) if st else None))
 
 
 class DeviceCounts:
@@ -105,10 +112,11 @@ class DeviceCounts:
         _lib.check(self.lib.ldgpu_count(self.h, _ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1))
 
     def count_device(self, d_bytes: int, n_bytes: int, d_offsets: int, d_doc_lang: int, n_docs: int,
-                     stream: int = 0) -> None:
+                     stream: Optional[int] = None) -> None:
+        st = (self.lib.ldgpu_ctx_stream(self.ctx) or 0) if stream is None else stream
         _lib.check(self.lib.ldgpu_count_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
                                                ctypes.c_void_p(d_doc_lang), n_docs,
-                                               ctypes.c_void_p(stream) if stream else None))
+                                               ctypes.c_void_p(st) if st else None))
 
     def size(self) -> int:
         n = ctypes.c_int64()
