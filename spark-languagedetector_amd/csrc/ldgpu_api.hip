@@ -301,31 +301,35 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
             memcpy(&drows[(size_t)i * n_langs], rows + src_row[i] * (int64_t)n_langs, sizeof(double) * n_langs);
     }
 
-    // key -> row slots
+    // key -> row slots (mask form: the row's value and first mask word inline)
     m->slot_cap = next_pow2(std::max<uint64_t>(16, 2 * (uint64_t)nk));
     const int slog = log2u(m->slot_cap);
-    std::vector<Slot> slots(m->slot_cap, Slot{kEmpty, 0, 0});
+    std::vector<Slot> slots(m->slot_cap, Slot{kEmpty, 0, 0, 0.0, 0});
     for (int64_t i = 0; i < nk; ++i) {
         uint64_t s = mix64(keys[i]) >> (64 - slog);
         while (slots[s].key != kEmpty) s = (s + 1) & (m->slot_cap - 1);
         slots[s].key = keys[i];
         slots[s].row = (uint32_t)i;
+        if (!dense) {
+            slots[s].val = vals[i];
+            slots[s].mask0 = masks[(size_t)i * S];
+        }
         if (row_ok && !row_ok[src_row[i]]) {
             slots[s].row |= kBadRow;
             m->has_bad = true;
         }
     }
 
-    // bit filter: >= 32 bits per key while it fits LDS (<= 64 KiB), else a
-    // global (L2 / Infinity-Cache resident) filter at 16 bits per key
-    uint64_t fbits = next_pow2(std::max<uint64_t>(1024, 32 * (uint64_t)nk));
-    m->lds_filter = fbits <= (1ull << kMaxLdsFilterLog2);
-    if (!m->lds_filter) fbits = std::min<uint64_t>(next_pow2(16 * (uint64_t)nk), 1ull << 31);
-    m->filter_log2 = log2u(fbits);
-    std::vector<uint32_t> filter(fbits / 32, 0u);
+    // blocked Bloom filter, ~0.8 keys per 32-bit word (2 bits per key): in LDS
+    // up to 64 KiB, else a global (L2 / Infinity-Cache resident) filter
+    uint64_t fwords = next_pow2(std::max<uint64_t>(256, (uint64_t)(0.8 * (double)nk + 1)));
+    fwords = std::min<uint64_t>(fwords, 1ull << 28);
+    m->lds_filter = fwords <= (1ull << kMaxLdsFilterWordsLog2);
+    m->filter_log2 = log2u(fwords);
+    std::vector<uint32_t> filter(fwords, 0u);
     for (int64_t i = 0; i < nk; ++i) {
-        const uint32_t bit = filter_hash_key(keys[i]) >> (32 - m->filter_log2);
-        filter[bit >> 5] |= 1u << (bit & 31);
+        const uint32_t h = filter_hash_key(keys[i]);
+        filter[h >> (32 - m->filter_log2)] |= filter_bits(h);
     }
 
     hipError_t e = hipSetDevice(ctx->device);
@@ -335,9 +339,11 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (e == hipSuccess) e = upload(&m->d_vals, vals, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_rows, drows, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
-    m->lds_bytes = (m->lds_filter ? (size_t)(fbits / 8) : 0) + (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
-    m->wg_per_cu = std::max<int>(1, std::min<int>(2, (int)(163840 / m->lds_bytes)));
-    if (e == hipSuccess) e = score_prepare(S, dense, m->lds_filter, m->lds_bytes);
+    m->lds_bytes = (m->lds_filter ? (size_t)fwords * 4 : 0) + (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
+    int resident = 0;
+    if (e == hipSuccess) e = score_prepare(S, dense, m->lds_filter, m->lds_bytes, &resident);
+    // persistent grid = what is resident; never more workgroups than the LDS admits
+    m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
     if (e != hipSuccess) {
         model_free(m);
         return fail(e == hipErrorOutOfMemory ? LDGPU_ENOMEM : LDGPU_EDEVICE, "model upload: %s",
@@ -358,7 +364,7 @@ extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_
     if (mode) *mode = m->dense ? 1 : 0;
     if (n_keys) *n_keys = m->n_keys;
     if (table_slots) *table_slots = (int64_t)m->slot_cap;
-    if (filter_bits) *filter_bits = (int64_t)1 << m->filter_log2;
+    if (filter_bits) *filter_bits = ((int64_t)1 << m->filter_log2) * 32;
     if (device_bytes) *device_bytes = (int64_t)m->device_bytes;
     return ok();
 }
@@ -380,7 +386,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.slot_mask = m->slot_cap - 1;
     p.filter = m->d_filter;
     p.filter_shift = (uint32_t)(32 - m->filter_log2);
-    p.filter_words = (uint32_t)(((uint64_t)1 << m->filter_log2) / 32);
+    p.filter_words = (uint32_t)((uint64_t)1 << m->filter_log2);
     p.masks = m->d_masks;
     p.vals = m->d_vals;
     p.rows = m->d_rows;

@@ -19,15 +19,26 @@ constexpr int kMaxLangs = 256;
 constexpr int kMaxGramLengths = 32;
 constexpr uint64_t kEmpty = 0;
 
-// Filter hash (LDS bit filter) -- cheap: two 32-bit multiplies, and for
-// klen <= 4 the high word is the constant klen << 24 so its product is
-// wave-uniform.
+// Filter hash -- cheap: 32-bit multiplies only, and for klen <= 4 the high
+// word is the constant klen << 24 so its product is wave-uniform.
 __host__ __device__ __forceinline__ uint32_t hi_mix(uint32_t hi) { return hi * 0x85EBCA77u; }
 __host__ __device__ __forceinline__ uint32_t filter_hash(uint32_t lo, uint32_t himix) {
     return (lo * 0x9E3779B1u) ^ himix;
 }
 __host__ __device__ __forceinline__ uint32_t filter_hash_key(uint64_t key) {
     return filter_hash((uint32_t)key, hi_mix((uint32_t)(key >> 32)));
+}
+
+// Blocked Bloom filter: a key sets / tests TWO bits of ONE 32-bit word, so a
+// probe is one LDS read.  word = h >> wshift (top bits of h); the two bit
+// positions come from a second multiplicative mix of h.
+__host__ __device__ __forceinline__ uint32_t filter_bits(uint32_t h) {
+    const uint32_t t = h * 0x2C1B3C6Du;
+    return (1u << (t >> 27)) | (1u << ((t >> 22) & 31u));
+}
+__host__ __device__ __forceinline__ bool filter_test(uint32_t word, uint32_t h) {
+    const uint32_t b = filter_bits(h);
+    return (word & b) == b;
 }
 
 // Slot hash for the device hash tables (splitmix64 finaliser).
@@ -53,12 +64,16 @@ __host__ __device__ __forceinline__ int64_t n_windows(int64_t len, int n) {
     return len == 0 ? 0 : (len < n ? 1 : len - n + 1);
 }
 
-// Slot of the SCORE hash table: key + row index (bit 31 set = row of the
-// wrong length, LDGPU_EROWLEN on hit).
+// Slot of the SCORE hash table (32 B = two dwordx4 loads): key, row index
+// (bit 31 set = row of the wrong length, LDGPU_EROWLEN on hit) and, for
+// mask-form tables, the row's value and its first 64-language mask word, so a
+// hit needs no further dependent load when L <= 64.
 struct alignas(16) Slot {
     uint64_t key;
     uint32_t row;
     uint32_t pad;
+    double val;
+    uint64_t mask0;
 };
 
 constexpr uint32_t kBadRow = 0x80000000u;

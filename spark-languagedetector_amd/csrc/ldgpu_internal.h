@@ -17,8 +17,8 @@ struct ScoreParams {
     const Slot* slots;          // open-addressed key -> row table
     uint32_t slot_shift;        // slot = mix64(key) >> slot_shift
     uint64_t slot_mask;
-    const uint32_t* filter;     // bit filter over filter_hash(key)
-    uint32_t filter_shift;      // bit index = hash >> filter_shift
+    const uint32_t* filter;     // blocked Bloom filter over filter_hash(key)
+    uint32_t filter_shift;      // word index = hash >> filter_shift
     uint32_t filter_words;
     const uint64_t* masks;      // mask mode: [rows][S] language bitmasks
     const double* vals;         // mask mode: [rows] the row's one nonzero value
@@ -31,14 +31,15 @@ struct ScoreParams {
 };
 
 // Launch configuration of the score kernel.
-constexpr int kScoreWaves = 16;            // waves per workgroup (1024 threads)
-constexpr int kQueueCap = 128;             // candidate keys per wave in LDS
-constexpr int kMaxLdsFilterLog2 = 19;      // 64 KiB bit filter in LDS
+constexpr int kScoreWaves = 8;             // waves per workgroup (512 threads)
+constexpr int kQueueCap = 320;             // candidate keys per wave in LDS (>= 256 + slack)
+constexpr int kMaxLdsFilterWordsLog2 = 14; // <= 64 KiB filter in LDS
 
 // slices = ceil(L / 64); dense = general fp64 rows; lds_filter = filter staged in LDS
 hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_filter, int grid,
                         hipStream_t stream);
-hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes);
+// sets the dynamic-LDS limit and returns the resident workgroups per CU
+hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes, int* blocks_per_cu);
 
 // -------------------------------------------------------------------- FIT
 struct CountParams {

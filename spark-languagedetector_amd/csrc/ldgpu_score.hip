@@ -8,29 +8,34 @@
 //       if table contains window: s = s + row   (daxpy, a = 1.0)     :145-149
 //   label = argmax(s), first maximum (breeze)                       :154
 //
-// Structure (one wave per document, persistent grid):
-//   probe phase    lanes = 64 consecutive window positions of one gram length;
-//                  each lane loads its window (3 dwords + v_alignbyte), packs
-//                  the u64 key, hashes it and tests one bit of the filter,
-//                  which is staged in LDS (<= 64 KiB).  Candidates are
-//                  appended to a per-wave LDS queue with ballot + mbcnt, so
-//                  the queue is in reference order (n outer, position inner).
-//   verify phase   (when the queue is nearly full and at the end of the
-//                  document) 64 queued keys at a time probe the global
-//                  open-addressed table (L2-resident); hits carry their row.
-//   accumulate     hits are replayed in queue order; lane l owns language l
-//                  (slices of 64 for L > 64) and does s_l = s_l + row_l, so
-//                  every s_l sees exactly the reference's sequence of fp64
-//                  adds: scores are bit-identical, not just within tolerance.
-//                  Mask-form rows (all nonzeros equal: every fit-produced row)
-//                  add v or skip (x + 0.0 == x since s never is -0.0).
-//   argmax         lane-local over slices, then a 6-step xor-shuffle
-//                  reduction on (value, index) with the breeze rule.
+// Structure (one wave per document, persistent grid, next document's bytes
+// prefetched into registers while the current one is scored):
+//   probe      a superblock = 256 window positions, 4 per lane at stride 64.
+//              Each lane loads the 8 bytes at each of its positions once
+//              (dword loads + v_alignbyte); every gram length n re-masks them
+//              into the packed u64 key, hashes it, and tests a blocked Bloom
+//              filter staged in LDS (2 bits of one 32-bit word: one ds_read).
+//              The 4 reads of a lane are independent, then 4 ballots append
+//              the candidates to a per-wave LDS queue with mbcnt, so the queue
+//              is in reference order: n outer, position inner.
+//   verify     64 queued keys at a time probe the global open-addressed table
+//              (32-B slots carrying key, row, value and mask word 0).
+//   accumulate hits are replayed in queue order; lane l owns language l
+//              (slices of 64 for L > 64) and does s_l = s_l + row_l, so every
+//              s_l sees exactly the reference's sequence of fp64 adds: scores
+//              are bit-identical, not just within tolerance.  Mask-form rows
+//              (all nonzeros equal: every fit-produced row) add v or skip
+//              (x + 0.0 == x because s never is -0.0).
+//   argmax     lane-local over slices, then a 6-step xor-shuffle reduction on
+//              (value, index) with the breeze rule.
+// Documents longer than 256 bytes loop n outer, superblocks inner.
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
 
 namespace {
+
+constexpr int kSub = 4;  // 64-position sub-blocks per superblock
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -46,20 +51,73 @@ __device__ __forceinline__ uint32_t ld_dw(const uint32_t* w, int64_t i, int64_t 
     return w[i < last ? i : last];
 }
 
+// Raw dwords of one superblock: lane's positions base + 64k + lane, k < 4,
+// need dwords (a >> 2) + {0, 1, 2}.
+struct SbWords {
+    uint32_t w[kSub][3];
+};
+
+__device__ __forceinline__ void load_sb(const uint32_t* W, int64_t base, int lane, int64_t last, SbWords& r) {
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const int64_t i = (base + 64 * k + lane) >> 2;
+        r.w[k][0] = ld_dw(W, i, last);
+        r.w[k][1] = ld_dw(W, i + 1, last);
+        r.w[k][2] = ld_dw(W, i + 2, last);
+    }
+}
+
+struct Windows {
+    uint32_t lo[kSub], hi[kSub];  // bytes [a, a+4) and [a+4, a+8) of each position
+};
+
+__device__ __forceinline__ void windows_of(const SbWords& r, int64_t base, int lane, Windows& x) {
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const uint32_t sh = (uint32_t)((base + 64 * k + lane) & 3);
+        x.lo[k] = __builtin_amdgcn_alignbyte(r.w[k][1], r.w[k][0], sh);
+        x.hi[k] = __builtin_amdgcn_alignbyte(r.w[k][2], r.w[k][1], sh);
+    }
+}
+
+struct GramCtx {
+    int64_t nwin;
+    uint32_t lomask, himask, hitag, himix_c;
+    bool big;  // klen > 4
+};
+
+__device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
+    GramCtx g;
+    g.nwin = n_windows(len, n);
+    const int klen = len < n ? (int)len : n;
+    g.lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
+    g.himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
+    g.hitag = (uint32_t)klen << 24;
+    g.himix_c = hi_mix(g.hitag);
+    g.big = klen > 4;
+    return g;
+}
+
 // Verify + accumulate the queued candidates (in queue order).
 template <int S, bool DENSE>
-__device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queue, int qn, double (&acc)[S],
-                                      int lane) {
+__device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queue, int qn, double (&acc)[S], int lane) {
     __builtin_amdgcn_wave_barrier();
     for (int q0 = 0; q0 < qn; q0 += 64) {
         const int j = q0 + lane;
         uint32_t row = 0xffffffffu;
+        double v = 0.0;
+        uint64_t m0 = 0;
         if (j < qn) {
             const uint64_t key = queue[j];
             uint64_t s = mix64(key) >> p.slot_shift;
             for (;;) {
                 const Slot e = p.slots[s];
-                if (e.key == key) { row = e.row; break; }
+                if (e.key == key) {
+                    row = e.row;
+                    v = e.val;
+                    m0 = e.mask0;
+                    break;
+                }
                 if (e.key == kEmpty) break;
                 s = (s + 1) & p.slot_mask;
             }
@@ -69,19 +127,14 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queu
         if (__ballot(bad)) {
             if (lane == 0) atomicOr(p.err, 1);
         }
-        uint64_t hits = __ballot(hit && !bad);
+        const bool good = hit && !bad;
+        uint64_t hits = __ballot(good);
         if (!hits) continue;
         if constexpr (!DENSE) {
             uint64_t mw[S];
-            double v = 0.0;
-            if (hit && !bad) {
+            mw[0] = good ? m0 : 0ull;
 #pragma unroll
-                for (int s = 0; s < S; ++s) mw[s] = p.masks[(size_t)row * S + s];
-                v = p.vals[row];
-            } else {
-#pragma unroll
-                for (int s = 0; s < S; ++s) mw[s] = 0;
-            }
+            for (int s = 1; s < S; ++s) mw[s] = good ? p.masks[(size_t)row * S + s] : 0ull;
             while (hits) {
                 const int h = __builtin_ctzll(hits);
                 hits &= hits - 1;
@@ -108,62 +161,35 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queu
     }
 }
 
-constexpr int kSub = 4;  // 64-position sub-blocks per superblock (loads issued together)
-
-// Window bytes of one position: lo = bytes[a..a+4), hi = bytes[a+4..a+8)
-// (dword loads + v_alignbyte; clamped at the last readable dword).
-__device__ __forceinline__ void load_window(const uint32_t* W, int64_t a, int64_t last, bool need_hi, uint32_t& lo,
-                                            uint32_t& hi) {
-    const int64_t i = a >> 2;
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w0 = ld_dw(W, i, last);
-    const uint32_t w1 = ld_dw(W, i + 1, last);
-    lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-    hi = 0;
-    if (need_hi) hi = __builtin_amdgcn_alignbyte(ld_dw(W, i + 2, last), w1, sh);
-}
-
-struct GramCtx {
-    int64_t nwin;
-    uint32_t lomask, himask, hitag, himix_c;
-    bool big;  // klen > 4
-};
-
-__device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
-    GramCtx g;
-    g.nwin = n_windows(len, n);
-    const int klen = len < n ? (int)len : n;
-    g.lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
-    g.himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
-    g.hitag = (uint32_t)klen << 24;
-    g.himix_c = hi_mix(g.hitag);
-    g.big = klen > 4;
-    return g;
-}
-
-// Filter-test 64 windows (one per lane) and append the candidates to the
-// wave's queue in lane (= position) order; flush when the queue is nearly full.
-template <int S, bool DENSE>
-__device__ __forceinline__ void probe_block(const ScoreParams& p, const uint32_t* filt, uint64_t* queue, int& qn,
-                                            double (&acc)[S], int lane, const GramCtx& g, uint32_t xlo, uint32_t xhi,
-                                            bool valid) {
-    const uint32_t lo = xlo & g.lomask;
-    uint32_t hi = g.hitag;
-    uint32_t himix = g.himix_c;
-    if (g.big) {
-        hi |= xhi & g.himask;
-        himix = hi_mix(hi);
+// Filter-test the (up to) 256 windows of one superblock for one gram length
+// and append the candidates to the queue in position order.  The caller
+// guarantees qn <= kQueueCap - 256.
+__device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* filt, uint64_t* queue, int& qn,
+                                         const GramCtx& g, const Windows& x, int64_t p0, int lane) {
+    uint32_t lo[kSub], hi[kSub], word[kSub], h[kSub];
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        lo[k] = x.lo[k] & g.lomask;
+        hi[k] = g.hitag | (x.hi[k] & g.himask);
+        h[k] = filter_hash(lo[k], g.big ? hi_mix(hi[k]) : g.himix_c);
+        word[k] = filt[h[k] >> p.filter_shift];
     }
-    const uint32_t bit = filter_hash(lo, himix) >> p.filter_shift;
-    const bool cand = valid && ((filt[bit >> 5] >> (bit & 31)) & 1u);
-    const uint64_t m = __ballot(cand);
-    if (m) {
-        const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (cand) queue[qn + off] = ((uint64_t)hi << 32) | lo;
-        qn += __popcll(m);
-        if (qn > kQueueCap - 64) {
-            flush<S, DENSE>(p, queue, qn, acc, lane);
-            qn = 0;
+    bool cand[kSub];
+    uint64_t m[kSub];
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const bool valid = p0 + 64 * k + lane < g.nwin;
+        cand[k] = valid & filter_test(word[k], h[k]);
+        m[k] = __ballot(cand[k]);
+    }
+    if ((m[0] | m[1] | m[2] | m[3]) == 0) return;
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        if (m[k]) {
+            const uint32_t off =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
+            if (cand[k]) queue[qn + off] = ((uint64_t)hi[k] << 32) | lo[k];
+            qn += __popcll(m[k]);
         }
     }
 }
@@ -175,7 +201,7 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t fwords = FLDS ? p.filter_words : 0u;
-    uint64_t* queue = reinterpret_cast<uint64_t*>(lds + ((fwords + 3u) & ~3u)) + wave * kQueueCap;
+    uint64_t* queue = reinterpret_cast<uint64_t*>(lds + fwords) + wave * kQueueCap;
     const uint32_t* filt = p.filter;
     if constexpr (FLDS) {
         const uint4* src = reinterpret_cast<const uint4*>(p.filter);
@@ -185,44 +211,55 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
         filt = lds;
     }
     const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
-    const bool need_hi = p.max_gram > 4;
     const int64_t stride = (int64_t)gridDim.x * kScoreWaves;
-    for (int64_t doc = (int64_t)blockIdx.x * kScoreWaves + wave; doc < p.n_docs; doc += stride) {
-        const int64_t b = p.offsets[doc];
-        const int64_t len = p.offsets[doc + 1] - b;
+    int64_t doc = (int64_t)blockIdx.x * kScoreWaves + wave;
+    if (doc >= p.n_docs) return;
+
+    // prefetch of the first document
+    int64_t nb = p.offsets[doc];
+    int64_t nlen = p.offsets[doc + 1] - nb;
+    SbWords nxt;
+    load_sb(W, nb, lane, p.last_dword, nxt);
+
+    for (; doc < p.n_docs; doc += stride) {
+        const int64_t b = nb, len = nlen;
+        const SbWords cur = nxt;
+        const int64_t next = doc + stride;
+        if (next < p.n_docs) {
+            nb = p.offsets[next];
+            nlen = p.offsets[next + 1] - nb;
+            load_sb(W, nb, lane, p.last_dword, nxt);
+        }
         double acc[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) acc[s] = 0.0;
         int qn = 0;
         if (len <= 64 * kSub) {
             // one superblock: every gram length reuses the same window bytes
-            uint32_t xlo[kSub], xhi[kSub];
-#pragma unroll
-            for (int k = 0; k < kSub; ++k) load_window(W, b + 64 * k + lane, p.last_dword, need_hi, xlo[k], xhi[k]);
+            Windows x;
+            windows_of(cur, b, lane, x);
             for (int gi = 0; gi < p.nG; ++gi) {
                 const GramCtx g = gram_ctx(len, p.G[gi]);
-#pragma unroll
-                for (int k = 0; k < kSub; ++k) {
-                    if (64 * k < g.nwin)
-                        probe_block<S, DENSE>(p, filt, queue, qn, acc, lane, g, xlo[k], xhi[k],
-                                              64 * k + lane < g.nwin);
+                if (qn > kQueueCap - 64 * kSub) {
+                    flush<S, DENSE>(p, queue, qn, acc, lane);
+                    qn = 0;
                 }
+                probe_sb(p, filt, queue, qn, g, x, 0, lane);
             }
         } else {
             // long documents: n outer (reference order), superblocks inner
             for (int gi = 0; gi < p.nG; ++gi) {
                 const GramCtx g = gram_ctx(len, p.G[gi]);
                 for (int64_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
-                    uint32_t xlo[kSub], xhi[kSub];
-#pragma unroll
-                    for (int k = 0; k < kSub; ++k)
-                        load_window(W, b + p0 + 64 * k + lane, p.last_dword, g.big, xlo[k], xhi[k]);
-#pragma unroll
-                    for (int k = 0; k < kSub; ++k) {
-                        if (p0 + 64 * k < g.nwin)
-                            probe_block<S, DENSE>(p, filt, queue, qn, acc, lane, g, xlo[k], xhi[k],
-                                                  p0 + 64 * k + lane < g.nwin);
+                    SbWords r;
+                    load_sb(W, b + p0, lane, p.last_dword, r);
+                    Windows x;
+                    windows_of(r, b + p0, lane, x);
+                    if (qn > kQueueCap - 64 * kSub) {
+                        flush<S, DENSE>(p, queue, qn, acc, lane);
+                        qn = 0;
                     }
+                    probe_sb(p, filt, queue, qn, g, x, p0, lane);
                 }
             }
         }
@@ -270,16 +307,17 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
 
 template <int S, bool DENSE, bool FLDS>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
-    const size_t lds = (FLDS ? ((p.filter_words + 3u) & ~3u) * 4u : 0u) +
-                       (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
+    const size_t lds = (FLDS ? (size_t)p.filter_words * 4u : 0u) + (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
     hipLaunchKernelGGL((score_kernel<S, DENSE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
 
 template <int S, bool DENSE, bool FLDS>
-hipError_t prepare_t(size_t lds) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&score_kernel<S, DENSE, FLDS>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+hipError_t prepare_t(size_t lds, int* blocks) {
+    const void* f = reinterpret_cast<const void*>(&score_kernel<S, DENSE, FLDS>);
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, kScoreWaves * 64, lds);
 }
 
 template <bool DENSE, bool FLDS>
@@ -294,12 +332,12 @@ hipError_t launch_s(const ScoreParams& p, int slices, int grid, hipStream_t stre
 }
 
 template <bool DENSE, bool FLDS>
-hipError_t prepare_s(int slices, size_t lds) {
+hipError_t prepare_s(int slices, size_t lds, int* blocks) {
     switch (slices) {
-        case 1: return prepare_t<1, DENSE, FLDS>(lds);
-        case 2: return prepare_t<2, DENSE, FLDS>(lds);
-        case 3: return prepare_t<3, DENSE, FLDS>(lds);
-        case 4: return prepare_t<4, DENSE, FLDS>(lds);
+        case 1: return prepare_t<1, DENSE, FLDS>(lds, blocks);
+        case 2: return prepare_t<2, DENSE, FLDS>(lds, blocks);
+        case 3: return prepare_t<3, DENSE, FLDS>(lds, blocks);
+        case 4: return prepare_t<4, DENSE, FLDS>(lds, blocks);
         default: return hipErrorInvalidValue;
     }
 }
@@ -316,11 +354,13 @@ hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_f
                       : launch_s<false, false>(p, slices, grid, stream);
 }
 
-hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes) {
+hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes, int* blocks_per_cu) {
     if (dense) {
-        return lds_filter ? prepare_s<true, true>(slices, lds_bytes) : prepare_s<true, false>(slices, lds_bytes);
+        return lds_filter ? prepare_s<true, true>(slices, lds_bytes, blocks_per_cu)
+                          : prepare_s<true, false>(slices, lds_bytes, blocks_per_cu);
     }
-    return lds_filter ? prepare_s<false, true>(slices, lds_bytes) : prepare_s<false, false>(slices, lds_bytes);
+    return lds_filter ? prepare_s<false, true>(slices, lds_bytes, blocks_per_cu)
+                      : prepare_s<false, false>(slices, lds_bytes, blocks_per_cu);
 }
 
 }  // namespace ldgpu
