@@ -96,7 +96,8 @@ int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets
 /* Device-resident variant, asynchronous on `stream` (a hipStream_t used as
  * given: NULL is HIP's null stream; ldgpu_ctx_stream() gives the context's).
  * d_bytes must be 4-byte aligned and n_bytes >= d_offsets[n_docs].
- * d_scores is nullable.  Offsets are trusted (validate with the host API). */
+ * d_scores is nullable.  Offsets are trusted (validate with the host API);
+ * documents must be shorter than 2^29 bytes (the host API checks this). */
 int ldgpu_score_device(ldgpu_model* model, const uint8_t* d_bytes, int64_t n_bytes,
                        const int64_t* d_offsets, int64_t n_docs, int32_t* d_labels,
                        double* d_scores, void* stream);

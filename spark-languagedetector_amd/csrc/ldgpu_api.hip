@@ -182,7 +182,8 @@ struct ldgpu_model {
     bool has_bad = false;
     int64_t n_keys = 0;
     uint64_t slot_cap = 0;
-    int filter_log2 = 10;
+    int filter_log2 = 10;     // bloom words (log2)
+    uint32_t len_mask = 0;    // bit k: some key has k bytes
     size_t lds_bytes = 0;
     int wg_per_cu = 1;
     size_t device_bytes = 0;
@@ -320,16 +321,34 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
         }
     }
 
-    // blocked Bloom filter, ~0.8 keys per 32-bit word (2 bits per key): in LDS
-    // up to 64 KiB, else a global (L2 / Infinity-Cache resident) filter
-    uint64_t fwords = next_pow2(std::max<uint64_t>(256, (uint64_t)(0.8 * (double)nk + 1)));
-    fwords = std::min<uint64_t>(fwords, 1ull << 28);
-    m->lds_filter = fwords <= (1ull << kMaxLdsFilterWordsLog2);
-    m->filter_log2 = log2u(fwords);
-    std::vector<uint32_t> filter(fwords, 0u);
+    // filter image: exact bitmaps of the 1- and 2-byte keys, then a blocked
+    // Bloom filter of the longer ones (~1.6 keys per 32-bit word; false
+    // positives only cost verification lanes).  The bloom is staged in LDS up
+    // to 64 KiB, else read from global memory (L2 / Infinity Cache).
+    int64_t n_long = 0;
     for (int64_t i = 0; i < nk; ++i) {
-        const uint32_t h = filter_hash_key(keys[i]);
-        filter[h >> (32 - m->filter_log2)] |= filter_bits(h);
+        const int kl = key_len(keys[i]);
+        m->len_mask |= 1u << kl;
+        n_long += kl >= 3;
+    }
+    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / 1.6) + 1));
+    bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
+    m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
+    m->filter_log2 = log2u(bwords);
+    const uint32_t bshift = 32u - (uint32_t)m->filter_log2;
+    std::vector<uint32_t> filter(kBloomBase + bwords, 0u);
+    for (int64_t i = 0; i < nk; ++i) {
+        const int kl = key_len(keys[i]);
+        if (kl == 1) {
+            const uint32_t b0 = (uint32_t)(keys[i] & 0xff);
+            filter[b0 >> 5] |= 1u << (b0 & 31);
+        } else if (kl == 2) {
+            const uint32_t b01 = (uint32_t)(keys[i] & 0xffff);
+            filter[kBmp1Words + (b01 >> 5)] |= 1u << (b01 & 31);
+        } else {
+            const uint32_t h = filter_hash_key(keys[i]);
+            filter[kBloomBase + (h >> bshift)] |= filter_bits(h, bshift);
+        }
     }
 
     hipError_t e = hipSetDevice(ctx->device);
@@ -339,7 +358,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (e == hipSuccess) e = upload(&m->d_vals, vals, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_rows, drows, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
-    m->lds_bytes = (m->lds_filter ? (size_t)fwords * 4 : 0) + (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
+    m->lds_bytes = score_lds_bytes(S, m->lds_filter, (uint32_t)bwords);
     int resident = 0;
     if (e == hipSuccess) e = score_prepare(S, dense, m->lds_filter, m->lds_bytes, &resident);
     // persistent grid = what is resident; never more workgroups than the LDS admits
@@ -364,7 +383,7 @@ extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_
     if (mode) *mode = m->dense ? 1 : 0;
     if (n_keys) *n_keys = m->n_keys;
     if (table_slots) *table_slots = (int64_t)m->slot_cap;
-    if (filter_bits) *filter_bits = ((int64_t)1 << m->filter_log2) * 32;
+    if (filter_bits) *filter_bits = ((int64_t)1 << m->filter_log2) * 32;  // bloom bits
     if (device_bytes) *device_bytes = (int64_t)m->device_bytes;
     return ok();
 }
@@ -385,19 +404,16 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.slot_shift = (uint32_t)(64 - slog);
     p.slot_mask = m->slot_cap - 1;
     p.filter = m->d_filter;
-    p.filter_shift = (uint32_t)(32 - m->filter_log2);
-    p.filter_words = (uint32_t)((uint64_t)1 << m->filter_log2);
+    p.bloom_shift = (uint32_t)(32 - m->filter_log2);
+    p.bloom_words = (uint32_t)((uint64_t)1 << m->filter_log2);
+    p.len_mask = m->len_mask;
     p.masks = m->d_masks;
     p.vals = m->d_vals;
     p.rows = m->d_rows;
     p.err = m->d_err;
     p.L = m->L;
     p.nG = m->nG;
-    p.max_gram = 0;
-    for (int i = 0; i < m->nG; ++i) {
-        p.G[i] = m->G[i];
-        p.max_gram = std::max(p.max_gram, m->G[i]);
-    }
+    for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
     const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
     HIP_TRY(launch_score(p, m->slices, m->dense, m->lds_filter, grid, st));
@@ -411,6 +427,9 @@ int check_row_error(ldgpu_model* m, hipStream_t st) {
     if (err) {
         int32_t z = 0;
         HIP_TRY(hipMemcpy(m->d_err, &z, sizeof z, hipMemcpyHostToDevice));
+        if (err & 2)
+            return fail(LDGPU_EUNSUPPORTED, "a document of %lld bytes or more exceeds the device path's limit",
+                        (long long)kMaxDocBytes);
         return fail(LDGPU_EROWLEN, "requirement failed: BLAS.axpy size mismatch (a hit gram's row length != %d)",
                     m->L);
     }
@@ -441,6 +460,10 @@ extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* 
     if (n_docs == 0) return ok();
     if (!out_labels) return fail(LDGPU_EINVAL, "out_labels is NULL");
     if (!bytes && offsets[n_docs] > offsets[0]) return fail(LDGPU_EINVAL, "bytes is NULL");
+    for (int64_t d = 0; d < n_docs; ++d)
+        if (offsets[d + 1] - offsets[d] >= kMaxDocBytes)
+            return fail(LDGPU_EUNSUPPORTED, "document %lld has %lld bytes: the device path's limit is %lld",
+                        (long long)d, (long long)(offsets[d + 1] - offsets[d]), (long long)kMaxDocBytes - 1);
     ldgpu_ctx* c = m->ctx;
     std::lock_guard<std::mutex> lock(c->mu);
     HIP_TRY(hipSetDevice(c->device));

@@ -29,17 +29,23 @@ __host__ __device__ __forceinline__ uint32_t filter_hash_key(uint64_t key) {
     return filter_hash((uint32_t)key, hi_mix((uint32_t)(key >> 32)));
 }
 
-// Blocked Bloom filter: a key sets / tests TWO bits of ONE 32-bit word, so a
-// probe is one LDS read.  word = h >> wshift (top bits of h); the two bit
-// positions come from a second multiplicative mix of h.
-__host__ __device__ __forceinline__ uint32_t filter_bits(uint32_t h) {
-    const uint32_t t = h * 0x2C1B3C6Du;
-    return (1u << (t >> 27)) | (1u << ((t >> 22) & 31u));
+// Blocked Bloom filter for keys of 3..7 bytes: a key sets / tests TWO bits of
+// ONE 32-bit word, so a probe is one LDS read and one multiply.  word = top
+// `wlog` bits of h; the two bit positions are the 10 bits below them.
+__host__ __device__ __forceinline__ uint32_t filter_bits(uint32_t h, uint32_t shift) {
+    return (1u << ((h >> (shift - 5)) & 31u)) | (1u << ((h >> (shift - 10)) & 31u));
 }
-__host__ __device__ __forceinline__ bool filter_test(uint32_t word, uint32_t h) {
-    const uint32_t b = filter_bits(h);
-    return (word & b) == b;
-}
+
+// Filter image (host-built, staged whole into LDS): a direct 256-bit bitmap
+// of the 1-byte keys, a direct 65536-bit bitmap of the 2-byte keys, then the
+// blocked Bloom words.
+constexpr uint32_t kBmp1Words = 8;
+constexpr uint32_t kBmp2Words = 2048;
+constexpr uint32_t kBloomBase = kBmp1Words + kBmp2Words;
+
+// Candidate queue entry: klen in the top 3 bits, window position below.
+constexpr uint32_t kPosBits = 29;
+constexpr int64_t kMaxDocBytes = (int64_t)1 << kPosBits;
 
 // Slot hash for the device hash tables (splitmix64 finaliser).
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t k) {

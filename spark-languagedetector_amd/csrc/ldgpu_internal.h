@@ -9,7 +9,7 @@ namespace ldgpu {
 // ------------------------------------------------------------------ SCORE
 struct ScoreParams {
     const uint8_t* bytes;       // 4-byte aligned
-    int64_t last_dword;         // index of the last readable dword of bytes (-1: none)
+    int64_t last_dword;         // index of the last readable dword of bytes
     const int64_t* offsets;     // [n_docs + 1]
     int64_t n_docs;
     int32_t* labels;            // [n_docs]
@@ -17,29 +17,36 @@ struct ScoreParams {
     const Slot* slots;          // open-addressed key -> row table
     uint32_t slot_shift;        // slot = mix64(key) >> slot_shift
     uint64_t slot_mask;
-    const uint32_t* filter;     // blocked Bloom filter over filter_hash(key)
-    uint32_t filter_shift;      // word index = hash >> filter_shift
-    uint32_t filter_words;
+    const uint32_t* filter;     // image: bmp1 | bmp2 | bloom (ldgpu_common.h)
+    uint32_t bloom_words;       // power of two
+    uint32_t bloom_shift;       // bloom word = hash >> bloom_shift (>= 10)
+    uint32_t len_mask;          // bit k set: the table holds keys of k bytes
     const uint64_t* masks;      // mask mode: [rows][S] language bitmasks
     const double* vals;         // mask mode: [rows] the row's one nonzero value
     const double* rows;         // dense mode: [rows][L]
-    int32_t* err;               // set to 1 when a window hits a wrong-length row
+    int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     int32_t L;
-    int32_t max_gram;           // max of G (windows need a high key word when > 4)
     int32_t nG;
     int32_t G[kMaxGramLengths];
 };
 
 // Launch configuration of the score kernel.
 constexpr int kScoreWaves = 8;             // waves per workgroup (512 threads)
-constexpr int kQueueCap = 320;             // candidate keys per wave in LDS (>= 256 + slack)
-constexpr int kMaxLdsFilterWordsLog2 = 14; // <= 64 KiB filter in LDS
+constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
+constexpr int kMaxLdsBloomLog2 = 14;       // bloom words in LDS up to 64 KiB
+constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
 
-// slices = ceil(L / 64); dense = general fp64 rows; lds_filter = filter staged in LDS
-hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_filter, int grid,
+// bytes of dynamic LDS the score kernel needs
+inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) {
+    return (size_t)(kBloomBase + (lds_bloom ? bloom_words : 0u)) * 4u +
+           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 8u * (slices + 1u));
+}
+
+// slices = ceil(L / 64); dense = general fp64 rows; lds_bloom = bloom staged in LDS
+hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_bloom, int grid,
                         hipStream_t stream);
 // sets the dynamic-LDS limit and returns the resident workgroups per CU
-hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes, int* blocks_per_cu);
+hipError_t score_prepare(int slices, bool dense, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu);
 
 // -------------------------------------------------------------------- FIT
 struct CountParams {

@@ -81,26 +81,33 @@ __device__ __forceinline__ void windows_of(const SbWords& r, int64_t base, int l
 }
 
 struct GramCtx {
-    int64_t nwin;
+    int32_t nwin;        // windows of this gram length (docs < 2^29 bytes)
+    int32_t klen;        // key length: n, or len for a partial window
     uint32_t lomask, himask, hitag, himix_c;
-    bool big;  // klen > 4
 };
 
 __device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
     GramCtx g;
-    g.nwin = n_windows(len, n);
-    const int klen = len < n ? (int)len : n;
+    g.nwin = (int32_t)n_windows(len, n);
+    g.klen = len < n ? (int)len : n;
+    const int klen = g.klen;
     g.lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
     g.himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
     g.hitag = (uint32_t)klen << 24;
     g.himix_c = hi_mix(g.hitag);
-    g.big = klen > 4;
     return g;
 }
 
+// Per-wave LDS regions.
+struct WaveLds {
+    uint32_t* queue;  // [kQueueCap] candidate entries (klen << 29 | position)
+    uint64_t* hits;   // [64][S + 1] verified hits of one chunk: value bits, mask words
+};
+
 // Verify + accumulate the queued candidates (in queue order).
 template <int S, bool DENSE>
-__device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queue, int qn, double (&acc)[S], int lane) {
+__device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, int64_t b,
+                                      const uint32_t* W, double (&acc)[S], int lane) {
     __builtin_amdgcn_wave_barrier();
     for (int q0 = 0; q0 < qn; q0 += 64) {
         const int j = q0 + lane;
@@ -108,17 +115,30 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queu
         double v = 0.0;
         uint64_t m0 = 0;
         if (j < qn) {
-            const uint64_t key = queue[j];
+            const uint32_t e = w.queue[j];
+            const int klen = (int)(e >> kPosBits);
+            const int64_t a = b + (int64_t)(e & ((1u << kPosBits) - 1u));
+            const int64_t i = a >> 2;
+            const uint32_t sh = (uint32_t)(a & 3);
+            const uint32_t w0 = ld_dw(W, i, p.last_dword), w1 = ld_dw(W, i + 1, p.last_dword);
+            uint64_t key = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            if (klen > 4) {
+                const uint32_t hi = __builtin_amdgcn_alignbyte(ld_dw(W, i + 2, p.last_dword), w1, sh);
+                key |= (uint64_t)(hi & ((1u << (8 * (klen - 4))) - 1u)) << 32;
+            } else if (klen < 4) {
+                key &= (1ull << (8 * klen)) - 1ull;
+            }
+            key |= (uint64_t)klen << 56;
             uint64_t s = mix64(key) >> p.slot_shift;
             for (;;) {
-                const Slot e = p.slots[s];
-                if (e.key == key) {
-                    row = e.row;
-                    v = e.val;
-                    m0 = e.mask0;
+                const Slot sl = p.slots[s];
+                if (sl.key == key) {
+                    row = sl.row;
+                    v = sl.val;
+                    m0 = sl.mask0;
                     break;
                 }
-                if (e.key == kEmpty) break;
+                if (sl.key == kEmpty) break;
                 s = (s + 1) & p.slot_mask;
             }
         }
@@ -128,27 +148,34 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queu
             if (lane == 0) atomicOr(p.err, 1);
         }
         const bool good = hit && !bad;
-        uint64_t hits = __ballot(good);
+        const uint64_t hits = __ballot(good);
         if (!hits) continue;
         if constexpr (!DENSE) {
-            uint64_t mw[S];
-            mw[0] = good ? m0 : 0ull;
+            // compact the hits into LDS in queue order, then every lane (one
+            // language each) replays them with broadcast reads
+            if (good) {
+                const uint32_t off =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(hits >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hits, 0u));
+                uint64_t* h = w.hits + off * (S + 1);
+                h[0] = (uint64_t)__double_as_longlong(v);
+                h[1] = m0;
 #pragma unroll
-            for (int s = 1; s < S; ++s) mw[s] = good ? p.masks[(size_t)row * S + s] : 0ull;
-            while (hits) {
-                const int h = __builtin_ctzll(hits);
-                hits &= hits - 1;
-                const double vv = rdlaned(v, h);
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    const uint64_t ms = rdlane64(mw[s], h);
-                    acc[s] = acc[s] + (((ms >> lane) & 1ull) ? vv : 0.0);
-                }
+                for (int s = 1; s < S; ++s) h[1 + s] = p.masks[(size_t)row * S + s];
             }
+            __builtin_amdgcn_wave_barrier();
+            const int nh = __popcll(hits);
+            for (int t = 0; t < nh; ++t) {
+                const uint64_t* h = w.hits + t * (S + 1);
+                const double vv = __longlong_as_double((long long)h[0]);
+#pragma unroll
+                for (int s = 0; s < S; ++s) acc[s] = acc[s] + (((h[1 + s] >> lane) & 1ull) ? vv : 0.0);
+            }
+            __builtin_amdgcn_wave_barrier();
         } else {
-            while (hits) {
-                const int h = __builtin_ctzll(hits);
-                hits &= hits - 1;
+            uint64_t hh = hits;
+            while (hh) {
+                const int h = __builtin_ctzll(hh);
+                hh &= hh - 1;
                 const uint32_t r = rdlane(row, h);
                 const double* rp = p.rows + (size_t)r * p.L;
 #pragma unroll
@@ -163,32 +190,49 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const uint64_t* queu
 
 // Filter-test the (up to) 256 windows of one superblock for one gram length
 // and append the candidates to the queue in position order.  The caller
-// guarantees qn <= kQueueCap - 256.
-__device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* filt, uint64_t* queue, int& qn,
-                                         const GramCtx& g, const Windows& x, int64_t p0, int lane) {
-    uint32_t lo[kSub], hi[kSub], word[kSub], h[kSub];
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        lo[k] = x.lo[k] & g.lomask;
-        hi[k] = g.hitag | (x.hi[k] & g.himask);
-        h[k] = filter_hash(lo[k], g.big ? hi_mix(hi[k]) : g.himix_c);
-        word[k] = filt[h[k] >> p.filter_shift];
-    }
+// guarantees qn <= kQueueCap - 256.  1- and 2-byte keys test exact LDS
+// bitmaps; longer keys a blocked Bloom filter.
+__device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* img, const uint32_t* bloom,
+                                         uint32_t* queue, int& qn, const GramCtx& g, const Windows& x, int32_t p0,
+                                         int lane) {
     bool cand[kSub];
+    const int32_t nw = g.nwin - p0;  // windows left from p0 (> 0)
+    if (g.klen <= 2) {
+        const uint32_t base = g.klen == 1 ? 0u : kBmp1Words;
+        uint32_t idx[kSub], word[kSub];
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            idx[k] = x.lo[k] & g.lomask;
+            word[k] = img[base + (idx[k] >> 5)];
+        }
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) cand[k] = (64 * k + lane < nw) & ((word[k] >> (idx[k] & 31u)) & 1u);
+    } else {
+        uint32_t h[kSub], word[kSub];
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            const uint32_t lo = x.lo[k] & g.lomask;
+            const uint32_t himix = g.klen > 4 ? hi_mix(g.hitag | (x.hi[k] & g.himask)) : g.himix_c;
+            h[k] = filter_hash(lo, himix);
+            word[k] = bloom[h[k] >> p.bloom_shift];
+        }
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            const uint32_t fb = filter_bits(h[k], p.bloom_shift);
+            cand[k] = (64 * k + lane < nw) & ((word[k] & fb) == fb);
+        }
+    }
     uint64_t m[kSub];
 #pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        const bool valid = p0 + 64 * k + lane < g.nwin;
-        cand[k] = valid & filter_test(word[k], h[k]);
-        m[k] = __ballot(cand[k]);
-    }
+    for (int k = 0; k < kSub; ++k) m[k] = __ballot(cand[k]);
     if ((m[0] | m[1] | m[2] | m[3]) == 0) return;
+    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)(p0 + lane);
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
         if (m[k]) {
             const uint32_t off =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            if (cand[k]) queue[qn + off] = ((uint64_t)hi[k] << 32) | lo[k];
+            if (cand[k]) queue[qn + off] = tag + 64u * k;
             qn += __popcll(m[k]);
         }
     }
@@ -200,16 +244,18 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t fwords = FLDS ? p.filter_words : 0u;
-    uint64_t* queue = reinterpret_cast<uint64_t*>(lds + fwords) + wave * kQueueCap;
-    const uint32_t* filt = p.filter;
-    if constexpr (FLDS) {
+    const uint32_t img_words = kBloomBase + (FLDS ? p.bloom_words : 0u);
+    {
         const uint4* src = reinterpret_cast<const uint4*>(p.filter);
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (uint32_t i = tid; i < (fwords >> 2); i += blockDim.x) dst[i] = src[i];
+        for (uint32_t i = tid; i < (img_words >> 2); i += blockDim.x) dst[i] = src[i];
         __syncthreads();
-        filt = lds;
     }
+    const uint32_t* bloom = FLDS ? lds + kBloomBase : p.filter + kBloomBase;
+    WaveLds wl;
+    wl.queue = lds + img_words + wave * kQueueCap;
+    wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * (S + 1);
+
     const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
     const int64_t stride = (int64_t)gridDim.x * kScoreWaves;
     int64_t doc = (int64_t)blockIdx.x * kScoreWaves + wave;
@@ -234,36 +280,40 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
 #pragma unroll
         for (int s = 0; s < S; ++s) acc[s] = 0.0;
         int qn = 0;
-        if (len <= 64 * kSub) {
+        if (len >= kMaxDocBytes) {
+            if (lane == 0) atomicOr(p.err, 2);
+        } else if (len <= 64 * kSub) {
             // one superblock: every gram length reuses the same window bytes
             Windows x;
             windows_of(cur, b, lane, x);
             for (int gi = 0; gi < p.nG; ++gi) {
                 const GramCtx g = gram_ctx(len, p.G[gi]);
+                if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
                 if (qn > kQueueCap - 64 * kSub) {
-                    flush<S, DENSE>(p, queue, qn, acc, lane);
+                    flush<S, DENSE>(p, wl, qn, b, W, acc, lane);
                     qn = 0;
                 }
-                probe_sb(p, filt, queue, qn, g, x, 0, lane);
+                probe_sb(p, lds, bloom, wl.queue, qn, g, x, 0, lane);
             }
         } else {
             // long documents: n outer (reference order), superblocks inner
             for (int gi = 0; gi < p.nG; ++gi) {
                 const GramCtx g = gram_ctx(len, p.G[gi]);
-                for (int64_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
+                if (!((p.len_mask >> g.klen) & 1u)) continue;
+                for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
                     SbWords r;
                     load_sb(W, b + p0, lane, p.last_dword, r);
                     Windows x;
                     windows_of(r, b + p0, lane, x);
                     if (qn > kQueueCap - 64 * kSub) {
-                        flush<S, DENSE>(p, queue, qn, acc, lane);
+                        flush<S, DENSE>(p, wl, qn, b, W, acc, lane);
                         qn = 0;
                     }
-                    probe_sb(p, filt, queue, qn, g, x, p0, lane);
+                    probe_sb(p, lds, bloom, wl.queue, qn, g, x, p0, lane);
                 }
             }
         }
-        if (qn) flush<S, DENSE>(p, queue, qn, acc, lane);
+        if (qn) flush<S, DENSE>(p, wl, qn, b, W, acc, lane);
 
         // argmax (breeze: first element, then strict '>' updates)
         double bv = acc[0];
@@ -307,7 +357,7 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
 
 template <int S, bool DENSE, bool FLDS>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
-    const size_t lds = (FLDS ? (size_t)p.filter_words * 4u : 0u) + (size_t)kScoreWaves * kQueueCap * sizeof(uint64_t);
+    const size_t lds = score_lds_bytes(S, FLDS, p.bloom_words);
     hipLaunchKernelGGL((score_kernel<S, DENSE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
