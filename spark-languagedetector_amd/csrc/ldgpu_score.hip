@@ -102,12 +102,38 @@ __device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
 struct WaveLds {
     uint32_t* queue;  // [kQueueCap] candidate entries (klen << 29 | position)
     uint64_t* hits;   // [64][S + 1] verified hits of one chunk: value bits, mask words
+    uint32_t* buf;    // [kBufBytes / 4 + 4] staged bytes of the current document group
 };
+
+// Where a document's bytes are read from: the wave's LDS buffer (staged
+// group: byte `base` of the buffer) or global memory (byte `base` of p.bytes).
+struct DocSrc {
+    const uint32_t* lds;  // nullptr = global
+    int64_t base;
+};
+
+__device__ __forceinline__ void window_words(const ScoreParams& p, const DocSrc& src, int64_t pos, uint32_t& w0,
+                                             uint32_t& w1, uint32_t& w2, uint32_t& sh) {
+    const int64_t a = src.base + pos;
+    sh = (uint32_t)(a & 3);
+    if (src.lds) {
+        const uint32_t i = (uint32_t)(a >> 2);
+        w0 = src.lds[i];
+        w1 = src.lds[i + 1];
+        w2 = src.lds[i + 2];
+    } else {
+        const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+        const int64_t i = a >> 2;
+        w0 = ld_dw(W, i, p.last_dword);
+        w1 = ld_dw(W, i + 1, p.last_dword);
+        w2 = ld_dw(W, i + 2, p.last_dword);
+    }
+}
 
 // Verify + accumulate the queued candidates (in queue order).
 template <int S, bool DENSE>
-__device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, int64_t b,
-                                      const uint32_t* W, double (&acc)[S], int lane) {
+__device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
+                                      double (&acc)[S], int lane) {
     __builtin_amdgcn_wave_barrier();
     for (int q0 = 0; q0 < qn; q0 += 64) {
         const int j = q0 + lane;
@@ -117,13 +143,11 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         if (j < qn) {
             const uint32_t e = w.queue[j];
             const int klen = (int)(e >> kPosBits);
-            const int64_t a = b + (int64_t)(e & ((1u << kPosBits) - 1u));
-            const int64_t i = a >> 2;
-            const uint32_t sh = (uint32_t)(a & 3);
-            const uint32_t w0 = ld_dw(W, i, p.last_dword), w1 = ld_dw(W, i + 1, p.last_dword);
+            uint32_t w0, w1, w2, sh;
+            window_words(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
             uint64_t key = __builtin_amdgcn_alignbyte(w1, w0, sh);
             if (klen > 4) {
-                const uint32_t hi = __builtin_amdgcn_alignbyte(ld_dw(W, i + 2, p.last_dword), w1, sh);
+                const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
                 key |= (uint64_t)(hi & ((1u << (8 * (klen - 4))) - 1u)) << 32;
             } else if (klen < 4) {
                 key &= (1ull << (8 * klen)) - 1ull;
@@ -238,6 +262,115 @@ __device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* i
     }
 }
 
+// Score one document (probe -> verify/accumulate -> argmax -> outputs).
+template <int S, bool DENSE>
+__device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                          const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
+                                          const DocSrc& src, int lane) {
+    double acc[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) acc[s] = 0.0;
+    int qn = 0;
+    if (len >= kMaxDocBytes) {
+        if (lane == 0) atomicOr(p.err, 2);
+    } else if (len <= 64 * kSub) {
+        // one superblock: every gram length reuses the same window bytes
+        Windows x;
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            uint32_t w0, w1, w2, sh;
+            window_words(p, src, 64 * k + lane, w0, w1, w2, sh);
+            x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        }
+        for (int gi = 0; gi < p.nG; ++gi) {
+            const GramCtx g = gram_ctx(len, p.G[gi]);
+            if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
+            if (qn > kQueueCap - 64 * kSub) {
+                flush<S, DENSE>(p, wl, qn, src, acc, lane);
+                qn = 0;
+            }
+            probe_sb(p, img, bloom, wl.queue, qn, g, x, 0, lane);
+        }
+    } else {
+        // long documents: n outer (reference order), superblocks inner
+        for (int gi = 0; gi < p.nG; ++gi) {
+            const GramCtx g = gram_ctx(len, p.G[gi]);
+            if (!((p.len_mask >> g.klen) & 1u)) continue;
+            for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
+                Windows x;
+#pragma unroll
+                for (int k = 0; k < kSub; ++k) {
+                    uint32_t w0, w1, w2, sh;
+                    window_words(p, src, p0 + 64 * k + lane, w0, w1, w2, sh);
+                    x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                    x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                }
+                if (qn > kQueueCap - 64 * kSub) {
+                    flush<S, DENSE>(p, wl, qn, src, acc, lane);
+                    qn = 0;
+                }
+                probe_sb(p, img, bloom, wl.queue, qn, g, x, p0, lane);
+            }
+        }
+    }
+    if (qn) flush<S, DENSE>(p, wl, qn, src, acc, lane);
+
+    // argmax (breeze: first element, then strict '>' updates)
+    double bv = acc[0];
+    int bi = lane;
+    bool bval = lane < p.L && !__builtin_isnan(bv);
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+        const int l = s * 64 + lane;
+        const double v = acc[s];
+        if (l < p.L && !__builtin_isnan(v) && (!bval || v > bv)) {
+            bv = v;
+            bi = l;
+            bval = true;
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double ov = __shfl_xor(bv, d);
+        const int oi = __shfl_xor(bi, d);
+        const bool oval = __shfl_xor((int)bval, d) != 0;
+        const bool better = oval && (!bval || ov > bv || (ov == bv && oi < bi));
+        if (better) {
+            bv = ov;
+            bi = oi;
+            bval = true;
+        }
+    }
+    const double s0 = rdlaned(acc[0], 0);
+    const int label = (!bval || __builtin_isnan(s0)) ? 0 : bi;
+    if (lane == 0) p.labels[doc] = label;
+    if (p.scores) {
+        double* out = p.scores + doc * (int64_t)p.L;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int l = s * 64 + lane;
+            if (l < p.L) out[l] = acc[s];
+        }
+    }
+}
+
+__device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) { return (int64_t)rdlane64((uint64_t)v, l); }
+
+// Issue the two 16-B-per-lane buffer loads of a group's bytes [s0, s0 + kBufBytes)
+// (range-checked: bytes past n_bytes read as 0, never fault).
+__device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int lane, uint4& r0, uint4& r1) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(p.bytes + s0));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)(p.bytes + s0) >> 32));
+    const int64_t left = p.n_bytes - s0;
+    const uint32_t nrec =
+        __builtin_amdgcn_readfirstlane((uint32_t)(left < 0 ? 0 : (left > 0x7fffffff ? 0x7fffffff : left)));
+    void* base = (void*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)nrec, 0x00020000);
+    r0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0));
+    r1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 1024 + 16 * lane, 0, 0));
+}
+
 template <int S, bool DENSE, bool FLDS>
 __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -255,103 +388,48 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * (S + 1);
+    wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 2 * (S + 1) + wave * kBufWords;
 
-    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
-    const int64_t stride = (int64_t)gridDim.x * kScoreWaves;
-    int64_t doc = (int64_t)blockIdx.x * kScoreWaves + wave;
-    if (doc >= p.n_docs) return;
+    // this wave's contiguous range of documents, walked in groups of p.group
+    const int64_t nwaves = (int64_t)gridDim.x * kScoreWaves;
+    const int64_t wg = (int64_t)blockIdx.x * kScoreWaves + wave;
+    const int64_t dbeg = (int64_t)((__int128)p.n_docs * wg / nwaves);
+    const int64_t dend = (int64_t)((__int128)p.n_docs * (wg + 1) / nwaves);
+    if (dbeg >= dend) return;
+    const int G = p.group;
 
-    // prefetch of the first document
-    int64_t nb = p.offsets[doc];
-    int64_t nlen = p.offsets[doc + 1] - nb;
-    SbWords nxt;
-    load_sb(W, nb, lane, p.last_dword, nxt);
+    // lane i <= G holds offsets[g0 + i] of the current group (clamped to dend)
+    int64_t g0 = dbeg;
+    int64_t offv = p.offsets[min(g0 + (int64_t)min(lane, G), dend)];
+    uint4 r0, r1;
+    group_load(p, rdlane_i64(offv, 0) & ~(int64_t)15, lane, r0, r1);
 
-    for (; doc < p.n_docs; doc += stride) {
-        const int64_t b = nb, len = nlen;
-        const SbWords cur = nxt;
-        const int64_t next = doc + stride;
-        if (next < p.n_docs) {
-            nb = p.offsets[next];
-            nlen = p.offsets[next + 1] - nb;
-            load_sb(W, nb, lane, p.last_dword, nxt);
+    while (g0 < dend) {
+        const int64_t g1 = min(g0 + (int64_t)G, dend);
+        const int cnt = (int)(g1 - g0);
+        // offsets of the next group (hidden behind this group's work)
+        const int64_t n1 = min(g1 + (int64_t)G, dend);
+        const int64_t offn = p.offsets[min(g1 + (int64_t)min(lane, G), n1)];
+        const int64_t s0 = rdlane_i64(offv, 0) & ~(int64_t)15;
+        const int64_t send = rdlane_i64(offv, cnt);
+        const bool staged = send - s0 <= kBufBytes;
+        if (staged) {
+            reinterpret_cast<uint4*>(wl.buf)[lane] = r0;
+            reinterpret_cast<uint4*>(wl.buf)[64 + lane] = r1;
         }
-        double acc[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) acc[s] = 0.0;
-        int qn = 0;
-        if (len >= kMaxDocBytes) {
-            if (lane == 0) atomicOr(p.err, 2);
-        } else if (len <= 64 * kSub) {
-            // one superblock: every gram length reuses the same window bytes
-            Windows x;
-            windows_of(cur, b, lane, x);
-            for (int gi = 0; gi < p.nG; ++gi) {
-                const GramCtx g = gram_ctx(len, p.G[gi]);
-                if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
-                if (qn > kQueueCap - 64 * kSub) {
-                    flush<S, DENSE>(p, wl, qn, b, W, acc, lane);
-                    qn = 0;
-                }
-                probe_sb(p, lds, bloom, wl.queue, qn, g, x, 0, lane);
-            }
-        } else {
-            // long documents: n outer (reference order), superblocks inner
-            for (int gi = 0; gi < p.nG; ++gi) {
-                const GramCtx g = gram_ctx(len, p.G[gi]);
-                if (!((p.len_mask >> g.klen) & 1u)) continue;
-                for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
-                    SbWords r;
-                    load_sb(W, b + p0, lane, p.last_dword, r);
-                    Windows x;
-                    windows_of(r, b + p0, lane, x);
-                    if (qn > kQueueCap - 64 * kSub) {
-                        flush<S, DENSE>(p, wl, qn, b, W, acc, lane);
-                        qn = 0;
-                    }
-                    probe_sb(p, lds, bloom, wl.queue, qn, g, x, p0, lane);
-                }
-            }
+        __builtin_amdgcn_wave_barrier();
+        if (g1 < dend) group_load(p, send & ~(int64_t)15, lane, r0, r1);  // next group's bytes
+        for (int i = 0; i < cnt; ++i) {
+            const int64_t b = rdlane_i64(offv, i);
+            const int64_t len = rdlane_i64(offv, i + 1) - b;
+            DocSrc src;
+            src.lds = staged ? wl.buf : nullptr;
+            src.base = staged ? b - s0 : b;
+            score_doc<S, DENSE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
         }
-        if (qn) flush<S, DENSE>(p, wl, qn, b, W, acc, lane);
-
-        // argmax (breeze: first element, then strict '>' updates)
-        double bv = acc[0];
-        int bi = lane;
-        bool bval = lane < p.L && !__builtin_isnan(bv);
-#pragma unroll
-        for (int s = 1; s < S; ++s) {
-            const int l = s * 64 + lane;
-            const double v = acc[s];
-            if (l < p.L && !__builtin_isnan(v) && (!bval || v > bv)) {
-                bv = v;
-                bi = l;
-                bval = true;
-            }
-        }
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const double ov = __shfl_xor(bv, d);
-            const int oi = __shfl_xor(bi, d);
-            const bool oval = __shfl_xor((int)bval, d) != 0;
-            const bool better = oval && (!bval || ov > bv || (ov == bv && oi < bi));
-            if (better) {
-                bv = ov;
-                bi = oi;
-                bval = true;
-            }
-        }
-        const double s0 = rdlaned(acc[0], 0);
-        const int label = (!bval || __builtin_isnan(s0)) ? 0 : bi;
-        if (lane == 0) p.labels[doc] = label;
-        if (p.scores) {
-            double* out = p.scores + doc * (int64_t)p.L;
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const int l = s * 64 + lane;
-                if (l < p.L) out[l] = acc[s];
-            }
-        }
+        __builtin_amdgcn_wave_barrier();
+        offv = offn;
+        g0 = g1;
     }
 }
 
