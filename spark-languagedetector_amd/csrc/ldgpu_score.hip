@@ -362,9 +362,10 @@ __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) { return (int64_
 __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int lane, uint4& r0, uint4& r1) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(p.bytes + s0));
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)(p.bytes + s0) >> 32));
-    const int64_t left = p.n_bytes - s0;
+    // whole dwords: the range check zeroes a dword with ANY byte past the end
+    const int64_t left = ((p.n_bytes + 3) & ~(int64_t)3) - s0;
     const uint32_t nrec =
-        __builtin_amdgcn_readfirstlane((uint32_t)(left < 0 ? 0 : (left > 0x7fffffff ? 0x7fffffff : left)));
+        __builtin_amdgcn_readfirstlane((uint32_t)(left < 0 ? 0 : (left > 0x7ffffff0 ? 0x7ffffff0 : left)));
     void* base = (void*)(((uint64_t)hi << 32) | lo);
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)nrec, 0x00020000);
     r0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0));
