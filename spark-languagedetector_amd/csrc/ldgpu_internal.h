@@ -33,7 +33,7 @@ struct ScoreParams {
 };
 
 // Launch configuration of the score kernel.
-constexpr int kScoreWaves = 10;            // waves per workgroup (640 threads)
+constexpr int kScoreWaves = 8;             // waves per workgroup (512 threads)
 constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
 constexpr int kBufBytes = 2048;            // staged bytes of a document group per wave
 constexpr int kBufWords = kBufBytes / 4 + 4;

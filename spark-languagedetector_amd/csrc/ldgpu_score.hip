@@ -112,11 +112,12 @@ struct DocSrc {
     int64_t base;
 };
 
+template <bool STAGED>
 __device__ __forceinline__ void window_words(const ScoreParams& p, const DocSrc& src, int64_t pos, uint32_t& w0,
                                              uint32_t& w1, uint32_t& w2, uint32_t& sh) {
     const int64_t a = src.base + pos;
     sh = (uint32_t)(a & 3);
-    if (src.lds) {
+    if constexpr (STAGED) {
         const uint32_t i = (uint32_t)(a >> 2);
         w0 = src.lds[i];
         w1 = src.lds[i + 1];
@@ -131,7 +132,7 @@ __device__ __forceinline__ void window_words(const ScoreParams& p, const DocSrc&
 }
 
 // Verify + accumulate the queued candidates (in queue order).
-template <int S, bool DENSE>
+template <int S, bool DENSE, bool STAGED>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
                                       double (&acc)[S], int lane) {
     __builtin_amdgcn_wave_barrier();
@@ -144,7 +145,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             const uint32_t e = w.queue[j];
             const int klen = (int)(e >> kPosBits);
             uint32_t w0, w1, w2, sh;
-            window_words(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
+            window_words<STAGED>(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
             uint64_t key = __builtin_amdgcn_alignbyte(w1, w0, sh);
             if (klen > 4) {
                 const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
@@ -188,7 +189,22 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             }
             __builtin_amdgcn_wave_barrier();
             const int nh = __popcll(hits);
-            for (int t = 0; t < nh; ++t) {
+            int t = 0;
+            // 4 broadcast reads in flight, then 4 ordered adds
+            for (; t + 4 <= nh; t += 4) {
+                uint64_t e[4][S + 1];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int s = 0; s <= S; ++s) e[u][s] = w.hits[(t + u) * (S + 1) + s];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double vv = __longlong_as_double((long long)e[u][0]);
+#pragma unroll
+                    for (int s = 0; s < S; ++s) acc[s] = acc[s] + (((e[u][1 + s] >> lane) & 1ull) ? vv : 0.0);
+                }
+            }
+            for (; t < nh; ++t) {
                 const uint64_t* h = w.hits + t * (S + 1);
                 const double vv = __longlong_as_double((long long)h[0]);
 #pragma unroll
@@ -263,7 +279,7 @@ __device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* i
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
-template <int S, bool DENSE>
+template <int S, bool DENSE, bool STAGED>
 __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                           const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
                                           const DocSrc& src, int lane) {
@@ -279,7 +295,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
 #pragma unroll
         for (int k = 0; k < kSub; ++k) {
             uint32_t w0, w1, w2, sh;
-            window_words(p, src, 64 * k + lane, w0, w1, w2, sh);
+            window_words<STAGED>(p, src, 64 * k + lane, w0, w1, w2, sh);
             x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
             x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
         }
@@ -287,7 +303,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
             const GramCtx g = gram_ctx(len, p.G[gi]);
             if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
             if (qn > kQueueCap - 64 * kSub) {
-                flush<S, DENSE>(p, wl, qn, src, acc, lane);
+                flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
                 qn = 0;
             }
             probe_sb(p, img, bloom, wl.queue, qn, g, x, 0, lane);
@@ -302,19 +318,19 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
 #pragma unroll
                 for (int k = 0; k < kSub; ++k) {
                     uint32_t w0, w1, w2, sh;
-                    window_words(p, src, p0 + 64 * k + lane, w0, w1, w2, sh);
+                    window_words<STAGED>(p, src, p0 + 64 * k + lane, w0, w1, w2, sh);
                     x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
                     x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
                 }
                 if (qn > kQueueCap - 64 * kSub) {
-                    flush<S, DENSE>(p, wl, qn, src, acc, lane);
+                    flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
                     qn = 0;
                 }
                 probe_sb(p, img, bloom, wl.queue, qn, g, x, p0, lane);
             }
         }
     }
-    if (qn) flush<S, DENSE>(p, wl, qn, src, acc, lane);
+    if (qn) flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
 
     // argmax (breeze: first element, then strict '>' updates)
     double bv = acc[0];
@@ -420,13 +436,20 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
         }
         __builtin_amdgcn_wave_barrier();
         if (g1 < dend) group_load(p, send & ~(int64_t)15, lane, r0, r1);  // next group's bytes
-        for (int i = 0; i < cnt; ++i) {
-            const int64_t b = rdlane_i64(offv, i);
-            const int64_t len = rdlane_i64(offv, i + 1) - b;
-            DocSrc src;
-            src.lds = staged ? wl.buf : nullptr;
-            src.base = staged ? b - s0 : b;
-            score_doc<S, DENSE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+        if (staged) {
+            for (int i = 0; i < cnt; ++i) {
+                const int64_t b = rdlane_i64(offv, i);
+                const int64_t len = rdlane_i64(offv, i + 1) - b;
+                const DocSrc src{wl.buf, b - s0};
+                score_doc<S, DENSE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+            }
+        } else {
+            for (int i = 0; i < cnt; ++i) {
+                const int64_t b = rdlane_i64(offv, i);
+                const int64_t len = rdlane_i64(offv, i + 1) - b;
+                const DocSrc src{nullptr, b};
+                score_doc<S, DENSE, false>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+            }
         }
         __builtin_amdgcn_wave_barrier();
         offv = offn;

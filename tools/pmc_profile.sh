@@ -18,6 +18,7 @@ PASSES=(
 i=0
 for pass in "${PASSES[@]}"; do
   i=$((i+1))
+  if [ -n "${ONLY:-}" ] && [[ " $ONLY " != *" $i "* ]]; then continue; fi
   echo "== pass $i: $pass"
   timeout -s KILL 240 rocprofv3 --pmc $pass --output-format csv -d "$PWD/$OUT/pass$i" -o run -- python3 bench.py "$@" > "$OUT/pass$i.log" 2>&1
   rc=$?
