@@ -35,7 +35,7 @@ struct ScoreParams {
 // Launch configuration of the score kernel.
 constexpr int kScoreWaves = 8;             // waves per workgroup (512 threads)
 constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
-constexpr int kBufBytes = 2048;            // staged bytes of a document group per wave
+constexpr int kBufBytes = 1024;            // staged bytes of a document group per wave
 constexpr int kBufWords = kBufBytes / 4 + 4;
 constexpr int kMaxLdsBloomLog2 = 14;       // bloom words in LDS up to 64 KiB
 constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
@@ -43,7 +43,7 @@ constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
 // bytes of dynamic LDS the score kernel needs
 inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) {
     return (size_t)(kBloomBase + (lds_bloom ? bloom_words : 0u)) * 4u +
-           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 8u * (slices + 1u) + kBufWords * 4u);
+           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + kBufWords * 4u);
 }
 
 // slices = ceil(L / 64); dense = general fp64 rows; lds_bloom = bloom staged in LDS

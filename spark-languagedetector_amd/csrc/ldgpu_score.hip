@@ -131,6 +131,51 @@ __device__ __forceinline__ void window_words(const ScoreParams& p, const DocSrc&
     }
 }
 
+// Max over the wave of a non-NaN double, by DPP row shifts / broadcasts (no
+// LDS traffic); the result is read from lane 63 and is wave-uniform.
+__device__ __forceinline__ double dpp_max_step_impl(double v, int olo, int ohi) {
+    const double o = __hiloint2double(ohi, olo);
+    double r;
+    asm volatile("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(v), "v"(o));
+    return r;
+}
+#define LDGPU_DPP_MAX(v, CTRL, RM)                                                                      \
+    do {                                                                                                \
+        const int lo_ = __double2loint(v), hi_ = __double2hiint(v);                                   \
+        const int olo_ = __builtin_amdgcn_update_dpp(0, lo_, CTRL, RM, 0xf, false);                     \
+        const int ohi_ = __builtin_amdgcn_update_dpp((int)0xfff00000, hi_, CTRL, RM, 0xf, false);       \
+        v = dpp_max_step_impl(v, olo_, ohi_);                                                           \
+    } while (0)
+
+__device__ __forceinline__ double wave_max_f64(double v) {
+    LDGPU_DPP_MAX(v, 0x111, 0xf);  // row_shr:1
+    LDGPU_DPP_MAX(v, 0x112, 0xf);  // row_shr:2
+    LDGPU_DPP_MAX(v, 0x114, 0xf);  // row_shr:4
+    LDGPU_DPP_MAX(v, 0x118, 0xf);  // row_shr:8
+    LDGPU_DPP_MAX(v, 0x142, 0xa);  // row_bcast:15
+    LDGPU_DPP_MAX(v, 0x143, 0xc);  // row_bcast:31
+    return rdlaned(v, 63);
+}
+
+// One verified hit as LDS quads: {value, mask word 0}, {mask 1, mask 2}, ...
+template <int S>
+constexpr int kHitQuads = (S + 2) / 2;
+
+// s_l = s_l + (bit l of the hit's mask ? value : 0.0) -- exact: x + 0.0 == x
+// because no accumulator is ever -0.0.
+template <int S>
+__device__ __forceinline__ void hit_add(const uint4 (&e)[kHitQuads<S>], double (&acc)[S], int lane) {
+    const double vv = __hiloint2double((int)e[0].y, (int)e[0].x);
+    const int half = lane >> 5, bit = lane & 31;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int w = 2 * (1 + s) + half;  // 32-bit word of mask s holding this lane's bit
+        const uint32_t mw = (w & 3) == 0 ? e[w >> 2].x : (w & 3) == 1 ? e[w >> 2].y : (w & 3) == 2 ? e[w >> 2].z
+                                                                                                  : e[w >> 2].w;
+        acc[s] = acc[s] + (((mw >> bit) & 1u) ? vv : 0.0);
+    }
+}
+
 // Verify + accumulate the queued candidates (in queue order).
 template <int S, bool DENSE, bool STAGED>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
@@ -176,39 +221,44 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         const uint64_t hits = __ballot(good);
         if (!hits) continue;
         if constexpr (!DENSE) {
-            // compact the hits into LDS in queue order, then every lane (one
-            // language each) replays them with broadcast reads
+            // compact the hits into LDS in queue order (entry: value, mask
+            // words; 16-B aligned), then every lane (one language each)
+            // replays them with broadcast ds_read_b128
+            constexpr int kQ = kHitQuads<S>;  // uint4 per entry
+            uint4* hq = reinterpret_cast<uint4*>(w.hits);
             if (good) {
                 const uint32_t off =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(hits >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hits, 0u));
-                uint64_t* h = w.hits + off * (S + 1);
-                h[0] = (uint64_t)__double_as_longlong(v);
-                h[1] = m0;
+                uint64_t words[2 * kQ];
+                words[0] = (uint64_t)__double_as_longlong(v);
+                words[1] = m0;
 #pragma unroll
-                for (int s = 1; s < S; ++s) h[1 + s] = p.masks[(size_t)row * S + s];
+                for (int s = 1; s < S; ++s) words[1 + s] = p.masks[(size_t)row * S + s];
+#pragma unroll
+                for (int s = S + 1; s < 2 * kQ; ++s) words[s] = 0;
+#pragma unroll
+                for (int q = 0; q < kQ; ++q)
+                    hq[off * kQ + q] = make_uint4((uint32_t)words[2 * q], (uint32_t)(words[2 * q] >> 32),
+                                                  (uint32_t)words[2 * q + 1], (uint32_t)(words[2 * q + 1] >> 32));
             }
             __builtin_amdgcn_wave_barrier();
             const int nh = __popcll(hits);
             int t = 0;
             // 4 broadcast reads in flight, then 4 ordered adds
             for (; t + 4 <= nh; t += 4) {
-                uint64_t e[4][S + 1];
+                uint4 e[4][kQ];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
 #pragma unroll
-                    for (int s = 0; s <= S; ++s) e[u][s] = w.hits[(t + u) * (S + 1) + s];
+                    for (int q = 0; q < kQ; ++q) e[u][q] = hq[(t + u) * kQ + q];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const double vv = __longlong_as_double((long long)e[u][0]);
-#pragma unroll
-                    for (int s = 0; s < S; ++s) acc[s] = acc[s] + (((e[u][1 + s] >> lane) & 1ull) ? vv : 0.0);
-                }
+                for (int u = 0; u < 4; ++u) hit_add<S>(e[u], acc, lane);
             }
             for (; t < nh; ++t) {
-                const uint64_t* h = w.hits + t * (S + 1);
-                const double vv = __longlong_as_double((long long)h[0]);
+                uint4 e[kQ];
 #pragma unroll
-                for (int s = 0; s < S; ++s) acc[s] = acc[s] + (((h[1 + s] >> lane) & 1ull) ? vv : 0.0);
+                for (int q = 0; q < kQ; ++q) e[q] = hq[t * kQ + q];
+                hit_add<S>(e, acc, lane);
             }
             __builtin_amdgcn_wave_barrier();
         } else {
@@ -332,34 +382,27 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
     }
     if (qn) flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
 
-    // argmax (breeze: first element, then strict '>' updates)
-    double bv = acc[0];
-    int bi = lane;
-    bool bval = lane < p.L && !__builtin_isnan(bv);
+    // argmax (breeze: first element, then strict '>' updates): the wave max M
+    // of the non-NaN scores by DPP (no LDS), then the first index holding M;
+    // a NaN first score keeps index 0.
+    double lv = -__builtin_inf();
 #pragma unroll
-    for (int s = 1; s < S; ++s) {
+    for (int s = 0; s < S; ++s) {
         const int l = s * 64 + lane;
-        const double v = acc[s];
-        if (l < p.L && !__builtin_isnan(v) && (!bval || v > bv)) {
-            bv = v;
-            bi = l;
-            bval = true;
-        }
+        if (l < p.L && !__builtin_isnan(acc[s]) && acc[s] > lv) lv = acc[s];
     }
+    const double M = wave_max_f64(lv);
+    int label = 0;
+    bool found = false;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const double ov = __shfl_xor(bv, d);
-        const int oi = __shfl_xor(bi, d);
-        const bool oval = __shfl_xor((int)bval, d) != 0;
-        const bool better = oval && (!bval || ov > bv || (ov == bv && oi < bi));
-        if (better) {
-            bv = ov;
-            bi = oi;
-            bval = true;
+    for (int s = 0; s < S; ++s) {
+        const uint64_t b = __ballot(s * 64 + lane < p.L && acc[s] == M);
+        if (!found && b) {
+            label = s * 64 + __builtin_ctzll(b);
+            found = true;
         }
     }
-    const double s0 = rdlaned(acc[0], 0);
-    const int label = (!bval || __builtin_isnan(s0)) ? 0 : bi;
+    if (__builtin_isnan(rdlaned(acc[0], 0))) label = 0;
     if (lane == 0) p.labels[doc] = label;
     if (p.scores) {
         double* out = p.scores + doc * (int64_t)p.L;
@@ -373,9 +416,9 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
 
 __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) { return (int64_t)rdlane64((uint64_t)v, l); }
 
-// Issue the two 16-B-per-lane buffer loads of a group's bytes [s0, s0 + kBufBytes)
+// Issue the 16-B-per-lane buffer load of a group's bytes [s0, s0 + kBufBytes)
 // (range-checked: bytes past n_bytes read as 0, never fault).
-__device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int lane, uint4& r0, uint4& r1) {
+__device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int lane, uint4& r0) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(p.bytes + s0));
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)(p.bytes + s0) >> 32));
     // whole dwords: the range check zeroes a dword with ANY byte past the end
@@ -385,7 +428,6 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
     void* base = (void*)(((uint64_t)hi << 32) | lo);
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)nrec, 0x00020000);
     r0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0));
-    r1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 1024 + 16 * lane, 0, 0));
 }
 
 template <int S, bool DENSE, bool FLDS>
@@ -404,8 +446,8 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
     const uint32_t* bloom = FLDS ? lds + kBloomBase : p.filter + kBloomBase;
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
-    wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * (S + 1);
-    wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 2 * (S + 1) + wave * kBufWords;
+    wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * 2 * kHitQuads<S>;
+    wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 4 * kHitQuads<S> + wave * kBufWords;
 
     // this wave's contiguous range of documents, walked in groups of p.group
     const int64_t nwaves = (int64_t)gridDim.x * kScoreWaves;
@@ -418,8 +460,8 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
     // lane i <= G holds offsets[g0 + i] of the current group (clamped to dend)
     int64_t g0 = dbeg;
     int64_t offv = p.offsets[min(g0 + (int64_t)min(lane, G), dend)];
-    uint4 r0, r1;
-    group_load(p, rdlane_i64(offv, 0) & ~(int64_t)15, lane, r0, r1);
+    uint4 r0;
+    group_load(p, rdlane_i64(offv, 0) & ~(int64_t)15, lane, r0);
 
     while (g0 < dend) {
         const int64_t g1 = min(g0 + (int64_t)G, dend);
@@ -430,12 +472,9 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
         const int64_t s0 = rdlane_i64(offv, 0) & ~(int64_t)15;
         const int64_t send = rdlane_i64(offv, cnt);
         const bool staged = send - s0 <= kBufBytes;
-        if (staged) {
-            reinterpret_cast<uint4*>(wl.buf)[lane] = r0;
-            reinterpret_cast<uint4*>(wl.buf)[64 + lane] = r1;
-        }
+        if (staged) reinterpret_cast<uint4*>(wl.buf)[lane] = r0;
         __builtin_amdgcn_wave_barrier();
-        if (g1 < dend) group_load(p, send & ~(int64_t)15, lane, r0, r1);  // next group's bytes
+        if (g1 < dend) group_load(p, send & ~(int64_t)15, lane, r0);  // next group's bytes
         if (staged) {
             for (int i = 0; i < cnt; ++i) {
                 const int64_t b = rdlane_i64(offv, i);
