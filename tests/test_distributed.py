@@ -1,0 +1,116 @@
+"""Multi-process paths (world size 2, gloo on 127.0.0.1): the FIT count merge
+(all_gather of key lists + all_reduce of dense counts) and sharded scoring.
+CPU tests feed the merge with the C oracle's per-shard counts; the gpu test
+runs the whole fit_distributed on cuda:0 from two ranks."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    for p in (os.path.join(ROOT, "spark-languagedetector_amd"), os.path.join(ROOT, "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _corpus():
+    from languagedetection import synth
+    ls = synth.make_languages(6, seed=21)
+    return ls, synth.generate(ls, 500, 0, 300, seed=22)
+
+
+def _merge_worker(rank, world, port, out_dir):
+    dist = _init(rank, world, port)
+    import ldoracle_c as OC
+    from languagedetection.distributed import merge_counts, shard_range
+    ls, (data, off, lang) = _corpus()
+    lo, hi = shard_range(len(off) - 1, rank, world)
+    sub_off = off[lo:hi + 1] - off[lo]
+    sub = data[off[lo]:off[hi]]
+    keys, cnt = OC.count(sub, sub_off, lang[lo:hi], 6, [1, 2, 3])
+    gk, gc = merge_counts(keys, cnt, 6)
+    np.save(os.path.join(out_dir, f"counts{rank}.npy"), gc)
+    with open(os.path.join(out_dir, f"keys{rank}.bin"), "wb") as f:
+        for k in gk:
+            f.write(bytes([len(k)]) + k)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _read_keys(path):
+    b = open(path, "rb").read()
+    out, i = [], 0
+    while i < len(b):
+        n = b[i]
+        out.append(b[i + 1:i + 1 + n])
+        i += 1 + n
+    return out
+
+
+def test_merge_counts_two_ranks(tmp_path):
+    import ldoracle_c as OC
+    mp.spawn(_merge_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    ls, (data, off, lang) = _corpus()
+    keys, cnt = OC.count(data, off, lang, 6, [1, 2, 3])
+    for r in range(2):
+        assert _read_keys(os.path.join(tmp_path, f"keys{r}.bin")) == keys
+        assert np.array_equal(np.load(os.path.join(tmp_path, f"counts{r}.npy")), cnt)
+
+
+def test_sort_keys_roundtrip_and_order():
+    from languagedetection.distributed import keys_of, shard_range, sort_keys
+    ks = [b"b", b"a", b"ab", b"\xff", b"zzzzzzz", b"\x00\x01"]
+    codes = sort_keys(ks)
+    assert keys_of(codes) == ks
+    order = [ks[i] for i in np.argsort(codes, kind="stable")]
+    assert order == sorted(ks, key=lambda k: (len(k), k))
+    cover = [shard_range(10, r, 3) for r in range(3)]
+    assert cover == [(0, 3), (3, 6), (6, 10)]
+
+
+def _fit_worker(rank, world, port, out_dir):
+    dist = _init(rank, world, port)
+    from languagedetection import synth
+    from languagedetection.distributed import fit_distributed, shard_range
+    ls, (data, off, lang) = _corpus()
+    rows = list(zip([ls.names[i] for i in lang], synth.texts(data, off)))
+    lo, hi = shard_range(len(rows), rank, world)
+    table = fit_distributed(rows[lo:hi], ls.names, [1, 2, 3], 80, device=0)
+    import json
+    with open(os.path.join(out_dir, f"table{rank}.json"), "w") as f:
+        json.dump({k.hex(): v for k, v in table.items()}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_fit_distributed_matches_single_process(tmp_path):
+    import json
+    import ldoracle as O
+    from languagedetection import synth
+    mp.spawn(_fit_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    ls, (data, off, lang) = _corpus()
+    rows = list(zip([ls.names[i] for i in lang], synth.texts(data, off)))
+    expect = O.filter_top_grams(O.fit_probabilities(rows, ls.names, [1, 2, 3]), ls.names, 80)
+    for r in range(2):
+        got = {bytes.fromhex(k): v for k, v in json.load(open(os.path.join(tmp_path, f"table{r}.json"))).items()}
+        assert got == expect
