@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -178,6 +179,7 @@ struct ldgpu_model {
     int32_t G[kMaxGramLengths] = {};
     int slices = 1;
     bool dense = false;
+    int mode = 0;             // kernel mode: 0 mask, 1 mask + finite values, 2 dense
     bool lds_filter = true;
     bool has_bad = false;
     int64_t n_keys = 0;
@@ -285,6 +287,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
 
     std::vector<uint64_t> masks;
     std::vector<double> vals, drows;
+    m->mode = dense ? 2 : 1;
     if (!dense) {
         masks.assign((size_t)nk * S, 0);
         vals.assign((size_t)nk, 0.0);
@@ -294,6 +297,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
                 if (rw[l] == 0.0) continue;
                 masks[(size_t)i * S + l / 64] |= 1ull << (l % 64);
                 vals[i] = rw[l];
+                if (!std::isfinite(rw[l])) m->mode = 0;
             }
         }
     } else {
@@ -360,9 +364,15 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
     m->lds_bytes = score_lds_bytes(S, m->lds_filter, (uint32_t)bwords);
     int resident = 0;
-    if (e == hipSuccess) e = score_prepare(S, dense, m->lds_filter, m->lds_bytes, &resident);
+    if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->lds_bytes, &resident);
     // persistent grid = what is resident; never more workgroups than the LDS admits
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
+    if (const char* ov = getenv("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
+    if (getenv("LDGPU_DEBUG"))
+        fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
+                        "resident_api=%d wg_per_cu=%d\n",
+                (long long)nk, m->mode, S, (unsigned long long)bwords, (int)m->lds_filter, m->lds_bytes, resident,
+                m->wg_per_cu);
     if (e != hipSuccess) {
         model_free(m);
         return fail(e == hipErrorOutOfMemory ? LDGPU_ENOMEM : LDGPU_EDEVICE, "model upload: %s",
@@ -420,7 +430,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
     const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
-    HIP_TRY(launch_score(p, m->slices, m->dense, m->lds_filter, grid, st));
+    HIP_TRY(launch_score(p, m->slices, m->mode, m->lds_filter, grid, st));
     return LDGPU_OK;
 }
 

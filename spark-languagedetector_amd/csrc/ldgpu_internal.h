@@ -46,11 +46,11 @@ inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) 
            (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + kBufWords * 4u);
 }
 
-// slices = ceil(L / 64); dense = general fp64 rows; lds_bloom = bloom staged in LDS
-hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_bloom, int grid,
-                        hipStream_t stream);
+// slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values
+// (fma accumulate), 2 = dense fp64 rows; lds_bloom = bloom staged in LDS
+hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream);
 // sets the dynamic-LDS limit and returns the resident workgroups per CU
-hipError_t score_prepare(int slices, bool dense, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu);
+hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu);
 
 // -------------------------------------------------------------------- FIT
 struct CountParams {

@@ -162,22 +162,31 @@ template <int S>
 constexpr int kHitQuads = (S + 2) / 2;
 
 // s_l = s_l + (bit l of the hit's mask ? value : 0.0) -- exact: x + 0.0 == x
-// because no accumulator is ever -0.0.
-template <int S>
+// because no accumulator is ever -0.0.  FIN (every table value finite):
+// s_l = fma(value, bit, s_l), where value * 1.0 and value * 0.0 are exact, so
+// the single rounding is that of s_l + value (or of s_l + 0.0 == s_l).
+template <int S, bool FIN>
 __device__ __forceinline__ void hit_add(const uint4 (&e)[kHitQuads<S>], double (&acc)[S], int lane) {
-    const double vv = __hiloint2double((int)e[0].y, (int)e[0].x);
-    const int half = lane >> 5, bit = lane & 31;
+    const double vv = __longlong_as_double((long long)(((uint64_t)e[0].y << 32) | e[0].x));
+    const bool upper = lane >= 32;
+    const uint32_t bit = (uint32_t)lane & 31u;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        const int w = 2 * (1 + s) + half;  // 32-bit word of mask s holding this lane's bit
-        const uint32_t mw = (w & 3) == 0 ? e[w >> 2].x : (w & 3) == 1 ? e[w >> 2].y : (w & 3) == 2 ? e[w >> 2].z
-                                                                                                  : e[w >> 2].w;
-        acc[s] = acc[s] + (((mw >> bit) & 1u) ? vv : 0.0);
+        const int w = 2 * (1 + s);  // 32-bit words w, w + 1 hold mask s
+        const uint4& q = e[w >> 2];
+        const uint32_t lo = (w & 3) == 0 ? q.x : q.z;
+        const uint32_t hi = (w & 3) == 0 ? q.y : q.w;
+        const uint32_t b = ((upper ? hi : lo) >> bit) & 1u;
+        if constexpr (FIN) {
+            acc[s] = __builtin_fma(vv, (double)b, acc[s]);
+        } else {
+            acc[s] = acc[s] + (b ? vv : 0.0);
+        }
     }
 }
 
 // Verify + accumulate the queued candidates (in queue order).
-template <int S, bool DENSE, bool STAGED>
+template <int S, int MODE, bool STAGED>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
                                       double (&acc)[S], int lane) {
     __builtin_amdgcn_wave_barrier();
@@ -220,6 +229,8 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         const bool good = hit && !bad;
         const uint64_t hits = __ballot(good);
         if (!hits) continue;
+        constexpr bool DENSE = MODE == 2;
+        constexpr bool FIN = MODE == 1;
         if constexpr (!DENSE) {
             // compact the hits into LDS in queue order (entry: value, mask
             // words; 16-B aligned), then every lane (one language each)
@@ -252,13 +263,13 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
 #pragma unroll
                     for (int q = 0; q < kQ; ++q) e[u][q] = hq[(t + u) * kQ + q];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) hit_add<S>(e[u], acc, lane);
+                for (int u = 0; u < 4; ++u) hit_add<S, FIN>(e[u], acc, lane);
             }
             for (; t < nh; ++t) {
                 uint4 e[kQ];
 #pragma unroll
                 for (int q = 0; q < kQ; ++q) e[q] = hq[t * kQ + q];
-                hit_add<S>(e, acc, lane);
+                hit_add<S, FIN>(e, acc, lane);
             }
             __builtin_amdgcn_wave_barrier();
         } else {
@@ -278,58 +289,70 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
     }
 }
 
-// Filter-test the (up to) 256 windows of one superblock for one gram length
-// and append the candidates to the queue in position order.  The caller
-// guarantees qn <= kQueueCap - 256.  1- and 2-byte keys test exact LDS
-// bitmaps; longer keys a blocked Bloom filter.
-__device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* img, const uint32_t* bloom,
-                                         uint32_t* queue, int& qn, const GramCtx& g, const Windows& x, int32_t p0,
-                                         int lane) {
-    bool cand[kSub];
-    const int32_t nw = g.nwin - p0;  // windows left from p0 (> 0)
-    if (g.klen <= 2) {
-        const uint32_t base = g.klen == 1 ? 0u : kBmp1Words;
-        uint32_t idx[kSub], word[kSub];
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            idx[k] = x.lo[k] & g.lomask;
-            word[k] = img[base + (idx[k] >> 5)];
-        }
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) cand[k] = (64 * k + lane < nw) & ((word[k] >> (idx[k] & 31u)) & 1u);
-    } else {
-        uint32_t h[kSub], word[kSub];
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            const uint32_t lo = x.lo[k] & g.lomask;
-            const uint32_t himix = g.klen > 4 ? hi_mix(g.hitag | (x.hi[k] & g.himask)) : g.himix_c;
-            h[k] = filter_hash(lo, himix);
-            word[k] = bloom[h[k] >> p.bloom_shift];
-        }
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            const uint32_t fb = filter_bits(h[k], p.bloom_shift);
-            cand[k] = (64 * k + lane < nw) & ((word[k] & fb) == fb);
-        }
-    }
-    uint64_t m[kSub];
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) m[k] = __ballot(cand[k]);
-    if ((m[0] | m[1] | m[2] | m[3]) == 0) return;
-    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)(p0 + lane);
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        if (m[k]) {
-            const uint32_t off =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            if (cand[k]) queue[qn + off] = tag + 64u * k;
-            qn += __popcll(m[k]);
-        }
+// Append one sub-block's candidates (pred) to the queue in lane order.
+__device__ __forceinline__ void append(uint32_t* queue, int& qn, bool pred, uint32_t tag) {
+    const uint64_t m = __ballot(pred);
+    if (m) {
+        const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (pred) queue[qn + off] = tag;
+        qn += __popcll(m);
     }
 }
 
+// 1- and 2-byte keys: exact LDS bitmaps.
+__device__ __forceinline__ void probe_direct(const uint32_t* img, uint32_t* queue, int& qn, const GramCtx& g,
+                                             const Windows& x, int32_t p0, int lane) {
+    const int32_t nw = g.nwin - p0;  // windows left from p0 (> 0)
+    const uint32_t base = g.klen == 1 ? 0u : kBmp1Words;
+    uint32_t idx[kSub], word[kSub];
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        idx[k] = x.lo[k] & g.lomask;
+        word[k] = img[base + (idx[k] >> 5)];
+    }
+    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)(p0 + lane);
+#pragma unroll
+    for (int k = 0; k < kSub; ++k)
+        append(queue, qn, (64 * k + lane < nw) && ((word[k] >> (idx[k] & 31u)) & 1u), tag + 64u * k);
+}
+
+// 3..7-byte keys: one multiply (two when BIG: 5..7 bytes), blocked Bloom.
+template <bool BIG>
+__device__ __forceinline__ void probe_bloom(const ScoreParams& p, const uint32_t* bloom, uint32_t* queue, int& qn,
+                                            const GramCtx& g, const Windows& x, int32_t p0, int lane) {
+    const int32_t nw = g.nwin - p0;
+    uint32_t h[kSub], word[kSub];
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const uint32_t lo = x.lo[k] & g.lomask;
+        const uint32_t himix = BIG ? hi_mix(g.hitag | (x.hi[k] & g.himask)) : g.himix_c;
+        h[k] = filter_hash(lo, himix);
+        word[k] = bloom[h[k] >> p.bloom_shift];
+    }
+    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)(p0 + lane);
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const uint32_t fb = filter_bits(h[k], p.bloom_shift);
+        append(queue, qn, (64 * k + lane < nw) && ((word[k] & fb) == fb), tag + 64u * k);
+    }
+}
+
+// Filter-test the (up to) 256 windows of one superblock for one gram length
+// and append the candidates to the queue in position order.  The caller
+// guarantees qn <= kQueueCap - 256.
+__device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* img, const uint32_t* bloom,
+                                         uint32_t* queue, int& qn, const GramCtx& g, const Windows& x, int32_t p0,
+                                         int lane) {
+    if (g.klen <= 2)
+        probe_direct(img, queue, qn, g, x, p0, lane);
+    else if (g.klen <= 4)
+        probe_bloom<false>(p, bloom, queue, qn, g, x, p0, lane);
+    else
+        probe_bloom<true>(p, bloom, queue, qn, g, x, p0, lane);
+}
+
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
-template <int S, bool DENSE, bool STAGED>
+template <int S, int MODE, bool STAGED>
 __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                           const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
                                           const DocSrc& src, int lane) {
@@ -353,7 +376,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
             const GramCtx g = gram_ctx(len, p.G[gi]);
             if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
             if (qn > kQueueCap - 64 * kSub) {
-                flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
+                flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
                 qn = 0;
             }
             probe_sb(p, img, bloom, wl.queue, qn, g, x, 0, lane);
@@ -373,14 +396,14 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
                     x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
                 }
                 if (qn > kQueueCap - 64 * kSub) {
-                    flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
+                    flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
                     qn = 0;
                 }
                 probe_sb(p, img, bloom, wl.queue, qn, g, x, p0, lane);
             }
         }
     }
-    if (qn) flush<S, DENSE, STAGED>(p, wl, qn, src, acc, lane);
+    if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
 
     // argmax (breeze: first element, then strict '>' updates): the wave max M
     // of the non-NaN scores by DPP (no LDS), then the first index holding M;
@@ -430,7 +453,7 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
     r0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0));
 }
 
-template <int S, bool DENSE, bool FLDS>
+template <int S, int MODE, bool FLDS>
 __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
@@ -480,14 +503,14 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{wl.buf, b - s0};
-                score_doc<S, DENSE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                score_doc<S, MODE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
             }
         } else {
             for (int i = 0; i < cnt; ++i) {
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{nullptr, b};
-                score_doc<S, DENSE, false>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                score_doc<S, MODE, false>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -496,62 +519,71 @@ __global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScorePara
     }
 }
 
-template <int S, bool DENSE, bool FLDS>
+template <int S, int MODE, bool FLDS>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
     const size_t lds = score_lds_bytes(S, FLDS, p.bloom_words);
-    hipLaunchKernelGGL((score_kernel<S, DENSE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
+    hipLaunchKernelGGL((score_kernel<S, MODE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
 
-template <int S, bool DENSE, bool FLDS>
+template <int S, int MODE, bool FLDS>
 hipError_t prepare_t(size_t lds, int* blocks) {
-    const void* f = reinterpret_cast<const void*>(&score_kernel<S, DENSE, FLDS>);
+    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, FLDS>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, kScoreWaves * 64, lds);
 }
 
-template <bool DENSE, bool FLDS>
+template <int MODE, bool FLDS>
 hipError_t launch_s(const ScoreParams& p, int slices, int grid, hipStream_t stream) {
     switch (slices) {
-        case 1: return launch_t<1, DENSE, FLDS>(p, grid, stream);
-        case 2: return launch_t<2, DENSE, FLDS>(p, grid, stream);
-        case 3: return launch_t<3, DENSE, FLDS>(p, grid, stream);
-        case 4: return launch_t<4, DENSE, FLDS>(p, grid, stream);
+        case 1: return launch_t<1, MODE, FLDS>(p, grid, stream);
+        case 2: return launch_t<2, MODE, FLDS>(p, grid, stream);
+        case 3: return launch_t<3, MODE, FLDS>(p, grid, stream);
+        case 4: return launch_t<4, MODE, FLDS>(p, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
-template <bool DENSE, bool FLDS>
+template <int MODE, bool FLDS>
 hipError_t prepare_s(int slices, size_t lds, int* blocks) {
     switch (slices) {
-        case 1: return prepare_t<1, DENSE, FLDS>(lds, blocks);
-        case 2: return prepare_t<2, DENSE, FLDS>(lds, blocks);
-        case 3: return prepare_t<3, DENSE, FLDS>(lds, blocks);
-        case 4: return prepare_t<4, DENSE, FLDS>(lds, blocks);
+        case 1: return prepare_t<1, MODE, FLDS>(lds, blocks);
+        case 2: return prepare_t<2, MODE, FLDS>(lds, blocks);
+        case 3: return prepare_t<3, MODE, FLDS>(lds, blocks);
+        case 4: return prepare_t<4, MODE, FLDS>(lds, blocks);
         default: return hipErrorInvalidValue;
     }
+}
+
+template <int MODE>
+hipError_t launch_m(const ScoreParams& p, int slices, bool lds_bloom, int grid, hipStream_t stream) {
+    return lds_bloom ? launch_s<MODE, true>(p, slices, grid, stream) : launch_s<MODE, false>(p, slices, grid, stream);
+}
+
+template <int MODE>
+hipError_t prepare_m(int slices, bool lds_bloom, size_t lds, int* blocks) {
+    return lds_bloom ? prepare_s<MODE, true>(slices, lds, blocks) : prepare_s<MODE, false>(slices, lds, blocks);
 }
 
 }  // namespace
 
-hipError_t launch_score(const ScoreParams& p, int slices, bool dense, bool lds_filter, int grid,
-                        hipStream_t stream) {
-    if (dense) {
-        return lds_filter ? launch_s<true, true>(p, slices, grid, stream)
-                          : launch_s<true, false>(p, slices, grid, stream);
+hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream) {
+    switch (mode) {
+        case 0: return launch_m<0>(p, slices, lds_bloom, grid, stream);
+        case 1: return launch_m<1>(p, slices, lds_bloom, grid, stream);
+        case 2: return launch_m<2>(p, slices, lds_bloom, grid, stream);
+        default: return hipErrorInvalidValue;
     }
-    return lds_filter ? launch_s<false, true>(p, slices, grid, stream)
-                      : launch_s<false, false>(p, slices, grid, stream);
 }
 
-hipError_t score_prepare(int slices, bool dense, bool lds_filter, size_t lds_bytes, int* blocks_per_cu) {
-    if (dense) {
-        return lds_filter ? prepare_s<true, true>(slices, lds_bytes, blocks_per_cu)
-                          : prepare_s<true, false>(slices, lds_bytes, blocks_per_cu);
+hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu) {
+    switch (mode) {
+        case 0: return prepare_m<0>(slices, lds_bloom, lds_bytes, blocks_per_cu);
+        case 1: return prepare_m<1>(slices, lds_bloom, lds_bytes, blocks_per_cu);
+        case 2: return prepare_m<2>(slices, lds_bloom, lds_bytes, blocks_per_cu);
+        default: return hipErrorInvalidValue;
     }
-    return lds_filter ? prepare_s<false, true>(slices, lds_bytes, blocks_per_cu)
-                      : prepare_s<false, false>(slices, lds_bytes, blocks_per_cu);
 }
 
 }  // namespace ldgpu
