@@ -326,16 +326,17 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     }
 
     // filter image: exact bitmaps of the 1- and 2-byte keys, then a blocked
-    // Bloom filter of the longer ones (~1.6 keys per 32-bit word; false
-    // positives only cost verification lanes).  The bloom is staged in LDS up
-    // to 64 KiB, else read from global memory (L2 / Infinity Cache).
+    // Bloom filter of the longer ones.  The bloom is staged in LDS up
+    // to 64 KiB, else read from global memory (L2 / Infinity Cache).  1.25-2.5
+    // keys per word keeps the false-positive rate at 1-3%: false positives
+    // only cost idle verification lanes, LDS costs resident workgroups.
     int64_t n_long = 0;
     for (int64_t i = 0; i < nk; ++i) {
         const int kl = key_len(keys[i]);
         m->len_mask |= 1u << kl;
         n_long += kl >= 3;
     }
-    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / 1.6) + 1));
+    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / 2.5) + 1));
     bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
     m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
     m->filter_log2 = log2u(bwords);
