@@ -111,10 +111,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; the modulo only matters when rehearsing several
+    # ranks on a one-GPU box (with LDGPU_BENCH_BACKEND=gloo)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = os.environ.get("LDGPU_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     ls = synth.make_languages(args.langs)
     if args.empty_table:
@@ -159,7 +166,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

@@ -205,3 +205,41 @@ def test_bench_shape_parity_sample():
     table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3, 4, 5], 500, ls.names)
     data, off, _ = synth.generate(ls, 20000, 256, 256, seed=synth.SEED_BASE + 2)
     check_parity(table, 20, [1, 2, 3, 4, 5], data, off)
+
+
+def test_config4_shape_parity_short_docs_100_langs():
+    """Config 4's shape: 100 languages (two 64-lane slices), ~64-byte docs,
+    grams 1-5, a fit-produced table (K=1000)."""
+    from languagedetection.api import LanguageDetector
+    ls = synth.make_languages(100, seed=synth.SEED_BASE + 4)
+    tdata, toff, tlang = synth.generate(ls, 3000, 100, 400, seed=synth.SEED_BASE + 104)
+    rows = list(zip([ls.names[i] for i in tlang], synth.texts(tdata, toff)))
+    table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3, 4, 5], 1000, ls.names)
+    data, off, _ = synth.generate(ls, 20000, 32, 96, seed=synth.SEED_BASE + 5)
+    m = check_parity(table, 100, [1, 2, 3, 4, 5], data, off)
+    assert m.info()["mode"] == 0
+
+
+def test_config5_shape_parity_large_profile_global_filter():
+    """Config 5's shape at reduced size: 200 languages (four slices), grams
+    1-7, a table too large for the LDS Bloom filter (global-filter variant)."""
+    rng = np.random.default_rng(55)
+    L, grams = 200, [1, 2, 3, 4, 5, 6, 7]
+    ls = synth.make_languages(L, seed=synth.SEED_BASE + 55)
+    data, off, _ = synth.generate(ls, 3000, 256, 256, seed=synth.SEED_BASE + 56)
+    raw = data.tobytes()
+    # table keys: windows sampled from the documents (so hits occur) + random keys
+    table = {}
+    w = math.log(2.0)
+    while len(table) < 120000:
+        d = int(rng.integers(0, 3000))
+        n = int(rng.integers(1, 8))
+        p = int(rng.integers(0, 256 - n))
+        key = raw[off[d] + p: off[d] + p + n]
+        mask = rng.random(L) < 0.01
+        mask[int(rng.integers(0, L))] = True
+        k = int(mask.sum())
+        table[key] = [math.log(1.0 + 1.0 / k) if b else 0.0 for b in mask]
+    m = check_parity(table, L, grams, data, off)
+    info = m.info()
+    assert info["filter_bits"] > 64 * 1024 * 8  # bloom beyond LDS: global-filter kernel
