@@ -4,9 +4,9 @@ Mirrors org.apache.spark.ml.feature.languagedetection (LanguageDetector,
 LanguageDetectorModel) over pandas DataFrames; the FIT counting and SCORE
 kernels run on gfx950 through libldgpu.so (include/ldgpu.h).
 """
-from .api import (FitValidationError, LanguageDetector, LanguageDetectorModel, NullPointerException,
-                  save_grams)
+from .api import (FitValidationError, LanguageDetector, LanguageDetectorModel, LanguageDetectorModelReader,
+                  LanguageDetectorModelWriter, NullPointerException, save_grams)
 from .runtime import DeviceCounts, DeviceModel
 
-__all__ = ["LanguageDetector", "LanguageDetectorModel", "FitValidationError", "NullPointerException",
-           "DeviceCounts", "DeviceModel", "save_grams"]
+__all__ = ["LanguageDetector", "LanguageDetectorModel", "LanguageDetectorModelReader", "LanguageDetectorModelWriter",
+           "FitValidationError", "NullPointerException", "DeviceCounts", "DeviceModel", "save_grams"]

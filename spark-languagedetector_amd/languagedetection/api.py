@@ -134,6 +134,21 @@ class LanguageDetectorModel(_Params):
         out[self.getOutputCol()] = [self.supportedLanguages[i] for i in labels]
         return out
 
+    # persistence (LanguageDetectorModel.scala:24-105): the reference's layout
+    def write(self) -> "LanguageDetectorModelWriter":
+        return LanguageDetectorModelWriter(self)
+
+    def save(self, path: str) -> None:
+        self.write().save(path)
+
+    @classmethod
+    def read(cls) -> "LanguageDetectorModelReader":
+        return LanguageDetectorModelReader()
+
+    @classmethod
+    def load(cls, path: str) -> "LanguageDetectorModel":
+        return cls.read().load(path)
+
     @staticmethod
     def detect(text, probabilityMap: Dict, supportedLanguages: Sequence[str], gramLengths: Sequence[int]) -> str:
         """detect(String | Array[Byte], ...) (:131-165); a str is encoded by the
@@ -147,6 +162,36 @@ class LanguageDetectorModel(_Params):
         labels, _ = m.score(data, offsets)
         m.close()
         return supportedLanguages[int(labels[0])]
+
+
+class LanguageDetectorModelWriter:
+    """LanguageDetectorModelWriter (LanguageDetectorModel.scala:27-60) with
+    MLWriter's save/overwrite behaviour."""
+
+    def __init__(self, instance: LanguageDetectorModel):
+        self.instance = instance
+        self._overwrite = False
+
+    def overwrite(self) -> "LanguageDetectorModelWriter":
+        self._overwrite = True
+        return self
+
+    def save(self, path: str) -> None:
+        from .persistence import save_model
+        save_model(self.instance, path, overwrite=self._overwrite)
+
+
+class LanguageDetectorModelReader:
+    """LanguageDetectorModelReader (LanguageDetectorModel.scala:62-105)."""
+
+    def load(self, path: str) -> LanguageDetectorModel:
+        from .persistence import load_model_parts
+        meta, table, langs, grams = load_model_parts(path)
+        m = LanguageDetectorModel(table, grams, langs, uid=meta.get("uid"))
+        for k, v in (meta.get("paramMap") or {}).items():   # DefaultParamsReader.getAndSetParams
+            if k in m._defaults:
+                m._set(k, v)
+        return m
 
 
 # ------------------------------------------------------------------------- FIT
