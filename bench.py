@@ -113,7 +113,7 @@ def fit_main(args, world, rank, local, dev, backend):
     """Config 3 (FIT): count every window of a synthetic multilingual corpus
     (docs of 1-7 KB) resident in HBM, merge across ranks (all_gather keys +
     all_reduce counts), build the K-profile table.  A step = one full fit."""
-    from languagedetection.distributed import merge_counts
+    from languagedetection.distributed import merge_counts_device
     grams = [int(x) for x in args.grams.split(",")]
     ls = synth.make_languages(args.langs)
     pool_docs = max(1, min(16384, args.fit_bytes // 4096))
@@ -135,11 +135,10 @@ def fit_main(args, world, rank, local, dev, backend):
         torch.cuda.synchronize(dev)
         t["count_s"] = time.perf_counter() - t0
         if world > 1:
-            keys, cnt = c.export()
+            merged = merge_counts_device(c)
             c.close()
-            gk, gc = merge_counts(keys, cnt, args.langs)
-            c = DeviceCounts(args.langs, grams, capacity_hint=len(gk), device=local)
-            c.add(gk, gc)
+            c = merged
+            torch.cuda.synchronize(dev)
             t["merge_s"] = time.perf_counter() - t0 - t["count_s"]
         distinct = c.size()
         table = c.fit_table(args.profile_size)

@@ -134,6 +134,18 @@ int ldgpu_counts_export(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_o
 int ldgpu_counts_add(ldgpu_counts* counts, int64_t n, const uint8_t* key_bytes,
                      const int64_t* key_offsets, const int64_t* counts_in);
 
+/* Device-resident forms of export / add (the multi-GPU merge keeps counts in
+ * HBM and exchanges them with RCCL).  Keys are packed u64: bytes little-endian
+ * in bits 0..55, length (1..7) in bits 56..63.  export_device writes the
+ * distinct grams (unordered) into caller buffers of `capacity` entries
+ * (keys[capacity], counts[capacity][n_langs] int64) and their number to
+ * *n_out; it fails with LDGPU_EINVAL if capacity is too small.  Both are
+ * synchronous with respect to `stream` (NULL = HIP's null stream). */
+int ldgpu_counts_export_device(ldgpu_counts* counts, int64_t capacity, uint64_t* d_keys,
+                               int64_t* d_counts, int64_t* n_out, void* stream);
+int ldgpu_counts_add_device(ldgpu_counts* counts, int64_t n, const uint64_t* d_keys,
+                            const int64_t* d_counts, void* stream);
+
 /* computeProbabilities + filterTopGrams: v_l = log(1 + [g in l] / k_g);
  * per language the profile_size largest v_l (ties: ascending (length, bytes));
  * the union of the chosen grams with their full rows.  Two calls: _size

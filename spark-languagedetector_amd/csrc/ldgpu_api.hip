@@ -98,14 +98,6 @@ int check_offsets(const int64_t* off, int64_t n_docs) {
     return LDGPU_OK;
 }
 
-// (length, unsigned bytes) order of a packed key
-inline uint64_t sort_key(uint64_t key) {
-    const int len = key_len(key);
-    uint64_t s = (uint64_t)len << 56;
-    for (int i = 0; i < len; ++i) s |= ((key >> (8 * i)) & 0xffull) << (48 - 8 * i);
-    return s;
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ context
@@ -874,11 +866,57 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     return ok();
 }
 
-// computeProbabilities + filterTopGrams (LanguageDetector.scala:75-132).
-extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
-    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+extern "C" int ldgpu_counts_export_device(ldgpu_counts* c, int64_t capacity, uint64_t* d_keys, int64_t* d_counts,
+                                          int64_t* n_out, void* stream) {
+    if (!c || !n_out) return fail(LDGPU_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
+    *n_out = (int64_t)c->size;
+    if ((int64_t)c->size > capacity)
+        return fail(LDGPU_EINVAL, "export_device: %llu grams exceed the capacity %lld", (unsigned long long)c->size,
+                    (long long)capacity);
+    if (c->size && (!d_keys || !d_counts)) return fail(LDGPU_EINVAL, "device pointer is NULL");
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long* d_n = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_n, sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d_n, 0, sizeof(unsigned long long), st);
+    if (e == hipSuccess)
+        e = launch_compact(count_params(c), c->cap, d_keys, reinterpret_cast<unsigned long long*>(d_counts), d_n, st);
+    unsigned long long got = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d_n);
+    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "export_device: %s", hipGetErrorString(e));
+    if (got != c->size) return fail(LDGPU_EDEVICE, "export_device: %llu grams, %llu expected", got,
+                                    (unsigned long long)c->size);
+    return ok();
+}
+
+extern "C" int ldgpu_counts_add_device(ldgpu_counts* c, int64_t n, const uint64_t* d_keys, const int64_t* d_counts,
+                                       void* stream) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
+    if (n == 0) return ok();
+    if (!d_keys || !d_counts) return fail(LDGPU_EINVAL, "device pointer is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipStreamSynchronize(st));
+    if (2 * (c->size + (uint64_t)n) > c->cap) {
+        if (int rc = grow(c, next_pow2(4 * (c->size + n) + 16))) return rc;
+    }
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream));
+    HIP_TRY(launch_counts_add(count_params(c), d_keys, reinterpret_cast<const unsigned long long*>(d_counts), nullptr,
+                              n, c->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    if (int rc = after_batch(c)) return rc;
+    return ok();
+}
+
+namespace {
+// Host build of the table from the full count table (used when some language
+// has fewer than K present grams: the zero-valued fill needs every gram).
+int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
     std::vector<uint64_t> keys;
     std::vector<unsigned long long> cnt;
     if (int rc = counts_pull(c, keys, cnt)) return rc;
@@ -945,6 +983,180 @@ extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows,
     c->tbl_valid = true;
     if (n_rows) *n_rows = (int64_t)out_keys.size();
     if (key_bytes) *key_bytes = nb;
+    return LDGPU_OK;
+}
+
+
+// Device build (SURVEY §8f "next" #3): presence masks, k and the
+// (language, k) histogram on the device; the host picks each language's
+// threshold class; the device flags the grams below it and emits the
+// threshold-class candidates; the host resolves their (length, bytes) order.
+// Only the chosen grams (<= L*K) and the candidates cross PCIe.
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() {
+        for (void* x : p)
+            if (x) (void)hipFree(x);
+    }
+    template <typename T>
+    hipError_t alloc(T** out, size_t n) {
+        void* x = nullptr;
+        hipError_t e = hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) p.push_back(x);
+        *out = (T*)x;
+        return e;
+    }
+};
+
+int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes, bool* fallback) {
+    *fallback = false;
+    const int L = c->L, S = (L + 63) / 64;
+    const int64_t n = (int64_t)c->size;
+    hipStream_t st = c->ctx->stream;
+    DevBufs db;
+    uint64_t *d_keys, *d_masks;
+    int32_t* d_k;
+    unsigned long long* d_n;
+    unsigned int* d_hist;
+    HIP_TRY(db.alloc(&d_keys, n));
+    HIP_TRY(db.alloc(&d_masks, (size_t)n * S));
+    HIP_TRY(db.alloc(&d_k, n));
+    HIP_TRY(db.alloc(&d_n, 2));
+    HIP_TRY(db.alloc(&d_hist, (size_t)L * (L + 1)));
+    HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(unsigned int) * L * (L + 1), st));
+    HIP_TRY(launch_presence(count_params(c), c->cap, S, d_keys, d_masks, d_k, d_n, d_hist, st));
+    std::vector<unsigned int> hist((size_t)L * (L + 1));
+    unsigned long long got = 0;
+    HIP_TRY(hipMemcpyAsync(hist.data(), d_hist, sizeof(unsigned int) * hist.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((int64_t)got != n) return fail(LDGPU_EDEVICE, "presence: %llu grams, %lld expected", got, (long long)n);
+
+    std::vector<int32_t> kstar(L, L + 1), need(L, 0);
+    uint64_t cand_cap = 0;
+    for (int l = 0; l < L; ++l) {
+        int64_t acc = 0;
+        for (int k = 1; k <= L; ++k) {
+            const int64_t ck = hist[(size_t)l * (L + 1) + k];
+            if (acc + ck >= K) {
+                kstar[l] = k;
+                need[l] = (int32_t)(K - acc);
+                cand_cap += (uint64_t)ck;
+                break;
+            }
+            acc += ck;
+        }
+        if (kstar[l] == L + 1 && acc < K) {
+            *fallback = true;  // zero-valued fill needed: every gram takes part
+            return LDGPU_OK;
+        }
+    }
+    int32_t *d_kstar, *d_need, *d_cl;
+    uint8_t* d_chosen;
+    uint64_t* d_ck;
+    uint32_t* d_ci;
+    unsigned int* d_cn;
+    HIP_TRY(db.alloc(&d_kstar, L));
+    HIP_TRY(db.alloc(&d_need, L));
+    HIP_TRY(db.alloc(&d_chosen, n));
+    HIP_TRY(db.alloc(&d_cl, cand_cap));
+    HIP_TRY(db.alloc(&d_ck, cand_cap));
+    HIP_TRY(db.alloc(&d_ci, cand_cap));
+    HIP_TRY(db.alloc(&d_cn, 1));
+    HIP_TRY(hipMemcpyAsync(d_kstar, kstar.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_need, need.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(d_cn, 0, sizeof(unsigned int), st));
+    HIP_TRY(launch_select(n, L, S, d_keys, d_masks, d_k, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn, st));
+    unsigned int cn = 0;
+    HIP_TRY(hipMemcpyAsync(&cn, d_cn, sizeof cn, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (cn != cand_cap) return fail(LDGPU_EDEVICE, "select: %u candidates, %llu expected", cn,
+                                    (unsigned long long)cand_cap);
+    std::vector<int32_t> cl(cn);
+    std::vector<uint64_t> ck(cn);
+    std::vector<uint32_t> ci(cn);
+    if (cn) {
+        HIP_TRY(hipMemcpyAsync(cl.data(), d_cl, sizeof(int32_t) * cn, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(ck.data(), d_ck, sizeof(uint64_t) * cn, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(ci.data(), d_ci, sizeof(uint32_t) * cn, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    // per language: the need[l] smallest (length, bytes) keys of its threshold class
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> per(L);
+    for (unsigned int i = 0; i < cn; ++i) per[cl[i]].push_back({ck[i], ci[i]});
+    std::vector<uint32_t> mark;
+    for (int l = 0; l < L; ++l) {
+        auto& v = per[l];
+        const size_t take = std::min<size_t>((size_t)std::max(need[l], 0), v.size());
+        if (take < v.size()) std::nth_element(v.begin(), v.begin() + take, v.end());
+        for (size_t i = 0; i < take; ++i) mark.push_back(v[i].second);
+    }
+    uint32_t* d_mark;
+    HIP_TRY(db.alloc(&d_mark, mark.size()));
+    if (!mark.empty())
+        HIP_TRY(hipMemcpyAsync(d_mark, mark.data(), sizeof(uint32_t) * mark.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_mark(d_mark, (int64_t)mark.size(), d_chosen, st));
+    const int64_t cap_out = std::min<int64_t>(n, (int64_t)L * std::max<int32_t>(K, 0));
+    uint64_t *d_ok, *d_om;
+    int32_t* d_okk;
+    HIP_TRY(db.alloc(&d_ok, cap_out));
+    HIP_TRY(db.alloc(&d_om, (size_t)cap_out * S));
+    HIP_TRY(db.alloc(&d_okk, cap_out));
+    HIP_TRY(hipMemsetAsync(d_n + 1, 0, sizeof(unsigned long long), st));
+    HIP_TRY(launch_gather_chosen(n, S, d_chosen, d_keys, d_masks, d_k, d_ok, d_om, d_okk, d_n + 1, st));
+    unsigned long long m = 0;
+    HIP_TRY(hipMemcpyAsync(&m, d_n + 1, sizeof m, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((int64_t)m > cap_out) return fail(LDGPU_EDEVICE, "top-K: %llu grams chosen, at most %lld expected", m,
+                                         (long long)cap_out);
+    std::vector<uint64_t> ok(m), om((size_t)m * S);
+    std::vector<int32_t> okk(m);
+    if (m) {
+        HIP_TRY(hipMemcpyAsync(ok.data(), d_ok, sizeof(uint64_t) * m, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(om.data(), d_om, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(okk.data(), d_okk, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    std::vector<double> w(L + 1, 0.0);
+    for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
+    std::vector<std::pair<uint64_t, uint64_t>> order(m);
+    for (uint64_t i = 0; i < m; ++i) order[i] = {sort_key(ok[i]), i};
+    std::sort(order.begin(), order.end());
+    std::vector<uint64_t> out_keys(m);
+    c->tbl_rows.assign((size_t)m * L, 0.0);
+    for (uint64_t r = 0; r < m; ++r) {
+        const uint64_t i = order[r].second;
+        out_keys[r] = ok[i];
+        for (int l = 0; l < L; ++l)
+            if ((om[i * S + l / 64] >> (l % 64)) & 1ull) c->tbl_rows[r * L + l] = w[okk[i]];
+    }
+    int64_t nb = 0;
+    for (uint64_t k : out_keys) nb += key_len(k);
+    c->tbl_bytes.assign((size_t)std::max<int64_t>(nb, 1), 0);
+    c->tbl_off.assign(out_keys.size() + 1, 0);
+    write_keys(out_keys, c->tbl_bytes.data(), c->tbl_off.data());
+    c->tbl_valid = true;
+    if (n_rows) *n_rows = (int64_t)m;
+    if (key_bytes) *key_bytes = nb;
+    return LDGPU_OK;
+}
+}  // namespace
+
+// computeProbabilities + filterTopGrams (LanguageDetector.scala:75-132).
+extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    if (K <= 0 || c->size == 0) {
+        if (int rc = fit_table_host(c, K, n_rows, key_bytes)) return rc;
+        return ok();
+    }
+    bool fallback = false;
+    if (int rc = fit_table_device(c, K, n_rows, key_bytes, &fallback)) return rc;
+    if (fallback) {
+        if (int rc = fit_table_host(c, K, n_rows, key_bytes)) return rc;
+    }
     return ok();
 }
 

@@ -65,6 +65,15 @@ inline uint64_t pack_key_host(const uint8_t* p, int len) {
     return k;
 }
 
+// (length, unsigned bytes) order of a packed key: length in the top byte,
+// the bytes big-endian below it (the build's top-K tie-break).
+__host__ __device__ __forceinline__ uint64_t sort_key(uint64_t key) {
+    const int len = key_len(key);
+    uint64_t s = (uint64_t)len << 56;
+    for (int i = 0; i < len; ++i) s |= ((key >> (8 * i)) & 0xffull) << (48 - 8 * i);
+    return s;
+}
+
 // Number of windows of Scala sliding(n) over len bytes (partial rule).
 __host__ __device__ __forceinline__ int64_t n_windows(int64_t len, int n) {
     return len == 0 ? 0 : (len < n ? 1 : len - n + 1);

@@ -19,6 +19,8 @@
 // add on the (slot, lang) counter.  An insert that exceeds kMaxProbe probes
 // appends (key, lang) to an overflow list that the host re-inserts after
 // growing the table.
+#include <algorithm>
+
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
@@ -201,6 +203,159 @@ hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys
                           unsigned long long* out_n, hipStream_t stream) {
     hipLaunchKernelGGL(compact_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out_keys,
                        out_counts, out_n);
+    return hipGetLastError();
+}
+
+}  // namespace ldgpu
+
+// ---------------------------------------------------------------------------
+// Device probability / top-K table (LanguageDetector.scala:75-132).
+//
+// computeProbabilities gives gram g the row v_l = log(1 + [g in l] / k_g),
+// k_g = #languages with g (:85-87), so a row is fully described by the
+// language mask of g.  filterTopGrams ranks, per language l, ALL grams by v_l
+// descending and keeps K (:113-119); since log(1 + 1/k) falls with k, the
+// order is: present grams by k ascending, then absent ones; ties by the
+// build's (length, bytes) rule.  The device computes masks, k and the
+// (language, k) histogram; the host turns the histogram into a threshold
+// class per language; the device flags every gram below a threshold and
+// emits the threshold-class candidates, whose (length, bytes) order the host
+// resolves with nth_element.
+namespace ldgpu {
+namespace {
+
+__global__ void presence_kernel(const CountParams p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
+                                int32_t* out_k, unsigned long long* out_n, unsigned int* hist) {
+    extern __shared__ unsigned int lhist[];
+    const int L = p.L;
+    const bool lds_hist = L <= 88;  // L * (L + 1) * 4 B <= 31 KiB
+    if (lds_hist) {
+        for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x) lhist[i] = 0u;
+        __syncthreads();
+    }
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool occ = i < cap && p.keys[i] != kEmpty;
+    const uint64_t m = __ballot(occ);
+    const int lane = threadIdx.x & 63;
+    if (m) {
+        unsigned long long base = 0;
+        const int leader = __builtin_ctzll(m);
+        if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
+        base = __shfl(base, leader);
+        if (occ) {
+            const uint32_t off =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const unsigned long long o = base + off;
+            int k = 0;
+            for (int s = 0; s < S; ++s) {
+                uint64_t w = 0;
+                for (int b = 0; b < 64 && s * 64 + b < L; ++b)
+                    if (p.counts[i * L + s * 64 + b] != 0ull) w |= 1ull << b;
+                out_masks[o * S + s] = w;
+                k += __popcll(w);
+            }
+            out_keys[o] = p.keys[i];
+            out_k[o] = k;
+            for (int l = 0; l < L; ++l) {
+                if (p.counts[i * L + l] != 0ull) {
+                    if (lds_hist)
+                        atomicAdd(&lhist[l * (L + 1) + k], 1u);
+                    else
+                        atomicAdd(&hist[l * (L + 1) + k], 1u);
+                }
+            }
+        }
+    }
+    if (lds_hist) {
+        __syncthreads();
+        for (int t = threadIdx.x; t < L * (L + 1); t += blockDim.x)
+            if (lhist[t]) atomicAdd(&hist[t], lhist[t]);
+    }
+}
+
+__global__ void select_kernel(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
+                              const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
+                              uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int k = ks[j];
+    uint8_t ch = 0;
+    for (int s = 0; s < S; ++s) {
+        uint64_t w = masks[j * S + s];
+        while (w) {
+            const int l = s * 64 + __builtin_ctzll(w);
+            w &= w - 1;
+            if (k < kstar[l]) {
+                ch = 1;
+            } else if (k == kstar[l] && need[l] > 0) {
+                const unsigned int at = atomicAdd(cand_n, 1u);
+                cand_lang[at] = l;
+                cand_key[at] = sort_key(keys[j]);
+                cand_idx[at] = (uint32_t)j;
+            }
+        }
+    }
+    chosen[j] = ch;
+}
+
+__global__ void mark_kernel(const uint32_t* idx, int64_t n, uint8_t* chosen) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) chosen[idx[i]] = 1;
+}
+
+__global__ void gather_chosen_kernel(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys,
+                                     const uint64_t* masks, const int32_t* ks, uint64_t* out_keys,
+                                     uint64_t* out_masks, int32_t* out_k, unsigned long long* out_n) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool c = j < n && chosen[j];
+    const uint64_t m = __ballot(c);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    const int leader = __builtin_ctzll(m);
+    if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (!c) return;
+    const unsigned long long o =
+        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    out_keys[o] = keys[j];
+    out_k[o] = ks[j];
+    for (int s = 0; s < S; ++s) out_masks[o * S + s] = masks[j * S + s];
+}
+
+unsigned grid_of(int64_t n, int b) { return (unsigned)std::max<int64_t>(1, (n + b - 1) / b); }
+
+}  // namespace
+
+hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
+                           int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream) {
+    const size_t lds = p.L <= 88 ? (size_t)p.L * (p.L + 1) * 4 : 0;
+    hipLaunchKernelGGL(presence_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), lds, stream, p, cap, S, out_keys,
+                       out_masks, out_k, out_n, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
+                         const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
+                         uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(select_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, L, S, keys, masks, ks, kstar,
+                       need, chosen, cand_lang, cand_key, cand_idx, cand_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mark_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, idx, n, chosen);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,
+                                const int32_t* ks, uint64_t* out_keys, uint64_t* out_masks, int32_t* out_k,
+                                unsigned long long* out_n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_chosen_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, S, chosen, keys, masks,
+                       ks, out_keys, out_masks, out_k, out_n);
     return hipGetLastError();
 }
 

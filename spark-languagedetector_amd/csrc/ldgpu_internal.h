@@ -88,4 +88,22 @@ hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_
 hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys,
                           unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
 
+// ---- device probability / top-K (computeProbabilities + filterTopGrams)
+// presence: compact occupied slots into keys[n], masks[n][S] (count > 0 per
+// language) and k[n] (= popcount), and histogram hist[l][k] over (gram, l).
+hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
+                           int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream);
+// select: chosen[j] = 1 when k_j < kstar[l] for some l in the gram's mask;
+// grams with k_j == kstar[l] (need[l] > 0) are appended as threshold
+// candidates (lang, sort key, index).
+hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
+                         const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
+                         uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream);
+// chosen[idx[i]] = 1
+hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream);
+// gather the chosen grams: out_keys[m], out_masks[m][S], out_k[m]
+hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,
+                                const int32_t* ks, uint64_t* out_keys, uint64_t* out_masks, int32_t* out_k,
+                                unsigned long long* out_n, hipStream_t stream);
+
 }  // namespace ldgpu

@@ -54,6 +54,8 @@ SIGNATURES = [
     ("ldgpu_counts_size", ctypes.c_int, [_p, _pi64, _pi64]),
     ("ldgpu_counts_export", ctypes.c_int, [_p, _p, _p, _p]),
     ("ldgpu_counts_add", ctypes.c_int, [_p, _i64, _p, _p, _p]),
+    ("ldgpu_counts_export_device", ctypes.c_int, [_p, _i64, _p, _p, _pi64, _p]),
+    ("ldgpu_counts_add_device", ctypes.c_int, [_p, _i64, _p, _p, _p]),
     ("ldgpu_fit_table_size", ctypes.c_int, [_p, _i32, _pi64, _pi64]),
     ("ldgpu_fit_table_export", ctypes.c_int, [_p, _p, _p, _p]),
 ]

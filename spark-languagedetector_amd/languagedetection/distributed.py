@@ -82,22 +82,53 @@ def merge_counts(keys: Sequence[bytes], counts: np.ndarray, n_langs: int, group=
     return keys_of(codes), dense.cpu().numpy()
 
 
+def merge_counts_device(local, group=None):
+    """The FIT merge on the GPUs: `local` is this rank's DeviceCounts; the
+    keys/counts stay in HBM (ldgpu_counts_export_device), the exchange is
+    all_gather + all_reduce(SUM) (RCCL over xGMI with backend "nccl"), and the
+    result is loaded into a new DeviceCounts (ldgpu_counts_add_device).
+    Returns the merged DeviceCounts, identical on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    from .runtime import DeviceCounts
+
+    keys, cnt = local.export_device()
+    gpu = keys.device
+    backend = dist.get_backend(group)
+    dev = torch.device("cpu") if backend == "gloo" else gpu
+    world = dist.get_world_size(group)
+    k = keys.to(dev)
+    c = cnt.to(dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([k.numel()], dtype=torch.int64, device=dev), group=group)
+    mx = int(max(int(x.item()) for x in sizes))
+    padded = torch.full((max(mx, 1),), -1, dtype=torch.int64, device=dev)
+    padded[:k.numel()] = k
+    gathered = [torch.empty_like(padded) for _ in range(world)]
+    dist.all_gather(gathered, padded, group=group)
+    union = torch.unique(torch.cat([g[:int(x.item())] for g, x in zip(gathered, sizes)]), sorted=True)
+    dense = torch.zeros((union.numel(), local.L), dtype=torch.int64, device=dev)
+    if k.numel():
+        dense[torch.searchsorted(union, k)] = c
+    dist.all_reduce(dense, op=dist.ReduceOp.SUM, group=group)
+    merged = DeviceCounts(local.L, local.gram_lengths, capacity_hint=int(union.numel()), device=local.device)
+    if union.numel():
+        merged.add_device(union.to(gpu), dense.to(gpu))
+    return merged
+
+
 def fit_distributed(rows: Sequence[Tuple[str, str]], supported_languages: Sequence[str],
                     gram_lengths: Sequence[int], profile_size: int, group=None,
                     device: Optional[int] = None) -> Dict[bytes, List[float]]:
     """LanguageDetector.computeGramProbabilities over all ranks: `rows` are
     this rank's training rows; every rank returns the same table."""
     from .api import LanguageDetector
-    from .runtime import DeviceCounts
 
     local = LanguageDetector.count_grams(rows, gram_lengths, supported_languages, device=device)
-    keys, cnt = local.export()
+    merged = merge_counts_device(local, group=group)
     local.close()
-    gkeys, gcnt = merge_counts(keys, cnt, len(supported_languages), group=group)
-    merged = DeviceCounts(len(supported_languages), gram_lengths, capacity_hint=len(gkeys), device=device)
     try:
-        if gkeys:
-            merged.add(gkeys, gcnt)
         return merged.fit_table(profile_size)
     finally:
         merged.close()

@@ -87,7 +87,9 @@ class DeviceCounts:
                  device: Optional[int] = None):
         self.lib = _lib.load()
         self.ctx = _lib.context(device)
+        self.device = device
         self.L = int(n_langs)
+        self.gram_lengths = list(gram_lengths)
         g = _grams(gram_lengths)
         out = ctypes.c_void_p()
         _lib.check(self.lib.ldgpu_counts_create(self.ctx, self.L, _ptr(g), len(g), int(capacity_hint),
@@ -139,6 +141,31 @@ class DeviceCounts:
         counts = np.ascontiguousarray(counts, dtype=np.int64).reshape(len(keys), self.L)
         kb, ko = pack(list(keys))
         _lib.check(self.lib.ldgpu_counts_add(self.h, len(keys), _ptr(kb), _ptr(ko), _ptr(counts)))
+
+    def export_device(self, stream: Optional[int] = None):
+        """(keys int64 [n] packed u64, counts int64 [n, L]) as torch tensors on
+        this context's GPU, unordered (ldgpu_counts_export_device)."""
+        import torch
+        n = self.size()
+        dev = torch.device("cuda", _lib.default_device() if self.device is None else self.device)
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        counts = torch.empty((max(n, 1), self.L), dtype=torch.int64, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream if stream is None else stream
+        got = ctypes.c_int64()
+        _lib.check(self.lib.ldgpu_counts_export_device(self.h, max(n, 1), ctypes.c_void_p(keys.data_ptr()),
+                                                       ctypes.c_void_p(counts.data_ptr()), ctypes.byref(got),
+                                                       ctypes.c_void_p(st) if st else None))
+        return keys[:got.value], counts[:got.value]
+
+    def add_device(self, keys, counts, stream: Optional[int] = None) -> None:
+        """Add device tensors (packed u64 keys as int64 [n], int64 counts [n, L])."""
+        import torch
+        keys = keys.contiguous()
+        counts = counts.contiguous()
+        st = torch.cuda.current_stream(keys.device).cuda_stream if stream is None else stream
+        _lib.check(self.lib.ldgpu_counts_add_device(self.h, int(keys.numel()), ctypes.c_void_p(keys.data_ptr()),
+                                                    ctypes.c_void_p(counts.data_ptr()),
+                                                    ctypes.c_void_p(st) if st else None))
 
     def fit_table(self, profile_size: int) -> Dict[bytes, List[float]]:
         """computeProbabilities + filterTopGrams -> {gram: row}."""

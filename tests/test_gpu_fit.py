@@ -136,3 +136,24 @@ def test_fit_then_transform_end_to_end():
     assert list(out["lang"]) == expect
     acc = np.mean([ls.names[l] == p for l, p in zip(lang, out["lang"])])
     assert acc > 0.9
+
+
+def test_device_export_add_roundtrip_and_device_top_k():
+    """ldgpu_counts_export_device / _add_device keep counts in HBM; the device
+    top-K path (no zero fill needed) equals the oracle's deterministic table."""
+    import torch
+    ls = synth.make_languages(12, seed=31)
+    data, off, lang = synth.generate(ls, 1500, 100, 800, seed=32)
+    a = DeviceCounts(12, [1, 2, 3, 4])
+    a.count(data, off, lang)
+    k, c = a.export_device()
+    b = DeviceCounts(12, [1, 2, 3, 4])
+    b.add_device(k, c)
+    b.add_device(k, c)
+    ka, ca = a.export()
+    kb, cb = b.export()
+    assert ka == kb and np.array_equal(2 * ca, cb)
+    rows = list(zip([ls.names[i] for i in lang], synth.texts(data, off)))
+    probs = O.fit_probabilities(rows, ls.names, [1, 2, 3, 4])
+    expect = O.filter_top_grams(probs, ls.names, 300)
+    assert a.fit_table(300) == expect
