@@ -180,6 +180,7 @@ struct ldgpu_model {
     uint32_t len_mask = 0;    // bit k: some key has k bytes
     size_t lds_bytes = 0;
     int wg_per_cu = 1;
+    int ablate = 0;           // diagnostics: LDGPU_ABLATE (never set in production)
     size_t device_bytes = 0;
     Slot* d_slots = nullptr;
     uint32_t* d_filter = nullptr;
@@ -361,6 +362,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     // persistent grid = what is resident; never more workgroups than the LDS admits
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
     if (const char* ov = getenv("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
+    if (const char* ab = getenv("LDGPU_ABLATE")) m->ablate = atoi(ab);
     if (getenv("LDGPU_DEBUG"))
         fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
                         "resident_api=%d wg_per_cu=%d\n",
@@ -419,6 +421,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.rows = m->d_rows;
     p.err = m->d_err;
     p.L = m->L;
+    p.ablate = m->ablate;
     p.nG = m->nG;
     for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
     const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;

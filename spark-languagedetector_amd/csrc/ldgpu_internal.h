@@ -28,6 +28,7 @@ struct ScoreParams {
     const double* rows;         // dense mode: [rows][L]
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     int32_t L;
+    int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe
     int32_t nG;
     int32_t G[kMaxGramLengths];
 };

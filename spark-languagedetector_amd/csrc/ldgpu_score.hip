@@ -375,6 +375,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
         for (int gi = 0; gi < p.nG; ++gi) {
             const GramCtx g = gram_ctx(len, p.G[gi]);
             if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
+            if (p.ablate & 2) continue;
             if (qn > kQueueCap - 64 * kSub) {
                 flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
                 qn = 0;
@@ -403,6 +404,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
             }
         }
     }
+    if (p.ablate & 1) qn = 0;
     if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
 
     // argmax (breeze: first element, then strict '>' updates): the wave max M
