@@ -34,7 +34,10 @@ struct ScoreParams {
 };
 
 // Launch configuration of the score kernel.
-constexpr int kScoreWaves = 8;             // waves per workgroup (512 threads)
+#ifndef LDGPU_SCORE_WAVES
+#define LDGPU_SCORE_WAVES 8
+#endif
+constexpr int kScoreWaves = LDGPU_SCORE_WAVES;  // waves per workgroup (512 threads)
 constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
 constexpr int kBufBytes = 1024;            // staged bytes of a document group per wave
 constexpr int kBufWords = kBufBytes / 4 + 4;

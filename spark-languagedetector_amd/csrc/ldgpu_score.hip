@@ -351,55 +351,6 @@ __device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* i
         probe_bloom<true>(p, bloom, queue, qn, g, x, p0, lane);
 }
 
-// Two-phase form of probe_sb for the short-document path: prep issues the 4
-// filter reads of one gram length (no waits), commit tests them and appends
-// the candidates.  Interleaving prep(n_a), prep(n_b), commit(n_a),
-// commit(n_b) keeps 8 LDS reads in flight per wave.
-struct Prep {
-    uint32_t w[kSub];  // filter word
-    uint32_t t[kSub];  // bits that must all be set in w
-};
-
-__device__ __forceinline__ void prep(const ScoreParams& p, const uint32_t* img, const uint32_t* bloom,
-                                     const GramCtx& g, const Windows& x, Prep& r) {
-    if (g.klen <= 2) {
-        const uint32_t base = g.klen == 1 ? 0u : kBmp1Words;
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            const uint32_t idx = x.lo[k] & g.lomask;
-            r.w[k] = img[base + (idx >> 5)];
-            r.t[k] = 1u << (idx & 31u);
-        }
-    } else if (g.klen <= 4) {
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            const uint32_t h = filter_hash(x.lo[k] & g.lomask, g.himix_c);
-            r.w[k] = bloom[h >> p.bloom_shift];
-            r.t[k] = filter_bits(h, p.bloom_shift);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            const uint32_t h = filter_hash(x.lo[k] & g.lomask, hi_mix(g.hitag | (x.hi[k] & g.himask)));
-            r.w[k] = bloom[h >> p.bloom_shift];
-            r.t[k] = filter_bits(h, p.bloom_shift);
-        }
-    }
-}
-
-__device__ __forceinline__ void commit(uint32_t* queue, int& qn, const GramCtx& g, const Prep& r, int lane) {
-    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)lane;
-#pragma unroll
-    for (int k = 0; k < kSub; ++k)
-        append(queue, qn, (64 * k + lane < g.nwin) && ((r.w[k] & r.t[k]) == r.t[k]), tag + 64u * k);
-}
-
-__device__ __forceinline__ bool gram_active(const ScoreParams& p, int64_t len, int gi) {
-    const int n = p.G[gi];
-    const int klen = len < n ? (int)len : n;
-    return ((p.len_mask >> klen) & 1u) && len > 0 && !(p.ablate & 2);
-}
-
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
 template <int S, int MODE, bool STAGED>
 __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
@@ -421,33 +372,15 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
             x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
             x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
         }
-        // gram lengths in pairs: both filter-read batches in flight, then
-        // the two commits in reference order (n_a before n_b)
-        int gi = 0;
-        for (;;) {
-            while (gi < p.nG && !gram_active(p, len, gi)) ++gi;
-            if (gi >= p.nG) break;
-            const int ga = gi++;
-            while (gi < p.nG && !gram_active(p, len, gi)) ++gi;
-            const bool two = gi < p.nG;
-            const int gb = two ? gi++ : ga;
-            const GramCtx A = gram_ctx(len, p.G[ga]);
-            const GramCtx B = gram_ctx(len, p.G[gb]);
-            Prep pa, pb;
-            prep(p, img, bloom, A, x, pa);
-            if (two) prep(p, img, bloom, B, x, pb);
+        for (int gi = 0; gi < p.nG; ++gi) {
+            const GramCtx g = gram_ctx(len, p.G[gi]);
+            if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
+            if (p.ablate & 2) continue;
             if (qn > kQueueCap - 64 * kSub) {
                 flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
                 qn = 0;
             }
-            commit(wl.queue, qn, A, pa, lane);
-            if (two) {
-                if (qn > kQueueCap - 64 * kSub) {
-                    flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
-                    qn = 0;
-                }
-                commit(wl.queue, qn, B, pb, lane);
-            }
+            probe_sb(p, img, bloom, wl.queue, qn, g, x, 0, lane);
         }
     } else {
         // long documents: n outer (reference order), superblocks inner
