@@ -318,18 +318,21 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
         }
     }
 
-    // filter image: exact bitmaps of the 1- and 2-byte keys, then a blocked
-    // Bloom filter of the longer ones.  The bloom is staged in LDS up
-    // to 64 KiB, else read from global memory (L2 / Infinity Cache).  1.25-2.5
-    // keys per word keeps the false-positive rate at 1-3%: false positives
-    // only cost idle verification lanes, LDS costs resident workgroups.
+    // filter image: exact bitmaps of the 1- and 2-byte keys, then the prefix
+    // Bloom filter of the longer ones (ldgpu_common.h).  The bloom is staged
+    // in LDS up to 64 KiB, else read from global memory (L2 / Infinity Cache).
+    // ~2 keys per 32-bit word (one bit each) keeps false positives at a few
+    // percent: they only cost verification lanes (~1 VALU op each, batched 64
+    // at a time), while LDS costs resident workgroups.
     int64_t n_long = 0;
     for (int64_t i = 0; i < nk; ++i) {
         const int kl = key_len(keys[i]);
         m->len_mask |= 1u << kl;
         n_long += kl >= 3;
     }
-    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / 2.5) + 1));
+    double kpw = 2.5;
+    if (const char* s = getenv("LDGPU_BLOOM_KPW")) kpw = std::max(0.05, atof(s));  // tuning experiments only
+    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
     bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
     m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
     m->filter_log2 = log2u(bwords);
@@ -344,8 +347,9 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
             const uint32_t b01 = (uint32_t)(keys[i] & 0xffff);
             filter[kBmp1Words + (b01 >> 5)] |= 1u << (b01 & 31);
         } else {
-            const uint32_t h = filter_hash_key(keys[i]);
-            filter[kBloomBase + (h >> bshift)] |= filter_bits(h, bshift);
+            const uint32_t lo = (uint32_t)keys[i];
+            const uint32_t hi = (uint32_t)(keys[i] >> 32) & ((1u << (8 * std::max(0, kl - 4))) - 1u);
+            filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (pf_bit(kl, lo, hi) & 31u);
         }
     }
 
@@ -424,6 +428,14 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.ablate = m->ablate;
     p.nG = m->nG;
     for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
+    p.maxg = 0;
+    p.n_fast = 0;
+    for (int i = 0; i < m->nG; ++i) {
+        p.maxg = std::max(p.maxg, m->G[i]);
+        if (!((m->len_mask >> m->G[i]) & 1u)) continue;  // no key of that length: never a hit
+        p.gpack[p.n_fast >> 4] |= (uint64_t)m->G[i] << (4 * (p.n_fast & 15));
+        ++p.n_fast;
+    }
     const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
     HIP_TRY(launch_score(p, m->slices, m->mode, m->lds_filter, grid, st));

@@ -19,26 +19,52 @@ constexpr int kMaxLangs = 256;
 constexpr int kMaxGramLengths = 32;
 constexpr uint64_t kEmpty = 0;
 
-// Filter hash -- cheap: 32-bit multiplies only, and for klen <= 4 the high
-// word is the constant klen << 24 so its product is wave-uniform.
-__host__ __device__ __forceinline__ uint32_t hi_mix(uint32_t hi) { return hi * 0x85EBCA77u; }
-__host__ __device__ __forceinline__ uint32_t filter_hash(uint32_t lo, uint32_t himix) {
-    return (lo * 0x9E3779B1u) ^ himix;
+// 24-bit multiplies: full-rate VALU ops on gfx950 (v_mul_u32_u24 /
+// v_mul_hi_u32_u24), where a 32-bit v_mul_lo_u32 is a multi-pass op.  The
+// compiler selects them from these exact forms; the host computes the same.
+__host__ __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) {
+    return (a & 0xffffffu) * (b & 0xffffffu);
 }
-__host__ __device__ __forceinline__ uint32_t filter_hash_key(uint64_t key) {
-    return filter_hash((uint32_t)key, hi_mix((uint32_t)(key >> 32)));
+__host__ __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
 }
 
-// Blocked Bloom filter for keys of 3..7 bytes: a key sets / tests TWO bits of
-// ONE 32-bit word, so a probe is one LDS read and one multiply.  word = top
-// `wlog` bits of h; the two bit positions are the 10 bits below them.
-__host__ __device__ __forceinline__ uint32_t filter_bits(uint32_t h, uint32_t shift) {
-    return (1u << ((h >> (shift - 5)) & 31u)) | (1u << ((h >> (shift - 10)) & 31u));
+// Prefix Bloom filter for keys of 3..7 bytes.  A key lives in ONE 32-bit word
+// chosen by its first three bytes (so every length >= 3 of a window position
+// shares the word: one LDS read per position) and sets ONE bit of it, chosen
+// from bytes the key owns by a length-specific 24-bit multiply.  With
+// lo = bytes 0..3 and hi = bytes 4..7 of the window (little-endian):
+//   word   = mul24(lo, kPfWord) >> (32 - wlog)             bytes 0..2
+//   bit(3) = mulhi24(lo, C3)                               bytes 0..2
+//   bit(4) = mulhi24(lo >> 8, C4)                          bytes 1..3
+//   bit(5) = mulhi24(lo >> 16 | hi << 16, C5)              bytes 2..4
+//   bit(6) = mulhi24(lo >> 24 | hi << 8, C6)               bytes 3..5
+//   bit(7) = mulhi24(x, C7) ^ mulhi24(x >> 8, C7b), x = lo >> 24 | hi << 8   bytes 3..6
+// (each mod 32).  No form reads a byte at or past klen, so the bytes after a
+// window never need masking.
+constexpr uint32_t kPfWord = 0x9E3779u;
+constexpr uint32_t kPfC3 = 0x7F4A7Du, kPfC4 = 0x58F1B5u, kPfC5 = 0xC2B2AFu, kPfC6 = 0x27D4EBu, kPfC7 = 0x165667u,
+                   kPfC7b = 0xD3A2E5u;
+
+__host__ __device__ __forceinline__ uint32_t pf_word(uint32_t lo, uint32_t shift) { return mul24(lo, kPfWord) >> shift; }
+
+// bit position (low 5 bits significant) of a key of klen (3..7) bytes
+__host__ __device__ __forceinline__ uint32_t pf_bit(int klen, uint32_t lo, uint32_t hi) {
+    switch (klen) {
+        case 3: return mulhi24(lo, kPfC3);
+        case 4: return mulhi24(lo >> 8, kPfC4);
+        case 5: return mulhi24((lo >> 16) | (hi << 16), kPfC5);
+        case 6: return mulhi24((lo >> 24) | (hi << 8), kPfC6);
+        default: {
+            const uint32_t x = (lo >> 24) | (hi << 8);
+            return mulhi24(x, kPfC7) ^ mulhi24(x >> 8, kPfC7b);
+        }
+    }
 }
 
 // Filter image (host-built, staged whole into LDS): a direct 256-bit bitmap
 // of the 1-byte keys, a direct 65536-bit bitmap of the 2-byte keys, then the
-// blocked Bloom words.
+// prefix Bloom words.
 constexpr uint32_t kBmp1Words = 8;
 constexpr uint32_t kBmp2Words = 2048;
 constexpr uint32_t kBloomBase = kBmp1Words + kBmp2Words;

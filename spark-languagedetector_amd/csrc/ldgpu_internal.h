@@ -31,6 +31,11 @@ struct ScoreParams {
     int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe
     int32_t nG;
     int32_t G[kMaxGramLengths];
+    // fast path (documents of maxg..256 bytes: every window full-length):
+    // the gram lengths with a table key, 4 bits each in order (16 per word)
+    uint64_t gpack[2];
+    int32_t n_fast;             // entries in gpack
+    int32_t maxg;               // max(G)
 };
 
 // Launch configuration of the score kernel.
@@ -38,6 +43,13 @@ struct ScoreParams {
 #define LDGPU_SCORE_WAVES 8
 #endif
 constexpr int kScoreWaves = LDGPU_SCORE_WAVES;  // waves per workgroup (512 threads)
+// occupancy target (HIP launch bound: waves per SIMD = WGs x waves / 4):
+// 3 workgroups = 24 waves per CU (6 per SIMD) caps the
+// kernel at 80 VGPRs; the LDS image is sized so that 3 fit (score_lds_bytes)
+#ifndef LDGPU_SCORE_MIN_WG
+#define LDGPU_SCORE_MIN_WG 3
+#endif
+constexpr int kScoreMinWgPerCu = LDGPU_SCORE_MIN_WG;
 constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
 constexpr int kBufBytes = 1024;            // staged bytes of a document group per wave
 constexpr int kBufWords = kBufBytes / 4 + 4;

@@ -12,12 +12,15 @@
 // prefetched into registers while the current one is scored):
 //   probe      a superblock = 256 window positions, 4 per lane at stride 64.
 //              Each lane loads the 8 bytes at each of its positions once
-//              (dword loads + v_alignbyte); every gram length n re-masks them
-//              into the packed u64 key, hashes it, and tests a blocked Bloom
-//              filter staged in LDS (2 bits of one 32-bit word: one ds_read).
-//              The 4 reads of a lane are independent, then 4 ballots append
-//              the candidates to a per-wave LDS queue with mbcnt, so the queue
-//              is in reference order: n outer, position inner.
+//              (dword loads + v_alignbyte) and, once per superblock, the
+//              filter words those positions need: the 1-byte and 2-byte
+//              exact-bitmap words and the prefix-Bloom word chosen by the
+//              position's first three bytes (shared by every key length
+//              >= 3, ldgpu_common.h).  Each gram length n then tests one bit
+//              of a word already in a register (a 24-bit multiply and a bit
+//              extract), and a ballot appends the candidates to a per-wave LDS
+//              queue with mbcnt, so the queue is in reference order: n outer,
+//              position inner.
 //   verify     64 queued keys at a time probe the global open-addressed table
 //              (32-B slots carrying key, row, value and mask word 0).
 //   accumulate hits are replayed in queue order; lane l owns language l
@@ -28,7 +31,9 @@
 //              (x + 0.0 == x because s never is -0.0).
 //   argmax     lane-local over slices, then a 6-step xor-shuffle reduction on
 //              (value, index) with the breeze rule.
-// Documents longer than 256 bytes loop n outer, superblocks inner.
+// Documents of max(G)..256 bytes take a fast path (all windows full-length,
+// one superblock); shorter (partial windows) and longer ones loop n outer,
+// superblocks inner.
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
@@ -51,50 +56,19 @@ __device__ __forceinline__ uint32_t ld_dw(const uint32_t* w, int64_t i, int64_t 
     return w[i < last ? i : last];
 }
 
-// Raw dwords of one superblock: lane's positions base + 64k + lane, k < 4,
-// need dwords (a >> 2) + {0, 1, 2}.
-struct SbWords {
-    uint32_t w[kSub][3];
-};
-
-__device__ __forceinline__ void load_sb(const uint32_t* W, int64_t base, int lane, int64_t last, SbWords& r) {
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        const int64_t i = (base + 64 * k + lane) >> 2;
-        r.w[k][0] = ld_dw(W, i, last);
-        r.w[k][1] = ld_dw(W, i + 1, last);
-        r.w[k][2] = ld_dw(W, i + 2, last);
-    }
-}
-
 struct Windows {
     uint32_t lo[kSub], hi[kSub];  // bytes [a, a+4) and [a+4, a+8) of each position
 };
 
-__device__ __forceinline__ void windows_of(const SbWords& r, int64_t base, int lane, Windows& x) {
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        const uint32_t sh = (uint32_t)((base + 64 * k + lane) & 3);
-        x.lo[k] = __builtin_amdgcn_alignbyte(r.w[k][1], r.w[k][0], sh);
-        x.hi[k] = __builtin_amdgcn_alignbyte(r.w[k][2], r.w[k][1], sh);
-    }
-}
-
 struct GramCtx {
-    int32_t nwin;        // windows of this gram length (docs < 2^29 bytes)
-    int32_t klen;        // key length: n, or len for a partial window
-    uint32_t lomask, himask, hitag, himix_c;
+    int32_t nwin;  // windows of this gram length (docs < 2^29 bytes)
+    int32_t klen;  // key length: n, or len for a partial window
 };
 
 __device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
     GramCtx g;
     g.nwin = (int32_t)n_windows(len, n);
     g.klen = len < n ? (int)len : n;
-    const int klen = g.klen;
-    g.lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
-    g.himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
-    g.hitag = (uint32_t)klen << 24;
-    g.himix_c = hi_mix(g.hitag);
     return g;
 }
 
@@ -289,66 +263,122 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
     }
 }
 
-// Append one sub-block's candidates (pred) to the queue in lane order.
-__device__ __forceinline__ void append(uint32_t* queue, int& qn, bool pred, uint32_t tag) {
-    const uint64_t m = __ballot(pred);
-    if (m) {
-        const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (pred) queue[qn + off] = tag;
-        qn += __popcll(m);
-    }
+// The prefix-Bloom words the positions of one superblock need (chosen by
+// each position's first three bytes and shared by every key length >= 3,
+// ldgpu_common.h): loaded once per superblock, they serve every gram length
+// >= 3 of the document.  The 1-/2-byte bitmap words are read per test (one
+// gram length each; caching them would cost 8 VGPRs of occupancy).
+struct FWords {
+    uint32_t w3[kSub];
+};
+
+__device__ __forceinline__ void load_fwords(const ScoreParams& p, const uint32_t* bloom, const Windows& x,
+                                            FWords& f) {
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) f.w3[k] = bloom[pf_word(x.lo[k], p.bloom_shift)];
 }
 
-// 1- and 2-byte keys: exact LDS bitmaps.
-__device__ __forceinline__ void probe_direct(const uint32_t* img, uint32_t* queue, int& qn, const GramCtx& g,
-                                             const Windows& x, int32_t p0, int lane) {
-    const int32_t nw = g.nwin - p0;  // windows left from p0 (> 0)
-    const uint32_t base = g.klen == 1 ? 0u : kBmp1Words;
-    uint32_t idx[kSub], word[kSub];
+// Filter-test the (up to) 256 windows of one superblock for one key length:
+// m[k] = candidate mask of sub-block k < NSB (bit i = position p0 + 64k + i;
+// NSB = sub-blocks holding a window).  A test is a bit extract of a word
+// already in a register; f holds the prefix-Bloom words when KLEN >= 3.
+// nw = windows left from the superblock's first position, in
+// (64 (NSB - 1), 64 NSB] when NSB < 4.  Straight-line code: no per-sub-block
+// branches for the compiler to merge values across.
+template <int KLEN, int NSB>
+__device__ __forceinline__ void test_len(const uint32_t* img, const FWords& f, const Windows& x, int32_t nw,
+                                         int lane, uint64_t (&m)[kSub]) {
+    uint32_t w[NSB];
 #pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        idx[k] = x.lo[k] & g.lomask;
-        word[k] = img[base + (idx[k] >> 5)];
+    for (int k = 0; k < NSB; ++k) {
+        if constexpr (KLEN == 1)
+            w[k] = img[(x.lo[k] >> 5) & 7u];
+        else if constexpr (KLEN == 2)
+            w[k] = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
+        else
+            w[k] = f.w3[k];
     }
-    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)(p0 + lane);
 #pragma unroll
-    for (int k = 0; k < kSub; ++k)
-        append(queue, qn, (64 * k + lane < nw) && ((word[k] >> (idx[k] & 31u)) & 1u), tag + 64u * k);
+    for (int k = 0; k < NSB; ++k) {
+        const uint32_t c = __builtin_amdgcn_ubfe(w[k], KLEN <= 2 ? x.lo[k] : pf_bit(KLEN, x.lo[k], x.hi[k]), 1);
+        m[k] = __builtin_amdgcn_ballot_w64(c != 0u && (k < NSB - 1 || lane < nw - 64 * k));
+    }
+#pragma unroll
+    for (int k = NSB; k < kSub; ++k) m[k] = 0;
 }
 
-// 3..7-byte keys: one multiply (two when BIG: 5..7 bytes), blocked Bloom.
-template <bool BIG>
-__device__ __forceinline__ void probe_bloom(const ScoreParams& p, const uint32_t* bloom, uint32_t* queue, int& qn,
-                                            const GramCtx& g, const Windows& x, int32_t p0, int lane) {
-    const int32_t nw = g.nwin - p0;
-    uint32_t h[kSub], word[kSub];
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        const uint32_t lo = x.lo[k] & g.lomask;
-        const uint32_t himix = BIG ? hi_mix(g.hitag | (x.hi[k] & g.himask)) : g.himix_c;
-        h[k] = filter_hash(lo, himix);
-        word[k] = bloom[h[k] >> p.bloom_shift];
-    }
-    const uint32_t tag = ((uint32_t)g.klen << kPosBits) | (uint32_t)(p0 + lane);
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        const uint32_t fb = filter_bits(h[k], p.bloom_shift);
-        append(queue, qn, (64 * k + lane < nw) && ((word[k] & fb) == fb), tag + 64u * k);
-    }
-}
-
-// Filter-test the (up to) 256 windows of one superblock for one gram length
-// and append the candidates to the queue in position order.  The caller
-// guarantees qn <= kQueueCap - 256.
-__device__ __forceinline__ void probe_sb(const ScoreParams& p, const uint32_t* img, const uint32_t* bloom,
-                                         uint32_t* queue, int& qn, const GramCtx& g, const Windows& x, int32_t p0,
-                                         int lane) {
-    if (g.klen <= 2)
-        probe_direct(img, queue, qn, g, x, p0, lane);
-    else if (g.klen <= 4)
-        probe_bloom<false>(p, bloom, queue, qn, g, x, p0, lane);
+template <int KLEN>
+__device__ __forceinline__ void test_nsb(const uint32_t* img, const FWords& f, const Windows& x, int32_t nw, int lane,
+                                         uint64_t (&m)[kSub]) {
+    if (nw > 192)
+        test_len<KLEN, 4>(img, f, x, nw, lane, m);
+    else if (nw > 128)
+        test_len<KLEN, 3>(img, f, x, nw, lane, m);
+    else if (nw > 64)
+        test_len<KLEN, 2>(img, f, x, nw, lane, m);
     else
-        probe_bloom<true>(p, bloom, queue, qn, g, x, p0, lane);
+        test_len<KLEN, 1>(img, f, x, nw, lane, m);
+}
+
+__device__ __forceinline__ void test_sb(const uint32_t* img, int klen, const FWords& f, const Windows& x, int32_t nw,
+                                        int lane, uint64_t (&m)[kSub]) {
+    switch (klen) {
+        case 1: test_nsb<1>(img, f, x, nw, lane, m); break;
+        case 2: test_nsb<2>(img, f, x, nw, lane, m); break;
+        case 3: test_nsb<3>(img, f, x, nw, lane, m); break;
+        case 4: test_nsb<4>(img, f, x, nw, lane, m); break;
+        case 5: test_nsb<5>(img, f, x, nw, lane, m); break;
+        case 6: test_nsb<6>(img, f, x, nw, lane, m); break;
+        default: test_nsb<7>(img, f, x, nw, lane, m); break;
+    }
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// per lane: bit `lane` of m ? a : b (one v_cndmask on the mask itself)
+__device__ __forceinline__ uint32_t select_by_mask(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+
+// Append the candidates of one superblock to the queue in position order;
+// the caller guarantees room for every set bit.  Every lane stores (no exec
+// juggling): a candidate to its queue rank, the others to their own word of
+// the wave's hit area (idle while probing), at byte address dummy_a.
+__device__ __forceinline__ void append_sb(uint32_t* queue, uint32_t dummy_a, int& qn, const uint64_t (&m)[kSub],
+                                          int klen, int32_t p0, int lane) {
+    const uint32_t tag0 = ((uint32_t)klen << kPosBits) | (uint32_t)(p0 + lane);
+    const uint32_t qbase = (uint32_t)(uintptr_t)queue;  // LDS offset (low half of the flat address)
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        if (m[k]) {
+            const uint32_t off =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
+            const uint32_t a = select_by_mask(m[k], qbase + 4u * ((uint32_t)qn + off), dummy_a);
+            *(lds_u32*)(size_t)a = tag0 + 64u * k;
+            qn += __popcll(m[k]);
+        }
+    }
+}
+
+__device__ __forceinline__ int count_sb(const uint64_t (&m)[kSub]) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) t += __popcll(m[k]);
+    return t;
+}
+
+template <bool STAGED>
+__device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc& src, int32_t p0, int lane,
+                                             Windows& x) {
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        uint32_t w0, w1, w2, sh;
+        window_words<STAGED>(p, src, p0 + 64 * k + lane, w0, w1, w2, sh);
+        x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    }
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
@@ -360,47 +390,55 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
 #pragma unroll
     for (int s = 0; s < S; ++s) acc[s] = 0.0;
     int qn = 0;
-    if (len >= kMaxDocBytes) {
-        if (lane == 0) atomicOr(p.err, 2);
-    } else if (len <= 64 * kSub) {
-        // one superblock: every gram length reuses the same window bytes
-        Windows x;
+    const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
+    if (len >= p.maxg && len <= 64 * kSub) {
+        // fast path: every window is full-length (klen = n) and one
+        // superblock covers the document, so every gram length reuses the
+        // same window bytes and prefix-Bloom words
+        if (p.n_fast && !(p.ablate & 2)) {
+            Windows x;
+            load_windows<STAGED>(p, src, 0, lane, x);
+            FWords f;
+            load_fwords(p, bloom, x, f);
+            uint64_t gq = p.gpack[0];
+            for (int gi = 0; gi < p.n_fast; ++gi) {
+                const int n = (int)(gq & 15u);
+                gq = (gi & 15) == 15 ? p.gpack[1] : gq >> 4;
+                // pin the tests inside this loop: hoisted out of it (they are
+                // loop-invariant), the tests of all 7 lengths would run per doc
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            uint32_t w0, w1, w2, sh;
-            window_words<STAGED>(p, src, 64 * k + lane, w0, w1, w2, sh);
-            x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        }
-        for (int gi = 0; gi < p.nG; ++gi) {
-            const GramCtx g = gram_ctx(len, p.G[gi]);
-            if (!((p.len_mask >> g.klen) & 1u) || g.nwin == 0) continue;  // no key of this length
-            if (p.ablate & 2) continue;
-            if (qn > kQueueCap - 64 * kSub) {
-                flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
-                qn = 0;
+                for (int k = 0; k < kSub; ++k) asm volatile("" : "+v"(x.lo[k]), "+v"(x.hi[k]), "+v"(f.w3[k]));
+                uint64_t m[kSub];
+                test_sb(img, n, f, x, (int32_t)len - n + 1, lane, m);
+                if (qn + count_sb(m) > kQueueCap) {  // rare: verify what is queued first
+                    flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
+                    qn = 0;
+                    load_windows<STAGED>(p, src, 0, lane, x);  // reloaded: not live across the flush
+                    load_fwords(p, bloom, x, f);
+                }
+                append_sb(wl.queue, dummy_a, qn, m, n, 0, lane);
             }
-            probe_sb(p, img, bloom, wl.queue, qn, g, x, 0, lane);
         }
+    } else if (len >= kMaxDocBytes) {
+        if (lane == 0) atomicOr(p.err, 2);
     } else {
-        // long documents: n outer (reference order), superblocks inner
+        // general path: partial windows (len < n) and long documents; n outer
+        // (reference order), superblocks inner
         for (int gi = 0; gi < p.nG; ++gi) {
             const GramCtx g = gram_ctx(len, p.G[gi]);
-            if (!((p.len_mask >> g.klen) & 1u)) continue;
+            if (!((p.len_mask >> g.klen) & 1u) || (p.ablate & 2)) continue;
             for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
                 Windows x;
-#pragma unroll
-                for (int k = 0; k < kSub; ++k) {
-                    uint32_t w0, w1, w2, sh;
-                    window_words<STAGED>(p, src, p0 + 64 * k + lane, w0, w1, w2, sh);
-                    x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                    x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                }
-                if (qn > kQueueCap - 64 * kSub) {
+                load_windows<STAGED>(p, src, p0, lane, x);
+                FWords f;
+                if (g.klen >= 3) load_fwords(p, bloom, x, f);
+                uint64_t m[kSub];
+                test_sb(img, g.klen, f, x, g.nwin - p0, lane, m);
+                if (qn + count_sb(m) > kQueueCap) {
                     flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
                     qn = 0;
                 }
-                probe_sb(p, img, bloom, wl.queue, qn, g, x, p0, lane);
+                append_sb(wl.queue, dummy_a, qn, m, g.klen, p0, lane);
             }
         }
     }
@@ -456,7 +494,7 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
 }
 
 template <int S, int MODE, bool FLDS>
-__global__ __launch_bounds__(kScoreWaves * 64) void score_kernel(const ScoreParams p) {
+__global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
