@@ -299,22 +299,50 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
             memcpy(&drows[(size_t)i * n_langs], rows + src_row[i] * (int64_t)n_langs, sizeof(double) * n_langs);
     }
 
-    // key -> row slots (mask form: the row's value and first mask word inline)
-    m->slot_cap = next_pow2(std::max<uint64_t>(16, 2 * (uint64_t)nk));
-    const int slog = log2u(m->slot_cap);
-    std::vector<Slot> slots(m->slot_cap, Slot{kEmpty, 0, 0, 0.0, 0});
-    for (int64_t i = 0; i < nk; ++i) {
-        uint64_t s = mix64(keys[i]) >> (64 - slog);
-        while (slots[s].key != kEmpty) s = (s + 1) & (m->slot_cap - 1);
-        slots[s].key = keys[i];
-        slots[s].row = (uint32_t)i;
-        if (!dense) {
-            slots[s].val = vals[i];
-            slots[s].mask0 = masks[(size_t)i * S];
+    // key -> row slots (mask form: the row's value and first mask word inline),
+    // 2-choice cuckoo hashing: a key sits in slot h >> (64 - log2 cap) or
+    // slot h & (cap - 1) of h = mix64(key), so the device verifies a candidate
+    // with two independent loads and no probe loop.  Load <= 0.4 (2.5 slots
+    // per key) lets the cuckoo walk settle in a few steps; a walk that does
+    // not settle doubles the table and starts over.
+    std::vector<Slot> slots;
+    for (m->slot_cap = next_pow2(std::max<uint64_t>(16, (uint64_t)(2.5 * (double)nk) + 1));;
+         m->slot_cap *= 2) {
+        const int slog = log2u(m->slot_cap);
+        const uint64_t cmask = m->slot_cap - 1;
+        auto pos1 = [&](uint64_t k) { return mix64(k) >> (64 - slog); };
+        auto pos2 = [&](uint64_t k) { return mix64(k) & cmask; };
+        slots.assign(m->slot_cap, Slot{kEmpty, 0, 0, 0.0, 0});
+        bool ok_all = true;
+        for (int64_t i = 0; i < nk && ok_all; ++i) {
+            Slot cur{keys[i], (uint32_t)i, 0, 0.0, 0};
+            if (!dense) {
+                cur.val = vals[i];
+                cur.mask0 = masks[(size_t)i * S];
+            }
+            if (row_ok && !row_ok[src_row[i]]) {
+                cur.row |= kBadRow;
+                m->has_bad = true;
+            }
+            uint64_t at = pos1(cur.key);
+            if (slots[at].key != kEmpty && slots[pos2(cur.key)].key == kEmpty) at = pos2(cur.key);
+            bool placed = false;
+            for (int step = 0; step < 2000; ++step) {
+                if (slots[at].key == kEmpty) {
+                    slots[at] = cur;
+                    placed = true;
+                    break;
+                }
+                std::swap(cur, slots[at]);  // evict; the evicted key moves to its other slot
+                const uint64_t a = pos1(cur.key), b = pos2(cur.key);
+                at = at == a ? b : a;
+            }
+            ok_all = placed;
         }
-        if (row_ok && !row_ok[src_row[i]]) {
-            slots[s].row |= kBadRow;
-            m->has_bad = true;
+        if (ok_all) break;
+        if (m->slot_cap >= (1ull << 34)) {
+            delete m;
+            return fail(LDGPU_ENOMEM, "key table: cuckoo placement failed");
         }
     }
 
@@ -414,7 +442,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.scores = d_scores;
     p.slots = m->d_slots;
     const int slog = log2u(m->slot_cap);
-    p.slot_shift = (uint32_t)(64 - slog);
+    p.slot_shift = (uint32_t)(64 - slog);  // slot 1 = h >> slot_shift, slot 2 = h & slot_mask
     p.slot_mask = m->slot_cap - 1;
     p.filter = m->d_filter;
     p.bloom_shift = (uint32_t)(32 - m->filter_log2);

@@ -174,25 +174,21 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             const int klen = (int)(e >> kPosBits);
             uint32_t w0, w1, w2, sh;
             window_words<STAGED>(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
-            uint64_t key = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            if (klen > 4) {
-                const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                key |= (uint64_t)(hi & ((1u << (8 * (klen - 4))) - 1u)) << 32;
-            } else if (klen < 4) {
-                key &= (1ull << (8 * klen)) - 1ull;
-            }
-            key |= (uint64_t)klen << 56;
-            uint64_t s = mix64(key) >> p.slot_shift;
-            for (;;) {
-                const Slot sl = p.slots[s];
-                if (sl.key == key) {
-                    row = sl.row;
-                    v = sl.val;
-                    m0 = sl.mask0;
-                    break;
-                }
-                if (sl.key == kEmpty) break;
-                s = (s + 1) & p.slot_mask;
+            const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
+                                 __builtin_amdgcn_alignbyte(w1, w0, sh);
+            const uint64_t key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
+            // 2-choice cuckoo table: the key is in one of two slots (or absent)
+            const uint64_t h = mix64(key);
+            const Slot a = p.slots[h >> p.slot_shift];
+            const Slot c = p.slots[h & p.slot_mask];
+            if (a.key == key) {
+                row = a.row;
+                v = a.val;
+                m0 = a.mask0;
+            } else if (c.key == key) {
+                row = c.row;
+                v = c.val;
+                m0 = c.mask0;
             }
         }
         const bool hit = row != 0xffffffffu;
