@@ -28,7 +28,7 @@ struct ScoreParams {
     const double* rows;         // dense mode: [rows][L]
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     int32_t L;
-    int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe
+    int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay
     int32_t nG;
     int32_t G[kMaxGramLengths];
     // fast path (documents of maxg..256 bytes: every window full-length):

@@ -223,7 +223,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                                                   (uint32_t)words[2 * q + 1], (uint32_t)(words[2 * q + 1] >> 32));
             }
             __builtin_amdgcn_wave_barrier();
-            const int nh = __popcll(hits);
+            const int nh = (p.ablate & 4) ? 0 : __popcll(hits);
             int t = 0;
             // 4 broadcast reads in flight, then 4 ordered adds
             for (; t + 4 <= nh; t += 4) {
