@@ -296,7 +296,7 @@ def main():
                                f"grams {args.grams}, profile size {args.profile_size}",
                    "docs_per_gpu": n_docs, "doc_bytes": doc_b, "languages": args.langs, "gram_lengths": grams,
                    "profile_size": args.profile_size, "table_rows": info["n_keys"],
-                   "table_mode": "mask" if info["mode"] == 0 else "dense",
+                   "table_mode": {0: "mask", 1: "dense", 2: "mask, one shared value (hit counts)"}[info["mode"]],
                    "parallelism": f"dp{world} (documents sharded, no collective)"},
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -82,8 +82,11 @@ int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
                        ldgpu_model** out);
 int ldgpu_model_destroy(ldgpu_model* model);
 
-/* mode: 0 = every row is one value times a language bitmask (fit-produced
- * tables), 1 = dense fp64 rows.  n_keys: keys resident on the device. */
+/* mode: 0 = every row is one value times a language bitmask, 1 = dense fp64
+ * rows, 2 = mask form where every row shares ONE finite value (fit-produced
+ * tables whose grams all have the same presence class, e.g. all unique to one
+ * language): scored from per-language hit counts.  n_keys: keys resident on
+ * the device. */
 int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
                      int64_t* table_slots, int64_t* filter_bits, int64_t* device_bytes);
 

@@ -171,7 +171,7 @@ struct ldgpu_model {
     int32_t G[kMaxGramLengths] = {};
     int slices = 1;
     bool dense = false;
-    int mode = 0;             // kernel mode: 0 mask, 1 mask + finite values, 2 dense
+    int mode = 0;             // kernel mode: 0 mask, 1 mask + finite values, 2 dense, 3 mask + one finite value
     bool lds_filter = true;
     bool has_bad = false;
     int64_t n_keys = 0;
@@ -187,15 +187,19 @@ struct ldgpu_model {
     uint64_t* d_masks = nullptr;
     double* d_vals = nullptr;
     double* d_rows = nullptr;
+    double* d_fold = nullptr;  // mode 3: fold[c], c = 0..kFoldMax
     int32_t* d_err = nullptr;
 };
+
+// mode 3 fold table: fold[c] = ((0.0 + v) + v) ... c times
+constexpr uint32_t kFoldMax = 8191;
 
 namespace {
 void model_free(ldgpu_model* m) {
     if (!m) return;
     if (m->ctx) (void)hipSetDevice(m->ctx->device);
     for (void* p : {(void*)m->d_slots, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
-                    (void*)m->d_err})
+                    (void*)m->d_fold, (void*)m->d_err})
         if (p) (void)hipFree(p);
     delete m;
 }
@@ -279,7 +283,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     m->n_keys = nk;
 
     std::vector<uint64_t> masks;
-    std::vector<double> vals, drows;
+    std::vector<double> vals, drows, fold;
     m->mode = dense ? 2 : 1;
     if (!dense) {
         masks.assign((size_t)nk * S, 0);
@@ -292,6 +296,32 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
                 vals[i] = rw[l];
                 if (!std::isfinite(rw[l])) m->mode = 0;
             }
+        }
+        // one value shared by every row with a nonzero entry: order-free
+        // per-language hit counts (mode 3) reproduce the fold exactly
+        bool have_v = false, uniform = m->mode == 1;
+        uint64_t vbits = 0;
+        for (int64_t i = 0; i < nk && uniform; ++i) {
+            bool any = false;
+            for (int s = 0; s < S; ++s) any |= masks[(size_t)i * S + s] != 0;
+            if (!any) continue;
+            uint64_t b;
+            memcpy(&b, &vals[i], 8);
+            if (!have_v) {
+                vbits = b;
+                have_v = true;
+            } else if (b != vbits) {
+                uniform = false;
+            }
+        }
+        if (const char* f = getenv("LDGPU_NO_COUNT_MODE")) uniform &= atoi(f) == 0;  // tests cover both paths
+        if (uniform) {
+            m->mode = 3;
+            double v;
+            memcpy(&v, &vbits, 8);
+            fold.resize(kFoldMax + 1);
+            fold[0] = 0.0;
+            for (uint32_t c = 1; c <= kFoldMax; ++c) fold[c] = fold[c - 1] + v;
         }
     } else {
         drows.resize((size_t)nk * n_langs);
@@ -387,6 +417,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (e == hipSuccess) e = upload(&m->d_masks, masks, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_vals, vals, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_rows, drows, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_fold, fold, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
     m->lds_bytes = score_lds_bytes(S, m->lds_filter, (uint32_t)bwords);
     int resident = 0;
@@ -417,7 +448,7 @@ extern "C" int ldgpu_model_destroy(ldgpu_model* m) {
 extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_keys, int64_t* table_slots,
                                 int64_t* filter_bits, int64_t* device_bytes) {
     if (!m) return fail(LDGPU_EINVAL, "model is NULL");
-    if (mode) *mode = m->dense ? 1 : 0;
+    if (mode) *mode = m->dense ? 1 : (m->mode == 3 ? 2 : 0);
     if (n_keys) *n_keys = m->n_keys;
     if (table_slots) *table_slots = (int64_t)m->slot_cap;
     if (filter_bits) *filter_bits = ((int64_t)1 << m->filter_log2) * 32;  // bloom bits
@@ -451,6 +482,8 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.masks = m->d_masks;
     p.vals = m->d_vals;
     p.rows = m->d_rows;
+    p.fold = m->d_fold;
+    p.fold_max = kFoldMax;
     p.err = m->d_err;
     p.L = m->L;
     p.ablate = m->ablate;

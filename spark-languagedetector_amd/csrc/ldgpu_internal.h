@@ -26,6 +26,8 @@ struct ScoreParams {
     const uint64_t* masks;      // mask mode: [rows][S] language bitmasks
     const double* vals;         // mask mode: [rows] the row's one nonzero value
     const double* rows;         // dense mode: [rows][L]
+    const double* fold;         // count mode: fold[c] = c left-folded adds of the value, c <= fold_max
+    uint32_t fold_max;
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     int32_t L;
     int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay
@@ -63,7 +65,8 @@ inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) 
 }
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values
-// (fma accumulate), 2 = dense fp64 rows; lds_bloom = bloom staged in LDS
+// (fma accumulate), 2 = dense fp64 rows, 3 = mask rows sharing one finite
+// value (per-language hit counts); lds_bloom = bloom staged in LDS
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream);
 // sets the dynamic-LDS limit and returns the resident workgroups per CU
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu);

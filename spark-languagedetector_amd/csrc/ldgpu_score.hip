@@ -76,8 +76,14 @@ __device__ __forceinline__ GramCtx gram_ctx(int64_t len, int n) {
 struct WaveLds {
     uint32_t* queue;  // [kQueueCap] candidate entries (klen << 29 | position)
     uint64_t* hits;   // [64][S + 1] verified hits of one chunk: value bits, mask words
+                      // (MODE 3: the document's per-language hit counters, count_area)
     uint32_t* buf;    // [kBufBytes / 4 + 4] staged bytes of the current document group
 };
+
+// MODE 3 per-language hit counters: after the first 64 words of the hit area,
+// which take the probe's dummy stores (append_sb); 64 + 64 S words fit the
+// area (64 x 16 x kHitQuads<S> bytes) for every S.
+__device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return reinterpret_cast<uint32_t*>(w.hits) + 64; }
 
 // Where a document's bytes are read from: the wave's LDS buffer (staged
 // group: byte `base` of the buffer) or global memory (byte `base` of p.bytes).
@@ -197,6 +203,24 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             if (lane == 0) atomicOr(p.err, 1);
         }
         const bool good = hit && !bad;
+        if constexpr (MODE == 3) {
+            // uniform-value table: order-free per-language hit counts (the
+            // score is the fold of that many adds of the one value, applied
+            // at the end of the document: count_scores)
+            if (good) {
+                uint32_t* cnt = count_area(w);
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    uint64_t mm = s == 0 ? m0 : p.masks[(size_t)row * S + s];
+                    while (mm) {
+                        const int l = __builtin_ctzll(mm);
+                        mm &= mm - 1;
+                        __hip_atomic_fetch_add(&cnt[64 * s + l], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+            continue;
+        }
         const uint64_t hits = __ballot(good);
         if (!hits) continue;
         constexpr bool DENSE = MODE == 2;
@@ -255,6 +279,30 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                     if (l < p.L) acc[s] = acc[s] + rp[l];
                 }
             }
+        }
+    }
+}
+
+// MODE 3: turn the document's per-language hit counts into scores and clear
+// the counters for the next document.  Every add the reference makes to s_l
+// is s_l + v (a member hit) or s_l + 0.0 (exact: s_l is never -0.0), so s_l is
+// the left fold of c_l adds of v: fold[c] (host-computed, bit-identical),
+// continued on the device past the table's end.
+template <int S>
+__device__ __forceinline__ void count_scores(const ScoreParams& p, const WaveLds& w, double (&acc)[S], int lane) {
+    uint32_t* cnt = count_area(w);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int l = 64 * s + lane;
+        if (l < p.L) {
+            const uint32_t c = cnt[l];
+            cnt[l] = 0;
+            double v = 0.0;
+            if (c) {
+                v = p.fold[c < p.fold_max ? c : p.fold_max];
+                for (uint32_t i = p.fold_max; i < c; ++i) v = v + p.fold[1];
+            }
+            acc[s] = v;
         }
     }
 }
@@ -440,6 +488,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
     }
     if (p.ablate & 1) qn = 0;
     if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
+    if constexpr (MODE == 3) count_scores<S>(p, wl, acc, lane);
 
     // argmax (breeze: first element, then strict '>' updates): the wave max M
     // of the non-NaN scores by DPP (no LDS), then the first index holding M;
@@ -507,6 +556,13 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     wl.queue = lds + img_words + wave * kQueueCap;
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * 2 * kHitQuads<S>;
     wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 4 * kHitQuads<S> + wave * kBufWords;
+
+    if constexpr (MODE == 3) {
+        uint32_t* cnt = count_area(wl);
+#pragma unroll
+        for (int s = 0; s < S; ++s) cnt[64 * s + lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+    }
 
     // this wave's contiguous range of documents, walked in groups of p.group
     const int64_t nwaves = (int64_t)gridDim.x * kScoreWaves;
@@ -609,6 +665,7 @@ hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_blo
         case 0: return launch_m<0>(p, slices, lds_bloom, grid, stream);
         case 1: return launch_m<1>(p, slices, lds_bloom, grid, stream);
         case 2: return launch_m<2>(p, slices, lds_bloom, grid, stream);
+        case 3: return launch_m<3>(p, slices, lds_bloom, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -618,6 +675,7 @@ hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes,
         case 0: return prepare_m<0>(slices, lds_bloom, lds_bytes, blocks_per_cu);
         case 1: return prepare_m<1>(slices, lds_bloom, lds_bytes, blocks_per_cu);
         case 2: return prepare_m<2>(slices, lds_bloom, lds_bytes, blocks_per_cu);
+        case 3: return prepare_m<3>(slices, lds_bloom, lds_bytes, blocks_per_cu);
         default: return hipErrorInvalidValue;
     }
 }

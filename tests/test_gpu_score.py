@@ -77,7 +77,8 @@ def test_detect_static_string_and_bytes():
     assert LanguageDetectorModel.detect("", table, ["de", "en"], [3]) == "de"  # no hit -> index 0
 
 
-def _random_table(rng, L, n_keys, grams, alphabet, mask_form):
+def _random_table(rng, L, n_keys, grams, alphabet, mask_form, uniform=None):
+    """uniform: one shared value for every row (the count-mode kernel)."""
     table = {}
     for _ in range(n_keys):
         n = int(rng.choice(grams))
@@ -86,7 +87,7 @@ def _random_table(rng, L, n_keys, grams, alphabet, mask_form):
             m = rng.random(L) < rng.uniform(0.02, 0.6)
             if not m.any():
                 m[int(rng.integers(0, L))] = True
-            v = math.log(1.0 + 1.0 / int(m.sum()))
+            v = uniform if uniform is not None else math.log(1.0 + 1.0 / int(m.sum()))
             table[k] = [v if b else 0.0 for b in m]
         else:
             table[k] = rng.normal(size=L).tolist()
@@ -108,6 +109,47 @@ def test_random_parity(L, grams, mask_form):
     data, off = encoding.pack(docs)
     m = check_parity(table, L, grams, data, off)
     assert m.info()["mode"] == (0 if mask_form else 1)
+
+
+@pytest.fixture(params=["count", "replay"])
+def uniform_path(request, monkeypatch):
+    """Uniform-value tables run the count kernel (mode 2); LDGPU_NO_COUNT_MODE
+    forces the ordered-replay kernel on the same table (mode 0)."""
+    if request.param == "replay":
+        monkeypatch.setenv("LDGPU_NO_COUNT_MODE", "1")
+    return 2 if request.param == "count" else 0
+
+
+@pytest.mark.parametrize("L,grams,v", [
+    (3, [1, 2, 3], math.log(2.0)), (20, [1, 2, 3, 4, 5], math.log(2.0)), (64, [2, 3], 1.0),
+    (65, [3, 1], 0.1), (130, [1, 2, 3, 4, 5, 6, 7], -0.7), (256, [4, 2], 1e-300),
+])
+def test_uniform_value_parity(L, grams, v, uniform_path):
+    """One value in every row (all of a fit table's grams in one presence
+    class): per-language counts folded through the value must equal the
+    reference's ordered daxpy fold bit for bit, negative and tiny values too."""
+    rng = np.random.default_rng(L * 11 + len(grams))
+    alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+    table = _random_table(rng, L, 400, grams, alphabet, True, uniform=v)
+    lens = rng.integers(0, 300, size=600)
+    lens[:8] = [0, 1, 2, 3, 6, 7, 64, 65]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, grams, data, off)
+    assert m.info()["mode"] == uniform_path
+
+
+def test_uniform_value_counts_past_fold_table(uniform_path):
+    """A language hit more than 8191 times in one document: the device
+    continues the fold past the host-built table."""
+    L = 3
+    table = {bytes([c]): [0.3 if (c % 3) == l else 0.0 for l in range(L)] for c in range(256)}
+    table[b"ab"] = [0.3, 0.3, 0.0]
+    rng = np.random.default_rng(17)
+    docs = [b"ab" * 9000, bytes(rng.integers(0, 256, size=30000, dtype=np.uint8)), b"", b"a"]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, [1, 2, 1], data, off)
+    assert m.info()["mode"] == uniform_path
 
 
 def test_long_documents_and_hot_keys():
@@ -204,7 +246,8 @@ def test_bench_shape_parity_sample():
     rows = list(zip([ls.names[i] for i in tlang], synth.texts(tdata, toff)))
     table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3, 4, 5], 500, ls.names)
     data, off, _ = synth.generate(ls, 20000, 256, 256, seed=synth.SEED_BASE + 2)
-    check_parity(table, 20, [1, 2, 3, 4, 5], data, off)
+    m = check_parity(table, 20, [1, 2, 3, 4, 5], data, off)
+    assert m.info()["mode"] == 2  # every chosen gram unique to one language: count kernel
 
 
 def test_config4_shape_parity_short_docs_100_langs():
@@ -217,7 +260,7 @@ def test_config4_shape_parity_short_docs_100_langs():
     table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3, 4, 5], 1000, ls.names)
     data, off, _ = synth.generate(ls, 20000, 32, 96, seed=synth.SEED_BASE + 5)
     m = check_parity(table, 100, [1, 2, 3, 4, 5], data, off)
-    assert m.info()["mode"] == 0
+    assert m.info()["mode"] in (0, 2)
 
 
 def test_config5_shape_parity_large_profile_global_filter():
