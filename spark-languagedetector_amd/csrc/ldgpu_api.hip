@@ -188,6 +188,8 @@ struct ldgpu_model {
     double* d_vals = nullptr;
     double* d_rows = nullptr;
     double* d_fold = nullptr;  // mode 3: fold[c], c = 0..kFoldMax
+    int count_sign = 0;        // mode 3: sign of the shared value
+    bool count_int_argmax = false;  // mode 3: label = first max of the counts (monotone fold)
     int32_t* d_err = nullptr;
 };
 
@@ -322,6 +324,10 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
             fold.resize(kFoldMax + 1);
             fold[0] = 0.0;
             for (uint32_t c = 1; c <= kFoldMax; ++c) fold[c] = fold[c - 1] + v;
+            // |v| far from overflow: fold[c] (c < 2^24) is strictly monotone
+            // (each add moves it: |v| >> ulp(c |v|) / 2), so argmax needs only c
+            m->count_sign = v > 0.0 ? 1 : (v < 0.0 ? -1 : 0);
+            m->count_int_argmax = std::fabs(v) < 1e300;
         }
     } else {
         drows.resize((size_t)nk * n_langs);
@@ -484,6 +490,9 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.rows = m->d_rows;
     p.fold = m->d_fold;
     p.fold_max = kFoldMax;
+    p.count_sign = m->count_sign;
+    // counts stay below 2^24: c <= windows of a document <= len * n_grams
+    p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;
     p.err = m->d_err;
     p.L = m->L;
     p.ablate = m->ablate;

@@ -28,6 +28,8 @@ struct ScoreParams {
     const double* rows;         // dense mode: [rows][L]
     const double* fold;         // count mode: fold[c] = c left-folded adds of the value, c <= fold_max
     uint32_t fold_max;
+    int32_t count_sign;         // count mode: sign of the value (fold[c] strictly monotone)
+    int64_t count_argmax_len;   // count mode: documents up to this length take count_argmax (-1: none)
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     int32_t L;
     int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay
@@ -61,7 +63,7 @@ constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
 // bytes of dynamic LDS the score kernel needs
 inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) {
     return (size_t)(kBloomBase + (lds_bloom ? bloom_words : 0u)) * 4u +
-           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + kBufWords * 4u);
+           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + kBufWords * 4u + 64u * 4u);
 }
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values

@@ -78,6 +78,7 @@ struct WaveLds {
     uint64_t* hits;   // [64][S + 1] verified hits of one chunk: value bits, mask words
                       // (MODE 3: the document's per-language hit counters, count_area)
     uint32_t* buf;    // [kBufBytes / 4 + 4] staged bytes of the current document group
+    uint32_t* labels; // [64] labels of the current group
 };
 
 // MODE 3 per-language hit counters: after the first 64 words of the hit area,
@@ -135,6 +136,16 @@ __device__ __forceinline__ double wave_max_f64(double v) {
     LDGPU_DPP_MAX(v, 0x142, 0xa);  // row_bcast:15
     LDGPU_DPP_MAX(v, 0x143, 0xc);  // row_bcast:31
     return rdlaned(v, 63);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return rdlane(v, 63);
 }
 
 // One verified hit as LDS quads: {value, mask word 0}, {mask 1, mask 2}, ...
@@ -307,6 +318,28 @@ __device__ __forceinline__ void count_scores(const ScoreParams& p, const WaveLds
     }
 }
 
+// MODE 3 label without scores: fold[c] is strictly monotone in c (host-checked:
+// sign of the value p.count_sign, no overflow while c < 2^24), so the first
+// maximum of the scores is the first maximum of c (value > 0), of -c
+// (value < 0) or index 0 (value 0).  One integer DPP max over
+// (key << 8 | 255 - l); clears the counters.
+template <int S>
+__device__ __forceinline__ int count_argmax(const ScoreParams& p, const WaveLds& w, int lane) {
+    uint32_t* cnt = count_area(w);
+    uint32_t best = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int l = 64 * s + lane;
+        if (l < p.L) {
+            const uint32_t c = cnt[l];
+            cnt[l] = 0;
+            const uint32_t k = p.count_sign > 0 ? c : (p.count_sign < 0 ? 0xffffffu - c : 0u);
+            best = max(best, (k << 8) | (uint32_t)(255 - l));
+        }
+    }
+    return 255 - (int)(wave_max_u32(best) & 255u);
+}
+
 // The prefix-Bloom words the positions of one superblock need (chosen by
 // each position's first three bytes and shared by every key length >= 3,
 // ldgpu_common.h): loaded once per superblock, they serve every gram length
@@ -427,7 +460,7 @@ __device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc&
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
 template <int S, int MODE, bool STAGED>
-__device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+__device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                           const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
                                           const DocSrc& src, int lane) {
     double acc[S];
@@ -488,7 +521,10 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
     }
     if (p.ablate & 1) qn = 0;
     if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
-    if constexpr (MODE == 3) count_scores<S>(p, wl, acc, lane);
+    if constexpr (MODE == 3) {
+        if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, wl, lane);
+        count_scores<S>(p, wl, acc, lane);
+    }
 
     // argmax (breeze: first element, then strict '>' updates): the wave max M
     // of the non-NaN scores by DPP (no LDS), then the first index holding M;
@@ -511,7 +547,6 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
         }
     }
     if (__builtin_isnan(rdlaned(acc[0], 0))) label = 0;
-    if (lane == 0) p.labels[doc] = label;
     if (p.scores) {
         double* out = p.scores + doc * (int64_t)p.L;
 #pragma unroll
@@ -520,6 +555,7 @@ __device__ __forceinline__ void score_doc(const ScoreParams& p, const WaveLds& w
             if (l < p.L) out[l] = acc[s];
         }
     }
+    return label;
 }
 
 __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) { return (int64_t)rdlane64((uint64_t)v, l); }
@@ -556,6 +592,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     wl.queue = lds + img_words + wave * kQueueCap;
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * 2 * kHitQuads<S>;
     wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 4 * kHitQuads<S> + wave * kBufWords;
+    wl.labels = lds + img_words + kScoreWaves * (kQueueCap + 64 * 4 * kHitQuads<S> + kBufWords) + wave * 64;
 
     if constexpr (MODE == 3) {
         uint32_t* cnt = count_area(wl);
@@ -595,16 +632,21 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{wl.buf, b - s0};
-                score_doc<S, MODE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                if (lane == 0) wl.labels[i] = lab;
             }
         } else {
             for (int i = 0; i < cnt; ++i) {
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{nullptr, b};
-                score_doc<S, MODE, false>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, false>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                if (lane == 0) wl.labels[i] = lab;
             }
         }
+        // the group's labels: one coalesced store
+        __builtin_amdgcn_wave_barrier();
+        if (lane < cnt) p.labels[g0 + lane] = (int32_t)wl.labels[lane];
         __builtin_amdgcn_wave_barrier();
         offv = offn;
         g0 = g1;
