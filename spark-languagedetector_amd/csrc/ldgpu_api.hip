@@ -413,7 +413,11 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
         } else {
             const uint32_t lo = (uint32_t)keys[i];
             const uint32_t hi = (uint32_t)(keys[i] >> 32) & ((1u << (8 * std::max(0, kl - 4))) - 1u);
-            filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (pf_bit(kl, lo, hi) & 31u);
+            const uint32_t b = pf_bit(kl, lo, hi);
+            filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (b & 31u);
+#ifdef LDGPU_BLOOM_K2
+            filter[kBloomBase + pf_word(lo, bshift)] |= 1u << ((b >> 5) & 31u);
+#endif
         }
     }
 
@@ -503,6 +507,9 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     for (int i = 0; i < m->nG; ++i) {
         p.maxg = std::max(p.maxg, m->G[i]);
         if (!((m->len_mask >> m->G[i]) & 1u)) continue;  // no key of that length: never a hit
+        // count mode: hit order is free, a repeated length is scanned once
+        p.fast_mask |= 1u << m->G[i];
+        if (m->mode == 3 && p.mult[m->G[i]]++) continue;
         p.gpack[p.n_fast >> 4] |= (uint64_t)m->G[i] << (4 * (p.n_fast & 15));
         ++p.n_fast;
     }

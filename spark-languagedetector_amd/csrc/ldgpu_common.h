@@ -32,34 +32,32 @@ __host__ __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
 // Prefix Bloom filter for keys of 3..7 bytes.  A key lives in ONE 32-bit word
 // chosen by its first three bytes (so every length >= 3 of a window position
 // shares the word: one LDS read per position) and sets ONE bit of it, chosen
-// from bytes the key owns by a length-specific 24-bit multiply.  With
+// by a length-specific 24-bit multiply of three bytes the key owns.  With
 // lo = bytes 0..3 and hi = bytes 4..7 of the window (little-endian):
-//   word   = mul24(lo, kPfWord) >> (32 - wlog)             bytes 0..2
-//   bit(3) = mulhi24(lo, C3)                               bytes 0..2
-//   bit(4) = mulhi24(lo >> 8, C4)                          bytes 1..3
-//   bit(5) = mulhi24(lo >> 16 | hi << 16, C5)              bytes 2..4
-//   bit(6) = mulhi24(lo >> 24 | hi << 8, C6)               bytes 3..5
-//   bit(7) = mulhi24(x, C7) ^ mulhi24(x >> 8, C7b), x = lo >> 24 | hi << 8   bytes 3..6
-// (each mod 32).  No form reads a byte at or past klen, so the bytes after a
-// window never need masking.
+//   word   = mul24(lo, kPfWord) >> (32 - wlog)                       bytes 0..2
+//   bit(n) = mulhi24(alignbit(hi, lo, pf_shift(n)), pf_mult(n)) mod 32
+// pf_shift(n) = 8 min(n - 3, 3): bytes n-3..n-1 for n <= 6, bytes 3..5 for
+// n = 7.  No form reads a byte at or past n, so the bytes after a window never
+// need masking, and every length runs the same two instructions.
 constexpr uint32_t kPfWord = 0x9E3779u;
-constexpr uint32_t kPfC3 = 0x7F4A7Du, kPfC4 = 0x58F1B5u, kPfC5 = 0xC2B2AFu, kPfC6 = 0x27D4EBu, kPfC7 = 0x165667u,
-                   kPfC7b = 0xD3A2E5u;
+
+// per-length bit multiplier (24 bits; a scalar op on the device)
+__host__ __device__ __forceinline__ constexpr uint32_t pf_mult(int klen) {
+    return ((uint32_t)klen * 0x6F4F2Bu + 0x7F4A7Du) & 0xFFFFFFu;
+}
 
 __host__ __device__ __forceinline__ uint32_t pf_word(uint32_t lo, uint32_t shift) { return mul24(lo, kPfWord) >> shift; }
 
-// bit position (low 5 bits significant) of a key of klen (3..7) bytes
+__host__ __device__ __forceinline__ constexpr uint32_t pf_shift(int klen) { return 8u * (uint32_t)(klen < 6 ? klen - 3 : 3); }
+
+// bit position (low 5 bits significant) from a length's (shift, multiplier)
+// (shift < 32: one v_alignbit_b32 on the device)
+__host__ __device__ __forceinline__ uint32_t pf_bit_c(uint32_t lo, uint32_t hi, uint32_t shift, uint32_t c) {
+    return mulhi24((uint32_t)(((((uint64_t)hi) << 32) | lo) >> shift), c);
+}
+
 __host__ __device__ __forceinline__ uint32_t pf_bit(int klen, uint32_t lo, uint32_t hi) {
-    switch (klen) {
-        case 3: return mulhi24(lo, kPfC3);
-        case 4: return mulhi24(lo >> 8, kPfC4);
-        case 5: return mulhi24((lo >> 16) | (hi << 16), kPfC5);
-        case 6: return mulhi24((lo >> 24) | (hi << 8), kPfC6);
-        default: {
-            const uint32_t x = (lo >> 24) | (hi << 8);
-            return mulhi24(x, kPfC7) ^ mulhi24(x >> 8, kPfC7b);
-        }
-    }
+    return pf_bit_c(lo, hi, pf_shift(klen), pf_mult(klen));
 }
 
 // Filter image (host-built, staged whole into LDS): a direct 256-bit bitmap

@@ -36,22 +36,26 @@ struct ScoreParams {
     int32_t nG;
     int32_t G[kMaxGramLengths];
     // fast path (documents of maxg..256 bytes: every window full-length):
-    // the gram lengths with a table key, 4 bits each in order (16 per word)
+    // the gram lengths with a table key, 4 bits each in order (16 per word);
+    // count mode: each distinct length once
     uint64_t gpack[2];
     int32_t n_fast;             // entries in gpack
     int32_t maxg;               // max(G)
+    uint32_t fast_mask;         // count mode fast path: bit n = n is in G and some key has n bytes
+    uint8_t mult[8];            // count mode: multiplicity of n in G (the fast path tests n once)
 };
 
 // Launch configuration of the score kernel.
 #ifndef LDGPU_SCORE_WAVES
-#define LDGPU_SCORE_WAVES 8
+#define LDGPU_SCORE_WAVES 12
 #endif
-constexpr int kScoreWaves = LDGPU_SCORE_WAVES;  // waves per workgroup (512 threads)
+constexpr int kScoreWaves = LDGPU_SCORE_WAVES;  // waves per workgroup (768 threads)
 // occupancy target (HIP launch bound: waves per SIMD = WGs x waves / 4):
-// 3 workgroups = 24 waves per CU (6 per SIMD) caps the
-// kernel at 80 VGPRs; the LDS image is sized so that 3 fit (score_lds_bytes)
+// 2 workgroups = 24 waves per CU (6 per SIMD) caps the kernel at 80 VGPRs;
+// two copies of the filter image + 24 waves' queues, hit areas and
+// double-buffered group staging fit the 160 KiB LDS (score_lds_bytes)
 #ifndef LDGPU_SCORE_MIN_WG
-#define LDGPU_SCORE_MIN_WG 3
+#define LDGPU_SCORE_MIN_WG 2
 #endif
 constexpr int kScoreMinWgPerCu = LDGPU_SCORE_MIN_WG;
 constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
@@ -63,7 +67,7 @@ constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
 // bytes of dynamic LDS the score kernel needs
 inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) {
     return (size_t)(kBloomBase + (lds_bloom ? bloom_words : 0u)) * 4u +
-           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + kBufWords * 4u + 64u * 4u);
+           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + 2u * kBufWords * 4u + 64u * 4u);
 }
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values

@@ -77,7 +77,7 @@ struct WaveLds {
     uint32_t* queue;  // [kQueueCap] candidate entries (klen << 29 | position)
     uint64_t* hits;   // [64][S + 1] verified hits of one chunk: value bits, mask words
                       // (MODE 3: the document's per-language hit counters, count_area)
-    uint32_t* buf;    // [kBufBytes / 4 + 4] staged bytes of the current document group
+    uint32_t* buf;    // [2][kBufBytes / 4 + 4] staged bytes of document groups (double buffer)
     uint32_t* labels; // [64] labels of the current group
 };
 
@@ -177,18 +177,22 @@ __device__ __forceinline__ void hit_add(const uint4 (&e)[kHitQuads<S>], double (
 }
 
 // Verify + accumulate the queued candidates (in queue order).
+// weighted (MODE 3 fast path, distinct gram lengths): a hit of a k-byte key
+// counts p.mult[k] times (k's multiplicity in gramLengths).
 template <int S, int MODE, bool STAGED>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
-                                      double (&acc)[S], int lane) {
+                                      double (&acc)[S], int lane, bool weighted = false) {
     __builtin_amdgcn_wave_barrier();
     for (int q0 = 0; q0 < qn; q0 += 64) {
         const int j = q0 + lane;
         uint32_t row = 0xffffffffu;
         double v = 0.0;
         uint64_t m0 = 0;
+        uint32_t inc = 1;
         if (j < qn) {
             const uint32_t e = w.queue[j];
             const int klen = (int)(e >> kPosBits);
+            if (MODE == 3 && weighted) inc = p.mult[klen];
             uint32_t w0, w1, w2, sh;
             window_words<STAGED>(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
             const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
@@ -226,7 +230,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                     while (mm) {
                         const int l = __builtin_ctzll(mm);
                         mm &= mm - 1;
-                        __hip_atomic_fetch_add(&cnt[64 * s + l], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&cnt[64 * s + l], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
             }
@@ -357,56 +361,72 @@ __device__ __forceinline__ void load_fwords(const ScoreParams& p, const uint32_t
 
 // Filter-test the (up to) 256 windows of one superblock for one key length:
 // m[k] = candidate mask of sub-block k < NSB (bit i = position p0 + 64k + i;
-// NSB = sub-blocks holding a window).  A test is a bit extract of a word
-// already in a register; f holds the prefix-Bloom words when KLEN >= 3.
+// NSB = sub-blocks holding a window).  Three bodies serve all lengths:
+//   KIND 1 / 2 (1-/2-byte keys): bit (lo & 0xff) / (lo & 0xffff) of the exact
+//   bitmaps;
+//   KIND 3 (3..7 bytes): bit pf_bit_c(lo, hi, sh, mul) of the position's
+//   prefix-Bloom word, already in a register (f).
 // nw = windows left from the superblock's first position, in
-// (64 (NSB - 1), 64 NSB] when NSB < 4.  Straight-line code: no per-sub-block
-// branches for the compiler to merge values across.
-template <int KLEN, int NSB>
-__device__ __forceinline__ void test_len(const uint32_t* img, const FWords& f, const Windows& x, int32_t nw,
-                                         int lane, uint64_t (&m)[kSub]) {
-    uint32_t w[NSB];
+// (64 (NSB - 1), 64 NSB] when NSB < 4: the last sub-block's ballot is cut to
+// its first nw - 64 (NSB - 1) lanes by a scalar mask.
+__device__ __forceinline__ uint64_t lanes_below(int32_t n) {  // n in [1, 64]
+    return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+}
+
+template <int KIND, int NSB>
+__device__ __forceinline__ void test_len(const uint32_t* img, uint32_t sh, uint32_t mul, const FWords& f,
+                                         const Windows& x, int32_t nw, uint64_t (&m)[kSub]) {
+    uint32_t w[NSB], bit[NSB];
 #pragma unroll
     for (int k = 0; k < NSB; ++k) {
-        if constexpr (KLEN == 1)
+        if constexpr (KIND == 1) {
             w[k] = img[(x.lo[k] >> 5) & 7u];
-        else if constexpr (KLEN == 2)
+            bit[k] = x.lo[k];
+        } else if constexpr (KIND == 2) {
             w[k] = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
-        else
+            bit[k] = x.lo[k];
+        } else {
             w[k] = f.w3[k];
+            bit[k] = mulhi24(__builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh), mul);
+        }
     }
 #pragma unroll
     for (int k = 0; k < NSB; ++k) {
-        const uint32_t c = __builtin_amdgcn_ubfe(w[k], KLEN <= 2 ? x.lo[k] : pf_bit(KLEN, x.lo[k], x.hi[k]), 1);
-        m[k] = __builtin_amdgcn_ballot_w64(c != 0u && (k < NSB - 1 || lane < nw - 64 * k));
+        uint32_t c = __builtin_amdgcn_ubfe(w[k], bit[k], 1);
+#ifdef LDGPU_BLOOM_K2
+        if constexpr (KIND == 3) c &= __builtin_amdgcn_ubfe(w[k], bit[k] >> 5, 1);
+#endif
+        m[k] = __builtin_amdgcn_ballot_w64(c != 0u);
     }
+    m[NSB - 1] &= lanes_below(nw - 64 * (NSB - 1));
 #pragma unroll
     for (int k = NSB; k < kSub; ++k) m[k] = 0;
 }
 
-template <int KLEN>
-__device__ __forceinline__ void test_nsb(const uint32_t* img, const FWords& f, const Windows& x, int32_t nw, int lane,
-                                         uint64_t (&m)[kSub]) {
+template <int KIND>
+__device__ __forceinline__ void test_nsb(const uint32_t* img, uint32_t sh, uint32_t mul, const FWords& f,
+                                         const Windows& x, int32_t nw, uint64_t (&m)[kSub]) {
     if (nw > 192)
-        test_len<KLEN, 4>(img, f, x, nw, lane, m);
+        test_len<KIND, 4>(img, sh, mul, f, x, nw, m);
     else if (nw > 128)
-        test_len<KLEN, 3>(img, f, x, nw, lane, m);
+        test_len<KIND, 3>(img, sh, mul, f, x, nw, m);
     else if (nw > 64)
-        test_len<KLEN, 2>(img, f, x, nw, lane, m);
+        test_len<KIND, 2>(img, sh, mul, f, x, nw, m);
     else
-        test_len<KLEN, 1>(img, f, x, nw, lane, m);
+        test_len<KIND, 1>(img, sh, mul, f, x, nw, m);
 }
 
+// FULL: every length has more than 192 windows (NSB = 4, no dispatch)
+template <bool FULL>
 __device__ __forceinline__ void test_sb(const uint32_t* img, int klen, const FWords& f, const Windows& x, int32_t nw,
-                                        int lane, uint64_t (&m)[kSub]) {
-    switch (klen) {
-        case 1: test_nsb<1>(img, f, x, nw, lane, m); break;
-        case 2: test_nsb<2>(img, f, x, nw, lane, m); break;
-        case 3: test_nsb<3>(img, f, x, nw, lane, m); break;
-        case 4: test_nsb<4>(img, f, x, nw, lane, m); break;
-        case 5: test_nsb<5>(img, f, x, nw, lane, m); break;
-        case 6: test_nsb<6>(img, f, x, nw, lane, m); break;
-        default: test_nsb<7>(img, f, x, nw, lane, m); break;
+                                        uint64_t (&m)[kSub]) {
+    const uint32_t sh = pf_shift(klen), mul = pf_mult(klen);
+    if (klen == 1) {
+        if (FULL) test_len<1, 4>(img, sh, mul, f, x, nw, m); else test_nsb<1>(img, sh, mul, f, x, nw, m);
+    } else if (klen == 2) {
+        if (FULL) test_len<2, 4>(img, sh, mul, f, x, nw, m); else test_nsb<2>(img, sh, mul, f, x, nw, m);
+    } else {
+        if (FULL) test_len<3, 4>(img, sh, mul, f, x, nw, m); else test_nsb<3>(img, sh, mul, f, x, nw, m);
     }
 }
 
@@ -458,6 +478,43 @@ __device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc&
     }
 }
 
+// Count-mode fast path, gram length N (straight-line code for N = 1..7, so
+// the tests of consecutive lengths overlap): test the document's one
+// superblock if N is a listed length with table keys, and queue the
+// candidates unless the queue would overflow (then `over` is set and the
+// document restarts on the general path).
+template <int N, bool FULL>
+__device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                            const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
+                                            bool& over, uint32_t dummy_a) {
+    if (over || !((p.fast_mask >> N) & 1u)) return;
+    constexpr int KIND = N < 3 ? N : 3;
+    constexpr uint32_t sh = N < 3 ? 0u : pf_shift(N), mul = N < 3 ? 0u : pf_mult(N);
+    uint64_t m[kSub];
+    if constexpr (FULL)
+        test_len<KIND, 4>(img, sh, mul, f, x, len - N + 1, m);
+    else
+        test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
+    if (qn + count_sb(m) > kQueueCap) {
+        over = true;
+        return;
+    }
+    append_sb(wl.queue, dummy_a, qn, m, N, 0, lane);
+}
+
+template <bool FULL>
+__device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                                const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
+                                                bool& over, uint32_t dummy_a) {
+    probe_count<1, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+    probe_count<2, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+    probe_count<3, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+    probe_count<4, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+    probe_count<5, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+    probe_count<6, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+    probe_count<7, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+}
+
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
 template <int S, int MODE, bool STAGED>
 __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
@@ -468,34 +525,54 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     for (int s = 0; s < S; ++s) acc[s] = 0.0;
     int qn = 0;
     const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
-    if (len >= p.maxg && len <= 64 * kSub) {
+    bool general = !(len >= p.maxg && len <= 64 * kSub);
+    if (!general) {
         // fast path: every window is full-length (klen = n) and one
         // superblock covers the document, so every gram length reuses the
-        // same window bytes and prefix-Bloom words
+        // same window bytes and prefix-Bloom words.  Count mode (hit order
+        // free): the host packs each DISTINCT length once and its hits count
+        // its multiplicity in gramLengths.  The candidates of all lengths
+        // are verified together; a document whose candidates overflow the
+        // queue (nothing verified yet) restarts on the general path, so no
+        // verification state is live in this loop.
         if (p.n_fast && !(p.ablate & 2)) {
             Windows x;
             load_windows<STAGED>(p, src, 0, lane, x);
             FWords f;
             load_fwords(p, bloom, x, f);
+            if constexpr (MODE == 3) {
+                if (len >= 192 + p.maxg)
+                    probe_count_all<true>(p, wl, img, f, x, (int32_t)len, lane, qn, general, dummy_a);
+                else
+                    probe_count_all<false>(p, wl, img, f, x, (int32_t)len, lane, qn, general, dummy_a);
+            }
             uint64_t gq = p.gpack[0];
-            for (int gi = 0; gi < p.n_fast; ++gi) {
+            for (int gi = 0; gi < (MODE == 3 ? 0 : p.n_fast); ++gi) {
                 const int n = (int)(gq & 15u);
                 gq = (gi & 15) == 15 ? p.gpack[1] : gq >> 4;
                 // pin the tests inside this loop: hoisted out of it (they are
-                // loop-invariant), the tests of all 7 lengths would run per doc
+                // loop-invariant), the tests of all lengths would run per doc
 #pragma unroll
                 for (int k = 0; k < kSub; ++k) asm volatile("" : "+v"(x.lo[k]), "+v"(x.hi[k]), "+v"(f.w3[k]));
                 uint64_t m[kSub];
-                test_sb(img, n, f, x, (int32_t)len - n + 1, lane, m);
-                if (qn + count_sb(m) > kQueueCap) {  // rare: verify what is queued first
-                    flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
-                    qn = 0;
-                    load_windows<STAGED>(p, src, 0, lane, x);  // reloaded: not live across the flush
-                    load_fwords(p, bloom, x, f);
+                if (len >= 192 + p.maxg)
+                    test_sb<true>(img, n, f, x, (int32_t)len - n + 1, m);
+                else
+                    test_sb<false>(img, n, f, x, (int32_t)len - n + 1, m);
+                if (qn + count_sb(m) > kQueueCap) {  // rare
+                    general = true;
+                    break;
                 }
                 append_sb(wl.queue, dummy_a, qn, m, n, 0, lane);
             }
+            if (!general) {
+                if (p.ablate & 1) qn = 0;
+                if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane, MODE == 3);
+            }
+            qn = 0;
         }
+    }
+    if (!general) {
     } else if (len >= kMaxDocBytes) {
         if (lane == 0) atomicOr(p.err, 2);
     } else {
@@ -510,7 +587,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                 FWords f;
                 if (g.klen >= 3) load_fwords(p, bloom, x, f);
                 uint64_t m[kSub];
-                test_sb(img, g.klen, f, x, g.nwin - p0, lane, m);
+                test_sb<false>(img, g.klen, f, x, g.nwin - p0, m);
                 if (qn + count_sb(m) > kQueueCap) {
                     flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
                     qn = 0;
@@ -560,6 +637,20 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
 
 __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) { return (int64_t)rdlane64((uint64_t)v, l); }
 
+// LDS-DMA of a group's bytes [s0, s0 + kBufBytes) into dst (wave-uniform LDS
+// address; lane i's 16 B land at dst + 16 i), range-checked: bytes past
+// n_bytes read as 0, never fault.
+__device__ __forceinline__ void group_dma(const ScoreParams& p, int64_t s0, uint32_t* dst, int lane) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(p.bytes + s0));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)(p.bytes + s0) >> 32));
+    const int64_t left = ((p.n_bytes + 3) & ~(int64_t)3) - s0;
+    const uint32_t nrec =
+        __builtin_amdgcn_readfirstlane((uint32_t)(left < 0 ? 0 : (left > 0x7ffffff0 ? 0x7ffffff0 : left)));
+    void* base = (void*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)nrec, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, 16 * lane, 0, 0, 0);
+}
+
 // Issue the 16-B-per-lane buffer load of a group's bytes [s0, s0 + kBufBytes)
 // (range-checked: bytes past n_bytes read as 0, never fault).
 __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int lane, uint4& r0) {
@@ -591,8 +682,8 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * 2 * kHitQuads<S>;
-    wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 4 * kHitQuads<S> + wave * kBufWords;
-    wl.labels = lds + img_words + kScoreWaves * (kQueueCap + 64 * 4 * kHitQuads<S> + kBufWords) + wave * 64;
+    wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 4 * kHitQuads<S> + wave * 2 * kBufWords;
+    wl.labels = lds + img_words + kScoreWaves * (kQueueCap + 64 * 4 * kHitQuads<S> + 2 * kBufWords) + wave * 64;
 
     if constexpr (MODE == 3) {
         uint32_t* cnt = count_area(wl);
@@ -609,29 +700,42 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     if (dbeg >= dend) return;
     const int G = p.group;
 
-    // lane i <= G holds offsets[g0 + i] of the current group (clamped to dend)
+    // lane i <= G holds offsets[g0 + i] of the current group (clamped to dend).
+    // Group bytes are staged by LDS-DMA into a double buffer: the next
+    // group's load is in flight while this group is scored, and no VGPR
+    // holds it.
+    uint32_t* const buf0 = wl.buf;
+    uint32_t* const buf1 = wl.buf + kBufWords;
     int64_t g0 = dbeg;
     int64_t offv = p.offsets[min(g0 + (int64_t)min(lane, G), dend)];
-    uint4 r0;
-    group_load(p, rdlane_i64(offv, 0) & ~(int64_t)15, lane, r0);
+    group_dma(p, rdlane_i64(offv, 0) & ~(int64_t)15, buf0, lane);
+    bool par = false;
+    int64_t prev_g0 = 0;
+    int prev_cnt = 0;
 
     while (g0 < dend) {
+        // this group's bytes (DMA issued one group ago) have landed, and the
+        // previous group's label store has drained
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
         const int64_t g1 = min(g0 + (int64_t)G, dend);
         const int cnt = (int)(g1 - g0);
-        // offsets of the next group (hidden behind this group's work)
-        const int64_t n1 = min(g1 + (int64_t)G, dend);
-        const int64_t offn = p.offsets[min(g1 + (int64_t)min(lane, G), n1)];
         const int64_t s0 = rdlane_i64(offv, 0) & ~(int64_t)15;
         const int64_t send = rdlane_i64(offv, cnt);
         const bool staged = send - s0 <= kBufBytes;
-        if (staged) reinterpret_cast<uint4*>(wl.buf)[lane] = r0;
+        uint32_t* const cur = par ? buf1 : buf0;
+        // offsets and bytes of the next group (hidden behind this group's work)
+        const int64_t n1 = min(g1 + (int64_t)G, dend);
+        const int64_t offn = p.offsets[min(g1 + (int64_t)min(lane, G), n1)];
+        if (g1 < dend) group_dma(p, send & ~(int64_t)15, par ? buf0 : buf1, lane);
+        // the previous group's labels: one coalesced store
+        if (lane < prev_cnt) p.labels[prev_g0 + lane] = (int32_t)wl.labels[lane];
         __builtin_amdgcn_wave_barrier();
-        if (g1 < dend) group_load(p, send & ~(int64_t)15, lane, r0);  // next group's bytes
         if (staged) {
             for (int i = 0; i < cnt; ++i) {
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
-                const DocSrc src{wl.buf, b - s0};
+                const DocSrc src{cur, b - s0};
                 const int lab = score_doc<S, MODE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
             }
@@ -644,13 +748,14 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 if (lane == 0) wl.labels[i] = lab;
             }
         }
-        // the group's labels: one coalesced store
         __builtin_amdgcn_wave_barrier();
-        if (lane < cnt) p.labels[g0 + lane] = (int32_t)wl.labels[lane];
-        __builtin_amdgcn_wave_barrier();
+        prev_g0 = g0;
+        prev_cnt = cnt;
         offv = offn;
         g0 = g1;
+        par = !par;
     }
+    if (lane < prev_cnt) p.labels[prev_g0 + lane] = (int32_t)wl.labels[lane];
 }
 
 template <int S, int MODE, bool FLDS>
