@@ -640,7 +640,15 @@ __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) { return (int64_
 // LDS-DMA of a group's bytes [s0, s0 + kBufBytes) into dst (wave-uniform LDS
 // address; lane i's 16 B land at dst + 16 i), range-checked: bytes past
 // n_bytes read as 0, never fault.
-__device__ __forceinline__ void group_dma(const ScoreParams& p, int64_t s0, uint32_t* dst, int lane) {
+// lane id recomputed in place (mbcnt): never spilled, never a scratch reload
+// (whose vmcnt wait would drain the in-flight group DMA)
+__device__ __forceinline__ uint32_t fresh_lane() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+__device__ __forceinline__ void group_dma(const ScoreParams& p, int64_t s0, uint32_t* dst) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(p.bytes + s0));
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)(p.bytes + s0) >> 32));
     const int64_t left = ((p.n_bytes + 3) & ~(int64_t)3) - s0;
@@ -648,7 +656,8 @@ __device__ __forceinline__ void group_dma(const ScoreParams& p, int64_t s0, uint
         __builtin_amdgcn_readfirstlane((uint32_t)(left < 0 ? 0 : (left > 0x7ffffff0 ? 0x7ffffff0 : left)));
     void* base = (void*)(((uint64_t)hi << 32) | lo);
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)nrec, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, 16 * lane, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, 16 * fresh_lane(), 0,
+                                             0, 0);
 }
 
 // Issue the 16-B-per-lane buffer load of a group's bytes [s0, s0 + kBufBytes)
@@ -708,7 +717,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     uint32_t* const buf1 = wl.buf + kBufWords;
     int64_t g0 = dbeg;
     int64_t offv = p.offsets[min(g0 + (int64_t)min(lane, G), dend)];
-    group_dma(p, rdlane_i64(offv, 0) & ~(int64_t)15, buf0, lane);
+    group_dma(p, rdlane_i64(offv, 0) & ~(int64_t)15, buf0);
     bool par = false;
     int64_t prev_g0 = 0;
     int prev_cnt = 0;
@@ -724,12 +733,15 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
         const int64_t send = rdlane_i64(offv, cnt);
         const bool staged = send - s0 <= kBufBytes;
         uint32_t* const cur = par ? buf1 : buf0;
-        // offsets and bytes of the next group (hidden behind this group's work)
+        // bytes and offsets of the next group (hidden behind this group's work)
+        if (g1 < dend) group_dma(p, send & ~(int64_t)15, par ? buf0 : buf1);
         const int64_t n1 = min(g1 + (int64_t)G, dend);
-        const int64_t offn = p.offsets[min(g1 + (int64_t)min(lane, G), n1)];
-        if (g1 < dend) group_dma(p, send & ~(int64_t)15, par ? buf0 : buf1, lane);
+        const int64_t offn = p.offsets[min(g1 + (int64_t)min((int)fresh_lane(), G), n1)];
         // the previous group's labels: one coalesced store
-        if (lane < prev_cnt) p.labels[prev_g0 + lane] = (int32_t)wl.labels[lane];
+        {
+            const uint32_t l = fresh_lane();
+            if ((int)l < prev_cnt) p.labels[prev_g0 + l] = (int32_t)wl.labels[l];
+        }
         __builtin_amdgcn_wave_barrier();
         if (staged) {
             for (int i = 0; i < cnt; ++i) {
