@@ -189,6 +189,7 @@ struct ldgpu_model {
     double* d_rows = nullptr;
     double* d_fold = nullptr;  // mode 3: fold[c], c = 0..kFoldMax
     int count_sign = 0;        // mode 3: sign of the shared value
+    uint32_t direct_off = 0, direct_words = 0;  // mode 3: direct tables in the image (ScoreParams)
     bool count_int_argmax = false;  // mode 3: label = first max of the counts (monotone fold)
     int32_t* d_err = nullptr;
 };
@@ -421,6 +422,48 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
         }
     }
 
+    // count mode with every 1-/2-byte key naming ONE language (fit tables of
+    // grams unique to a language): direct tables after the image (see
+    // ScoreParams::direct_*), so those keys are counted from LDS unverified
+    uint32_t image_words = kBloomBase + (m->lds_filter ? (uint32_t)bwords : 0u);
+    if (m->mode == 3 && m->lds_filter && n_langs <= 255 && !getenv("LDGPU_NO_DIRECT")) {
+        std::vector<uint8_t> lang1(256, 0xff), lang2of(65536, 0xff);
+        bool ok = true;
+        for (int64_t i = 0; i < nk && ok; ++i) {
+            const int kl = key_len(keys[i]);
+            if (kl > 2) continue;
+            int bits = 0, lang = 0;
+            for (int s = 0; s < S; ++s) {
+                const uint64_t w = masks[(size_t)i * S + s];
+                if (w && !bits) lang = 64 * s + __builtin_ctzll(w);
+                bits += __builtin_popcountll(w);
+            }
+            ok = bits == 1 && !(row_ok && !row_ok[src_row[i]]);
+            if (kl == 1) lang1[keys[i] & 0xff] = (uint8_t)lang;
+            else lang2of[keys[i] & 0xffff] = (uint8_t)lang;
+        }
+        if (ok) {
+            std::vector<uint16_t> base2(2048);
+            std::vector<uint8_t> lang2;
+            for (uint32_t wd = 0; wd < 2048; ++wd) {
+                base2[wd] = (uint16_t)lang2.size();
+                for (uint32_t b = 0; b < 32; ++b)
+                    if ((filter[kBmp1Words + wd] >> b) & 1u) lang2.push_back(lang2of[wd * 32 + b]);
+            }
+            const uint32_t dwords = 64u + 1024u + (uint32_t)((lang2.size() + 16) / 16) * 4u;  // uint4-padded
+            if (score_lds_bytes(S, 3, image_words + dwords) * 2 <= 163840) {
+                m->direct_off = image_words;
+                m->direct_words = dwords;
+                filter.resize(image_words + dwords, 0u);
+                uint8_t* d = reinterpret_cast<uint8_t*>(filter.data() + image_words);
+                memcpy(d, lang1.data(), 256);
+                memcpy(d + 256, base2.data(), 4096);
+                memcpy(d + 256 + 4096, lang2.data(), lang2.size());
+                image_words += dwords;
+            }
+        }
+    }
+
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = upload(&m->d_slots, slots, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_filter, filter, &m->device_bytes);
@@ -429,7 +472,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (e == hipSuccess) e = upload(&m->d_rows, drows, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_fold, fold, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
-    m->lds_bytes = score_lds_bytes(S, m->lds_filter, (uint32_t)bwords);
+    m->lds_bytes = score_lds_bytes(S, m->mode, image_words);
     int resident = 0;
     if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->lds_bytes, &resident);
     // persistent grid = what is resident; never more workgroups than the LDS admits
@@ -437,9 +480,9 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (const char* ov = getenv("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
     if (const char* ab = getenv("LDGPU_ABLATE")) m->ablate = atoi(ab);
     if (getenv("LDGPU_DEBUG"))
-        fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
+        fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d direct=%u slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
                         "resident_api=%d wg_per_cu=%d\n",
-                (long long)nk, m->mode, S, (unsigned long long)bwords, (int)m->lds_filter, m->lds_bytes, resident,
+                (long long)nk, m->mode, m->direct_words, S, (unsigned long long)bwords, (int)m->lds_filter, m->lds_bytes, resident,
                 m->wg_per_cu);
     if (e != hipSuccess) {
         model_free(m);
@@ -494,6 +537,8 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.rows = m->d_rows;
     p.fold = m->d_fold;
     p.fold_max = kFoldMax;
+    p.direct_off = m->direct_off;
+    p.direct_words = m->direct_words;
     p.count_sign = m->count_sign;
     // counts stay below 2^24: c <= windows of a document <= len * n_grams
     p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;

@@ -43,6 +43,11 @@ struct ScoreParams {
     int32_t maxg;               // max(G)
     uint32_t fast_mask;         // count mode fast path: bit n = n is in G and some key has n bytes
     uint8_t mult[8];            // count mode: multiplicity of n in G (the fast path tests n once)
+    // count mode, direct tables (every 1-/2-byte key names one language):
+    // image words [direct_off, + direct_words) = lang1[256] u8 (0xff: no key),
+    // base2[2048] u16 (rank of each 2-byte bitmap word), lang2[n2] u8
+    uint32_t direct_off;
+    uint32_t direct_words;      // 0: no direct tables
 };
 
 // Launch configuration of the score kernel.
@@ -64,10 +69,18 @@ constexpr int kBufWords = kBufBytes / 4 + 4;
 constexpr int kMaxLdsBloomLog2 = 14;       // bloom words in LDS up to 64 KiB
 constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
 
-// bytes of dynamic LDS the score kernel needs
-inline size_t score_lds_bytes(int slices, bool lds_bloom, uint32_t bloom_words) {
-    return (size_t)(kBloomBase + (lds_bloom ? bloom_words : 0u)) * 4u +
-           (size_t)kScoreWaves * (kQueueCap * 4u + 64u * 16u * ((slices + 2u) / 2u) + 2u * kBufWords * 4u + 64u * 4u);
+// per-wave hit area (u32 words): ordered modes hold 64 verified hits of
+// (S + 2) / 2 uint4 each; count mode (3) holds the probe's 64 dummy-store
+// words and the 64 S per-language counters
+constexpr uint32_t hit_area_words(int slices, int mode) {
+    return mode == 3 ? 64u * (1u + (uint32_t)slices) : 64u * 4u * (((uint32_t)slices + 2u) / 2u);
+}
+
+// bytes of dynamic LDS the score kernel needs; image_words = the filter image
+// staged in LDS (bitmaps, the bloom when it fits, direct tables)
+inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words) {
+    return (size_t)image_words * 4u +
+           (size_t)kScoreWaves * (kQueueCap * 4u + hit_area_words(slices, mode) * 4u + 2u * kBufWords * 4u + 64u * 4u);
 }
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values

@@ -82,8 +82,7 @@ struct WaveLds {
 };
 
 // MODE 3 per-language hit counters: after the first 64 words of the hit area,
-// which take the probe's dummy stores (append_sb); 64 + 64 S words fit the
-// area (64 x 16 x kHitQuads<S> bytes) for every S.
+// which take the probe's dummy stores (append_sb); hit_area_words(S, 3).
 __device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return reinterpret_cast<uint32_t*>(w.hits) + 64; }
 
 // Where a document's bytes are read from: the wave's LDS buffer (staged
@@ -445,7 +444,11 @@ __device__ __forceinline__ uint32_t select_by_mask(uint64_t m, uint32_t a, uint3
 // the wave's hit area (idle while probing), at byte address dummy_a.
 __device__ __forceinline__ void append_sb(uint32_t* queue, uint32_t dummy_a, int& qn, const uint64_t (&m)[kSub],
                                           int klen, int32_t p0, int lane) {
-    const uint32_t tag0 = ((uint32_t)klen << kPosBits) | (uint32_t)(p0 + lane);
+    // opaque lane: the tags are then built here, not hoisted out of the
+    // document loop as loop invariants (which the allocator spills)
+    uint32_t l = (uint32_t)lane;
+    asm volatile("" : "+v"(l));
+    const uint32_t tag0 = ((uint32_t)klen << kPosBits) | ((uint32_t)p0 + l);
     const uint32_t qbase = (uint32_t)(uintptr_t)queue;  // LDS offset (low half of the flat address)
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
@@ -478,6 +481,46 @@ __device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc&
     }
 }
 
+// Count-mode direct tables (ScoreParams::direct_*): a 1-/2-byte window that is
+// a key (exact bitmaps: never a false positive) names its one language in
+// LDS, and its count is added there -- no queue, no verification.  Windows of
+// the last sub-block past nw are masked per lane.
+template <int N>
+__device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                             const Windows& x, int32_t nw, int lane) {
+    const uint8_t* l1 = reinterpret_cast<const uint8_t*>(img + p.direct_off);
+    const uint16_t* b2 = reinterpret_cast<const uint16_t*>(img + p.direct_off + 64);
+    const uint8_t* l2 = reinterpret_cast<const uint8_t*>(img + p.direct_off + 64 + 1024);
+    uint32_t* cnt = count_area(wl);
+    const uint32_t inc = p.mult[N];
+    uint32_t lang[kSub];
+    bool hit[kSub];
+    if constexpr (N == 1) {
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) lang[k] = l1[x.lo[k] & 0xffu];
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) hit[k] = lang[k] != 0xffu && 64 * k + lane < nw;
+    } else {
+        uint32_t w[kSub], idx[kSub], base[kSub];
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            idx[k] = (x.lo[k] >> 5) & 2047u;
+            w[k] = img[kBmp1Words + idx[k]];
+            base[k] = b2[idx[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            const uint32_t b = x.lo[k] & 31u;
+            hit[k] = ((w[k] >> b) & 1u) && 64 * k + lane < nw;
+            // rank of the key among the 2-byte keys (in range for every lane)
+            lang[k] = l2[base[k] + __builtin_popcount(w[k] & ((1u << b) - 1u))];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kSub; ++k)
+        if (hit[k]) __hip_atomic_fetch_add(&cnt[lang[k]], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Count-mode fast path, gram length N (straight-line code for N = 1..7, so
 // the tests of consecutive lengths overlap): test the document's one
 // superblock if N is a listed length with table keys, and queue the
@@ -488,6 +531,12 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                             bool& over, uint32_t dummy_a) {
     if (over || !((p.fast_mask >> N) & 1u)) return;
+    if constexpr (N <= 2) {
+        if (p.direct_words) {
+            direct_count<N>(p, wl, img, x, len - N + 1, lane);
+            return;
+        }
+    }
     constexpr int KIND = N < 3 ? N : 3;
     constexpr uint32_t sh = N < 3 ? 0u : pf_shift(N), mul = N < 3 ? 0u : pf_mult(N);
     uint64_t m[kSub];
@@ -680,7 +729,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t img_words = kBloomBase + (FLDS ? p.bloom_words : 0u);
+    const uint32_t img_words = kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words;
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.filter);
         uint4* dst = reinterpret_cast<uint4*>(lds);
@@ -690,9 +739,10 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     const uint32_t* bloom = FLDS ? lds + kBloomBase : p.filter + kBloomBase;
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
-    wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap) + wave * 64 * 2 * kHitQuads<S>;
-    wl.buf = lds + img_words + kScoreWaves * kQueueCap + kScoreWaves * 64 * 4 * kHitQuads<S> + wave * 2 * kBufWords;
-    wl.labels = lds + img_words + kScoreWaves * (kQueueCap + 64 * 4 * kHitQuads<S> + 2 * kBufWords) + wave * 64;
+    constexpr uint32_t kHitW = hit_area_words(S, MODE);
+    wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap + wave * kHitW);
+    wl.buf = lds + img_words + kScoreWaves * (kQueueCap + kHitW) + wave * 2 * kBufWords;
+    wl.labels = lds + img_words + kScoreWaves * (kQueueCap + kHitW + 2 * kBufWords) + wave * 64;
 
     if constexpr (MODE == 3) {
         uint32_t* cnt = count_area(wl);
@@ -772,7 +822,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
 
 template <int S, int MODE, bool FLDS>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
-    const size_t lds = score_lds_bytes(S, FLDS, p.bloom_words);
+    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words);
     hipLaunchKernelGGL((score_kernel<S, MODE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }

@@ -152,6 +152,33 @@ def test_uniform_value_counts_past_fold_table(uniform_path):
     assert m.info()["mode"] == uniform_path
 
 
+@pytest.mark.parametrize("direct", [True, False])
+@pytest.mark.parametrize("L,grams", [(20, [1, 2, 3, 4, 5]), (100, [2, 1, 2, 3]), (255, [1, 2, 7])])
+def test_single_language_keys_direct_tables(L, grams, direct, monkeypatch):
+    """Every row one language, one shared value (a fit table of grams unique
+    to a language): 1-/2-byte keys are counted from the LDS direct tables,
+    longer ones verified; LDGPU_NO_DIRECT forces them all through verification.
+    Docs of every length class: partial windows, the 256-byte fast path, long."""
+    if not direct:
+        monkeypatch.setenv("LDGPU_NO_DIRECT", "1")
+    rng = np.random.default_rng(L + 3 * len(grams))
+    alphabet = np.frombuffer(b"abcdefghij ", dtype=np.uint8)
+    v = math.log(2.0)
+    table = {}
+    for _ in range(600):
+        n = int(rng.choice(grams))
+        k = bytes(rng.choice(alphabet, size=n))
+        row = [0.0] * L
+        row[int(rng.integers(0, L))] = v
+        table[k] = row
+    lens = rng.integers(0, 400, size=800)
+    lens[:10] = [0, 1, 2, 3, 6, 7, 64, 65, 256, 255]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, grams, data, off)
+    assert m.info()["mode"] == 2
+
+
 def test_long_documents_and_hot_keys():
     """Every 1-gram in the table: every window hits, so the per-wave candidate
     queue flushes many times per document (order must survive the flushes)."""
