@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--train-docs", type=int, default=1000, help="training docs per language for the table")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--empty-table", action="store_true", help="calibration: table with no keys")
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--mode", choices=["score", "fit"], default="score",
@@ -92,6 +93,30 @@ def cpu_baseline(args, table, grams, data, off):
     return {"value": round(n / dt, 1), "unit": "docs/s", "cores": threads, "kind": "port",
             "sample": f"first {n} of the GPU's documents ({args.doc_bytes} B each), same table, "
                       f"{threads} pthreads, {dt:.1f} s"}
+
+
+def host_path(model, data, off, acc_labels):
+    """The host-buffer boundary (ldgpu_score: the JNI shim's call), PCIe
+    copies included -- reported beside `value`, never as it.  Pageable numpy
+    buffers (staged through pinned memory) and ldgpu_host_alloc buffers."""
+    from languagedetection.runtime import PinnedArray
+    n = len(off) - 1
+    res = {"note": "ldgpu_score over the same documents: H2D + score + D2H, 64 MiB chunks pipelined on two streams"}
+    model.score(data[: int(off[min(n, 100000)])], off[: min(n, 100000) + 1])  # warm the staging buffers
+    t0 = time.perf_counter()
+    lab, _ = model.score(data, off)
+    res["pageable_docs_per_s"] = round(n / (time.perf_counter() - t0), 1)
+    pin = PinnedArray(len(data), np.uint8)
+    pin.array[:] = data
+    pout = PinnedArray(n, np.int32)
+    model.score(pin.array, off, out=pout.array)
+    t0 = time.perf_counter()
+    model.score(pin.array, off, out=pout.array)
+    res["pinned_docs_per_s"] = round(n / (time.perf_counter() - t0), 1)
+    res["labels_match_device_path"] = bool(np.array_equal(lab, acc_labels) and np.array_equal(pout.array, acc_labels))
+    pin.close()
+    pout.close()
+    return res
 
 
 def traffic_from_profiles(workload_key):
@@ -277,6 +302,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and table:
         cpu = cpu_baseline(args, table, grams, data, off)
+    host = None
+    if rank == 0 and world == 1 and not args.no_host_path and table:
+        host = host_path(model, data, off, acc_labels=d_lab.cpu().numpy())
 
     total_docs = n_docs * world * args.steps
     line = {
@@ -300,6 +328,7 @@ def main():
                    "parallelism": f"dp{world} (documents sharded, no collective)"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "host_path": host,
         "fit_setup": fit_info,
         "label_accuracy_vs_generator": acc,
     }

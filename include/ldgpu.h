@@ -66,6 +66,13 @@ int ldgpu_ctx_destroy(ldgpu_ctx* ctx);
 int ldgpu_ctx_synchronize(ldgpu_ctx* ctx);
 void* ldgpu_ctx_stream(ldgpu_ctx* ctx);      /* the context's hipStream_t */
 
+/* Page-locked host memory for the host-buffer APIs: documents packed straight
+ * into it (a JNI shim wraps it in direct ByteBuffers) are copied to the device
+ * without a staging copy; labels written into it skip one too.  Replaces the
+ * JVM-owned row buffers of transform (LanguageDetectorModel.scala:225-238). */
+int ldgpu_host_alloc(ldgpu_ctx* ctx, int64_t n_bytes, void** out);
+int ldgpu_host_free(ldgpu_ctx* ctx, void* p);
+
 /* ------------------------------------------------------------------ SCORE */
 typedef struct ldgpu_model ldgpu_model;
 
@@ -92,7 +99,10 @@ int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
 
 /* Host buffers in, host buffers out; synchronous.  out_scores is nullable
  * ([n_docs][n_langs] fp64).  out_labels[d] is the index into the supported
- * languages of argmax(scores of d): first maximum, all-zero -> 0. */
+ * languages of argmax(scores of d): first maximum, all-zero -> 0.  Chunks of
+ * documents are pipelined over two streams (copy-in / score / copy-out of one
+ * chunk overlap the host staging of the next); buffers from ldgpu_host_alloc
+ * are copied from / to directly, pageable ones through pinned staging. */
 int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets,
                 int64_t n_docs, int32_t* out_labels, double* out_scores);
 

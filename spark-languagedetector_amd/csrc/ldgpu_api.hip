@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -75,6 +76,59 @@ struct DevBuf {
     }
 };
 
+// pinned (page-locked) host buffer that only grows: the H2D / D2H copies of
+// the host-buffer API run from it at full PCIe rate, asynchronously
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(n, 1 << 20);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// true when host pointer q lies in page-locked memory (ldgpu_host_alloc,
+// hipHostMalloc, hipHostRegister): then it is copied from / to directly
+bool is_pinned(const void* q) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// memcpy split over up to 8 threads (pageable -> pinned staging is the host
+// path's bound when the caller's buffers are pageable)
+void par_memcpy(void* dst, const void* src, size_t n) {
+    const size_t kMin = 4u << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned t = (unsigned)std::min<size_t>(std::min(8u, hw), std::max<size_t>(1, n / kMin));
+    if (t <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t part = (n + t - 1) / t;
+    for (unsigned i = 1; i < t; ++i) {
+        const size_t a = std::min(n, part * i), b = std::min(n, part * (i + 1));
+        if (a < b) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    }
+    memcpy(dst, src, std::min(n, part));
+    for (auto& x : th) x.join();
+}
+
 int check_grams(const int32_t* G, int32_t nG) {
     if (nG < 0 || nG > LDGPU_MAX_GRAM_LENGTHS)
         return fail(LDGPU_EINVAL, "number of gram lengths %d outside [0, %d]", nG, LDGPU_MAX_GRAM_LENGTHS);
@@ -101,12 +155,24 @@ int check_offsets(const int64_t* off, int64_t n_docs) {
 }  // namespace
 
 // ------------------------------------------------------------------ context
+// one stage of the host-buffer scoring pipeline (ldgpu_score): pinned
+// staging + device buffers of one chunk, on its own stream
+struct ScoreStage {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    DevBuf bytes, offsets, labels, scores;
+    HostBuf h_bytes, h_offsets, h_labels, h_scores;
+    int64_t d0 = 0, nd = 0;
+    bool busy = false;
+};
+
 struct ldgpu_ctx {
     int device = 0;
     int cus = 256;
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf bytes, offsets, labels, scores, langs;
+    ScoreStage stage[2];
 };
 
 extern "C" const char* ldgpu_version(void) { return "ldgpu 0.1.0 (gfx950)"; }
@@ -133,8 +199,12 @@ extern "C" int ldgpu_ctx_create(int32_t device, ldgpu_ctx** out) {
     c->device = device;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (auto& st : c->stage) {
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&st.done, hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
-        delete c;
+        (void)ldgpu_ctx_destroy(c);
         return fail(LDGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     *out = c;
@@ -150,7 +220,14 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
     c->labels.release();
     c->scores.release();
     c->langs.release();
-    (void)hipStreamDestroy(c->stream);
+    for (auto& st : c->stage) {
+        if (st.stream) (void)hipStreamSynchronize(st.stream);
+        for (DevBuf* b : {&st.bytes, &st.offsets, &st.labels, &st.scores}) b->release();
+        for (HostBuf* b : {&st.h_bytes, &st.h_offsets, &st.h_labels, &st.h_scores}) b->release();
+        if (st.done) (void)hipEventDestroy(st.done);
+        if (st.stream) (void)hipStreamDestroy(st.stream);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return ok();
 }
@@ -163,6 +240,22 @@ extern "C" int ldgpu_ctx_synchronize(ldgpu_ctx* c) {
 }
 
 extern "C" void* ldgpu_ctx_stream(ldgpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int ldgpu_host_alloc(ldgpu_ctx* c, int64_t n_bytes, void** out) {
+    if (!c || !out) return fail(LDGPU_EINVAL, "ctx/out is NULL");
+    if (n_bytes < 0) return fail(LDGPU_EINVAL, "n_bytes < 0");
+    HIP_TRY(hipSetDevice(c->device));
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, (size_t)std::max<int64_t>(n_bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(LDGPU_ENOMEM, "hipHostMalloc(%lld): %s", (long long)n_bytes, hipGetErrorString(e));
+    return ok();
+}
+
+extern "C" int ldgpu_host_free(ldgpu_ctx* c, void* p) {
+    if (!c) return fail(LDGPU_EINVAL, "ctx is NULL");
+    if (p) HIP_TRY(hipHostFree(p));
+    return ok();
+}
 
 // -------------------------------------------------------------------- model
 struct ldgpu_model {
@@ -564,6 +657,12 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     return LDGPU_OK;
 }
 
+// the whole byte range the documents span lies in pinned memory
+bool nb_total_pinned(const uint8_t* bytes, const int64_t* offsets, int64_t n_docs) {
+    if (offsets[n_docs] <= offsets[0]) return true;
+    return is_pinned(bytes + offsets[0]) && is_pinned(bytes + offsets[n_docs] - 1);
+}
+
 int check_row_error(ldgpu_model* m, hipStream_t st) {
     int32_t err = 0;
     HIP_TRY(hipMemcpyAsync(&err, m->d_err, sizeof err, hipMemcpyDeviceToHost, st));
@@ -611,35 +710,80 @@ extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* 
     ldgpu_ctx* c = m->ctx;
     std::lock_guard<std::mutex> lock(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    const int64_t kChunkBytes = 256ll << 20, kChunkDocs = 8ll << 20;
-    std::vector<int64_t> off;
+    // Two-stage pipeline over chunks of documents, one stream per stage: while
+    // the GPU copies and scores chunk i, the host stages chunk i + 1 into the
+    // other stage's pinned buffers (a caller buffer already in pinned memory is
+    // copied from directly) and hands back the labels of chunk i - 1.
+    const int64_t kChunkBytes = 64ll << 20, kChunkDocs = 1ll << 20;
+    const bool pinned_in = nb_total_pinned(bytes, offsets, n_docs);
+    const bool pinned_out = is_pinned(out_labels) && (!out_scores || is_pinned(out_scores));
+    auto retire = [&](ScoreStage& st) -> int {
+        if (!st.busy) return LDGPU_OK;
+        HIP_TRY(hipEventSynchronize(st.done));
+        st.busy = false;
+        if (!pinned_out) {
+            memcpy(out_labels + st.d0, st.h_labels.p, sizeof(int32_t) * st.nd);
+            if (out_scores) par_memcpy(out_scores + st.d0 * m->L, st.h_scores.p, sizeof(double) * st.nd * m->L);
+        }
+        return LDGPU_OK;
+    };
     int64_t d0 = 0;
-    while (d0 < n_docs) {
+    int k = 0;
+    int rc = LDGPU_OK;
+    while (d0 < n_docs && rc == LDGPU_OK) {
         int64_t d1 = d0 + 1;
         while (d1 < n_docs && d1 - d0 < kChunkDocs && offsets[d1 + 1] - offsets[d0] <= kChunkBytes) ++d1;
         const int64_t nd = d1 - d0, b0 = offsets[d0], nb = offsets[d1] - b0;
-        off.resize(nd + 1);
-        for (int64_t i = 0; i <= nd; ++i) off[i] = offsets[d0 + i] - b0;
-        HIP_TRY(c->bytes.ensure((size_t)nb + 16));
-        HIP_TRY(c->offsets.ensure(sizeof(int64_t) * (nd + 1)));
-        HIP_TRY(c->labels.ensure(sizeof(int32_t) * nd));
-        if (out_scores) HIP_TRY(c->scores.ensure(sizeof(double) * nd * m->L));
-        if (nb) HIP_TRY(hipMemcpyAsync(c->bytes.p, bytes + b0, nb, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->offsets.p, off.data(), sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice,
-                               c->stream));
-        if (int rc = score_launch(m, (const uint8_t*)c->bytes.p, nb, (const int64_t*)c->offsets.p, nd,
-                                  (int32_t*)c->labels.p, out_scores ? (double*)c->scores.p : nullptr, c->stream))
-            return rc;
-        HIP_TRY(hipMemcpyAsync(out_labels + d0, c->labels.p, sizeof(int32_t) * nd, hipMemcpyDeviceToHost,
-                               c->stream));
+        ScoreStage& st = c->stage[k & 1];
+        if ((rc = retire(st))) break;
+        HIP_TRY(st.bytes.ensure((size_t)nb + 16));
+        HIP_TRY(st.offsets.ensure(sizeof(int64_t) * (nd + 1)));
+        HIP_TRY(st.labels.ensure(sizeof(int32_t) * nd));
+        if (out_scores) HIP_TRY(st.scores.ensure(sizeof(double) * nd * m->L));
+        HIP_TRY(st.h_offsets.ensure(sizeof(int64_t) * (nd + 1)));
+        int64_t* ho = (int64_t*)st.h_offsets.p;
+        for (int64_t i = 0; i <= nd; ++i) ho[i] = offsets[d0 + i] - b0;
+        const uint8_t* src = bytes + b0;
+        if (nb && !pinned_in) {
+            HIP_TRY(st.h_bytes.ensure((size_t)nb));
+            par_memcpy(st.h_bytes.p, src, (size_t)nb);
+            src = (const uint8_t*)st.h_bytes.p;
+        }
+        if (nb) HIP_TRY(hipMemcpyAsync(st.bytes.p, src, nb, hipMemcpyHostToDevice, st.stream));
+        HIP_TRY(hipMemcpyAsync(st.offsets.p, ho, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, st.stream));
+        if ((rc = score_launch(m, (const uint8_t*)st.bytes.p, nb, (const int64_t*)st.offsets.p, nd,
+                               (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, st.stream)))
+            break;
+        int32_t* lab_dst = out_labels + d0;
+        double* sc_dst = out_scores ? out_scores + d0 * m->L : nullptr;
+        if (!pinned_out) {
+            HIP_TRY(st.h_labels.ensure(sizeof(int32_t) * nd));
+            lab_dst = (int32_t*)st.h_labels.p;
+            if (out_scores) {
+                HIP_TRY(st.h_scores.ensure(sizeof(double) * nd * m->L));
+                sc_dst = (double*)st.h_scores.p;
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(lab_dst, st.labels.p, sizeof(int32_t) * nd, hipMemcpyDeviceToHost, st.stream));
         if (out_scores)
-            HIP_TRY(hipMemcpyAsync(out_scores + d0 * m->L, c->scores.p, sizeof(double) * nd * m->L,
-                                   hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipMemcpyAsync(sc_dst, st.scores.p, sizeof(double) * nd * m->L, hipMemcpyDeviceToHost,
+                                   st.stream));
+        HIP_TRY(hipEventRecord(st.done, st.stream));
+        st.d0 = d0;
+        st.nd = nd;
+        st.busy = true;
         d0 = d1;
+        ++k;
     }
+    // drain in chunk order (also after an error, so no copy outlives the call)
+    for (int i = 0; i < 2; ++i) {
+        const int r = retire(c->stage[(k + i) & 1]);
+        if (!rc) rc = r;
+    }
+    if (rc) return rc;
     if (m->has_bad) {
-        if (int rc = check_row_error(m, c->stream)) return rc;
+        for (auto& st : c->stage) HIP_TRY(hipStreamSynchronize(st.stream));
+        if (int r = check_row_error(m, c->stream)) return r;
     }
     return ok();
 }

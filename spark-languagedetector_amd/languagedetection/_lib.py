@@ -42,6 +42,8 @@ SIGNATURES = [
     ("ldgpu_ctx_destroy", ctypes.c_int, [_p]),
     ("ldgpu_ctx_synchronize", ctypes.c_int, [_p]),
     ("ldgpu_ctx_stream", _p, [_p]),
+    ("ldgpu_host_alloc", ctypes.c_int, [_p, _i64, _pp]),
+    ("ldgpu_host_free", ctypes.c_int, [_p, _p]),
     ("ldgpu_model_create", ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _i32, _p, _i32, _pp]),
     ("ldgpu_model_destroy", ctypes.c_int, [_p]),
     ("ldgpu_model_info", ctypes.c_int, [_p, _pi32, _pi64, _pi64, _pi64, _pi64]),

@@ -19,6 +19,35 @@ def _grams(gram_lengths: Sequence[int]) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(list(gram_lengths), dtype=np.int32))
 
 
+class PinnedArray:
+    """Page-locked host memory (ldgpu_host_alloc) viewed as a numpy array:
+    host-buffer scoring copies from / to it directly, with no staging copy."""
+
+    def __init__(self, shape, dtype, device: Optional[int] = None):
+        self.lib = _lib.load()
+        self.ctx = _lib.context(device)
+        dt = np.dtype(dtype)
+        shape = (shape,) if isinstance(shape, int) else tuple(shape)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = ctypes.c_void_p()
+        _lib.check(self.lib.ldgpu_host_alloc(self.ctx, n, ctypes.byref(p)))
+        self.p = p.value
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(self.p)
+        self.array = np.frombuffer(buf, dtype=np.uint8, count=n).view(dt).reshape(shape)
+
+    def close(self):
+        if getattr(self, "p", None):
+            self.array = None
+            self.lib.ldgpu_host_free(self.ctx, ctypes.c_void_p(self.p))
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DeviceModel:
     """A gram -> probability-row table resident on one GPU
     (LanguageDetectorModel's broadcast table, LanguageDetectorModel.scala:222)."""
@@ -53,13 +82,18 @@ class DeviceModel:
         return {"mode": mode.value, "n_keys": vals[0].value, "table_slots": vals[1].value,
                 "filter_bits": vals[2].value, "device_bytes": vals[3].value}
 
-    def score(self, data: np.ndarray, offsets: np.ndarray, want_scores: bool = False
-              ) -> Tuple[np.ndarray, Optional[np.ndarray]]:
-        """Host buffers -> (labels int32[n], scores fp64[n, L] or None)."""
+    def score(self, data: np.ndarray, offsets: np.ndarray, want_scores: bool = False,
+              out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """Host buffers -> (labels int32[n], scores fp64[n, L] or None);
+        `out` (e.g. a PinnedArray's array) receives the labels."""
         data = np.ascontiguousarray(data, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         n = len(offsets) - 1
-        labels = np.zeros(max(n, 0), dtype=np.int32)
+        if out is not None:
+            labels = out
+            assert labels.dtype == np.int32 and labels.shape == (max(n, 0),) and labels.flags.c_contiguous
+        else:
+            labels = np.zeros(max(n, 0), dtype=np.int32)
         scores = np.zeros((max(n, 0), self.L), dtype=np.float64) if want_scores else None
         _lib.check(self.lib.ldgpu_score(self.h, _ptr(data), _ptr(offsets), n, _ptr(labels), _ptr(scores)))
         return labels, scores

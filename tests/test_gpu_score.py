@@ -264,6 +264,31 @@ def test_device_pointer_api_with_torch():
     assert np.array_equal(bits(d_sc.cpu().numpy()), bits(os_))
 
 
+def test_host_path_chunked_pinned_and_pageable():
+    """ldgpu_score pipelines chunks (64 MiB / 1M documents) over two streams:
+    1.3M documents span several chunks; pageable and pinned (ldgpu_host_alloc)
+    inputs and outputs give the oracle's labels and scores."""
+    from languagedetection.runtime import PinnedArray
+    ls = synth.make_languages(6, seed=21)
+    pdata, poff, _ = synth.generate(ls, 20000, 20, 120, seed=22)
+    data, off, _ = synth.tile(pdata, poff, np.zeros(20000, np.int32), 1_300_000)
+    tdata, toff, tlang = synth.generate(ls, 600, 100, 400, seed=23)
+    rows = list(zip([ls.names[i] for i in tlang], synth.texts(tdata, toff)))
+    from languagedetection.api import LanguageDetector
+    table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3], 300, ls.names)
+    m = DeviceModel(table, 6, [1, 2, 3])
+    ol, os_ = oracle_c(table, 6, [1, 2, 3], data, off)
+    lab, sc = m.score(data, off, want_scores=True)
+    assert np.array_equal(lab, ol) and np.array_equal(bits(sc), bits(os_))
+    pin = PinnedArray(len(data) + 16, np.uint8)
+    pin.array[:len(data)] = data
+    pout = PinnedArray(len(off) - 1, np.int32)
+    lab2, _ = m.score(pin.array[:len(data)], off, out=pout.array)
+    assert np.array_equal(pout.array, ol)
+    pin.close()
+    pout.close()
+
+
 def test_bench_shape_parity_sample():
     """The headline configuration's shape (L=20, grams 1-5, 256-byte docs) on a
     fit-produced table, 20k documents, against the C restatement."""

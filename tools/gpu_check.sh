@@ -22,6 +22,6 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python -u bench.py "$@"
-step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline
+step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-path
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; 2>/dev/null
 echo "== done"; cat "$OUT/kernel_stats.csv" 2>/dev/null | head -20

@@ -11,7 +11,7 @@ for spec in "$@"; do
   name=${spec%%|*}; envs=${spec#*|}
   for e in $envs; do export "$e"; done
   timeout -s KILL 240 rocprofv3 --pmc $CTR --output-format csv -d "$PWD/$OUT/$name/pass1" -o run -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --docs 4000000 > "$OUT/$name.log" 2>&1
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path --docs 4000000 > "$OUT/$name.log" 2>&1
   rc=$?
   for e in $envs; do unset "${e%%=*}"; done
   echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/$name.log"; exit $rc; }
