@@ -41,13 +41,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--docs", type=int, default=10_000_000, help="documents per GPU")
-    ap.add_argument("--doc-bytes", type=int, default=256)
-    ap.add_argument("--langs", type=int, default=20)
-    ap.add_argument("--grams", type=str, default="1,2,3,4,5")
-    ap.add_argument("--profile-size", type=int, default=500)
+    ap.add_argument("--config", type=int, choices=[2, 4, 5], default=2,
+                    help="BASELINE.json config: 2 = headline (default), 4 = short text, 5 = large profile")
+    ap.add_argument("--docs", type=int, default=None, help="documents per GPU")
+    ap.add_argument("--doc-bytes", type=int, default=None, help="fixed document length (sets min = max)")
+    ap.add_argument("--doc-min", type=int, default=None)
+    ap.add_argument("--doc-max", type=int, default=None)
+    ap.add_argument("--langs", type=int, default=None)
+    ap.add_argument("--grams", type=str, default=None)
+    ap.add_argument("--profile-size", type=int, default=None)
     ap.add_argument("--pool", type=int, default=250_000, help="distinct generated docs, tiled to --docs")
-    ap.add_argument("--train-docs", type=int, default=1000, help="training docs per language for the table")
+    ap.add_argument("--train-docs", type=int, default=None, help="training docs per language for the table")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
@@ -56,11 +60,27 @@ def parse():
     ap.add_argument("--mode", choices=["score", "fit"], default="score",
                     help="score = the headline metric (config 2); fit = config 3's count + table build")
     ap.add_argument("--fit-bytes", type=int, default=1 << 30, help="fit mode: corpus bytes per GPU")
-    return ap.parse_args()
+    args = ap.parse_args()
+    # SURVEY §8d shapes; explicit flags override
+    preset = {2: dict(docs=10_000_000, doc_min=256, doc_max=256, langs=20, grams="1,2,3,4,5", profile_size=500,
+                      train_docs=1000),
+              4: dict(docs=25_000_000, doc_min=32, doc_max=96, langs=100, grams="1,2,3,4,5", profile_size=1000,
+                      train_docs=300),
+              5: dict(docs=10_000_000, doc_min=256, doc_max=256, langs=200, grams="1,2,3,4,5,6,7",
+                      profile_size=50_000, train_docs=80)}[args.config]
+    if args.doc_bytes is not None:
+        args.doc_min = args.doc_max = args.doc_bytes
+    for k, v in preset.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    args.doc_bytes = args.doc_min
+    return args
 
 
 def build_table(args, ls, device):
-    """FIT on the GPU (the reference's LanguageDetector.fit path) -> profile table."""
+    """FIT on the GPU (the reference's LanguageDetector.fit path) -> the
+    profile table in mask form (packed arrays), plus it as a {gram: row} dict
+    when small enough for the CPU baseline."""
     grams = [int(x) for x in args.grams.split(",")]
     lang = np.repeat(np.arange(args.langs, dtype=np.int32), args.train_docs)
     data, off, lang = synth.generate(ls, len(lang), 200, 2000, seed=synth.SEED_BASE + 100, doc_lang=lang)
@@ -68,12 +88,23 @@ def build_table(args, ls, device):
     counts = DeviceCounts(args.langs, grams, capacity_hint=1 << 20, device=device)
     counts.count(data, off, lang)
     n_distinct = counts.size()
-    table = counts.fit_table(args.profile_size)
+    kb, ko, masks, vals = counts.fit_table_masks(args.profile_size)
     fit_s = time.perf_counter() - t0
     counts.close()
+    n = len(ko) - 1
+    table = None
+    if n * args.langs <= 50_000_000:
+        b = kb.tobytes()
+        table = {}
+        for i in range(n):
+            row = [0.0] * args.langs
+            for l in range(args.langs):
+                if (int(masks[i, l // 64]) >> (l % 64)) & 1:
+                    row[l] = float(vals[i])
+            table[b[ko[i]:ko[i + 1]]] = row
     fit_info = {"train_docs": int(len(lang)), "train_bytes": int(off[-1]), "distinct_grams": int(n_distinct),
-                "table_rows": len(table), "host_wall_s": round(fit_s, 3)}
-    return table, grams, fit_info
+                "table_rows": int(n), "host_wall_s": round(fit_s, 3)}
+    return (kb, ko, masks, vals), table, grams, fit_info
 
 
 def cpu_baseline(args, table, grams, data, off):
@@ -91,7 +122,7 @@ def cpu_baseline(args, table, grams, data, off):
     t.score(grams, data, off[:n + 1], nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 1), "unit": "docs/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of the GPU's documents ({args.doc_bytes} B each), same table, "
+            "sample": f"first {n} of the GPU's documents ({args.doc_min}-{args.doc_max} B), same table, "
                       f"{threads} pthreads, {dt:.1f} s"}
 
 
@@ -240,14 +271,15 @@ def main():
     ls = synth.make_languages(args.langs)
     if args.empty_table:
         table, grams, fit_info = {}, [int(x) for x in args.grams.split(",")], {}
+        model = DeviceModel(table, args.langs, grams, device=local)
     else:
-        table, grams, fit_info = build_table(args, ls, local)
-    model = DeviceModel(table, args.langs, grams, device=local)
+        packed, table, grams, fit_info = build_table(args, ls, local)
+        model = DeviceModel.from_masks(*packed, args.langs, grams, device=local)
 
     # this rank's documents: a generated pool tiled to --docs, resident in HBM
     pool = min(args.pool, args.docs)
-    pdata, poff, plang = synth.generate(ls, pool, args.doc_bytes, args.doc_bytes,
-                                        seed=synth.SEED_BASE + 2 + 1000 * rank)
+    pdata, poff, plang = synth.generate(ls, pool, args.doc_min, args.doc_max,
+                                        seed=synth.SEED_BASE + args.config + 1000 * rank)
     data, off, _ = synth.tile(pdata, poff, plang, args.docs)
     n_docs = len(off) - 1
     n_bytes = int(off[-1])
@@ -288,25 +320,37 @@ def main():
     acc = float((d_lab[:pool].cpu().numpy() == plang[:n_docs][:pool]).mean()) if table else None
 
     info = model.info()
-    doc_b = args.doc_bytes
-    algo_per_doc = doc_b + 8 + 4                          # bytes + int64 offset + int32 label
-    table_bytes = info["device_bytes"]                    # read once per launch (amortised)
-    algo_per_launch = n_docs * algo_per_doc + table_bytes
+    doc_b = n_bytes / max(n_docs, 1)                      # mean document bytes
+    windows = int(sum(synth_windows(off, n) for n in grams))
+    algo_per_launch = n_bytes + 12 * n_docs               # bytes + int64 offset + int32 label
+    algo_per_launch += info["device_bytes"]               # the table, read once per launch (amortised)
+    if args.config == 5:
+        # table far beyond LDS / L2: SURVEY §8d charges one 64-B HBM sector per window probe
+        algo_per_launch += 64 * windows
     achieved = algo_per_launch / (kernel_ms * 1e-3) / 1e9
-    workload_key = f"score:docs={n_docs}:bytes={doc_b}:L={args.langs}:G={args.grams}:K={args.profile_size}"
+    workload_key = (f"score:docs={n_docs}:bytes={args.doc_min}-{args.doc_max}:L={args.langs}:G={args.grams}"
+                    f":K={args.profile_size}")
+    if args.config == 2:
+        workload_key = f"score:docs={n_docs}:bytes={args.doc_min}:L={args.langs}:G={args.grams}:K={args.profile_size}"
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(workload_key),
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo_per_launch),
-                "lookups_per_s": round(n_docs * sum(max(doc_b - n + 1, 1) for n in grams) / (kernel_ms * 1e-3), 1)}
+                "lookups_per_s": round(windows / (kernel_ms * 1e-3), 1)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and table:
         cpu = cpu_baseline(args, table, grams, data, off)
     host = None
-    if rank == 0 and world == 1 and not args.no_host_path and table:
+    if rank == 0 and world == 1 and not args.no_host_path and not args.empty_table:
         host = host_path(model, data, off, acc_labels=d_lab.cpu().numpy())
 
     total_docs = n_docs * world * args.steps
+    doc_desc = f"{args.doc_min} B" if args.doc_min == args.doc_max else f"U[{args.doc_min},{args.doc_max}] B"
+    if args.config != 2:
+        line_note = {4: "config 4 is quoted on 1B docs over 8 GPUs (1.25e8 per GPU); --docs sets this run's count",
+                     5: "config 5: table of up to L*K rows far beyond LDS: bloom in L2/MALL, slots in HBM"}[args.config]
+    else:
+        line_note = None
     line = {
         "metric": METRIC,
         "value": round(total_docs / elapsed, 1),
@@ -320,9 +364,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (Markov-chain text per language, SURVEY.md §8d generator; table FIT on the GPU)",
-        "config": {"workload": f"config2: score {n_docs} x {doc_b} B docs per GPU, {args.langs} languages, "
-                               f"grams {args.grams}, profile size {args.profile_size}",
-                   "docs_per_gpu": n_docs, "doc_bytes": doc_b, "languages": args.langs, "gram_lengths": grams,
+        "config": {"workload": f"config{args.config}: score {n_docs} x {doc_desc} docs per GPU, {args.langs} "
+                               f"languages, grams {args.grams}, profile size {args.profile_size}",
+                   "docs_per_gpu": n_docs, "doc_bytes": round(doc_b, 2), "languages": args.langs,
+                   "gram_lengths": grams,
                    "profile_size": args.profile_size, "table_rows": info["n_keys"],
                    "table_mode": {0: "mask", 1: "dense", 2: "mask, one shared value (hit counts)"}[info["mode"]],
                    "parallelism": f"dp{world} (documents sharded, no collective)"},
@@ -332,6 +377,8 @@ def main():
         "fit_setup": fit_info,
         "label_accuracy_vs_generator": acc,
     }
+    if line_note:
+        line["note"] = line_note
     if rank == 0:
         s = json.dumps(line)
         print(s, flush=True)

@@ -87,6 +87,13 @@ int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
                        const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
                        int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
                        ldgpu_model** out);
+/* Mask form of the same table (what a fit produces, and what a table too
+ * large for dense rows is carried in): row i is vals[i] at the languages set
+ * in masks[i*S .. (i+1)*S), S = ceil(n_langs / 64), 0.0 elsewhere. */
+int ldgpu_model_create_masks(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                             const int64_t* key_offsets, const uint64_t* masks, const double* vals,
+                             int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                             ldgpu_model** out);
 int ldgpu_model_destroy(ldgpu_model* model);
 
 /* mode: 0 = every row is one value times a language bitmask, 1 = dense fp64
@@ -167,6 +174,11 @@ int ldgpu_fit_table_size(ldgpu_counts* counts, int32_t profile_size, int64_t* n_
                          int64_t* key_bytes);
 int ldgpu_fit_table_export(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
                            double* rows);
+/* The same table in mask form (masks [n_rows][ceil(L/64)], vals [n_rows]):
+ * 8 (S + 1) bytes per row instead of 8 L -- what ldgpu_model_create_masks
+ * takes (config-5 tables: 10M rows x 200 languages). */
+int ldgpu_fit_table_export_masks(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
+                                 uint64_t* masks, double* vals);
 
 #ifdef __cplusplus
 }

@@ -311,27 +311,35 @@ hipError_t upload(T** dst, const std::vector<T>& src, size_t* total) {
 }
 }  // namespace
 
-extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
-                                  const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
-                                  int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
-                                  ldgpu_model** out) {
+namespace {
+// A table parsed into device form: unique packed keys (Scala toMap semantics:
+// a later duplicate key wins; keys longer than every window, which can never
+// be hit, are dropped), per key a wrong-length flag, and either mask form
+// (masks [n][S], vals [n]) or dense fp64 rows [n][L].
+struct ParsedTable {
+    std::vector<uint64_t> keys;
+    std::vector<uint8_t> bad;
+    bool dense = false;
+    std::vector<uint64_t> masks;
+    std::vector<double> vals, drows;
+};
+
+int check_model_args(ldgpu_ctx* ctx, ldgpu_model** out, int64_t n_rows, int32_t n_langs,
+                     const int32_t* gram_lengths, int32_t n_grams) {
     if (!ctx || !out) return fail(LDGPU_EINVAL, "ctx/out is NULL");
     if (n_langs < 1) return fail(LDGPU_EINVAL, "No values in array: the model has no supported languages");
     if (n_langs > LDGPU_MAX_LANGS)
         return fail(LDGPU_EUNSUPPORTED, "%d languages exceed the device path's limit of %d", n_langs,
                     LDGPU_MAX_LANGS);
     if (n_rows < 0) return fail(LDGPU_EINVAL, "n_rows < 0");
-    if (n_rows > 0 && (!key_bytes || !key_offsets || !rows)) return fail(LDGPU_EINVAL, "table pointer is NULL");
-    if (int rc = check_grams(gram_lengths, n_grams)) return rc;
-    int maxg = 0;
-    for (int i = 0; i < n_grams; ++i) maxg = std::max(maxg, gram_lengths[i]);
+    return check_grams(gram_lengths, n_grams);
+}
 
-    // host map, Scala toMap semantics (a later duplicate key wins); keys longer
-    // than every window (> max gram length) can never be hit and stay host-side.
+// unique keys -> source row index (later duplicates win)
+int unique_keys(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets, int maxg,
+                std::vector<uint64_t>& keys, std::vector<int64_t>& src_row) {
     std::unordered_map<uint64_t, int64_t> idx;
     idx.reserve((size_t)n_rows * 2 + 1);
-    std::vector<uint64_t> keys;
-    std::vector<int64_t> src_row;
     for (int64_t r = 0; r < n_rows; ++r) {
         const int64_t len = key_offsets[r + 1] - key_offsets[r];
         if (len < 0) return fail(LDGPU_EINVAL, "key_offsets decrease at row %lld", (long long)r);
@@ -346,12 +354,36 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
             src_row[it->second] = r;
         }
     }
-    const int64_t nk = (int64_t)keys.size();
+    return LDGPU_OK;
+}
+
+int max_gram(const int32_t* G, int32_t nG) {
+    int maxg = 0;
+    for (int i = 0; i < nG; ++i) maxg = std::max(maxg, G[i]);
+    return maxg;
+}
+
+int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ParsedTable& t,
+                ldgpu_model** out);
+}  // namespace
+
+extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                                  const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
+                                  int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                                  ldgpu_model** out) {
+    if (int rc = check_model_args(ctx, out, n_rows, n_langs, gram_lengths, n_grams)) return rc;
+    if (n_rows > 0 && (!key_bytes || !key_offsets || !rows)) return fail(LDGPU_EINVAL, "table pointer is NULL");
+    ParsedTable t;
+    std::vector<int64_t> src_row;
+    if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row))
+        return rc;
+    const int64_t nk = (int64_t)t.keys.size();
     const int S = (n_langs + 63) / 64;
+    t.bad.resize(nk);
+    for (int64_t i = 0; i < nk; ++i) t.bad[i] = row_ok && !row_ok[src_row[i]];
 
     // mask form: every nonzero entry of every row bitwise equal within the row
-    bool dense = false;
-    for (int64_t i = 0; i < nk && !dense; ++i) {
+    for (int64_t i = 0; i < nk && !t.dense; ++i) {
         const double* rw = rows + src_row[i] * (int64_t)n_langs;
         uint64_t v = 0;
         bool have = false;
@@ -363,11 +395,68 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
                 v = b;
                 have = true;
             } else if (b != v) {
-                dense = true;
+                t.dense = true;
                 break;
             }
         }
     }
+    if (!t.dense) {
+        t.masks.assign((size_t)nk * S, 0);
+        t.vals.assign((size_t)nk, 0.0);
+        for (int64_t i = 0; i < nk; ++i) {
+            const double* rw = rows + src_row[i] * (int64_t)n_langs;
+            for (int l = 0; l < n_langs; ++l) {
+                if (rw[l] == 0.0) continue;
+                t.masks[(size_t)i * S + l / 64] |= 1ull << (l % 64);
+                t.vals[i] = rw[l];
+            }
+        }
+    } else {
+        t.drows.resize((size_t)nk * n_langs);
+        for (int64_t i = 0; i < nk; ++i)
+            memcpy(&t.drows[(size_t)i * n_langs], rows + src_row[i] * (int64_t)n_langs, sizeof(double) * n_langs);
+    }
+    return model_build(ctx, n_langs, gram_lengths, n_grams, t, out);
+}
+
+extern "C" int ldgpu_model_create_masks(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                                        const int64_t* key_offsets, const uint64_t* masks, const double* vals,
+                                        int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                                        ldgpu_model** out) {
+    if (int rc = check_model_args(ctx, out, n_rows, n_langs, gram_lengths, n_grams)) return rc;
+    if (n_rows > 0 && (!key_bytes || !key_offsets || !masks || !vals))
+        return fail(LDGPU_EINVAL, "table pointer is NULL");
+    ParsedTable t;
+    std::vector<int64_t> src_row;
+    if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row))
+        return rc;
+    const int64_t nk = (int64_t)t.keys.size();
+    const int S = (n_langs + 63) / 64;
+    t.bad.assign(nk, 0);
+    t.masks.resize((size_t)nk * S);
+    t.vals.resize(nk);
+    for (int64_t i = 0; i < nk; ++i) {
+        memcpy(&t.masks[(size_t)i * S], masks + src_row[i] * S, sizeof(uint64_t) * S);
+        if (n_langs % 64) t.masks[(size_t)i * S + S - 1] &= (1ull << (n_langs % 64)) - 1ull;
+        t.vals[i] = vals[src_row[i]];
+        // a row whose value is 0.0 (or -0.0) is the all-zero row
+        if (t.vals[i] == 0.0)
+            for (int s = 0; s < S; ++s) t.masks[(size_t)i * S + s] = 0;
+    }
+    return model_build(ctx, n_langs, gram_lengths, n_grams, t, out);
+}
+
+namespace {
+int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ParsedTable& t,
+                ldgpu_model** out) {
+    const int64_t nk = (int64_t)t.keys.size();
+    const int S = (n_langs + 63) / 64;
+    const bool dense = t.dense;
+    std::vector<uint64_t>& keys = t.keys;
+    std::vector<uint64_t>& masks = t.masks;
+    std::vector<double>& vals = t.vals;
+    std::vector<double>& drows = t.drows;
+    std::vector<double> fold;
 
     auto* m = new ldgpu_model();
     m->ctx = ctx;
@@ -377,21 +466,12 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     m->slices = S;
     m->dense = dense;
     m->n_keys = nk;
-
-    std::vector<uint64_t> masks;
-    std::vector<double> vals, drows, fold;
     m->mode = dense ? 2 : 1;
     if (!dense) {
-        masks.assign((size_t)nk * S, 0);
-        vals.assign((size_t)nk, 0.0);
-        for (int64_t i = 0; i < nk; ++i) {
-            const double* rw = rows + src_row[i] * (int64_t)n_langs;
-            for (int l = 0; l < n_langs; ++l) {
-                if (rw[l] == 0.0) continue;
-                masks[(size_t)i * S + l / 64] |= 1ull << (l % 64);
-                vals[i] = rw[l];
-                if (!std::isfinite(rw[l])) m->mode = 0;
-            }
+        for (int64_t i = 0; i < nk && m->mode == 1; ++i) {
+            bool any = false;
+            for (int s = 0; s < S; ++s) any |= masks[(size_t)i * S + s] != 0;
+            if (any && !std::isfinite(vals[i])) m->mode = 0;
         }
         // one value shared by every row with a nonzero entry: order-free
         // per-language hit counts (mode 3) reproduce the fold exactly
@@ -423,10 +503,6 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
             m->count_sign = v > 0.0 ? 1 : (v < 0.0 ? -1 : 0);
             m->count_int_argmax = std::fabs(v) < 1e300;
         }
-    } else {
-        drows.resize((size_t)nk * n_langs);
-        for (int64_t i = 0; i < nk; ++i)
-            memcpy(&drows[(size_t)i * n_langs], rows + src_row[i] * (int64_t)n_langs, sizeof(double) * n_langs);
     }
 
     // key -> row slots (mask form: the row's value and first mask word inline),
@@ -450,7 +526,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
                 cur.val = vals[i];
                 cur.mask0 = masks[(size_t)i * S];
             }
-            if (row_ok && !row_ok[src_row[i]]) {
+            if (t.bad[i]) {
                 cur.row |= kBadRow;
                 m->has_bad = true;
             }
@@ -531,7 +607,7 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
                 if (w && !bits) lang = 64 * s + __builtin_ctzll(w);
                 bits += __builtin_popcountll(w);
             }
-            ok = bits == 1 && !(row_ok && !row_ok[src_row[i]]);
+            ok = bits == 1 && !t.bad[i];
             if (kl == 1) lang1[keys[i] & 0xff] = (uint8_t)lang;
             else lang2of[keys[i] & 0xffff] = (uint8_t)lang;
         }
@@ -585,6 +661,8 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     *out = m;
     return ok();
 }
+
+}  // namespace
 
 extern "C" int ldgpu_model_destroy(ldgpu_model* m) {
     model_free(m);
@@ -806,7 +884,8 @@ struct ldgpu_counts {
     bool tbl_valid = false;
     std::vector<uint8_t> tbl_bytes;
     std::vector<int64_t> tbl_off;
-    std::vector<double> tbl_rows;
+    std::vector<uint64_t> tbl_masks;  // [rows][S] presence masks of the chosen grams
+    std::vector<double> tbl_vals;     // [rows] log(1 + 1/k): the value of every nonzero entry
 };
 
 namespace {
@@ -1250,11 +1329,17 @@ int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_byt
         }
     }
     std::vector<uint64_t> out_keys;
-    c->tbl_rows.clear();
+    const int S = (L + 63) / 64;
+    c->tbl_masks.clear();
+    c->tbl_vals.clear();
     for (size_t i = 0; i < n; ++i) {
         if (!chosen[i]) continue;
         out_keys.push_back(keys[i]);
-        for (int l = 0; l < L; ++l) c->tbl_rows.push_back(cnt[i * L + l] ? w[kg[i]] : 0.0);
+        c->tbl_masks.resize(c->tbl_masks.size() + S, 0);
+        uint64_t* mk = &c->tbl_masks[c->tbl_masks.size() - S];
+        for (int l = 0; l < L; ++l)
+            if (cnt[i * L + l]) mk[l / 64] |= 1ull << (l % 64);
+        c->tbl_vals.push_back(w[kg[i]]);
     }
     int64_t nb = 0;
     for (uint64_t k : out_keys) nb += key_len(k);
@@ -1405,12 +1490,13 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     for (uint64_t i = 0; i < m; ++i) order[i] = {sort_key(ok[i]), i};
     std::sort(order.begin(), order.end());
     std::vector<uint64_t> out_keys(m);
-    c->tbl_rows.assign((size_t)m * L, 0.0);
+    c->tbl_masks.assign((size_t)m * S, 0);
+    c->tbl_vals.assign((size_t)m, 0.0);
     for (uint64_t r = 0; r < m; ++r) {
         const uint64_t i = order[r].second;
         out_keys[r] = ok[i];
-        for (int l = 0; l < L; ++l)
-            if ((om[i * S + l / 64] >> (l % 64)) & 1ull) c->tbl_rows[r * L + l] = w[okk[i]];
+        memcpy(&c->tbl_masks[r * S], &om[i * S], sizeof(uint64_t) * S);
+        c->tbl_vals[r] = w[okk[i]];
     }
     int64_t nb = 0;
     for (uint64_t k : out_keys) nb += key_len(k);
@@ -1448,6 +1534,24 @@ extern "C" int ldgpu_fit_table_export(ldgpu_counts* c, uint8_t* key_bytes, int64
     if (c->tbl_off[n] && !key_bytes) return fail(LDGPU_EINVAL, "key_bytes is NULL");
     if (c->tbl_off[n]) memcpy(key_bytes, c->tbl_bytes.data(), (size_t)c->tbl_off[n]);
     memcpy(key_offsets, c->tbl_off.data(), sizeof(int64_t) * (n + 1));
-    if (!c->tbl_rows.empty()) memcpy(rows, c->tbl_rows.data(), sizeof(double) * c->tbl_rows.size());
+    const int L = c->L, S = (L + 63) / 64;
+    for (size_t r = 0; r < n; ++r)
+        for (int l = 0; l < L; ++l)
+            rows[r * L + l] = ((c->tbl_masks[r * S + l / 64] >> (l % 64)) & 1ull) ? c->tbl_vals[r] : 0.0;
+    return ok();
+}
+
+extern "C" int ldgpu_fit_table_export_masks(ldgpu_counts* c, uint8_t* key_bytes, int64_t* key_offsets,
+                                            uint64_t* masks, double* vals) {
+    if (!c || !key_offsets || !masks || !vals) return fail(LDGPU_EINVAL, "NULL argument");
+    if (!c->tbl_valid) return fail(LDGPU_EINVAL, "call ldgpu_fit_table_size first");
+    const size_t n = c->tbl_off.size() - 1;
+    if (c->tbl_off[n] && !key_bytes) return fail(LDGPU_EINVAL, "key_bytes is NULL");
+    if (c->tbl_off[n]) memcpy(key_bytes, c->tbl_bytes.data(), (size_t)c->tbl_off[n]);
+    memcpy(key_offsets, c->tbl_off.data(), sizeof(int64_t) * (n + 1));
+    if (n) {
+        memcpy(masks, c->tbl_masks.data(), sizeof(uint64_t) * c->tbl_masks.size());
+        memcpy(vals, c->tbl_vals.data(), sizeof(double) * n);
+    }
     return ok();
 }

@@ -45,6 +45,7 @@ SIGNATURES = [
     ("ldgpu_host_alloc", ctypes.c_int, [_p, _i64, _pp]),
     ("ldgpu_host_free", ctypes.c_int, [_p, _p]),
     ("ldgpu_model_create", ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _i32, _p, _i32, _pp]),
+    ("ldgpu_model_create_masks", ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _i32, _p, _i32, _pp]),
     ("ldgpu_model_destroy", ctypes.c_int, [_p]),
     ("ldgpu_model_info", ctypes.c_int, [_p, _pi32, _pi64, _pi64, _pi64, _pi64]),
     ("ldgpu_score", ctypes.c_int, [_p, _p, _p, _i64, _p, _p]),
@@ -60,6 +61,7 @@ SIGNATURES = [
     ("ldgpu_counts_add_device", ctypes.c_int, [_p, _i64, _p, _p, _p]),
     ("ldgpu_fit_table_size", ctypes.c_int, [_p, _i32, _pi64, _pi64]),
     ("ldgpu_fit_table_export", ctypes.c_int, [_p, _p, _p, _p]),
+    ("ldgpu_fit_table_export_masks", ctypes.c_int, [_p, _p, _p, _p, _p]),
 ]
 
 _lib = None

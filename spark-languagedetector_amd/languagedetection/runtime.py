@@ -64,6 +64,28 @@ class DeviceModel:
                                                self.L, _ptr(g), len(g), ctypes.byref(out)))
         self.h = out.value
 
+    @classmethod
+    def from_masks(cls, key_bytes: np.ndarray, key_offsets: np.ndarray, masks: np.ndarray, vals: np.ndarray,
+                   n_langs: int, gram_lengths: Sequence[int], device: Optional[int] = None) -> "DeviceModel":
+        """A mask-form table (row i = vals[i] at the languages set in masks[i])
+        as packed arrays, e.g. DeviceCounts.fit_table_masks (ldgpu_model_create_masks)."""
+        self = cls.__new__(cls)
+        self.lib = _lib.load()
+        self.ctx = _lib.context(device)
+        self.L = int(n_langs)
+        self.gram_lengths = list(gram_lengths)
+        kb = np.ascontiguousarray(key_bytes, dtype=np.uint8)
+        ko = np.ascontiguousarray(key_offsets, dtype=np.int64)
+        mk = np.ascontiguousarray(masks, dtype=np.uint64)
+        vv = np.ascontiguousarray(vals, dtype=np.float64)
+        assert mk.shape == (len(ko) - 1, (self.L + 63) // 64) and vv.shape == (len(ko) - 1,)
+        g = _grams(gram_lengths)
+        out = ctypes.c_void_p()
+        _lib.check(self.lib.ldgpu_model_create_masks(self.ctx, len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(mk), _ptr(vv),
+                                                     self.L, _ptr(g), len(g), ctypes.byref(out)))
+        self.h = out.value
+        return self
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.ldgpu_model_destroy(self.h)
@@ -212,3 +234,20 @@ class DeviceCounts:
         _lib.check(self.lib.ldgpu_fit_table_export(self.h, _ptr(kb), _ptr(ko), _ptr(rows)))
         b = kb.tobytes()
         return {b[ko[i]:ko[i + 1]]: rows[i].tolist() for i in range(n.value)}
+
+    def fit_table_masks(self, profile_size: int):
+        """The fit table in mask form, as packed arrays: (key_bytes uint8,
+        key_offsets int64 [n+1], masks uint64 [n, S], vals fp64 [n]) -- what
+        DeviceModel.from_masks takes; no per-row Python objects, so tables of
+        10M rows x 200 languages stay cheap."""
+        n = ctypes.c_int64()
+        nb = ctypes.c_int64()
+        _lib.check(self.lib.ldgpu_fit_table_size(self.h, int(profile_size), ctypes.byref(n), ctypes.byref(nb)))
+        S = (self.L + 63) // 64
+        kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        ko = np.zeros(n.value + 1, dtype=np.int64)
+        masks = np.zeros((max(n.value, 1), S), dtype=np.uint64)
+        vals = np.zeros(max(n.value, 1), dtype=np.float64)
+        _lib.check(self.lib.ldgpu_fit_table_export_masks(self.h, _ptr(kb), _ptr(ko), _ptr(masks), _ptr(vals)))
+        return kb, ko, masks[:n.value], vals[:n.value]
+

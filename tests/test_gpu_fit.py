@@ -157,3 +157,31 @@ def test_device_export_add_roundtrip_and_device_top_k():
     probs = O.fit_probabilities(rows, ls.names, [1, 2, 3, 4])
     expect = O.filter_top_grams(probs, ls.names, 300)
     assert a.fit_table(300) == expect
+
+
+@pytest.mark.parametrize("L,grams,K", [(20, [1, 2, 3, 4, 5], 300), (70, [1, 2, 3], 50), (8, [2, 3], 100000)])
+def test_fit_table_mask_form_and_model_from_masks(L, grams, K):
+    """ldgpu_fit_table_export_masks carries the same table as the dense export
+    (row = val at the mask's languages), and a model built from it
+    (ldgpu_model_create_masks) scores bit-identically to the dense-built one."""
+    from languagedetection.runtime import DeviceModel
+    ls = synth.make_languages(L, seed=300 + L)
+    data, off, lang = synth.generate(ls, 40 * L, 50, 300, seed=L + 1)
+    counts = DeviceCounts(L, grams)
+    counts.count(data, off, lang)
+    dense = counts.fit_table(K)
+    kb, ko, masks, vals = counts.fit_table_masks(K)
+    b = kb.tobytes()
+    assert len(ko) - 1 == len(dense)
+    for i in range(len(ko) - 1):
+        row = dense[b[ko[i]:ko[i + 1]]]
+        exp = [vals[i] if (int(masks[i, l // 64]) >> (l % 64)) & 1 else 0.0 for l in range(L)]
+        assert row == exp
+    counts.close()
+    sdata, soff, _ = synth.generate(ls, 3000, 0, 300, seed=L + 2)
+    m1 = DeviceModel(dense, L, grams)
+    m2 = DeviceModel.from_masks(kb, ko, masks, vals, L, grams)
+    assert m1.info()["mode"] == m2.info()["mode"]
+    l1, s1 = m1.score(sdata, soff, want_scores=True)
+    l2, s2 = m2.score(sdata, soff, want_scores=True)
+    assert np.array_equal(l1, l2) and np.array_equal(s1.view(np.uint64), s2.view(np.uint64))
