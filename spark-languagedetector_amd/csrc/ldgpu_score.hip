@@ -526,11 +526,21 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 // superblock if N is a listed length with table keys, and queue the
 // candidates unless the queue would overflow (then `over` is set and the
 // document restarts on the general path).
-template <int N, bool FULL>
+// Count-mode verify of a full queue in the middle of a document's probe
+// (hit-dense tables: config 5's 10M keys); counts are order-free, so the
+// probe just continues.
+template <int S, bool STAGED>
+__device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds& wl, int qn, const DocSrc& src,
+                                            int lane) {
+    double acc[S];  // unused in count mode
+    flush<S, 3, STAGED>(p, wl, qn, src, acc, lane, true);
+}
+
+template <int N, bool FULL, int S, bool STAGED>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
-                                            bool& over, uint32_t dummy_a) {
-    if (over || !((p.fast_mask >> N) & 1u)) return;
+                                            const DocSrc& src, uint32_t dummy_a) {
+    if (!((p.fast_mask >> N) & 1u)) return;
     if constexpr (N <= 2) {
         if (p.direct_words) {
             direct_count<N>(p, wl, img, x, len - N + 1, lane);
@@ -545,23 +555,23 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
     else
         test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
     if (qn + count_sb(m) > kQueueCap) {
-        over = true;
-        return;
+        flush_count<S, STAGED>(p, wl, qn, src, lane);
+        qn = 0;
     }
     append_sb(wl.queue, dummy_a, qn, m, N, 0, lane);
 }
 
-template <bool FULL>
+template <bool FULL, int S, bool STAGED>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
-                                                bool& over, uint32_t dummy_a) {
-    probe_count<1, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
-    probe_count<2, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
-    probe_count<3, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
-    probe_count<4, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
-    probe_count<5, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
-    probe_count<6, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
-    probe_count<7, FULL>(p, wl, img, f, x, len, lane, qn, over, dummy_a);
+                                                const DocSrc& src, uint32_t dummy_a) {
+    probe_count<1, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<2, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<3, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<4, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<5, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<6, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<7, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
@@ -591,9 +601,9 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             load_fwords(p, bloom, x, f);
             if constexpr (MODE == 3) {
                 if (len >= 192 + p.maxg)
-                    probe_count_all<true>(p, wl, img, f, x, (int32_t)len, lane, qn, general, dummy_a);
+                    probe_count_all<true, S, STAGED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
                 else
-                    probe_count_all<false>(p, wl, img, f, x, (int32_t)len, lane, qn, general, dummy_a);
+                    probe_count_all<false, S, STAGED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
             }
             uint64_t gq = p.gpack[0];
             for (int gi = 0; gi < (MODE == 3 ? 0 : p.n_fast); ++gi) {
