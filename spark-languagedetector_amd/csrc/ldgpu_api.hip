@@ -276,6 +276,8 @@ struct ldgpu_model {
     int ablate = 0;           // diagnostics: LDGPU_ABLATE (never set in production)
     size_t device_bytes = 0;
     Slot* d_slots = nullptr;
+    Bucket* d_buckets = nullptr;  // count mode key table
+    uint64_t n_buckets = 0;
     uint32_t* d_filter = nullptr;
     uint64_t* d_masks = nullptr;
     double* d_vals = nullptr;
@@ -285,6 +287,7 @@ struct ldgpu_model {
     uint32_t direct_off = 0, direct_words = 0;  // mode 3: direct tables in the image (ScoreParams)
     bool count_int_argmax = false;  // mode 3: label = first max of the counts (monotone fold)
     int32_t* d_err = nullptr;
+    unsigned long long* d_stats = nullptr;  // LDGPU_STATS diagnostics (printed at destroy)
 };
 
 // mode 3 fold table: fold[c] = ((0.0 + v) + v) ... c times
@@ -294,7 +297,13 @@ namespace {
 void model_free(ldgpu_model* m) {
     if (!m) return;
     if (m->ctx) (void)hipSetDevice(m->ctx->device);
-    for (void* p : {(void*)m->d_slots, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
+    if (m->d_stats) {
+        unsigned long long st[2] = {0, 0};
+        if (hipMemcpy(st, m->d_stats, sizeof st, hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "[ldgpu] stats: candidates verified %llu, hits %llu\n", st[0], st[1]);
+        (void)hipFree(m->d_stats);
+    }
+    for (void* p : {(void*)m->d_slots, (void*)m->d_buckets, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
                     (void*)m->d_fold, (void*)m->d_err})
         if (p) (void)hipFree(p);
     delete m;
@@ -365,6 +374,63 @@ int max_gram(const int32_t* G, int32_t nG) {
 
 int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ParsedTable& t,
                 ldgpu_model** out);
+
+// Place every key in nb 4-slot buckets (count mode).  Primary bucket while it
+// has room, else the secondary (raising the primary's overflow flag), else a
+// bounded random walk of evictions; false when it does not settle.
+bool bucket_place(const std::vector<uint64_t>& keys, const std::vector<uint64_t>& masks, int S,
+                  const std::vector<uint8_t>& bad, uint64_t nb, std::vector<Bucket>& out) {
+    out.assign(nb, Bucket{});
+    const int lg = log2u(nb);
+    auto prim = [&](uint64_t k) { return mix64(k) >> (64 - lg); };
+    auto sec = [&](uint64_t k) { return mix64(k) & (nb - 1); };
+    auto key_at = [&](uint64_t b, int s) { return out[b].k[s] & ~kBucketOverflow; };
+    auto put = [&](uint64_t b, int s, uint64_t k, uint64_t pay) {
+        out[b].k[s] = (out[b].k[s] & kBucketOverflow) | k;
+        out[b].p[s] = pay;
+        if (b != prim(k)) out[prim(k)].k[0] |= kBucketOverflow;
+    };
+    auto free_slot = [&](uint64_t b) {
+        for (int s = 0; s < 4; ++s)
+            if (key_at(b, s) == kEmpty) return s;
+        return -1;
+    };
+    uint64_t rng = 0x9E3779B97F4A7C15ull;
+    for (size_t i = 0; i < keys.size(); ++i) {
+        uint32_t lang = 0xffffffffu;
+        int bits = 0;
+        for (int s = 0; s < S; ++s) {
+            const uint64_t w = masks[i * S + s];
+            if (w && !bits) lang = 64u * (uint32_t)s + (uint32_t)__builtin_ctzll(w);
+            bits += __builtin_popcountll(w);
+        }
+        if (bits != 1) lang = 0xffffffffu;
+        uint64_t k = keys[i];
+        uint64_t pay = ((uint64_t)lang << 32) | (uint32_t)i | (bad[i] ? kBadRow : 0u);
+        bool placed = false;
+        for (int step = 0; step < 1000 && !placed; ++step) {
+            const uint64_t b1 = prim(k), b2 = sec(k);
+            int s;
+            if ((s = free_slot(b1)) >= 0) {
+                put(b1, s, k, pay);
+                placed = true;
+            } else if ((s = free_slot(b2)) >= 0) {
+                put(b2, s, k, pay);
+                placed = true;
+            } else {
+                // evict a random resident of the secondary bucket; it retries its own buckets
+                rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+                s = (int)(rng >> 62);
+                const uint64_t vk = key_at(b2, s), vp = out[b2].p[s];
+                put(b2, s, k, pay);
+                k = vk;
+                pay = vp;
+            }
+        }
+        if (!placed) return false;
+    }
+    return true;
+}
 }  // namespace
 
 extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
@@ -512,19 +578,47 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // per key) lets the cuckoo walk settle in a few steps; a walk that does
     // not settle doubles the table and starts over.
     std::vector<Slot> slots;
-    for (m->slot_cap = next_pow2(std::max<uint64_t>(16, (uint64_t)(2.5 * (double)nk) + 1));;
-         m->slot_cap *= 2) {
+    std::vector<Bucket> buckets;
+    // count mode with a table beyond the caches (> 2^20 keys: 32 MiB of slots):
+    // 2-choice buckets of 4 slots (Bucket, ldgpu_common.h) at load 0.4-0.75,
+    // so most lookups read ONE HBM line instead of two slots; cache-resident
+    // tables keep the two independent slot loads (one dependent step less)
+    // (such a table's bloom never fits LDS: the keyed kernels, which alone read buckets)
+    const bool use_buckets = m->mode == 3 && nk > (1 << 20);
+    if (use_buckets) {
+        for (m->n_buckets = next_pow2(std::max<uint64_t>(16, (uint64_t)nk / 3 + 1));; m->n_buckets *= 2) {
+            if (bucket_place(keys, masks, S, t.bad, m->n_buckets, buckets)) break;
+            if (m->n_buckets >= (1ull << 32)) {
+                delete m;
+                return fail(LDGPU_ENOMEM, "key table: bucket placement failed");
+            }
+        }
+        m->slot_cap = m->n_buckets * 4;
+        for (int64_t i = 0; i < nk; ++i) m->has_bad |= t.bad[i] != 0;
+    }
+    for (m->slot_cap = use_buckets ? m->slot_cap
+                                   : next_pow2(std::max<uint64_t>(16, (uint64_t)(2.5 * (double)nk) + 1));
+         !use_buckets; m->slot_cap *= 2) {
         const int slog = log2u(m->slot_cap);
         const uint64_t cmask = m->slot_cap - 1;
         auto pos1 = [&](uint64_t k) { return mix64(k) >> (64 - slog); };
         auto pos2 = [&](uint64_t k) { return mix64(k) & cmask; };
-        slots.assign(m->slot_cap, Slot{kEmpty, 0, 0, 0.0, 0});
+        slots.assign(m->slot_cap, Slot{kEmpty, 0, 0xffffffffu, 0.0, 0});
         bool ok_all = true;
         for (int64_t i = 0; i < nk && ok_all; ++i) {
-            Slot cur{keys[i], (uint32_t)i, 0, 0.0, 0};
+            Slot cur{keys[i], (uint32_t)i, 0xffffffffu, 0.0, 0};
             if (!dense) {
                 cur.val = vals[i];
                 cur.mask0 = masks[(size_t)i * S];
+                // the row's one language, when it has exactly one (count mode reads it
+                // instead of the mask words)
+                int bits = 0;
+                for (int s = 0; s < S; ++s) {
+                    const uint64_t w = masks[(size_t)i * S + s];
+                    if (w && !bits) cur.pad = 64u * (uint32_t)s + (uint32_t)__builtin_ctzll(w);
+                    bits += __builtin_popcountll(w);
+                }
+                if (bits != 1) cur.pad = 0xffffffffu;
             }
             if (t.bad[i]) {
                 cur.row |= kBadRow;
@@ -583,11 +677,13 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         } else {
             const uint32_t lo = (uint32_t)keys[i];
             const uint32_t hi = (uint32_t)(keys[i] >> 32) & ((1u << (8 * std::max(0, kl - 4))) - 1u);
-            const uint32_t b = pf_bit(kl, lo, hi);
-            filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (b & 31u);
-#ifdef LDGPU_BLOOM_K2
-            filter[kBloomBase + pf_word(lo, bshift)] |= 1u << ((b >> 5) & 31u);
-#endif
+            if (m->lds_filter) {  // prefix bloom
+                const uint32_t b = pf_bit(kl, lo, hi);
+                filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (b & 31u);
+            } else {  // keyed bloom (kb_hash)
+                const uint32_t h = kb_hash(lo, hi, (uint32_t)kl);
+                filter[kBloomBase + (h >> bshift)] |= 1u << ((h >> (bshift - 5)) & 31u);
+            }
         }
     }
 
@@ -635,6 +731,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
 
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = upload(&m->d_slots, slots, &m->device_bytes);
+    if (e == hipSuccess && use_buckets) e = upload(&m->d_buckets, buckets, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_filter, filter, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_masks, masks, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_vals, vals, &m->device_bytes);
@@ -648,6 +745,10 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
     if (const char* ov = getenv("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
     if (const char* ab = getenv("LDGPU_ABLATE")) m->ablate = atoi(ab);
+    if (getenv("LDGPU_STATS") && e == hipSuccess) {
+        e = hipMalloc((void**)&m->d_stats, 2 * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemset(m->d_stats, 0, 2 * sizeof(unsigned long long));
+    }
     if (getenv("LDGPU_DEBUG"))
         fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d direct=%u slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
                         "resident_api=%d wg_per_cu=%d\n",
@@ -696,9 +797,11 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.labels = d_labels;
     p.scores = d_scores;
     p.slots = m->d_slots;
-    const int slog = log2u(m->slot_cap);
-    p.slot_shift = (uint32_t)(64 - slog);  // slot 1 = h >> slot_shift, slot 2 = h & slot_mask
-    p.slot_mask = m->slot_cap - 1;
+    p.buckets = m->d_buckets;
+    // slot (bucket) 1 = h >> slot_shift, slot (bucket) 2 = h & slot_mask
+    const uint64_t n_index = m->d_buckets ? m->n_buckets : m->slot_cap;
+    p.slot_shift = (uint32_t)(64 - log2u(n_index));
+    p.slot_mask = n_index - 1;
     p.filter = m->d_filter;
     p.bloom_shift = (uint32_t)(32 - m->filter_log2);
     p.bloom_words = (uint32_t)((uint64_t)1 << m->filter_log2);
@@ -714,6 +817,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     // counts stay below 2^24: c <= windows of a document <= len * n_grams
     p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;
     p.err = m->d_err;
+    p.stats = m->d_stats;
     p.L = m->L;
     p.ablate = m->ablate;
     p.nG = m->nG;

@@ -60,6 +60,17 @@ __host__ __device__ __forceinline__ uint32_t pf_bit(int klen, uint32_t lo, uint3
     return pf_bit_c(lo, hi, pf_shift(klen), pf_mult(klen));
 }
 
+// Keyed bloom (tables whose bloom exceeds LDS): for a key of klen >= 3 bytes
+// (lo / hi = its bytes, masked to klen) word = h >> (32 - wlog), bit =
+// (h >> (27 - wlog)) mod 32 of h = kb_hash -- three 24-bit multiplies over
+// bytes 0..2, 3..5 and (6, length), whose top bits depend on every input bit.
+__host__ __device__ __forceinline__ uint32_t kb_hash(uint32_t lo, uint32_t hi, uint32_t klen) {
+    const uint32_t a = lo & 0xffffffu;
+    const uint32_t b = (lo >> 24) | (hi << 8);
+    const uint32_t c = (hi >> 16) | (klen << 8);
+    return mul24(a, 0x9E3779u) ^ mul24(b, 0x85EBCAu) ^ mul24(c ^ (a >> 12), 0xC2B2AFu);
+}
+
 // Filter image (host-built, staged whole into LDS): a direct 256-bit bitmap
 // of the 1-byte keys, a direct 65536-bit bitmap of the 2-byte keys, then the
 // prefix Bloom words.
@@ -110,11 +121,23 @@ __host__ __device__ __forceinline__ int64_t n_windows(int64_t len, int n) {
 struct alignas(16) Slot {
     uint64_t key;
     uint32_t row;
-    uint32_t pad;
+    uint32_t pad;   // the row's one language when it has exactly one, else 0xffffffff
     double val;
     uint64_t mask0;
 };
 
 constexpr uint32_t kBadRow = 0x80000000u;
+
+// Count-mode key table: 2-choice buckets of 4 slots, one 64-B line each.
+// p[i] = row | (the row's one language, or 0xffffffff) << 32.  A key goes
+// to its primary bucket (h >> (64 - log2 buckets)) while it has room, else to
+// its secondary one (h & (buckets - 1)), and then its primary bucket's
+// overflow flag (bit 63 of k[0]: never set in a key, whose top byte is its
+// length <= 7) is raised -- so most lookups read ONE line.
+struct alignas(64) Bucket {
+    uint64_t k[4];
+    uint64_t p[4];
+};
+constexpr uint64_t kBucketOverflow = 1ull << 63;
 
 }  // namespace ldgpu

@@ -16,7 +16,8 @@ struct ScoreParams {
     int32_t group;              // documents per staged group (1..63)
     int32_t* labels;            // [n_docs]
     double* scores;             // nullable [n_docs][L]
-    const Slot* slots;          // open-addressed key -> row table
+    const Slot* slots;          // open-addressed key -> row table (modes 0-2)
+    const Bucket* buckets;      // count mode: bucketed key -> (row, language) table; slot_shift/mask index it
     uint32_t slot_shift;        // slot = mix64(key) >> slot_shift
     uint64_t slot_mask;
     const uint32_t* filter;     // image: bmp1 | bmp2 | bloom (ldgpu_common.h)
@@ -31,6 +32,7 @@ struct ScoreParams {
     int32_t count_sign;         // count mode: sign of the value (fold[c] strictly monotone)
     int64_t count_argmax_len;   // count mode: documents up to this length take count_argmax (-1: none)
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
+    unsigned long long* stats;  // diagnostics build (-DLDGPU_STATS, env LDGPU_STATS): [0] candidates verified, [1] hits
     int32_t L;
     int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay
     int32_t nG;

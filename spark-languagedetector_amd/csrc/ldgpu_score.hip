@@ -176,9 +176,23 @@ __device__ __forceinline__ void hit_add(const uint4 (&e)[kHitQuads<S>], double (
 }
 
 // Verify + accumulate the queued candidates (in queue order).
+// Look key up in one bucket (one 64-B line: 4 keys, then 4 payloads).
+__device__ __forceinline__ bool bucket_find(const Bucket* b, uint64_t key, uint64_t& pay) {
+    const uint4* q = reinterpret_cast<const uint4*>(b);
+    const uint4 k01 = q[0], k23 = q[1];
+    const uint64_t k0 = (((uint64_t)k01.y << 32) | k01.x) & ~kBucketOverflow;
+    const uint64_t k1 = ((uint64_t)k01.w << 32) | k01.z;
+    const uint64_t k2 = ((uint64_t)k23.y << 32) | k23.x;
+    const uint64_t k3 = ((uint64_t)k23.w << 32) | k23.z;
+    const int sl = k0 == key ? 0 : (k1 == key ? 1 : (k2 == key ? 2 : (k3 == key ? 3 : -1)));
+    if (sl < 0) return false;
+    pay = b->p[sl];
+    return true;
+}
+
 // weighted (MODE 3 fast path, distinct gram lengths): a hit of a k-byte key
 // counts p.mult[k] times (k's multiplicity in gramLengths).
-template <int S, int MODE, bool STAGED>
+template <int S, int MODE, bool STAGED, bool KEYED>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
                                       double (&acc)[S], int lane, bool weighted = false) {
     __builtin_amdgcn_wave_barrier();
@@ -187,6 +201,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         uint32_t row = 0xffffffffu;
         double v = 0.0;
         uint64_t m0 = 0;
+        uint32_t lang1 = 0xffffffffu;  // count mode: the row's one language (Slot::pad)
         uint32_t inc = 1;
         if (j < qn) {
             const uint32_t e = w.queue[j];
@@ -197,18 +212,34 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
                                  __builtin_amdgcn_alignbyte(w1, w0, sh);
             const uint64_t key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
-            // 2-choice cuckoo table: the key is in one of two slots (or absent)
             const uint64_t h = mix64(key);
-            const Slot a = p.slots[h >> p.slot_shift];
-            const Slot c = p.slots[h & p.slot_mask];
-            if (a.key == key) {
-                row = a.row;
-                v = a.val;
-                m0 = a.mask0;
-            } else if (c.key == key) {
-                row = c.row;
-                v = c.val;
-                m0 = c.mask0;
+            if (MODE == 3 && KEYED && p.buckets) {  // (buckets only for tables beyond the caches)
+                // 4-slot buckets, one 64-B line each: the key is in its primary
+                // bucket, or -- only if that bucket's overflow flag is set -- in
+                // its secondary one (Bucket, ldgpu_common.h)
+                uint64_t pay = 0;
+                bool found = bucket_find(p.buckets + (h >> p.slot_shift), key, pay);
+                if (!found && (p.buckets[h >> p.slot_shift].k[0] & kBucketOverflow))
+                    found = bucket_find(p.buckets + (h & p.slot_mask), key, pay);
+                if (found) {
+                    row = (uint32_t)pay;
+                    lang1 = (uint32_t)(pay >> 32);
+                }
+            } else {
+                // 2-choice cuckoo table: the key is in one of two slots (or absent)
+                const Slot a = p.slots[h >> p.slot_shift];
+                const Slot c = p.slots[h & p.slot_mask];
+                if (a.key == key) {
+                    row = a.row;
+                    v = a.val;
+                    m0 = a.mask0;
+                    lang1 = a.pad;
+                } else if (c.key == key) {
+                    row = c.row;
+                    v = c.val;
+                    m0 = c.mask0;
+                    lang1 = c.pad;
+                }
             }
         }
         const bool hit = row != 0xffffffffu;
@@ -217,15 +248,28 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             if (lane == 0) atomicOr(p.err, 1);
         }
         const bool good = hit && !bad;
+#ifdef LDGPU_STATS
+        if (p.stats) {  // diagnostics build: candidates verified, hits
+            const int ng = __popcll(__ballot(good));
+            if (lane == 0) {
+                atomicAdd(&p.stats[0], (unsigned long long)min(64, qn - q0));
+                atomicAdd(&p.stats[1], (unsigned long long)ng);
+            }
+        }
+#endif
         if constexpr (MODE == 3) {
             // uniform-value table: order-free per-language hit counts (the
             // score is the fold of that many adds of the one value, applied
             // at the end of the document: count_scores)
-            if (good) {
+            if (S > 1 && good && lang1 != 0xffffffffu) {
+                // single-language row: no mask words to read (no extra lines)
+                __hip_atomic_fetch_add(&count_area(w)[lang1], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (good) {
                 uint32_t* cnt = count_area(w);
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    uint64_t mm = s == 0 ? m0 : p.masks[(size_t)row * S + s];
+                    // S = 1: the slot's mask word (buckets: S > 1 only reach here for multi-language rows)
+                    uint64_t mm = (S == 1 && !(KEYED && p.buckets)) ? m0 : p.masks[(size_t)row * S + s];
                     while (mm) {
                         const int l = __builtin_ctzll(mm);
                         mm &= mm - 1;
@@ -348,14 +392,28 @@ __device__ __forceinline__ int count_argmax(const ScoreParams& p, const WaveLds&
 // ldgpu_common.h): loaded once per superblock, they serve every gram length
 // >= 3 of the document.  The 1-/2-byte bitmap words are read per test (one
 // gram length each; caching them would cost 8 VGPRs of occupancy).
+// Keyed tables (bloom too large for LDS, read from L2/MALL): one word per
+// (position, length) chosen by the whole key instead (kb_hash,
+// ldgpu_common.h) -- a big table's keys share few 3-byte prefixes, which
+// would saturate prefix words; gb / gshift locate that bloom.
 struct FWords {
     uint32_t w3[kSub];
+    const uint32_t* gb;
+    uint32_t gshift;
 };
 
+template <bool KEYED>
 __device__ __forceinline__ void load_fwords(const ScoreParams& p, const uint32_t* bloom, const Windows& x,
                                             FWords& f) {
+    if constexpr (KEYED) {
+        f.gb = bloom;
+        f.gshift = p.bloom_shift;
 #pragma unroll
-    for (int k = 0; k < kSub; ++k) f.w3[k] = bloom[pf_word(x.lo[k], p.bloom_shift)];
+        for (int k = 0; k < kSub; ++k) f.w3[k] = 0;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) f.w3[k] = bloom[pf_word(x.lo[k], p.bloom_shift)];
+    }
 }
 
 // Filter-test the (up to) 256 windows of one superblock for one key length:
@@ -364,7 +422,8 @@ __device__ __forceinline__ void load_fwords(const ScoreParams& p, const uint32_t
 //   KIND 1 / 2 (1-/2-byte keys): bit (lo & 0xff) / (lo & 0xffff) of the exact
 //   bitmaps;
 //   KIND 3 (3..7 bytes): bit pf_bit_c(lo, hi, sh, mul) of the position's
-//   prefix-Bloom word, already in a register (f).
+//   prefix-Bloom word, already in a register (f);
+//   KIND 4 (3..7 bytes, keyed bloom): the key's own word, loaded here.
 // nw = windows left from the superblock's first position, in
 // (64 (NSB - 1), 64 NSB] when NSB < 4: the last sub-block's ballot is cut to
 // its first nw - 64 (NSB - 1) lanes by a scalar mask.
@@ -384,17 +443,20 @@ __device__ __forceinline__ void test_len(const uint32_t* img, uint32_t sh, uint3
         } else if constexpr (KIND == 2) {
             w[k] = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
             bit[k] = x.lo[k];
-        } else {
+        } else if constexpr (KIND == 3) {
             w[k] = f.w3[k];
             bit[k] = mulhi24(__builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh), mul);
+        } else {  // KIND 4, keyed bloom: sh = key length, mul = unused
+            const uint32_t lo = sh >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * sh)) - 1u);
+            const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh - 4))) - 1u);
+            const uint32_t h = kb_hash(lo, hi, sh);
+            w[k] = f.gb[h >> f.gshift];
+            bit[k] = h >> (f.gshift - 5);
         }
     }
 #pragma unroll
     for (int k = 0; k < NSB; ++k) {
-        uint32_t c = __builtin_amdgcn_ubfe(w[k], bit[k], 1);
-#ifdef LDGPU_BLOOM_K2
-        if constexpr (KIND == 3) c &= __builtin_amdgcn_ubfe(w[k], bit[k] >> 5, 1);
-#endif
+        const uint32_t c = __builtin_amdgcn_ubfe(w[k], bit[k], 1);
         m[k] = __builtin_amdgcn_ballot_w64(c != 0u);
     }
     m[NSB - 1] &= lanes_below(nw - 64 * (NSB - 1));
@@ -416,16 +478,17 @@ __device__ __forceinline__ void test_nsb(const uint32_t* img, uint32_t sh, uint3
 }
 
 // FULL: every length has more than 192 windows (NSB = 4, no dispatch)
-template <bool FULL>
+template <bool FULL, bool KEYED>
 __device__ __forceinline__ void test_sb(const uint32_t* img, int klen, const FWords& f, const Windows& x, int32_t nw,
                                         uint64_t (&m)[kSub]) {
-    const uint32_t sh = pf_shift(klen), mul = pf_mult(klen);
+    const uint32_t sh = KEYED ? (uint32_t)klen : pf_shift(klen), mul = pf_mult(klen);
+    constexpr int K3 = KEYED ? 4 : 3;
     if (klen == 1) {
         if (FULL) test_len<1, 4>(img, sh, mul, f, x, nw, m); else test_nsb<1>(img, sh, mul, f, x, nw, m);
     } else if (klen == 2) {
         if (FULL) test_len<2, 4>(img, sh, mul, f, x, nw, m); else test_nsb<2>(img, sh, mul, f, x, nw, m);
     } else {
-        if (FULL) test_len<3, 4>(img, sh, mul, f, x, nw, m); else test_nsb<3>(img, sh, mul, f, x, nw, m);
+        if (FULL) test_len<K3, 4>(img, sh, mul, f, x, nw, m); else test_nsb<K3>(img, sh, mul, f, x, nw, m);
     }
 }
 
@@ -529,14 +592,14 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 // Count-mode verify of a full queue in the middle of a document's probe
 // (hit-dense tables: config 5's 10M keys); counts are order-free, so the
 // probe just continues.
-template <int S, bool STAGED>
+template <int S, bool STAGED, bool KEYED>
 __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds& wl, int qn, const DocSrc& src,
                                             int lane) {
     double acc[S];  // unused in count mode
-    flush<S, 3, STAGED>(p, wl, qn, src, acc, lane, true);
+    if (!(p.ablate & 1)) flush<S, 3, STAGED, KEYED>(p, wl, qn, src, acc, lane, true);
 }
 
-template <int N, bool FULL, int S, bool STAGED>
+template <int N, bool FULL, int S, bool STAGED, bool KEYED>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                             const DocSrc& src, uint32_t dummy_a) {
@@ -547,35 +610,35 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
             return;
         }
     }
-    constexpr int KIND = N < 3 ? N : 3;
-    constexpr uint32_t sh = N < 3 ? 0u : pf_shift(N), mul = N < 3 ? 0u : pf_mult(N);
+    constexpr int KIND = N < 3 ? N : (KEYED ? 4 : 3);
+    constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
     uint64_t m[kSub];
     if constexpr (FULL)
         test_len<KIND, 4>(img, sh, mul, f, x, len - N + 1, m);
     else
         test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
     if (qn + count_sb(m) > kQueueCap) {
-        flush_count<S, STAGED>(p, wl, qn, src, lane);
+        flush_count<S, STAGED, KEYED>(p, wl, qn, src, lane);
         qn = 0;
     }
     append_sb(wl.queue, dummy_a, qn, m, N, 0, lane);
 }
 
-template <bool FULL, int S, bool STAGED>
+template <bool FULL, int S, bool STAGED, bool KEYED>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                                 const DocSrc& src, uint32_t dummy_a) {
-    probe_count<1, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<2, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<3, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<4, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<5, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<6, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<7, FULL, S, STAGED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<1, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<2, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<3, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<4, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<5, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<6, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    probe_count<7, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
-template <int S, int MODE, bool STAGED>
+template <int S, int MODE, bool STAGED, bool KEYED>
 __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                           const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
                                           const DocSrc& src, int lane) {
@@ -598,12 +661,12 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             Windows x;
             load_windows<STAGED>(p, src, 0, lane, x);
             FWords f;
-            load_fwords(p, bloom, x, f);
+            load_fwords<KEYED>(p, bloom, x, f);
             if constexpr (MODE == 3) {
                 if (len >= 192 + p.maxg)
-                    probe_count_all<true, S, STAGED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
+                    probe_count_all<true, S, STAGED, KEYED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
                 else
-                    probe_count_all<false, S, STAGED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
+                    probe_count_all<false, S, STAGED, KEYED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
             }
             uint64_t gq = p.gpack[0];
             for (int gi = 0; gi < (MODE == 3 ? 0 : p.n_fast); ++gi) {
@@ -615,9 +678,9 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                 for (int k = 0; k < kSub; ++k) asm volatile("" : "+v"(x.lo[k]), "+v"(x.hi[k]), "+v"(f.w3[k]));
                 uint64_t m[kSub];
                 if (len >= 192 + p.maxg)
-                    test_sb<true>(img, n, f, x, (int32_t)len - n + 1, m);
+                    test_sb<true, KEYED>(img, n, f, x, (int32_t)len - n + 1, m);
                 else
-                    test_sb<false>(img, n, f, x, (int32_t)len - n + 1, m);
+                    test_sb<false, KEYED>(img, n, f, x, (int32_t)len - n + 1, m);
                 if (qn + count_sb(m) > kQueueCap) {  // rare
                     general = true;
                     break;
@@ -626,7 +689,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             }
             if (!general) {
                 if (p.ablate & 1) qn = 0;
-                if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane, MODE == 3);
+                if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane, MODE == 3);
             }
             qn = 0;
         }
@@ -644,11 +707,11 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                 Windows x;
                 load_windows<STAGED>(p, src, p0, lane, x);
                 FWords f;
-                if (g.klen >= 3) load_fwords(p, bloom, x, f);
+                if (g.klen >= 3) load_fwords<KEYED>(p, bloom, x, f);
                 uint64_t m[kSub];
-                test_sb<false>(img, g.klen, f, x, g.nwin - p0, m);
+                test_sb<false, KEYED>(img, g.klen, f, x, g.nwin - p0, m);
                 if (qn + count_sb(m) > kQueueCap) {
-                    flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
+                    flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
                     qn = 0;
                 }
                 append_sb(wl.queue, dummy_a, qn, m, g.klen, p0, lane);
@@ -656,7 +719,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
         }
     }
     if (p.ablate & 1) qn = 0;
-    if (qn) flush<S, MODE, STAGED>(p, wl, qn, src, acc, lane);
+    if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
         if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, wl, lane);
         count_scores<S>(p, wl, acc, lane);
@@ -808,7 +871,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{cur, b - s0};
-                const int lab = score_doc<S, MODE, true>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, true, !FLDS>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
             }
         } else {
@@ -816,7 +879,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{nullptr, b};
-                const int lab = score_doc<S, MODE, false>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, false, !FLDS>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
             }
         }
