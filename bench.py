@@ -379,6 +379,7 @@ def main():
     }
     if line_note:
         line["note"] = line_note
+    model.close()
     if rank == 0:
         s = json.dumps(line)
         print(s, flush=True)
