@@ -42,6 +42,8 @@ namespace {
 
 constexpr int kSub = 4;  // 64-position sub-blocks per superblock
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -226,19 +228,23 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                     lang1 = (uint32_t)(pay >> 32);
                 }
             } else {
-                // 2-choice cuckoo table: the key is in one of two slots (or absent)
-                const Slot a = p.slots[h >> p.slot_shift];
-                const Slot c = p.slots[h & p.slot_mask];
-                if (a.key == key) {
-                    row = a.row;
-                    v = a.val;
-                    m0 = a.mask0;
-                    lang1 = a.pad;
-                } else if (c.key == key) {
-                    row = c.row;
-                    v = c.val;
-                    m0 = c.mask0;
-                    lang1 = c.pad;
+                // 2-choice cuckoo table: the key is in one of two slots (or
+                // absent).  Both slots' four 16-B loads are issued before any
+                // compare (the register pin keeps the compiler from sinking
+                // the second slot's loads behind the first one's key test), so
+                // a candidate costs one L2 round trip, not three.
+                const u32x4* sl = reinterpret_cast<const u32x4*>(p.slots);
+                const uint64_t ia = h >> p.slot_shift, ic = h & p.slot_mask;
+                u32x4 a0 = sl[2 * ia], a1 = sl[2 * ia + 1], c0 = sl[2 * ic], c1 = sl[2 * ic + 1];
+                asm volatile("" : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1));
+                const bool ha = ((((uint64_t)a0.y) << 32) | a0.x) == key;
+                const bool hc = ((((uint64_t)c0.y) << 32) | c0.x) == key;
+                const u32x4 s0 = ha ? a0 : c0, s1 = ha ? a1 : c1;
+                if (ha || hc) {  // Slot: key, row, pad | val, mask0
+                    row = s0.z;
+                    lang1 = s0.w;
+                    v = __longlong_as_double((long long)((((uint64_t)s1.y) << 32) | s1.x));
+                    m0 = (((uint64_t)s1.w) << 32) | s1.z;
                 }
             }
         }
