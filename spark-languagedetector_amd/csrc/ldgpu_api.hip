@@ -982,7 +982,7 @@ struct ldgpu_counts {
     uint64_t* d_ovf_keys = nullptr;
     int32_t* d_ovf_lang = nullptr;
     unsigned int* d_ovf_n = nullptr;
-    uint32_t ovf_cap = 1u << 24;  // windows per sub-launch
+    uint32_t ovf_cap = 1u << 20;  // windows per sub-launch; grown per call up to kOvfMax
     uint64_t size = 0;
     // cached fit table (ldgpu_fit_table_size -> _export)
     bool tbl_valid = false;
@@ -1090,11 +1090,45 @@ int64_t doc_windows(const ldgpu_counts* c, int64_t len) {
     return w;
 }
 
+// Sub-launches hold <= ovf_cap windows (so the overflow list can never lose an
+// entry), and one launch must carry enough documents to fill the chip: one
+// wave per document, 2 x kCountWaves waves per CU => ~8k documents of 1-7 KB
+// = ~1.6e8 windows at grams 1..5.  The list (12 B per window) is grown to the
+// call's window count, capped at kOvfMax (1.5 GiB of HBM).
+constexpr uint32_t kOvfMax = 1u << 27;
+
+int ensure_ovf(ldgpu_counts* c, int64_t windows) {
+    const uint64_t want = std::min<uint64_t>(kOvfMax, next_pow2((uint64_t)std::max<int64_t>(windows, 1)));
+    if (want <= c->ovf_cap) return LDGPU_OK;
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    (void)hipFree(c->d_ovf_keys);
+    (void)hipFree(c->d_ovf_lang);
+    c->d_ovf_keys = nullptr;
+    c->d_ovf_lang = nullptr;
+    hipError_t e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * want);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * want);
+    if (e != hipSuccess) {
+        // fall back to the smallest list that still makes progress
+        (void)hipFree(c->d_ovf_keys);
+        c->d_ovf_keys = nullptr;
+        c->ovf_cap = 1u << 20;
+        e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
+        if (e != hipSuccess) return fail(LDGPU_ENOMEM, "overflow list: %s", hipGetErrorString(e));
+        return LDGPU_OK;
+    }
+    c->ovf_cap = (uint32_t)want;
+    return LDGPU_OK;
+}
+
 // Count documents [0, n_docs) of d_offsets / d_lang (h_off: the same offsets on
 // the host, used to plan sub-launches of at most ovf_cap windows each, so the
 // overflow list can never lose an entry).
 int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                  const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
+    int64_t total = 0;
+    for (int64_t d = 0; d < n_docs; ++d) total += doc_windows(c, h_off[d + 1] - h_off[d]);
+    if (int rc = ensure_ovf(c, total)) return rc;
     int64_t d0 = 0;
     while (d0 < n_docs) {
         int64_t d1 = d0, win = 0;
