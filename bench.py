@@ -187,18 +187,24 @@ def fit_main(args, world, rank, local, dev, backend):
         t = {}
         t0 = time.perf_counter()
         c = DeviceCounts(args.langs, grams, capacity_hint=1 << 22, device=local)
+        torch.cuda.synchronize(dev)
+        t["create_s"] = time.perf_counter() - t0
         c.count_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), d_lang.data_ptr(), n_docs, stream.cuda_stream)
         torch.cuda.synchronize(dev)
-        t["count_s"] = time.perf_counter() - t0
+        t["count_s"] = time.perf_counter() - t0 - t["create_s"]
         if world > 1:
             merged = merge_counts_device(c)
             c.close()
             c = merged
             torch.cuda.synchronize(dev)
-            t["merge_s"] = time.perf_counter() - t0 - t["count_s"]
+            t["merge_s"] = time.perf_counter() - t0 - t["create_s"] - t["count_s"]
         distinct = c.size()
+        t1 = time.perf_counter()
         table = c.fit_table(args.profile_size)
+        t["table_s"] = time.perf_counter() - t1
+        t2 = time.perf_counter()
         c.close()
+        t["close_s"] = time.perf_counter() - t2
         t["total_s"] = time.perf_counter() - t0
         return t, distinct, len(table)
 
@@ -230,7 +236,7 @@ def fit_main(args, world, rank, local, dev, backend):
                    "distinct_grams": parts[-1][1], "table_rows": parts[-1][2],
                    "parallelism": f"dp{world} (corpus sharded; all_gather + all_reduce merge)"},
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
-                     for k in ("count_s", "merge_s", "total_s")},
+                     for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
         "count_windows_per_s": round(windows / count_s, 1),
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6), "traffic": None},

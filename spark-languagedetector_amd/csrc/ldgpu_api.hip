@@ -1546,7 +1546,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
             if (acc + ck >= K) {
                 kstar[l] = k;
                 need[l] = (int32_t)(K - acc);
-                cand_cap += (uint64_t)ck;
+                if (need[l] > 0) cand_cap += (uint64_t)ck;
                 break;
             }
             acc += ck;
@@ -1577,30 +1577,17 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(hipStreamSynchronize(st));
     if (cn != cand_cap) return fail(LDGPU_EDEVICE, "select: %u candidates, %llu expected", cn,
                                     (unsigned long long)cand_cap);
-    std::vector<int32_t> cl(cn);
-    std::vector<uint64_t> ck(cn);
-    std::vector<uint32_t> ci(cn);
-    if (cn) {
-        HIP_TRY(hipMemcpyAsync(cl.data(), d_cl, sizeof(int32_t) * cn, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(ck.data(), d_ck, sizeof(uint64_t) * cn, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(ci.data(), d_ci, sizeof(uint32_t) * cn, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
-    // per language: the need[l] smallest (length, bytes) keys of its threshold class
-    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> per(L);
-    for (unsigned int i = 0; i < cn; ++i) per[cl[i]].push_back({ck[i], ci[i]});
-    std::vector<uint32_t> mark;
-    for (int l = 0; l < L; ++l) {
-        auto& v = per[l];
-        const size_t take = std::min<size_t>((size_t)std::max(need[l], 0), v.size());
-        if (take < v.size()) std::nth_element(v.begin(), v.begin() + take, v.end());
-        for (size_t i = 0; i < take; ++i) mark.push_back(v[i].second);
-    }
-    uint32_t* d_mark;
-    HIP_TRY(db.alloc(&d_mark, mark.size()));
-    if (!mark.empty())
-        HIP_TRY(hipMemcpyAsync(d_mark, mark.data(), sizeof(uint32_t) * mark.size(), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_mark(d_mark, (int64_t)mark.size(), d_chosen, st));
+    // per language: the need[l] smallest (length, bytes) keys of its threshold
+    // class, picked on the device (candidates of language l form segment l)
+    std::vector<int64_t> seg(L + 1, 0);
+    for (int l = 0; l < L; ++l)
+        seg[l + 1] = seg[l] + (need[l] > 0 && kstar[l] <= L ? (int64_t)hist[(size_t)l * (L + 1) + kstar[l]] : 0);
+    if (seg[L] != (int64_t)cn)
+        return fail(LDGPU_EDEVICE, "select: %u candidates, %lld by class", cn, (long long)seg[L]);
+    int64_t* d_seg;
+    HIP_TRY(db.alloc(&d_seg, L + 1));
+    HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), sizeof(int64_t) * (L + 1), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_topk_candidates((int64_t)cn, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, st));
     const int64_t cap_out = std::min<int64_t>(n, (int64_t)L * std::max<int32_t>(K, 0));
     uint64_t *d_ok, *d_om;
     int32_t* d_okk;

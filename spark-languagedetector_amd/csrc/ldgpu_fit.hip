@@ -21,6 +21,8 @@
 // growing the table.
 #include <algorithm>
 
+#include <hipcub/hipcub.hpp>
+
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
@@ -325,6 +327,27 @@ __global__ void gather_chosen_kernel(int64_t n, int S, const uint8_t* chosen, co
 
 unsigned grid_of(int64_t n, int b) { return (unsigned)std::max<int64_t>(1, (n + b - 1) / b); }
 
+__global__ void iota_kernel(int64_t n, uint32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)i;
+}
+
+__global__ void cand_lang_kernel(int64_t n, const uint32_t* perm, const int32_t* cand_lang, uint32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)cand_lang[perm[i]];
+}
+
+// candidates grouped by language, ascending (length, bytes) within a group:
+// the first need[l] of group l are language l's picks
+__global__ void cand_mark_kernel(int64_t n, const uint32_t* lang_sorted, const uint32_t* perm,
+                                 const int64_t* seg_start, const int32_t* need, const uint32_t* cand_idx,
+                                 uint8_t* chosen) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t l = lang_sorted[i];
+    if (i - seg_start[l] < (int64_t)need[l]) chosen[cand_idx[perm[i]]] = 1;
+}
+
 }  // namespace
 
 hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
@@ -342,6 +365,56 @@ hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const ui
     hipLaunchKernelGGL(select_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, L, S, keys, masks, ks, kstar,
                        need, chosen, cand_lang, cand_key, cand_idx, cand_n);
     return hipGetLastError();
+}
+
+// Threshold-class tie resolution on the device (filterTopGrams' take(K),
+// LanguageDetector.scala:113-119, under the build's (length, bytes) tie rule):
+// two stable LSD radix sorts -- by sort_key (59 bits), then by language
+// (8 bits) -- leave each language's candidates contiguous and in tie order.
+// Sort keys are unique per gram, so this picks exactly the set nth_element
+// picked on the host.  Synchronises `stream` before returning (scratch freed).
+hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const uint64_t* cand_key,
+                                  const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
+                                  uint8_t* chosen, hipStream_t stream) {
+    if (cn <= 0) return hipSuccess;
+    const int n = (int)cn;
+    uint64_t* key_out = nullptr;
+    uint32_t *perm_a = nullptr, *perm_b = nullptr, *lang_a = nullptr, *lang_b = nullptr;
+    void* tmp = nullptr;
+    size_t tmp1 = 0, tmp2 = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp1, cand_key, key_out, perm_a, perm_b, n, 0, 59,
+                                                      stream);
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, 8, stream);
+    if (e == hipSuccess) e = hipMalloc((void**)&key_out, sizeof(uint64_t) * cn);
+    if (e == hipSuccess) e = hipMalloc((void**)&perm_a, sizeof(uint32_t) * cn);
+    if (e == hipSuccess) e = hipMalloc((void**)&perm_b, sizeof(uint32_t) * cn);
+    if (e == hipSuccess) e = hipMalloc((void**)&lang_a, sizeof(uint32_t) * cn);
+    if (e == hipSuccess) e = hipMalloc((void**)&lang_b, sizeof(uint32_t) * cn);
+    if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(std::max(tmp1, tmp2), 16));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(iota_kernel, dim3(grid_of(cn, 256)), dim3(256), 0, stream, cn, perm_a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp1, cand_key, key_out, perm_a, perm_b, n, 0, 59, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(cand_lang_kernel, dim3(grid_of(cn, 256)), dim3(256), 0, stream, cn, perm_b, cand_lang,
+                           lang_a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, 8, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(cand_mark_kernel, dim3(grid_of(cn, 256)), dim3(256), 0, stream, cn, lang_b, perm_a,
+                           seg_start, need, cand_idx, chosen);
+        e = hipGetLastError();
+    }
+    const hipError_t s = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = s;
+    for (void* q : {(void*)key_out, (void*)perm_a, (void*)perm_b, (void*)lang_a, (void*)lang_b, tmp})
+        if (q) (void)hipFree(q);
+    return e;
 }
 
 hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream) {

@@ -140,6 +140,9 @@ hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const ui
                          const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
                          uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream);
 // chosen[idx[i]] = 1
+hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const uint64_t* cand_key,
+                                  const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
+                                  uint8_t* chosen, hipStream_t stream);
 hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream);
 // gather the chosen grams: out_keys[m], out_masks[m][S], out_k[m]
 hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,
