@@ -126,6 +126,33 @@ def cpu_baseline(args, table, grams, data, off):
                       f"{threads} pthreads, {dt:.1f} s"}
 
 
+def cpu_baseline_fit(args, grams, data, off, lang):
+    """FIT on the oracle's C restatement (computeGrams + reduceGrams into a
+    host hash table, kind 'port', one thread), rank 0, bounded sample of the
+    same corpus; unit = corpus bytes/s like the line's value."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ldoracle_c as OC
+    L = OC.lib()
+    g = np.asarray(grams, dtype=np.int32)
+
+    def run(n):
+        o = np.ascontiguousarray(off[:n + 1], dtype=np.int64)
+        t0 = time.perf_counter()
+        h = L.ldo_count(OC._ptr(data), OC._ptr(o), OC._ptr(lang), n, args.langs, OC._ptr(g), len(g))
+        dt = time.perf_counter() - t0
+        L.ldo_counts_destroy(h)
+        return dt
+
+    probe = min(200, len(off) - 1)
+    rate = int(off[probe]) / max(run(probe), 1e-9)
+    target = rate * args.cpu_seconds
+    n = int(min(len(off) - 1, max(probe, np.searchsorted(off, target))))
+    dt = run(n)
+    return {"value": round(int(off[n]) / dt, 1), "unit": "bytes/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} documents ({int(off[n])} corpus bytes) of the GPU's corpus, "
+                      f"oracle/ldoracle.c ldo_count, 1 thread, {dt:.1f} s"}
+
+
 def host_path(model, data, off, acc_labels):
     """The host-buffer boundary (ldgpu_score: the JNI shim's call), PCIe
     copies included -- reported beside `value`, never as it.  Pageable numpy
@@ -241,6 +268,8 @@ def fit_main(args, world, rank, local, dev, backend):
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6), "traffic": None},
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_fit(args, grams, data, off, lang)
     if rank == 0:
         print(json.dumps(line), flush=True)
         if args.json_out:
