@@ -1131,10 +1131,14 @@ int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const
     if (int rc = ensure_ovf(c, total)) return rc;
     int64_t d0 = 0;
     while (d0 < n_docs) {
+        // also keep a launch within ~8 windows per slot of the current table:
+        // a launch much larger than the table overflows most of its new keys
+        // (re-inserted after a grow sized by the overflow count, i.e. far too big)
+        const int64_t limit = std::min<int64_t>((int64_t)c->ovf_cap, std::max<int64_t>(1 << 24, 8 * (int64_t)c->cap));
         int64_t d1 = d0, win = 0;
         while (d1 < n_docs) {
             const int64_t w = doc_windows(c, h_off[d1 + 1] - h_off[d1]);
-            if (d1 > d0 && win + w > (int64_t)c->ovf_cap) break;
+            if (d1 > d0 && win + w > limit) break;
             win += w;
             ++d1;
         }
