@@ -53,10 +53,17 @@ __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t
     return -1;
 }
 
+// Diagnostics build only (tools/build_variant.sh ... -DLDGPU_FIT_ABLATE=n):
+// bit 0 skips the counter add, bit 1 skips the whole global update.
+#ifndef LDGPU_FIT_ABLATE
+#define LDGPU_FIT_ABLATE 0
+#endif
+
 __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
+    if (LDGPU_FIT_ABLATE & 2) return;
     const int64_t s = find_or_insert(p, key);
     if (s >= 0) {
-        atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
+        if (!(LDGPU_FIT_ABLATE & 1)) atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
     } else {
         // overflow: one entry per unit count (c == 1 on this path except for
         // the 1-gram histogram flush, which repeats the entry c times)
