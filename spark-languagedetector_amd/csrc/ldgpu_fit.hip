@@ -14,7 +14,8 @@
 // hottest keys: every document hits ' ', 'e', ...) are first aggregated in a
 // per-wave 256-bin LDS histogram and flushed once per document, so the global
 // atomics on those rows drop from one per byte to one per distinct byte per
-// document.  Longer keys insert straight into the global table: find-or-CAS
+// document; 2-byte keys likewise go through a per-wave LDS hash (kH2 slots,
+// flushed once per document; a key that finds no slot goes global).  Longer keys insert straight into the global table: find-or-CAS
 // the key (relaxed agent-scope loads, device-scope CAS), then one u64 atomic
 // add on the (slot, lang) counter.  An insert that exceeds kMaxProbe probes
 // appends (key, lang) to an overflow list that the host re-inserts after
@@ -54,7 +55,8 @@ __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t
 }
 
 // Diagnostics build only (tools/build_variant.sh ... -DLDGPU_FIT_ABLATE=n):
-// bit 0 skips the counter add, bit 1 skips the whole global update.
+// bit 0 skips the counter add, bit 1 skips the whole global update, bit 2
+// adds 32-bit instead of 64-bit (timing only).
 #ifndef LDGPU_FIT_ABLATE
 #define LDGPU_FIT_ABLATE 0
 #endif
@@ -63,7 +65,10 @@ __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, in
     if (LDGPU_FIT_ABLATE & 2) return;
     const int64_t s = find_or_insert(p, key);
     if (s >= 0) {
-        if (!(LDGPU_FIT_ABLATE & 1)) atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
+        if (LDGPU_FIT_ABLATE & 4)  // timing probe: a 32-bit add on the counter's low word
+            atomicAdd(reinterpret_cast<unsigned int*>(&p.counts[(size_t)s * p.L + lang]), (unsigned int)c);
+        else if (!(LDGPU_FIT_ABLATE & 1))
+            atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
     } else {
         // overflow: one entry per unit count (c == 1 on this path except for
         // the 1-gram histogram flush, which repeats the entry c times)
@@ -77,13 +82,23 @@ __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, in
     }
 }
 
+// per-wave LDS aggregation of a document's 2-byte keys (one language per
+// document): open-addressed, kH2 slots, tag = key bytes + 1 (0 = empty)
+constexpr uint32_t kH2 = 384;
+constexpr int kH2Probe = 8;
+
 __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountParams p) {
     __shared__ unsigned int hist[kCountWaves][256];
+    __shared__ unsigned int tag2[kCountWaves][kH2];
+    __shared__ unsigned int cnt2[kCountWaves][kH2];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     unsigned int* h1 = hist[wave];
+    unsigned int* k2 = tag2[wave];
+    unsigned int* c2 = cnt2[wave];
     for (int i = lane; i < 256; i += 64) h1[i] = 0u;
+    for (int i = lane; i < (int)kH2; i += 64) k2[i] = c2[i] = 0u;
     const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
     const int64_t stride = (int64_t)gridDim.x * kCountWaves;
     for (int64_t doc = (int64_t)blockIdx.x * kCountWaves + wave; doc < p.n_docs; doc += stride) {
@@ -91,7 +106,7 @@ __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountPara
         if (lang < 0 || lang >= p.L) continue;
         const int64_t b = p.offsets[doc];
         const int64_t len = p.offsets[doc + 1] - b;
-        bool used_hist = false;
+        bool used_hist = false, used2 = false;
         for (int gi = 0; gi < p.nG; ++gi) {
             const int n = p.G[gi];
             const int64_t nwin = n_windows(len, n);
@@ -113,6 +128,22 @@ __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountPara
                     used_hist = true;
                     continue;
                 }
+                if (klen == 2) {
+                    const uint32_t tag = lo + 1u;
+                    uint32_t slot = (uint32_t)(((uint64_t)(lo * 0x9E3779B1u) * kH2) >> 32);
+                    bool done = false;
+                    for (int t = 0; t < kH2Probe; ++t) {
+                        const unsigned int old = atomicCAS(&k2[slot], 0u, tag);
+                        if (old == 0u || old == tag) {
+                            atomicAdd(&c2[slot], 1u);
+                            done = true;
+                            break;
+                        }
+                        slot = slot + 1u == kH2 ? 0u : slot + 1u;
+                    }
+                    used2 = true;
+                    if (done) continue;
+                }
                 uint32_t hi = hitag;
                 if (klen > 4) {
                     const uint32_t w2 = ld_dw(W, i + 2, p.last_dword);
@@ -120,6 +151,19 @@ __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountPara
                 }
                 add_count(p, ((uint64_t)hi << 32) | lo, lang, 1ull);
             }
+        }
+        if (__ballot(used2)) {
+            __builtin_amdgcn_wave_barrier();
+            for (int i = lane; i < (int)kH2; i += 64) {
+                const unsigned int tag = k2[i];
+                if (tag) {
+                    const unsigned int c = c2[i];
+                    k2[i] = 0u;
+                    c2[i] = 0u;
+                    add_count(p, ((uint64_t)2 << 56) | (uint64_t)(tag - 1u), lang, (unsigned long long)c);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
         if (__ballot(used_hist)) {
             __builtin_amdgcn_wave_barrier();
