@@ -14,8 +14,8 @@
 // hottest keys: every document hits ' ', 'e', ...) are first aggregated in a
 // per-wave 256-bin LDS histogram and flushed once per document, so the global
 // atomics on those rows drop from one per byte to one per distinct byte per
-// document; 2-byte keys likewise go through a per-wave LDS hash (kH2 slots,
-// flushed once per document; a key that finds no slot goes global).  Longer keys insert straight into the global table: find-or-CAS
+// document; 2- and 3-byte keys likewise go through a per-wave LDS hash (kH2
+// slots, flushed after each gram length; a key that finds no slot goes global).  Longer keys insert straight into the global table: find-or-CAS
 // the key (relaxed agent-scope loads, device-scope CAS), then one u64 atomic
 // add on the (slot, lang) counter.  An insert that exceeds kMaxProbe probes
 // appends (key, lang) to an overflow list that the host re-inserts after
@@ -82,8 +82,8 @@ __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, in
     }
 }
 
-// per-wave LDS aggregation of a document's 2-byte keys (one language per
-// document): open-addressed, kH2 slots, tag = key bytes + 1 (0 = empty)
+// per-wave LDS aggregation of a document's 2- and 3-byte keys (one language
+// per document): open-addressed, kH2 slots, tag = bytes | length << 24 (0 = empty)
 constexpr uint32_t kH2 = 384;
 constexpr int kH2Probe = 8;
 
@@ -128,8 +128,8 @@ __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountPara
                     used_hist = true;
                     continue;
                 }
-                if (klen == 2) {
-                    const uint32_t tag = lo + 1u;
+                if (klen == 2 || klen == 3) {
+                    const uint32_t tag = lo | ((uint32_t)klen << 24);  // never 0
                     uint32_t slot = (uint32_t)(((uint64_t)(lo * 0x9E3779B1u) * kH2) >> 32);
                     bool done = false;
                     for (int t = 0; t < kH2Probe; ++t) {
@@ -151,19 +151,21 @@ __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountPara
                 }
                 add_count(p, ((uint64_t)hi << 32) | lo, lang, 1ull);
             }
-        }
-        if (__ballot(used2)) {
-            __builtin_amdgcn_wave_barrier();
-            for (int i = lane; i < (int)kH2; i += 64) {
-                const unsigned int tag = k2[i];
-                if (tag) {
-                    const unsigned int c = c2[i];
-                    k2[i] = 0u;
-                    c2[i] = 0u;
-                    add_count(p, ((uint64_t)2 << 56) | (uint64_t)(tag - 1u), lang, (unsigned long long)c);
+            if (__ballot(used2)) {  // flush this length's LDS-aggregated keys
+                used2 = false;
+                __builtin_amdgcn_wave_barrier();
+                for (int i = lane; i < (int)kH2; i += 64) {
+                    const unsigned int tag = k2[i];
+                    if (tag) {
+                        const unsigned int c = c2[i];
+                        k2[i] = 0u;
+                        c2[i] = 0u;
+                        add_count(p, ((uint64_t)(tag >> 24) << 56) | (uint64_t)(tag & 0xffffffu), lang,
+                                  (unsigned long long)c);
+                    }
                 }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
         }
         if (__ballot(used_hist)) {
             __builtin_amdgcn_wave_barrier();
