@@ -19,6 +19,8 @@ reference cannot run without a JVM).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -107,11 +109,25 @@ def build_table(args, ls, device):
     return (kb, ko, masks, vals), table, grams, fit_info
 
 
+def host_cores() -> int:
+    """The host cores this process may use (N = nproc of the
+    allocation).  On the GPU pool the machine is shared and the allocation's
+    share is published as OMP_NUM_THREADS (16 per GPU); elsewhere the CPU
+    affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return int(os.cpu_count() or 1)
+
+
 def cpu_baseline(args, table, grams, data, off):
     """The oracle's C restatement (kind 'port'), on rank 0, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ldoracle_c as OC
-    threads = int(min(16, os.cpu_count() or 1))
+    threads = host_cores()
     t = OC.Table(table, args.langs)
     probe = min(20_000, len(off) - 1)
     t0 = time.perf_counter()
@@ -119,11 +135,11 @@ def cpu_baseline(args, table, grams, data, off):
     rate = probe / max(time.perf_counter() - t0, 1e-9)
     n = int(min(len(off) - 1, max(probe, rate * args.cpu_seconds)))
     t0 = time.perf_counter()
-    t.score(grams, data, off[:n + 1], nthreads=threads)
+    labels, _ = t.score(grams, data, off[:n + 1], nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 1), "unit": "docs/s", "cores": threads, "kind": "port",
             "sample": f"first {n} of the GPU's documents ({args.doc_min}-{args.doc_max} B), same table, "
-                      f"{threads} pthreads, {dt:.1f} s"}
+                      f"{threads} pthreads, {dt:.1f} s"}, labels
 
 
 def cpu_baseline_fit(args, grams, data, off, lang):
@@ -284,8 +300,29 @@ def synth_windows(off, n):
     return np.where(lens == 0, 0, np.where(lens < n, 1, lens - n + 1)).sum()
 
 
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start N rank processes (one per GPU,
+    torch.distributed.run on 127.0.0.1) as CHILDREN -- before this process
+    touches the GPU -- and exit with their status.  Under a launcher the
+    world size must equal --gpus."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks")
+        return
+    if args.gpus <= 1:
+        return
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     args = parse()
+    launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -373,8 +410,14 @@ def main():
                 "lookups_per_s": round(windows / (kernel_ms * 1e-3), 1)}
 
     cpu = None
+    oracle_check = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and table:
-        cpu = cpu_baseline(args, table, grams, data, off)
+        cpu, ol = cpu_baseline(args, table, grams, data, off)
+        # the timed kernel's own labels (the last step's) against the oracle's
+        # on the CPU sample: the exact code path the value measures
+        dl = d_lab[:len(ol)].cpu().numpy()
+        oracle_check = {"labels_match_oracle": bool(np.array_equal(dl, ol)), "docs_checked": int(len(ol)),
+                        "mismatches": int((dl != ol).sum())}
     host = None
     if rank == 0 and world == 1 and not args.no_host_path and not args.empty_table:
         host = host_path(model, data, off, acc_labels=d_lab.cpu().numpy())
@@ -408,6 +451,8 @@ def main():
                    "parallelism": f"dp{world} (documents sharded, no collective)"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "labels_match_oracle": None if oracle_check is None else oracle_check["labels_match_oracle"],
+        "oracle_check": oracle_check,
         "host_path": host,
         "fit_setup": fit_info,
         "label_accuracy_vs_generator": acc,

@@ -85,17 +85,10 @@ static void hm_grow(hmap* m) {
 /* -------------------------------------------------------------------- score */
 typedef struct {
     hmap m; int32_t L; const double* rows; uint8_t* blob;
+    const uint64_t* masks; const double* vals; /* mask form: row i = vals[i] at the set bits, 0.0 elsewhere */
 } ldo_table;
 
-ldo_table* ldo_table_create(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets,
-                            const double* rows, int32_t L) {
-    ldo_table* t = (ldo_table*)calloc(1, sizeof(ldo_table));
-    int64_t nb = key_offsets[n_rows] - key_offsets[0];
-    t->blob = (uint8_t*)malloc((size_t)(nb > 0 ? nb : 1));
-    memcpy(t->blob, key_bytes + key_offsets[0], (size_t)nb);
-    double* r = (double*)malloc(sizeof(double) * (size_t)(n_rows * L > 0 ? n_rows * L : 1));
-    memcpy(r, rows, sizeof(double) * (size_t)(n_rows * L));
-    t->rows = r; t->L = L;
+static void index_keys(ldo_table* t, int64_t n_rows, const int64_t* key_offsets) {
     hm_init(&t->m, n_rows);
     for (int64_t i = 0; i < n_rows; ++i) {
         const uint8_t* p = t->blob + (key_offsets[i] - key_offsets[0]);
@@ -109,12 +102,43 @@ ldo_table* ldo_table_create(int64_t n_rows, const uint8_t* key_bytes, const int6
             t->m.e[s].idx = i; t->m.e[s].p = p;
         }
     }
+}
+
+ldo_table* ldo_table_create(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets,
+                            const double* rows, int32_t L) {
+    ldo_table* t = (ldo_table*)calloc(1, sizeof(ldo_table));
+    int64_t nb = key_offsets[n_rows] - key_offsets[0];
+    t->blob = (uint8_t*)malloc((size_t)(nb > 0 ? nb : 1));
+    memcpy(t->blob, key_bytes + key_offsets[0], (size_t)nb);
+    double* r = (double*)malloc(sizeof(double) * (size_t)(n_rows * L > 0 ? n_rows * L : 1));
+    memcpy(r, rows, sizeof(double) * (size_t)(n_rows * L));
+    t->rows = r; t->L = L;
+    index_keys(t, n_rows, key_offsets);
+    return t;
+}
+
+/* The same map given in mask form (rows too large to expand: 10M x 200):
+ * row i is vals[i] at the languages set in masks[i][0 .. ceil(L/64)), 0.0
+ * elsewhere -- scored as exactly that dense row. */
+ldo_table* ldo_table_create_masks(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets,
+                                  const uint64_t* masks, const double* vals, int32_t L) {
+    ldo_table* t = (ldo_table*)calloc(1, sizeof(ldo_table));
+    int64_t nb = key_offsets[n_rows] - key_offsets[0];
+    const int64_t S = (L + 63) / 64;
+    t->blob = (uint8_t*)malloc((size_t)(nb > 0 ? nb : 1));
+    memcpy(t->blob, key_bytes + key_offsets[0], (size_t)nb);
+    uint64_t* m = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n_rows * S > 0 ? n_rows * S : 1));
+    double* v = (double*)malloc(sizeof(double) * (size_t)(n_rows > 0 ? n_rows : 1));
+    memcpy(m, masks, sizeof(uint64_t) * (size_t)(n_rows * S));
+    memcpy(v, vals, sizeof(double) * (size_t)n_rows);
+    t->masks = m; t->vals = v; t->L = L;
+    index_keys(t, n_rows, key_offsets);
     return t;
 }
 
 void ldo_table_destroy(ldo_table* t) {
     if (!t) return;
-    free(t->m.e); free((void*)t->rows); free(t->blob); free(t);
+    free(t->m.e); free((void*)t->rows); free((void*)t->masks); free((void*)t->vals); free(t->blob); free(t);
 }
 
 static int32_t score_one(const ldo_table* t, const int32_t* G, int32_t nG, const uint8_t* d, int64_t len,
@@ -128,6 +152,12 @@ static int32_t score_one(const ldo_table* t, const int32_t* G, int32_t nG, const
         for (int64_t p = 0; p < nw; ++p) {
             int64_t r = hm_find(&t->m, d + p, wl, hbytes(d + p, wl));
             if (r < 0) continue;
+            if (t->masks) {
+                const uint64_t* mk = t->masks + r * ((L + 63) / 64);
+                const double v = t->vals[r];
+                for (int32_t l = 0; l < L; ++l) s[l] = s[l] + 1.0 * (((mk[l / 64] >> (l % 64)) & 1u) ? v : 0.0);
+                continue;
+            }
             const double* row = t->rows + r * L;
             for (int32_t l = 0; l < L; ++l) s[l] = s[l] + 1.0 * row[l];
         }

@@ -35,6 +35,8 @@ def lib():
         L = ctypes.CDLL(_SO)
         L.ldo_table_create.restype = _p
         L.ldo_table_create.argtypes = [_i64, _p, _p, _p, _i32]
+        L.ldo_table_create_masks.restype = _p
+        L.ldo_table_create_masks.argtypes = [_i64, _p, _p, _p, _p, _i32]
         L.ldo_table_destroy.argtypes = [_p]
         L.ldo_score.restype = ctypes.c_int
         L.ldo_score.argtypes = [_p, _p, _i32, _p, _p, _i64, _p, _p, _i32]
@@ -72,6 +74,21 @@ class Table:
         rows = np.asarray([list(table[k]) for k in keys], dtype=np.float64).reshape(len(keys), n_langs)
         rows = np.ascontiguousarray(rows)
         self._h = lib().ldo_table_create(len(keys), _ptr(blob), _ptr(off), _ptr(rows), n_langs)
+
+    @classmethod
+    def from_masks(cls, key_bytes: np.ndarray, key_offsets: np.ndarray, masks: np.ndarray, vals: np.ndarray,
+                   n_langs: int) -> "Table":
+        """Mask form (row i = vals[i] at the set bits of masks[i], 0.0 elsewhere)
+        from packed arrays: tables too large for a dict of dense rows."""
+        self = cls.__new__(cls)
+        self.L = n_langs
+        kb = np.ascontiguousarray(key_bytes, dtype=np.uint8)
+        ko = np.ascontiguousarray(key_offsets, dtype=np.int64)
+        mk = np.ascontiguousarray(masks, dtype=np.uint64)
+        vv = np.ascontiguousarray(vals, dtype=np.float64)
+        assert mk.shape == (len(ko) - 1, (n_langs + 63) // 64) and vv.shape == (len(ko) - 1,)
+        self._h = lib().ldo_table_create_masks(len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(mk), _ptr(vv), n_langs)
+        return self
 
     def __del__(self):
         if getattr(self, "_h", None):

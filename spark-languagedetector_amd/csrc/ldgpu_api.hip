@@ -18,6 +18,10 @@
 
 using namespace ldgpu;
 
+// LDGPU_* environment switches: read only by the diagnostics build
+// (ldgpu_internal.h); the product library sees none of them.
+static const char* diag_env(const char* name) { return LDGPU_DIAG ? getenv(name) : nullptr; }
+
 // ------------------------------------------------------------------- errors
 namespace {
 thread_local std::string g_err;
@@ -166,14 +170,71 @@ struct ScoreStage {
     bool busy = false;
 };
 
+// One ldgpu_score call's pipeline: two stages plus the call's own error word
+// (a wrong-length row hit by THIS call's documents).  Contexts keep a pool:
+// concurrent callers (Spark task threads of one executor, Spark.scala:11
+// local[4]) each take a pipeline and run on their own streams.
+struct ScorePipe {
+    ScoreStage stage[2];
+    int32_t* d_err = nullptr;
+};
+
 struct ldgpu_ctx {
     int device = 0;
     int cus = 256;
     hipStream_t stream = nullptr;
-    std::mutex mu;
+    std::mutex mu;                     // FIT calls and the ctx stream
     DevBuf bytes, offsets, labels, scores, langs;
-    ScoreStage stage[2];
+    std::mutex pool_mu;                // guards `pipes` / `free_pipes` only
+    std::vector<ScorePipe*> pipes, free_pipes;
 };
+
+namespace {
+void pipe_destroy(ScorePipe* pp) {
+    for (auto& st : pp->stage) {
+        if (st.stream) (void)hipStreamSynchronize(st.stream);
+        for (DevBuf* b : {&st.bytes, &st.offsets, &st.labels, &st.scores}) b->release();
+        for (HostBuf* b : {&st.h_bytes, &st.h_offsets, &st.h_labels, &st.h_scores}) b->release();
+        if (st.done) (void)hipEventDestroy(st.done);
+        if (st.stream) (void)hipStreamDestroy(st.stream);
+    }
+    if (pp->d_err) (void)hipFree(pp->d_err);
+    delete pp;
+}
+
+// a free pipeline of the context, created on demand (nullptr + error on failure)
+ScorePipe* pipe_acquire(ldgpu_ctx* c) {
+    {
+        std::lock_guard<std::mutex> g(c->pool_mu);
+        if (!c->free_pipes.empty()) {
+            ScorePipe* pp = c->free_pipes.back();
+            c->free_pipes.pop_back();
+            return pp;
+        }
+    }
+    auto* pp = new ScorePipe();
+    hipError_t e = hipSuccess;
+    for (auto& st : pp->stage) {
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&st.done, hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipMalloc((void**)&pp->d_err, sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(pp->d_err, 0, sizeof(int32_t));
+    if (e != hipSuccess) {
+        pipe_destroy(pp);
+        fail(LDGPU_EDEVICE, "score pipeline: %s", hipGetErrorString(e));
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(c->pool_mu);
+    c->pipes.push_back(pp);
+    return pp;
+}
+
+void pipe_release(ldgpu_ctx* c, ScorePipe* pp) {
+    std::lock_guard<std::mutex> g(c->pool_mu);
+    c->free_pipes.push_back(pp);
+}
+}  // namespace
 
 extern "C" const char* ldgpu_version(void) { return "ldgpu 0.1.0 (gfx950)"; }
 extern "C" const char* ldgpu_last_error(void) { return g_err.c_str(); }
@@ -199,10 +260,6 @@ extern "C" int ldgpu_ctx_create(int32_t device, ldgpu_ctx** out) {
     c->device = device;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    for (auto& st : c->stage) {
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&st.done, hipEventDisableTiming);
-    }
     if (e != hipSuccess) {
         (void)ldgpu_ctx_destroy(c);
         return fail(LDGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -220,13 +277,7 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
     c->labels.release();
     c->scores.release();
     c->langs.release();
-    for (auto& st : c->stage) {
-        if (st.stream) (void)hipStreamSynchronize(st.stream);
-        for (DevBuf* b : {&st.bytes, &st.offsets, &st.labels, &st.scores}) b->release();
-        for (HostBuf* b : {&st.h_bytes, &st.h_offsets, &st.h_labels, &st.h_scores}) b->release();
-        if (st.done) (void)hipEventDestroy(st.done);
-        if (st.stream) (void)hipStreamDestroy(st.stream);
-    }
+    for (ScorePipe* pp : c->pipes) pipe_destroy(pp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return ok();
@@ -273,7 +324,7 @@ struct ldgpu_model {
     uint32_t len_mask = 0;    // bit k: some key has k bytes
     size_t lds_bytes = 0;
     int wg_per_cu = 1;
-    int ablate = 0;           // diagnostics: LDGPU_ABLATE (never set in production)
+    int ablate = 0;           // diagnostics build only: LDGPU_ABLATE
     size_t device_bytes = 0;
     Slot* d_slots = nullptr;
     Bucket* d_buckets = nullptr;  // count mode key table
@@ -556,7 +607,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                 uniform = false;
             }
         }
-        if (const char* f = getenv("LDGPU_NO_COUNT_MODE")) uniform &= atoi(f) == 0;  // tests cover both paths
+        if (const char* f = diag_env("LDGPU_NO_COUNT_MODE")) uniform &= atoi(f) == 0;  // tests cover both paths
         if (uniform) {
             m->mode = 3;
             double v;
@@ -659,7 +710,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         n_long += kl >= 3;
     }
     double kpw = 2.5;
-    if (const char* s = getenv("LDGPU_BLOOM_KPW")) kpw = std::max(0.05, atof(s));  // tuning experiments only
+    if (const char* s = diag_env("LDGPU_BLOOM_KPW")) kpw = std::max(0.05, atof(s));  // tuning experiments only
     uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
     bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
     m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
@@ -691,7 +742,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // grams unique to a language): direct tables after the image (see
     // ScoreParams::direct_*), so those keys are counted from LDS unverified
     uint32_t image_words = kBloomBase + (m->lds_filter ? (uint32_t)bwords : 0u);
-    if (m->mode == 3 && m->lds_filter && n_langs <= 255 && !getenv("LDGPU_NO_DIRECT")) {
+    if (m->mode == 3 && m->lds_filter && n_langs <= 255 && !diag_env("LDGPU_NO_DIRECT")) {
         std::vector<uint8_t> lang1(256, 0xff), lang2of(65536, 0xff);
         bool ok = true;
         for (int64_t i = 0; i < nk && ok; ++i) {
@@ -743,13 +794,13 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->lds_bytes, &resident);
     // persistent grid = what is resident; never more workgroups than the LDS admits
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
-    if (const char* ov = getenv("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
-    if (const char* ab = getenv("LDGPU_ABLATE")) m->ablate = atoi(ab);
-    if (getenv("LDGPU_STATS") && e == hipSuccess) {
+    if (const char* ov = diag_env("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
+    if (const char* ab = diag_env("LDGPU_ABLATE")) m->ablate = atoi(ab);
+    if (diag_env("LDGPU_STATS") && e == hipSuccess) {
         e = hipMalloc((void**)&m->d_stats, 2 * sizeof(unsigned long long));
         if (e == hipSuccess) e = hipMemset(m->d_stats, 0, 2 * sizeof(unsigned long long));
     }
-    if (getenv("LDGPU_DEBUG"))
+    if (diag_env("LDGPU_DEBUG"))
         fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d direct=%u slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
                         "resident_api=%d wg_per_cu=%d\n",
                 (long long)nk, m->mode, m->direct_words, S, (unsigned long long)bwords, (int)m->lds_filter, m->lds_bytes, resident,
@@ -783,7 +834,7 @@ extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_
 
 namespace {
 int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
-                 int32_t* d_labels, double* d_scores, hipStream_t st) {
+                 int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st) {
     if (n_docs == 0) return LDGPU_OK;
     ScoreParams p{};
     p.bytes = d_bytes;
@@ -816,7 +867,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.count_sign = m->count_sign;
     // counts stay below 2^24: c <= windows of a document <= len * n_grams
     p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;
-    p.err = m->d_err;
+    p.err = d_err;
     p.stats = m->d_stats;
     p.L = m->L;
     p.ablate = m->ablate;
@@ -845,13 +896,13 @@ bool nb_total_pinned(const uint8_t* bytes, const int64_t* offsets, int64_t n_doc
     return is_pinned(bytes + offsets[0]) && is_pinned(bytes + offsets[n_docs] - 1);
 }
 
-int check_row_error(ldgpu_model* m, hipStream_t st) {
+int check_row_error(ldgpu_model* m, int32_t* d_err, hipStream_t st) {
     int32_t err = 0;
-    HIP_TRY(hipMemcpyAsync(&err, m->d_err, sizeof err, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&err, d_err, sizeof err, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (err) {
         int32_t z = 0;
-        HIP_TRY(hipMemcpy(m->d_err, &z, sizeof z, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_err, &z, sizeof z, hipMemcpyHostToDevice));
         if (err & 2)
             return fail(LDGPU_EUNSUPPORTED, "a document of %lld bytes or more exceeds the device path's limit",
                         (long long)kMaxDocBytes);
@@ -871,13 +922,20 @@ extern "C" int ldgpu_score_device(ldgpu_model* m, const uint8_t* d_bytes, int64_
     if (((uintptr_t)d_bytes & 3) != 0) return fail(LDGPU_EINVAL, "d_bytes must be 4-byte aligned");
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(m->ctx->device));
-    if (int rc = score_launch(m, d_bytes, n_bytes, d_offsets, n_docs, d_labels, d_scores, st)) return rc;
+    if (int rc = score_launch(m, d_bytes, n_bytes, d_offsets, n_docs, d_labels, d_scores, m->d_err, st)) return rc;
     if (m->has_bad) {
-        if (int rc = check_row_error(m, st)) return rc;
+        if (int rc = check_row_error(m, m->d_err, st)) return rc;
     }
     return ok();
 }
 
+namespace {
+int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_t* offsets, int64_t n_docs,
+               int32_t* out_labels, double* out_scores);
+}  // namespace
+
+// Thread-safe and concurrent: each call scores on a pipeline (two streams,
+// pinned staging, its own error word) taken from the context's pool.
 extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* offsets, int64_t n_docs,
                            int32_t* out_labels, double* out_scores) {
     if (!m) return fail(LDGPU_EINVAL, "model is NULL");
@@ -890,8 +948,18 @@ extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* 
             return fail(LDGPU_EUNSUPPORTED, "document %lld has %lld bytes: the device path's limit is %lld",
                         (long long)d, (long long)(offsets[d + 1] - offsets[d]), (long long)kMaxDocBytes - 1);
     ldgpu_ctx* c = m->ctx;
-    std::lock_guard<std::mutex> lock(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    ScorePipe* pp = pipe_acquire(c);
+    if (!pp) return LDGPU_EDEVICE;
+    const int rc = score_host(m, pp, bytes, offsets, n_docs, out_labels, out_scores);
+    pipe_release(c, pp);
+    if (rc) return rc;
+    return ok();
+}
+
+namespace {
+int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_t* offsets, int64_t n_docs,
+               int32_t* out_labels, double* out_scores) {
     // Two-stage pipeline over chunks of documents, one stream per stage: while
     // the GPU copies and scores chunk i, the host stages chunk i + 1 into the
     // other stage's pinned buffers (a caller buffer already in pinned memory is
@@ -916,7 +984,7 @@ extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* 
         int64_t d1 = d0 + 1;
         while (d1 < n_docs && d1 - d0 < kChunkDocs && offsets[d1 + 1] - offsets[d0] <= kChunkBytes) ++d1;
         const int64_t nd = d1 - d0, b0 = offsets[d0], nb = offsets[d1] - b0;
-        ScoreStage& st = c->stage[k & 1];
+        ScoreStage& st = pp->stage[k & 1];
         if ((rc = retire(st))) break;
         HIP_TRY(st.bytes.ensure((size_t)nb + 16));
         HIP_TRY(st.offsets.ensure(sizeof(int64_t) * (nd + 1)));
@@ -934,7 +1002,8 @@ extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* 
         if (nb) HIP_TRY(hipMemcpyAsync(st.bytes.p, src, nb, hipMemcpyHostToDevice, st.stream));
         HIP_TRY(hipMemcpyAsync(st.offsets.p, ho, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, st.stream));
         if ((rc = score_launch(m, (const uint8_t*)st.bytes.p, nb, (const int64_t*)st.offsets.p, nd,
-                               (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, st.stream)))
+                               (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, pp->d_err,
+                               st.stream)))
             break;
         int32_t* lab_dst = out_labels + d0;
         double* sc_dst = out_scores ? out_scores + d0 * m->L : nullptr;
@@ -959,16 +1028,17 @@ extern "C" int ldgpu_score(ldgpu_model* m, const uint8_t* bytes, const int64_t* 
     }
     // drain in chunk order (also after an error, so no copy outlives the call)
     for (int i = 0; i < 2; ++i) {
-        const int r = retire(c->stage[(k + i) & 1]);
+        const int r = retire(pp->stage[(k + i) & 1]);
         if (!rc) rc = r;
     }
     if (rc) return rc;
     if (m->has_bad) {
-        for (auto& st : c->stage) HIP_TRY(hipStreamSynchronize(st.stream));
-        if (int r = check_row_error(m, c->stream)) return r;
+        for (auto& st : pp->stage) HIP_TRY(hipStreamSynchronize(st.stream));
+        if (int r = check_row_error(m, pp->d_err, pp->stage[0].stream)) return r;
     }
-    return ok();
+    return LDGPU_OK;
 }
+}  // namespace
 
 // ---------------------------------------------------------------------- FIT
 struct ldgpu_counts {
@@ -1099,25 +1169,27 @@ constexpr uint32_t kOvfMax = 1u << 27;
 
 int ensure_ovf(ldgpu_counts* c, int64_t windows) {
     const uint64_t want = std::min<uint64_t>(kOvfMax, next_pow2((uint64_t)std::max<int64_t>(windows, 1)));
-    if (want <= c->ovf_cap) return LDGPU_OK;
+    if (want <= c->ovf_cap && c->d_ovf_keys && c->d_ovf_lang) return LDGPU_OK;
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
-    (void)hipFree(c->d_ovf_keys);
-    (void)hipFree(c->d_ovf_lang);
-    c->d_ovf_keys = nullptr;
-    c->d_ovf_lang = nullptr;
-    hipError_t e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * want);
-    if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * want);
-    if (e != hipSuccess) {
-        // fall back to the smallest list that still makes progress
-        (void)hipFree(c->d_ovf_keys);
+    auto drop = [&] {
+        if (c->d_ovf_keys) (void)hipFree(c->d_ovf_keys);
+        if (c->d_ovf_lang) (void)hipFree(c->d_ovf_lang);
         c->d_ovf_keys = nullptr;
-        c->ovf_cap = 1u << 20;
-        e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
-        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
-        if (e != hipSuccess) return fail(LDGPU_ENOMEM, "overflow list: %s", hipGetErrorString(e));
-        return LDGPU_OK;
-    }
-    c->ovf_cap = (uint32_t)want;
+        c->d_ovf_lang = nullptr;
+        c->ovf_cap = 0;
+    };
+    auto take = [&](uint64_t n) {
+        hipError_t e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * n);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * n);
+        if (e == hipSuccess) c->ovf_cap = (uint32_t)n;
+        else drop();
+        return e;
+    };
+    drop();
+    // fall back to the smallest list that still makes progress
+    hipError_t e = take(std::max<uint64_t>(want, 1u << 20));
+    if (e != hipSuccess) e = take(1u << 20);
+    if (e != hipSuccess) return fail(LDGPU_ENOMEM, "overflow list: %s", hipGetErrorString(e));
     return LDGPU_OK;
 }
 

@@ -70,8 +70,8 @@ __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, in
         else if (!(LDGPU_FIT_ABLATE & 1))
             atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
     } else {
-        // overflow: one entry per unit count (c == 1 on this path except for
-        // the 1-gram histogram flush, which repeats the entry c times)
+        // overflow: one entry per unit count -- an LDS flush (1-gram
+        // histogram, 2-/3-byte hash) passes c > 1 and repeats the entry c times
         for (unsigned long long r = 0; r < c; ++r) {
             const unsigned int at = atomicAdd(p.ovf_n, 1u);
             if (at < p.ovf_cap) {

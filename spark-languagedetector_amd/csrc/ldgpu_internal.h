@@ -4,6 +4,14 @@
 
 #include "ldgpu_common.h"
 
+// Diagnostics build (lib/libldgpu_diag.so, -DLDGPU_DIAG=1): only there does
+// the library read the LDGPU_* environment switches (path selection for tests,
+// timing ablations, statistics).  The product library (lib/libldgpu.so) never
+// consults the environment, and its kernels contain no ablation branch.
+#ifndef LDGPU_DIAG
+#define LDGPU_DIAG 0
+#endif
+
 namespace ldgpu {
 
 // ------------------------------------------------------------------ SCORE
@@ -34,7 +42,8 @@ struct ScoreParams {
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     unsigned long long* stats;  // diagnostics build (-DLDGPU_STATS, env LDGPU_STATS): [0] candidates verified, [1] hits
     int32_t L;
-    int32_t ablate;             // diagnostics only (LDGPU_ABLATE): bit 0 skip verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay
+    int32_t ablate;             // diagnostics build only (LDGPU_ABLATE; compiled out otherwise): bit 0 skip
+                                // verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay
     int32_t nG;
     int32_t G[kMaxGramLengths];
     // fast path (documents of maxg..256 bytes: every window full-length):

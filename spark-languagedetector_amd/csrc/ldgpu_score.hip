@@ -42,6 +42,9 @@ namespace {
 
 constexpr int kSub = 4;  // 64-position sub-blocks per superblock
 
+// timing ablations exist only in the diagnostics build (LDGPU_DIAG)
+__device__ __forceinline__ bool ablated(const ScoreParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
@@ -311,7 +314,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                                                   (uint32_t)words[2 * q + 1], (uint32_t)(words[2 * q + 1] >> 32));
             }
             __builtin_amdgcn_wave_barrier();
-            const int nh = (p.ablate & 4) ? 0 : __popcll(hits);
+            const int nh = ablated(p, 4) ? 0 : __popcll(hits);
             int t = 0;
             // 4 broadcast reads in flight, then 4 ordered adds
             for (; t + 4 <= nh; t += 4) {
@@ -602,7 +605,7 @@ template <int S, bool STAGED, bool KEYED>
 __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds& wl, int qn, const DocSrc& src,
                                             int lane) {
     double acc[S];  // unused in count mode
-    if (!(p.ablate & 1)) flush<S, 3, STAGED, KEYED>(p, wl, qn, src, acc, lane, true);
+    if (!ablated(p, 1)) flush<S, 3, STAGED, KEYED>(p, wl, qn, src, acc, lane, true);
 }
 
 template <int N, bool FULL, int S, bool STAGED, bool KEYED>
@@ -663,7 +666,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
         // are verified together; a document whose candidates overflow the
         // queue (nothing verified yet) restarts on the general path, so no
         // verification state is live in this loop.
-        if (p.n_fast && !(p.ablate & 2)) {
+        if (p.n_fast && !ablated(p, 2)) {
             Windows x;
             load_windows<STAGED>(p, src, 0, lane, x);
             FWords f;
@@ -694,7 +697,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                 append_sb(wl.queue, dummy_a, qn, m, n, 0, lane);
             }
             if (!general) {
-                if (p.ablate & 1) qn = 0;
+                if (ablated(p, 1)) qn = 0;
                 if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane, MODE == 3);
             }
             qn = 0;
@@ -708,7 +711,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
         // (reference order), superblocks inner
         for (int gi = 0; gi < p.nG; ++gi) {
             const GramCtx g = gram_ctx(len, p.G[gi]);
-            if (!((p.len_mask >> g.klen) & 1u) || (p.ablate & 2)) continue;
+            if (!((p.len_mask >> g.klen) & 1u) || ablated(p, 2)) continue;
             for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
                 Windows x;
                 load_windows<STAGED>(p, src, p0, lane, x);
@@ -724,7 +727,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             }
         }
     }
-    if (p.ablate & 1) qn = 0;
+    if (ablated(p, 1)) qn = 0;
     if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
         if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, wl, lane);

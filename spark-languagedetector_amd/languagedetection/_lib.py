@@ -15,6 +15,10 @@ from typing import List, Optional
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.environ.get("LDGPU_LIB", os.path.join(PKG_ROOT, "lib", "libldgpu.so"))
+# diagnostics build (make -C spark-languagedetector_amd diag): the only one that
+# reads the LDGPU_* path / ablation switches from the environment; tests load
+# it explicitly (variant="diag") to cover the alternative kernel paths
+DIAG_LIB_PATH = os.path.join(PKG_ROOT, "lib", "libldgpu_diag.so")
 
 LDGPU_OK = 0
 LDGPU_EINVAL = 1
@@ -64,7 +68,7 @@ SIGNATURES = [
     ("ldgpu_fit_table_export_masks", ctypes.c_int, [_p, _p, _p, _p, _p]),
 ]
 
-_lib = None
+_libs = {}
 _lock = threading.Lock()
 
 
@@ -74,17 +78,17 @@ class LdgpuError(RuntimeError):
         self.code = code
 
 
-def load(path: Optional[str] = None):
-    """Load libldgpu.so (raises if it has not been built)."""
-    global _lib
+def load(path: Optional[str] = None, variant: str = "product"):
+    """Load libldgpu.so (or, variant="diag", libldgpu_diag.so); raises if it
+    has not been built."""
     with _lock:
-        if _lib is not None and path is None:
-            return _lib
-        p = path or LIB_PATH
+        if path is None and variant in _libs:
+            return _libs[variant]
+        p = path or (DIAG_LIB_PATH if variant == "diag" else LIB_PATH)
         if not os.path.exists(p):
             raise ImportError(
-                f"libldgpu.so not found at {p}: build it with `make -C spark-languagedetector_amd` "
-                "(or __graft_entry__.build()); there is no CPU fallback")
+                f"{os.path.basename(p)} not found at {p}: build it with `make -C spark-languagedetector_amd"
+                f"{' diag' if variant == 'diag' else ''}` (or __graft_entry__.build()); there is no CPU fallback")
         try:
             import torch  # noqa: F401  -- share torch's HIP runtime (same SONAME)
         except Exception:
@@ -95,7 +99,7 @@ def load(path: Optional[str] = None):
             fn.restype = res
             fn.argtypes = args
         if path is None:
-            _lib = lib
+            _libs[variant] = lib
         return lib
 
 
@@ -103,10 +107,10 @@ def exported_symbols() -> List[str]:
     return [s[0] for s in SIGNATURES]
 
 
-def check(rc: int) -> None:
+def check(rc: int, lib=None) -> None:
     if rc == LDGPU_OK:
         return
-    msg = load().ldgpu_last_error().decode("utf-8", "replace")
+    msg = (lib or load()).ldgpu_last_error().decode("utf-8", "replace")
     if rc in (LDGPU_EINVAL, LDGPU_EROWLEN):
         raise ValueError(msg)
     if rc == LDGPU_ENOMEM:
@@ -124,19 +128,19 @@ def default_device() -> int:
     return int(os.environ.get("LDGPU_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
 
-def context(device: Optional[int] = None) -> int:
-    """A process-wide context per device (one executor per GPU)."""
+def context(device: Optional[int] = None, variant: str = "product") -> int:
+    """A process-wide context per device (one executor per GPU) and library."""
     d = default_device() if device is None else int(device)
     with _lock:
-        h = _ctx.get(d)
+        h = _ctx.get((variant, d))
     if h is not None:
         return h
-    lib = load()
+    lib = load(variant=variant)
     out = ctypes.c_void_p()
-    check(lib.ldgpu_ctx_create(d, ctypes.byref(out)))
+    check(lib.ldgpu_ctx_create(d, ctypes.byref(out)), lib)
     with _lock:
-        _ctx.setdefault(d, out.value)
-        return _ctx[d]
+        _ctx.setdefault((variant, d), out.value)
+        return _ctx[(variant, d)]
 
 
 def device_count() -> int:

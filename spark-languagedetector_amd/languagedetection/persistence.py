@@ -11,8 +11,14 @@ and LanguageDetectorModelReader.load (:68-104) reads them back.
 
 The reference collects supportedLanguages without an ordering key (:82-87);
 with several part files Spark may return them permuted relative to the
-probability rows.  We write one part file per dataset (order preserved) and
-read part files in name order, which is the order Spark lists them in.
+probability rows.  The writer therefore pins the order explicitly: the
+metadata JSON carries a top-level "languageOrder" list (DefaultParamsWriter's
+extraMetadata slot: the reference's reader, DefaultParamsReader.loadMetadata,
+ignores unknown top-level fields, and the parquet datasets keep exactly the
+reference's schema, so a reference Spark job can still read the model).  The
+reader uses it when present (after checking it names the same languages as
+the parquet dataset) and otherwise reads part files in name order, the order
+Spark lists them in.
 """
 from __future__ import annotations
 
@@ -53,7 +59,8 @@ def save_model(model, path: str, overwrite: bool = True) -> None:
             raise IOError(f"Path {path} already exists. To overwrite it, please use write.overwrite().save(path)")
         shutil.rmtree(path)
     meta = {"class": MODEL_CLASS, "timestamp": int(time.time() * 1000), "sparkVersion": SPARK_VERSION,
-            "uid": model.uid, "paramMap": model.extractParamMap()}
+            "uid": model.uid, "paramMap": model.extractParamMap(),
+            "languageOrder": list(model.supportedLanguages)}
     os.makedirs(os.path.join(path, "metadata"), exist_ok=True)
     with open(os.path.join(path, "metadata", "part-00000"), "w") as f:
         f.write(json.dumps(meta, separators=(",", ":")) + "\n")
@@ -82,5 +89,10 @@ def load_model_parts(path: str) -> Tuple[dict, Dict[bytes, List[float]], List[st
     for k, v in zip(probs.column("_1").to_pylist(), probs.column("_2").to_pylist()):
         table[bytes((int(x) & 0xFF) for x in k)] = list(v)   # .toMap: a later duplicate wins
     langs = [str(x) for x in _read_parquet_dir(os.path.join(path, "supportedLanguages")).column("value").to_pylist()]
+    order = meta.get("languageOrder")
+    if order is not None:
+        if sorted(map(str, order)) != sorted(langs):
+            raise ValueError(f"metadata languageOrder {order} does not match the supportedLanguages dataset {langs}")
+        langs = [str(x) for x in order]
     grams = [int(x) for x in _read_parquet_dir(os.path.join(path, "gramLengths")).column("value").to_pylist()]
     return meta, table, langs, grams

@@ -19,7 +19,14 @@ def _grams(gram_lengths: Sequence[int]) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(list(gram_lengths), dtype=np.int32))
 
 
-class PinnedArray:
+class _Owner:
+    lib = None
+
+    def _check(self, rc: int) -> None:
+        _lib.check(rc, self.lib)
+
+
+class PinnedArray(_Owner):
     """Page-locked host memory (ldgpu_host_alloc) viewed as a numpy array:
     host-buffer scoring copies from / to it directly, with no staging copy."""
 
@@ -30,7 +37,7 @@ class PinnedArray:
         shape = (shape,) if isinstance(shape, int) else tuple(shape)
         n = int(np.prod(shape)) * dt.itemsize
         p = ctypes.c_void_p()
-        _lib.check(self.lib.ldgpu_host_alloc(self.ctx, n, ctypes.byref(p)))
+        self._check(self.lib.ldgpu_host_alloc(self.ctx, n, ctypes.byref(p)))
         self.p = p.value
         buf = (ctypes.c_uint8 * max(n, 1)).from_address(self.p)
         self.array = np.frombuffer(buf, dtype=np.uint8, count=n).view(dt).reshape(shape)
@@ -48,30 +55,33 @@ class PinnedArray:
             pass
 
 
-class DeviceModel:
+class DeviceModel(_Owner):
     """A gram -> probability-row table resident on one GPU
     (LanguageDetectorModel's broadcast table, LanguageDetectorModel.scala:222)."""
 
-    def __init__(self, table: Dict, n_langs: int, gram_lengths: Sequence[int], device: Optional[int] = None):
-        self.lib = _lib.load()
-        self.ctx = _lib.context(device)
+    def __init__(self, table: Dict, n_langs: int, gram_lengths: Sequence[int], device: Optional[int] = None,
+                 variant: str = "product"):
+        """variant="diag": the diagnostics library (tests of alternative paths)."""
+        self.lib = _lib.load(variant=variant)
+        self.ctx = _lib.context(device, variant)
         self.L = int(n_langs)
         self.gram_lengths = list(gram_lengths)
         kb, ko, rows, ok = pack_table(table, self.L)
         g = _grams(gram_lengths)
         out = ctypes.c_void_p()
-        _lib.check(self.lib.ldgpu_model_create(self.ctx, len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(rows), _ptr(ok),
+        self._check(self.lib.ldgpu_model_create(self.ctx, len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(rows), _ptr(ok),
                                                self.L, _ptr(g), len(g), ctypes.byref(out)))
         self.h = out.value
 
     @classmethod
     def from_masks(cls, key_bytes: np.ndarray, key_offsets: np.ndarray, masks: np.ndarray, vals: np.ndarray,
-                   n_langs: int, gram_lengths: Sequence[int], device: Optional[int] = None) -> "DeviceModel":
+                   n_langs: int, gram_lengths: Sequence[int], device: Optional[int] = None,
+                   variant: str = "product") -> "DeviceModel":
         """A mask-form table (row i = vals[i] at the languages set in masks[i])
         as packed arrays, e.g. DeviceCounts.fit_table_masks (ldgpu_model_create_masks)."""
         self = cls.__new__(cls)
-        self.lib = _lib.load()
-        self.ctx = _lib.context(device)
+        self.lib = _lib.load(variant=variant)
+        self.ctx = _lib.context(device, variant)
         self.L = int(n_langs)
         self.gram_lengths = list(gram_lengths)
         kb = np.ascontiguousarray(key_bytes, dtype=np.uint8)
@@ -81,7 +91,7 @@ class DeviceModel:
         assert mk.shape == (len(ko) - 1, (self.L + 63) // 64) and vv.shape == (len(ko) - 1,)
         g = _grams(gram_lengths)
         out = ctypes.c_void_p()
-        _lib.check(self.lib.ldgpu_model_create_masks(self.ctx, len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(mk), _ptr(vv),
+        self._check(self.lib.ldgpu_model_create_masks(self.ctx, len(ko) - 1, _ptr(kb), _ptr(ko), _ptr(mk), _ptr(vv),
                                                      self.L, _ptr(g), len(g), ctypes.byref(out)))
         self.h = out.value
         return self
@@ -100,7 +110,7 @@ class DeviceModel:
     def info(self) -> Dict[str, int]:
         mode = ctypes.c_int32()
         vals = [ctypes.c_int64() for _ in range(4)]
-        _lib.check(self.lib.ldgpu_model_info(self.h, ctypes.byref(mode), *[ctypes.byref(v) for v in vals]))
+        self._check(self.lib.ldgpu_model_info(self.h, ctypes.byref(mode), *[ctypes.byref(v) for v in vals]))
         return {"mode": mode.value, "n_keys": vals[0].value, "table_slots": vals[1].value,
                 "filter_bits": vals[2].value, "device_bytes": vals[3].value}
 
@@ -117,7 +127,7 @@ class DeviceModel:
         else:
             labels = np.zeros(max(n, 0), dtype=np.int32)
         scores = np.zeros((max(n, 0), self.L), dtype=np.float64) if want_scores else None
-        _lib.check(self.lib.ldgpu_score(self.h, _ptr(data), _ptr(offsets), n, _ptr(labels), _ptr(scores)))
+        self._check(self.lib.ldgpu_score(self.h, _ptr(data), _ptr(offsets), n, _ptr(labels), _ptr(scores)))
         return labels, scores
 
     def stream(self) -> int:
@@ -130,13 +140,13 @@ class DeviceModel:
         async on `stream` (a hipStream_t; 0 = the null stream, None = the
         context's stream)."""
         st = self.stream() if stream is None else stream
-        _lib.check(self.lib.ldgpu_score_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
+        self._check(self.lib.ldgpu_score_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
                                                n_docs, ctypes.c_void_p(d_labels),
                                                ctypes.c_void_p(d_scores) if d_scores else None,
                                                ctypes.c_void_p(st) if st else None))
 
 
-class DeviceCounts:
+class DeviceCounts(_Owner):
     """A (gram, language) -> count table on one GPU (computeGrams + reduceGrams)."""
 
     def __init__(self, n_langs: int, gram_lengths: Sequence[int], capacity_hint: int = 0,
@@ -148,7 +158,7 @@ class DeviceCounts:
         self.gram_lengths = list(gram_lengths)
         g = _grams(gram_lengths)
         out = ctypes.c_void_p()
-        _lib.check(self.lib.ldgpu_counts_create(self.ctx, self.L, _ptr(g), len(g), int(capacity_hint),
+        self._check(self.lib.ldgpu_counts_create(self.ctx, self.L, _ptr(g), len(g), int(capacity_hint),
                                                 ctypes.byref(out)))
         self.h = out.value
 
@@ -167,36 +177,36 @@ class DeviceCounts:
         data = np.ascontiguousarray(data, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         doc_lang = np.ascontiguousarray(doc_lang, dtype=np.int32)
-        _lib.check(self.lib.ldgpu_count(self.h, _ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1))
+        self._check(self.lib.ldgpu_count(self.h, _ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1))
 
     def count_device(self, d_bytes: int, n_bytes: int, d_offsets: int, d_doc_lang: int, n_docs: int,
                      stream: Optional[int] = None) -> None:
         st = (self.lib.ldgpu_ctx_stream(self.ctx) or 0) if stream is None else stream
-        _lib.check(self.lib.ldgpu_count_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
+        self._check(self.lib.ldgpu_count_device(self.h, ctypes.c_void_p(d_bytes), n_bytes, ctypes.c_void_p(d_offsets),
                                                ctypes.c_void_p(d_doc_lang), n_docs,
                                                ctypes.c_void_p(st) if st else None))
 
     def size(self) -> int:
         n = ctypes.c_int64()
-        _lib.check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), None))
+        self._check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), None))
         return n.value
 
     def export(self) -> Tuple[List[bytes], np.ndarray]:
         """Distinct grams sorted by (length, bytes) and int64 counts [n, L]."""
         n = ctypes.c_int64()
         nb = ctypes.c_int64()
-        _lib.check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), ctypes.byref(nb)))
+        self._check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), ctypes.byref(nb)))
         kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
         ko = np.zeros(n.value + 1, dtype=np.int64)
         cnt = np.zeros((n.value, self.L), dtype=np.int64)
-        _lib.check(self.lib.ldgpu_counts_export(self.h, _ptr(kb), _ptr(ko), _ptr(cnt)))
+        self._check(self.lib.ldgpu_counts_export(self.h, _ptr(kb), _ptr(ko), _ptr(cnt)))
         b = kb.tobytes()
         return [b[ko[i]:ko[i + 1]] for i in range(n.value)], cnt
 
     def add(self, keys: Sequence[bytes], counts: np.ndarray) -> None:
         counts = np.ascontiguousarray(counts, dtype=np.int64).reshape(len(keys), self.L)
         kb, ko = pack(list(keys))
-        _lib.check(self.lib.ldgpu_counts_add(self.h, len(keys), _ptr(kb), _ptr(ko), _ptr(counts)))
+        self._check(self.lib.ldgpu_counts_add(self.h, len(keys), _ptr(kb), _ptr(ko), _ptr(counts)))
 
     def export_device(self, stream: Optional[int] = None):
         """(keys int64 [n] packed u64, counts int64 [n, L]) as torch tensors on
@@ -208,7 +218,7 @@ class DeviceCounts:
         counts = torch.empty((max(n, 1), self.L), dtype=torch.int64, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream if stream is None else stream
         got = ctypes.c_int64()
-        _lib.check(self.lib.ldgpu_counts_export_device(self.h, max(n, 1), ctypes.c_void_p(keys.data_ptr()),
+        self._check(self.lib.ldgpu_counts_export_device(self.h, max(n, 1), ctypes.c_void_p(keys.data_ptr()),
                                                        ctypes.c_void_p(counts.data_ptr()), ctypes.byref(got),
                                                        ctypes.c_void_p(st) if st else None))
         return keys[:got.value], counts[:got.value]
@@ -219,7 +229,7 @@ class DeviceCounts:
         keys = keys.contiguous()
         counts = counts.contiguous()
         st = torch.cuda.current_stream(keys.device).cuda_stream if stream is None else stream
-        _lib.check(self.lib.ldgpu_counts_add_device(self.h, int(keys.numel()), ctypes.c_void_p(keys.data_ptr()),
+        self._check(self.lib.ldgpu_counts_add_device(self.h, int(keys.numel()), ctypes.c_void_p(keys.data_ptr()),
                                                     ctypes.c_void_p(counts.data_ptr()),
                                                     ctypes.c_void_p(st) if st else None))
 
@@ -227,11 +237,11 @@ class DeviceCounts:
         """computeProbabilities + filterTopGrams -> {gram: row}."""
         n = ctypes.c_int64()
         nb = ctypes.c_int64()
-        _lib.check(self.lib.ldgpu_fit_table_size(self.h, int(profile_size), ctypes.byref(n), ctypes.byref(nb)))
+        self._check(self.lib.ldgpu_fit_table_size(self.h, int(profile_size), ctypes.byref(n), ctypes.byref(nb)))
         kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
         ko = np.zeros(n.value + 1, dtype=np.int64)
         rows = np.zeros((n.value, self.L), dtype=np.float64)
-        _lib.check(self.lib.ldgpu_fit_table_export(self.h, _ptr(kb), _ptr(ko), _ptr(rows)))
+        self._check(self.lib.ldgpu_fit_table_export(self.h, _ptr(kb), _ptr(ko), _ptr(rows)))
         b = kb.tobytes()
         return {b[ko[i]:ko[i + 1]]: rows[i].tolist() for i in range(n.value)}
 
@@ -242,12 +252,12 @@ class DeviceCounts:
         10M rows x 200 languages stay cheap."""
         n = ctypes.c_int64()
         nb = ctypes.c_int64()
-        _lib.check(self.lib.ldgpu_fit_table_size(self.h, int(profile_size), ctypes.byref(n), ctypes.byref(nb)))
+        self._check(self.lib.ldgpu_fit_table_size(self.h, int(profile_size), ctypes.byref(n), ctypes.byref(nb)))
         S = (self.L + 63) // 64
         kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
         ko = np.zeros(n.value + 1, dtype=np.int64)
         masks = np.zeros((max(n.value, 1), S), dtype=np.uint64)
         vals = np.zeros(max(n.value, 1), dtype=np.float64)
-        _lib.check(self.lib.ldgpu_fit_table_export_masks(self.h, _ptr(kb), _ptr(ko), _ptr(masks), _ptr(vals)))
+        self._check(self.lib.ldgpu_fit_table_export_masks(self.h, _ptr(kb), _ptr(ko), _ptr(masks), _ptr(vals)))
         return kb, ko, masks[:n.value], vals[:n.value]
 

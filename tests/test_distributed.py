@@ -114,3 +114,62 @@ def test_fit_distributed_matches_single_process(tmp_path):
     for r in range(2):
         got = {bytes.fromhex(k): v for k, v in json.load(open(os.path.join(tmp_path, f"table{r}.json"))).items()}
         assert got == expect
+
+
+def _score_worker(rank, world, port, out_dir):
+    dist = _init(rank, world, port)
+    from languagedetection import LanguageDetectorModel, synth
+    from languagedetection.distributed import score_sharded
+    ls = synth.make_languages(5, seed=71)
+    data, off, _ = synth.generate(ls, 3001, 0, 300, seed=72)
+    table = {b"a": [0.5, 0.0, 0.0, 0.0, 0.1], b"th": [0.0, 1.0, 0.0, 0.0, 0.0], b"ing": [0.0, 0.0, 0.3, 0.3, 0.0]}
+    model = LanguageDetectorModel(table, [1, 2, 3], ls.names, device=0)
+    labels = score_sharded(model, synth.texts(data, off))
+    np.save(os.path.join(out_dir, f"labels{rank}.npy"), labels)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_score_sharded_two_ranks(tmp_path):
+    """SCORE data parallelism: each rank scores its contiguous
+    share, no collective on the data path; the all_gathered labels equal the
+    oracle's over the whole (odd-sized) set on every rank."""
+    import ldoracle as O
+    from languagedetection import synth
+    mp.spawn(_score_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    ls = synth.make_languages(5, seed=71)
+    data, off, _ = synth.generate(ls, 3001, 0, 300, seed=72)
+    table = {b"a": [0.5, 0.0, 0.0, 0.0, 0.1], b"th": [0.0, 1.0, 0.0, 0.0, 0.0], b"ing": [0.0, 0.0, 0.3, 0.3, 0.0]}
+    expect = [O.argmax_first(O.detect_scores(O.score_encode(t), table, 5, [1, 2, 3])) for t in synth.texts(data, off)]
+    for r in range(2):
+        assert np.load(os.path.join(tmp_path, f"labels{r}.npy")).tolist() == expect
+
+
+def test_bench_refuses_mismatched_world_size():
+    """--gpus must equal the launcher's WORLD_SIZE (no silent one-GPU run)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_launches_two_ranks():
+    """bench.py --gpus 2 without a launcher starts two rank processes (gloo
+    rehearsal on one GPU: both ranks on cuda:0) and reports n_gpus 2 with
+    weak-scaling accounting (value = docs of both ranks / max-rank time)."""
+    import json
+    import subprocess
+    env = dict(os.environ, LDGPU_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--docs", "200000", "--pool", "20000", "--no-cpu-baseline",
+                        "--no-host-path"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["docs_per_gpu"] == 200000
+    assert abs(line["value"] - 2 * 200000 * 3 / (line["ms_per_step"] * 3 / 1e3)) / line["value"] < 1e-3

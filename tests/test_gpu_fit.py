@@ -185,3 +185,50 @@ def test_fit_table_mask_form_and_model_from_masks(L, grams, K):
     l1, s1 = m1.score(sdata, soff, want_scores=True)
     l2, s2 = m2.score(sdata, soff, want_scores=True)
     assert np.array_equal(l1, l2) and np.array_equal(s1.view(np.uint64), s2.view(np.uint64))
+
+
+def _topk_table_from_counts(keys, cnt, L, K):
+    """filterTopGrams (LanguageDetector.scala:100-132) over oracle counts,
+    vectorised: v_l = log(1 + [l] / k); per language the K largest v_l, ties
+    by ascending (length, bytes) = index order of the sorted keys."""
+    pres = cnt > 0
+    k = pres.sum(axis=1)
+    w = np.zeros(len(keys))
+    w[k > 0] = np.log(1.0 + 1.0 / k[k > 0])
+    chosen = np.zeros(len(keys), dtype=bool)
+    idx = np.arange(len(keys))
+    for l in range(L):
+        v = np.where(pres[:, l], w, 0.0)
+        order = np.lexsort((idx, -v))
+        chosen[order[:K]] = True
+    return {keys[i]: [float(w[i]) if pres[i, l] else 0.0 for l in range(L)] for i in np.nonzero(chosen)[0]}
+
+
+def test_config3_shape_counts_and_table():
+    """Config 3's shape at test size: documents of 1-7 KB (U[1024, 7168]),
+    20 languages, grams 1-5, ~40 MB of corpus through the device-resident
+    path (ldgpu_count_device, as bench.py --mode fit).  Counts bit-exact
+    against the C restatement, the K=500 table equal to the top-K rule
+    applied to the oracle's counts."""
+    import torch
+    L, grams, K = 20, [1, 2, 3, 4, 5], 500
+    ls = synth.make_languages(L)
+    data, off, lang = synth.generate(ls, 10000, 1024, 7168, seed=synth.SEED_BASE + 3)
+    dev = torch.device("cuda", 0)
+    n = int(off[-1])
+    d_bytes = torch.zeros(((n + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n].copy_(torch.from_numpy(data))
+    d_off = torch.from_numpy(off).to(dev)
+    d_lang = torch.from_numpy(lang).to(dev)
+    counts = DeviceCounts(L, grams, capacity_hint=1 << 16)
+    counts.count_device(d_bytes.data_ptr(), n, d_off.data_ptr(), d_lang.data_ptr(), len(off) - 1,
+                        torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(data, off, lang, L, grams)
+    assert len(keys) == len(okeys) and keys == okeys
+    assert np.array_equal(cnt, ocnt)
+    table = counts.fit_table(K)
+    expect = _topk_table_from_counts(okeys, ocnt, L, K)
+    assert table.keys() == expect.keys()
+    assert all(table[g] == expect[g] for g in expect)

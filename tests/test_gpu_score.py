@@ -35,8 +35,8 @@ def oracle_c(table, L, grams, data, off, scores=True):
     return t.score(grams, data, off, want_scores=scores, nthreads=8)
 
 
-def check_parity(table, L, grams, data, off):
-    m = DeviceModel(table, L, grams)
+def check_parity(table, L, grams, data, off, variant="product"):
+    m = DeviceModel(table, L, grams, variant=variant)
     labels, scores = m.score(data, off, want_scores=True)
     ol, os_ = oracle_c(table, L, grams, data, off)
     assert np.array_equal(labels, ol), np.nonzero(labels != ol)[0][:10]
@@ -114,10 +114,13 @@ def test_random_parity(L, grams, mask_form):
 @pytest.fixture(params=["count", "replay"])
 def uniform_path(request, monkeypatch):
     """Uniform-value tables run the count kernel (mode 2); LDGPU_NO_COUNT_MODE
-    forces the ordered-replay kernel on the same table (mode 0)."""
+    in the diagnostics library (the product library reads no environment)
+    forces the ordered-replay kernel on the same table (mode 0).
+    Returns (expected mode, library variant)."""
     if request.param == "replay":
         monkeypatch.setenv("LDGPU_NO_COUNT_MODE", "1")
-    return 2 if request.param == "count" else 0
+        return 0, "diag"
+    return 2, "product"
 
 
 @pytest.mark.parametrize("L,grams,v", [
@@ -135,8 +138,8 @@ def test_uniform_value_parity(L, grams, v, uniform_path):
     lens[:8] = [0, 1, 2, 3, 6, 7, 64, 65]
     docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
     data, off = encoding.pack(docs)
-    m = check_parity(table, L, grams, data, off)
-    assert m.info()["mode"] == uniform_path
+    m = check_parity(table, L, grams, data, off, variant=uniform_path[1])
+    assert m.info()["mode"] == uniform_path[0]
 
 
 def test_uniform_value_counts_past_fold_table(uniform_path):
@@ -148,8 +151,8 @@ def test_uniform_value_counts_past_fold_table(uniform_path):
     rng = np.random.default_rng(17)
     docs = [b"ab" * 9000, bytes(rng.integers(0, 256, size=30000, dtype=np.uint8)), b"", b"a"]
     data, off = encoding.pack(docs)
-    m = check_parity(table, L, [1, 2, 1], data, off)
-    assert m.info()["mode"] == uniform_path
+    m = check_parity(table, L, [1, 2, 1], data, off, variant=uniform_path[1])
+    assert m.info()["mode"] == uniform_path[0]
 
 
 @pytest.mark.parametrize("direct", [True, False])
@@ -157,8 +160,9 @@ def test_uniform_value_counts_past_fold_table(uniform_path):
 def test_single_language_keys_direct_tables(L, grams, direct, monkeypatch):
     """Every row one language, one shared value (a fit table of grams unique
     to a language): 1-/2-byte keys are counted from the LDS direct tables,
-    longer ones verified; LDGPU_NO_DIRECT forces them all through verification.
-    Docs of every length class: partial windows, the 256-byte fast path, long."""
+    longer ones verified; LDGPU_NO_DIRECT (diagnostics library) forces them all
+    through verification.  Docs of every length class: partial windows, the
+    256-byte fast path, long."""
     if not direct:
         monkeypatch.setenv("LDGPU_NO_DIRECT", "1")
     rng = np.random.default_rng(L + 3 * len(grams))
@@ -175,7 +179,7 @@ def test_single_language_keys_direct_tables(L, grams, direct, monkeypatch):
     lens[:10] = [0, 1, 2, 3, 6, 7, 64, 65, 256, 255]
     docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
     data, off = encoding.pack(docs)
-    m = check_parity(table, L, grams, data, off)
+    m = check_parity(table, L, grams, data, off, variant="product" if direct else "diag")
     assert m.info()["mode"] == 2
 
 
@@ -338,3 +342,105 @@ def test_config5_shape_parity_large_profile_global_filter():
     m = check_parity(table, L, grams, data, off)
     info = m.info()
     assert info["filter_bits"] > 64 * 1024 * 8  # bloom beyond LDS: global-filter kernel
+
+
+def _windows(data, off, n, rng, count):
+    """`count` random n-byte windows of the documents (table keys that hit)."""
+    d = rng.integers(0, len(off) - 1, size=count)
+    lens = off[d + 1] - off[d]
+    ok = lens >= n
+    d, lens = d[ok], lens[ok]
+    p = off[d] + (rng.random(len(d)) * (lens - n + 1)).astype(np.int64)
+    return [bytes(data[q:q + n]) for q in p.tolist()]
+
+
+@pytest.mark.parametrize("L", [20, 100])
+def test_count_mode_bucket_table_over_2pow20_keys(L):
+    """Config 5's timed path: a count-mode table (every row one shared value)
+    of more than 2^20 keys lives in 4-slot buckets (Bucket, ldgpu_common.h:
+    bucket_place / bucket_find, secondary buckets behind overflow flags) with
+    the keyed bloom in global memory.  Labels AND fp64 scores against the C
+    oracle on documents of every length class."""
+    rng = np.random.default_rng(1000 + L)
+    ls = synth.make_languages(L, seed=synth.SEED_BASE + 500 + L)
+    data, off, _ = synth.generate(ls, 6000, 0, 400, seed=synth.SEED_BASE + 501)
+    keys = set()
+    for n in range(1, 8):
+        keys.update(_windows(data, off, n, rng, 120_000))
+    while len(keys) < 1_150_000:  # misses: random keys of 3..7 bytes
+        n = int(rng.integers(3, 8))
+        keys.update(bytes(r) for r in rng.integers(0, 256, size=(50_000, n), dtype=np.uint8))
+    keys = sorted(keys)
+    kb, ko = encoding.pack(keys)
+    S = (L + 63) // 64
+    masks = np.zeros((len(keys), S), dtype=np.uint64)
+    lang1 = rng.integers(0, L, size=len(keys))
+    masks[np.arange(len(keys)), lang1 // 64] = (np.uint64(1) << (lang1 % 64).astype(np.uint64))
+    multi = rng.random(len(keys)) < 0.2      # some rows name several languages (mask words read)
+    extra = rng.integers(0, L, size=len(keys))
+    masks[multi, extra[multi] // 64] |= (np.uint64(1) << (extra[multi] % 64).astype(np.uint64))
+    vals = np.full(len(keys), math.log(2.0))
+    grams = [1, 2, 3, 4, 5, 6, 7]
+    m = DeviceModel.from_masks(kb, ko, masks, vals, L, grams)
+    info = m.info()
+    assert info["mode"] == 2 and info["n_keys"] == len(keys) > (1 << 20)
+    assert info["table_slots"] < 2.5 * len(keys)          # buckets (cuckoo slots would be >= 2.5 per key)
+    assert info["filter_bits"] > 64 * 1024 * 8             # keyed bloom in global memory
+    t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals, L)
+    ol, os_ = t.score(grams, data, off, want_scores=True, nthreads=8)
+    lab, sc = m.score(data, off, want_scores=True)
+    assert np.array_equal(lab, ol), np.nonzero(lab != ol)[0][:10]
+    assert np.array_equal(bits(sc), bits(os_))
+    # the labels-only path (count_argmax) the bench times
+    lab2, _ = m.score(data, off)
+    assert np.array_equal(lab2, ol)
+
+
+def test_concurrent_callers_share_one_context():
+    """Spark runs several task threads per executor (Spark.scala:11 local[4]):
+    4 threads call ldgpu_score on one model / context at once (ctypes drops
+    the GIL) and each gets the single-thread labels and scores."""
+    import threading
+    from languagedetection.api import LanguageDetector
+    ls = synth.make_languages(8, seed=41)
+    tdata, toff, tlang = synth.generate(ls, 800, 100, 400, seed=42)
+    rows = list(zip([ls.names[i] for i in tlang], synth.texts(tdata, toff)))
+    table = LanguageDetector.computeGramProbabilities(rows, [1, 2, 3, 4], 300, ls.names)
+    m = DeviceModel(table, 8, [1, 2, 3, 4])
+    batches = [synth.generate(ls, 20000 + 5000 * i, 0, 300, seed=43 + i)[:2] for i in range(4)]
+    expect = [m.score(d, o, want_scores=True) for d, o in batches]
+    got = [None] * 4
+    errors = []
+
+    def run(i):
+        try:
+            for _ in range(3):
+                got[i] = m.score(*batches[i], want_scores=True)
+                assert np.array_equal(got[i][0], expect[i][0])
+                assert np.array_equal(bits(got[i][1]), bits(expect[i][1]))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    ol, _ = oracle_c(table, 8, [1, 2, 3, 4], *batches[0])
+    assert np.array_equal(expect[0][0], ol)
+
+
+def test_product_library_ignores_env_switches(monkeypatch):
+    """Diagnostics switches exist only in libldgpu_diag.so: with them set, the
+    product library still takes the count path and gives the oracle's labels."""
+    for k, v in (("LDGPU_ABLATE", "7"), ("LDGPU_NO_COUNT_MODE", "1"), ("LDGPU_NO_DIRECT", "1"),
+                 ("LDGPU_WG_PER_CU", "1"), ("LDGPU_BLOOM_KPW", "0.05")):
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(77)
+    alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+    table = _random_table(rng, 20, 400, [1, 2, 3], alphabet, True, uniform=math.log(2.0))
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in rng.integers(0, 300, size=500)]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, 20, [1, 2, 3], data, off)
+    assert m.info()["mode"] == 2

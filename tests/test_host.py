@@ -112,3 +112,12 @@ def test_no_gpu_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(Exception):
         _lib.context(0)
+
+
+def test_product_library_reads_no_env_switches():
+    """The LDGPU_* path / ablation switches live only in the diagnostics build
+    (lib/libldgpu_diag.so): no such name appears in the product library."""
+    from languagedetection import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"LDGPU_" not in blob
+    assert b"LDGPU_ABLATE" in open(_lib.DIAG_LIB_PATH, "rb").read()

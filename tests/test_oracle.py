@@ -158,3 +158,27 @@ def test_c_oracle_matches_python_count():
     got = {(langs[l], k): int(cnt[i, l]) for i, k in enumerate(keys) for l in range(3) if cnt[i, l]}
     assert got == reduced
     assert keys == sorted(keys, key=O.key_order)
+
+
+def test_c_oracle_mask_form_equals_dense_rows():
+    """OC.Table.from_masks (ldo_table_create_masks) scores exactly as the
+    dense table it stands for (used for tables too large for dense rows)."""
+    import numpy as np
+    rng = np.random.default_rng(8)
+    L = 70
+    keys = sorted({bytes(rng.integers(97, 100, size=int(rng.integers(1, 5)), dtype=np.uint8)) for _ in range(300)})
+    masks = rng.integers(0, 2**63, size=(len(keys), 2), dtype=np.uint64)
+    masks[:, 1] &= np.uint64((1 << 6) - 1)
+    vals = rng.normal(size=len(keys))
+    dense = {k: [float(vals[i]) if (int(masks[i, l // 64]) >> (l % 64)) & 1 else 0.0 for l in range(L)]
+             for i, k in enumerate(keys)}
+    off = np.zeros(len(keys) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    kb = np.frombuffer(b"".join(keys), dtype=np.uint8)
+    docs = [bytes(rng.integers(97, 100, size=int(n), dtype=np.uint8)) for n in rng.integers(0, 60, size=200)]
+    doff = np.zeros(len(docs) + 1, dtype=np.int64)
+    doff[1:] = np.cumsum([len(d) for d in docs])
+    dd = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
+    l1, s1 = OC.Table(dense, L).score([1, 2, 3], dd, doff, want_scores=True)
+    l2, s2 = OC.Table.from_masks(kb, off, masks, vals, L).score([1, 2, 3], dd, doff, want_scores=True)
+    assert np.array_equal(l1, l2) and np.array_equal(s1.view(np.uint64), s2.view(np.uint64))
