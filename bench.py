@@ -145,28 +145,38 @@ def cpu_baseline(args, table, grams, data, off):
 def cpu_baseline_fit(args, grams, data, off, lang):
     """FIT on the oracle's C restatement (computeGrams + reduceGrams into a
     host hash table, kind 'port', one thread), rank 0, bounded sample of the
-    same corpus; unit = corpus bytes/s like the line's value."""
+    same corpus; unit = corpus bytes/s like the line's value.  Also returns
+    the sample's oracle counts (key bytes, offsets, counts) for the parity
+    check of the GPU path on the same documents."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ldoracle_c as OC
     L = OC.lib()
     g = np.asarray(grams, dtype=np.int32)
 
-    def run(n):
+    def run(n, keep=False):
         o = np.ascontiguousarray(off[:n + 1], dtype=np.int64)
         t0 = time.perf_counter()
         h = L.ldo_count(OC._ptr(data), OC._ptr(o), OC._ptr(lang), n, args.langs, OC._ptr(g), len(g))
         dt = time.perf_counter() - t0
+        out = None
+        if keep:
+            k = L.ldo_counts_size(h)
+            kb = np.zeros(max(L.ldo_counts_key_bytes(h), 1), dtype=np.uint8)
+            ko = np.zeros(k + 1, dtype=np.int64)
+            cnt = np.zeros((k, args.langs), dtype=np.int64)
+            L.ldo_counts_export(h, OC._ptr(kb), OC._ptr(ko), OC._ptr(cnt))
+            out = (kb[:int(ko[-1])], ko, cnt)
         L.ldo_counts_destroy(h)
-        return dt
+        return dt, out
 
     probe = min(200, len(off) - 1)
-    rate = int(off[probe]) / max(run(probe), 1e-9)
+    rate = int(off[probe]) / max(run(probe)[0], 1e-9)
     target = rate * args.cpu_seconds
     n = int(min(len(off) - 1, max(probe, np.searchsorted(off, target))))
-    dt = run(n)
+    dt, exported = run(n, keep=True)
     return {"value": round(int(off[n]) / dt, 1), "unit": "bytes/s", "cores": 1, "kind": "port",
             "sample": f"first {n} documents ({int(off[n])} corpus bytes) of the GPU's corpus, "
-                      f"oracle/ldoracle.c ldo_count, 1 thread, {dt:.1f} s"}
+                      f"oracle/ldoracle.c ldo_count, 1 thread, {dt:.1f} s"}, n, exported
 
 
 def host_path(model, data, off, acc_labels):
@@ -212,8 +222,9 @@ def fit_main(args, world, rank, local, dev, backend):
     """Config 3 (FIT): count every window of a synthetic multilingual corpus
     (docs of 1-7 KB) resident in HBM, merge across ranks (all_gather keys +
     all_reduce counts), build the K-profile table.  A step = one full fit."""
-    from languagedetection.distributed import merge_counts_device
+    from languagedetection.distributed import Communicator, merge_counts_device
     grams = [int(x) for x in args.grams.split(",")]
+    comm = Communicator(device=local) if world > 1 else None
     ls = synth.make_languages(args.langs)
     pool_docs = max(1, min(16384, args.fit_bytes // 4096))
     pdata, poff, plang = synth.generate(ls, pool_docs, 1024, 7168, seed=synth.SEED_BASE + 3 + 1000 * rank)
@@ -236,9 +247,7 @@ def fit_main(args, world, rank, local, dev, backend):
         torch.cuda.synchronize(dev)
         t["count_s"] = time.perf_counter() - t0 - t["create_s"]
         if world > 1:
-            merged = merge_counts_device(c)
-            c.close()
-            c = merged
+            merge_counts_device(c, comm)   # owner exchange (RCCL with backend nccl)
             torch.cuda.synchronize(dev)
             t["merge_s"] = time.perf_counter() - t0 - t["create_s"] - t["count_s"]
         distinct = c.size()
@@ -266,7 +275,16 @@ def fit_main(args, world, rank, local, dev, backend):
         elapsed = float(tt.item())
     count_s = float(np.mean([p[0]["count_s"] for p in parts]))
     windows = sum(int(synth_windows(off, n)) for n in grams)
-    algo = n_bytes + 12 * n_docs  # corpus bytes + offset + language id per document
+    # one more count, untimed, for the table statistics: SURVEY §8d charges the
+    # corpus byte, 12 B per document (offset + language id) and 16 B per
+    # distinct (gram, language) count written
+    c = DeviceCounts(args.langs, grams, capacity_hint=1 << 22, device=local)
+    c.count_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), d_lang.data_ptr(), n_docs, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    st = c.stats()
+    c.close()
+    assert st["total"] == windows, (st, windows)   # every window counted exactly once
+    algo = n_bytes + 12 * n_docs + 16 * st["pairs"]
     line = {
         "metric": "corpus bytes/sec fitted (config 3: count + merge + probability/top-K table)",
         "value": round(n_bytes * world * args.steps / elapsed, 1), "unit": "bytes/s", "n_gpus": world,
@@ -276,16 +294,29 @@ def fit_main(args, world, rank, local, dev, backend):
         "config": {"workload": f"config3-shaped: fit {n_bytes} corpus bytes per GPU, {args.langs} languages, "
                                f"grams {args.grams}, profile size {args.profile_size}",
                    "docs_per_gpu": n_docs, "corpus_bytes_per_gpu": n_bytes, "windows_per_gpu": windows,
-                   "distinct_grams": parts[-1][1], "table_rows": parts[-1][2],
-                   "parallelism": f"dp{world} (corpus sharded; all_gather + all_reduce merge)"},
+                   "distinct_grams": parts[-1][1], "distinct_gram_language_pairs": st["pairs"],
+                   "table_rows": parts[-1][2],
+                   "parallelism": f"dp{world} (corpus sharded; owner-exchange merge + distributed top-K)"},
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
                      for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
         "count_windows_per_s": round(windows / count_s, 1),
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6), "traffic": None},
+                     "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
+                     "traffic": traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}"),
+                     "kernel": "count (emit + part2 + reduce + merge)", "count_ms": round(count_s * 1e3, 3),
+                     "algorithmic_bytes_per_count": int(algo)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_fit(args, grams, data, off, lang)
+        line["cpu_baseline"], n_s, (okb, oko, ocnt) = cpu_baseline_fit(args, grams, data, off, lang)
+        # the GPU count of the same sample documents against the oracle's
+        c = DeviceCounts(args.langs, grams, device=local)
+        c.count_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), d_lang.data_ptr(), n_s, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        gkb, gko, gcnt = c.export_arrays()
+        c.close()
+        ok = (np.array_equal(gko, oko) and np.array_equal(gkb, okb) and np.array_equal(gcnt, ocnt))
+        line["counts_match_oracle"] = bool(ok)
+        line["oracle_check"] = {"docs_checked": int(n_s), "grams_checked": int(len(oko) - 1)}
     if rank == 0:
         print(json.dumps(line), flush=True)
         if args.json_out:

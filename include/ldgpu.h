@@ -143,6 +143,10 @@ int ldgpu_count_device(ldgpu_counts* counts, const uint8_t* d_bytes, int64_t n_b
 
 /* Distinct grams and their total key bytes. */
 int ldgpu_counts_size(ldgpu_counts* counts, int64_t* n_grams, int64_t* key_bytes);
+/* Distinct grams, distinct (gram, language) pairs -- the rows reduceGrams
+ * emits (LanguageDetector.scala:57-65) -- and the sum of all counts (= the
+ * windows counted).  Any output pointer may be NULL. */
+int ldgpu_counts_stats(ldgpu_counts* counts, int64_t* n_grams, int64_t* n_pairs, int64_t* total);
 /* Export sorted by (length, unsigned bytes): key_bytes, key_offsets[n+1],
  * counts[n][n_langs] (raw int64 sums; the JVM sums wrap at 2^31). */
 int ldgpu_counts_export(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
@@ -165,6 +169,48 @@ int ldgpu_counts_export_device(ldgpu_counts* counts, int64_t capacity, uint64_t*
                                int64_t* d_counts, int64_t* n_out, void* stream);
 int ldgpu_counts_add_device(ldgpu_counts* counts, int64_t n, const uint64_t* d_keys,
                             const int64_t* d_counts, void* stream);
+
+/* ------------------------------------------------------- multi-GPU FIT merge
+ * Replaces the reference's shuffles of reduceGrams / computeProbabilities /
+ * filterTopGrams (LanguageDetector.scala:57-65, :79-81, :110-126) when the
+ * corpus is sharded over executors, one GPU each.  A communicator spans the
+ * ranks of one fit; two transports run the same merge:
+ *   RCCL over xGMI  -- ldgpu_comm_create_rccl; rank 0 makes the id with
+ *                      ldgpu_comm_unique_id and the caller hands it to every
+ *                      rank (Spark: a driver broadcast);
+ *   host callbacks  -- ldgpu_comm_create_host; the caller provides an
+ *                      all-gather and an all-to-all over host memory (an
+ *                      executor's own transport; gloo in the tests). */
+typedef struct ldgpu_comm ldgpu_comm;
+#define LDGPU_COMM_ID_BYTES 128
+
+typedef struct {
+    void* user;
+    /* recv = world * bytes, rank r's block at r * bytes; returns 0 on success */
+    int (*allgather)(void* user, const void* send, int64_t bytes, void* recv);
+    /* send_bytes[r] bytes to rank r (blocks in rank order), recv_bytes[r]
+     * from rank r (blocks in rank order); returns 0 on success */
+    int (*alltoallv)(void* user, const void* send, const int64_t* send_bytes, void* recv,
+                     const int64_t* recv_bytes);
+} ldgpu_host_coll;
+
+int ldgpu_comm_unique_id(uint8_t* out_id /* LDGPU_COMM_ID_BYTES */);
+int ldgpu_comm_create_rccl(ldgpu_ctx* ctx, const uint8_t* id, int32_t rank, int32_t world, ldgpu_comm** out);
+int ldgpu_comm_create_host(ldgpu_ctx* ctx, int32_t rank, int32_t world, const ldgpu_host_coll* coll,
+                           ldgpu_comm** out);
+int ldgpu_comm_destroy(ldgpu_comm* comm);
+
+/* Owner-partitioned exchange: gram g belongs to rank owner(g) (a hash of its
+ * key), every rank sends its counts of the grams it does not own to their
+ * owners (one all-to-all), and afterwards holds the GLOBAL counts (sums over
+ * all ranks, bit-exact) of exactly the grams it owns.  ldgpu_counts_export /
+ * _size / _stats then describe the owned shard; ldgpu_fit_table_size on the
+ * merged table runs the global top-K through the communicator (a (language,
+ * class) histogram all-reduce, an all-gather of each rank's tie candidates,
+ * an all-gather of the chosen rows), and every rank exports the same table.
+ * Collective: every rank calls it.  Counting more documents into a merged
+ * table is an error (LDGPU_EINVAL). */
+int ldgpu_counts_merge(ldgpu_counts* counts, ldgpu_comm* comm);
 
 /* computeProbabilities + filterTopGrams: v_l = log(1 + [g in l] / k_g);
  * per language the profile_size largest v_l (ties: ascending (length, bytes));

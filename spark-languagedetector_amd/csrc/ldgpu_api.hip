@@ -13,6 +13,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/ldgpu.h"
 #include "ldgpu_internal.h"
 
@@ -187,6 +189,10 @@ struct ldgpu_ctx {
     DevBuf bytes, offsets, labels, scores, langs;
     std::mutex pool_mu;                // guards `pipes` / `free_pipes` only
     std::vector<ScorePipe*> pipes, free_pipes;
+    // FIT v2 batch scratch (records, buckets, reduce output), shared by the
+    // context's count tables under `mu` and kept between fits: multi-GB
+    // allocations per fit would cost more than the counting itself
+    DevBuf f_rec, f_rec2, f_bstart, f_bhdr, f_nblk, f_cnt3, f_wg, f_p2, f_boff, f_okl, f_ocnt, f_on;
 };
 
 namespace {
@@ -277,6 +283,9 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
     c->labels.release();
     c->scores.release();
     c->langs.release();
+    for (DevBuf* b : {&c->f_rec, &c->f_rec2, &c->f_bstart, &c->f_bhdr, &c->f_nblk, &c->f_cnt3, &c->f_wg, &c->f_p2,
+                      &c->f_boff, &c->f_okl, &c->f_ocnt, &c->f_on})
+        b->release();
     for (ScorePipe* pp : c->pipes) pipe_destroy(pp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1051,9 +1060,16 @@ struct ldgpu_counts {
     unsigned long long* d_size = nullptr;
     uint64_t* d_ovf_keys = nullptr;
     int32_t* d_ovf_lang = nullptr;
+    unsigned long long* d_ovf_cnt = nullptr;
     unsigned int* d_ovf_n = nullptr;
     uint32_t ovf_cap = 1u << 20;  // windows per sub-launch; grown per call up to kOvfMax
     uint64_t size = 0;
+    // FIT v2 (radix-partitioned records, ldgpu_fit.hip): the record format
+    // ((sentinel << lb | lang) << cb | count) and the per-batch scratch
+    bool v2 = false;
+    uint32_t lb = 0, cb = 0;
+    int64_t batch_windows = 0;  // kBatchWindows (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
+    ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
     // cached fit table (ldgpu_fit_table_size -> _export)
     bool tbl_valid = false;
     std::vector<uint8_t> tbl_bytes;
@@ -1072,6 +1088,7 @@ CountParams count_params(const ldgpu_counts* c) {
     p.size = c->d_size;
     p.ovf_keys = c->d_ovf_keys;
     p.ovf_lang = c->d_ovf_lang;
+    p.ovf_cnt = c->d_ovf_cnt;
     p.ovf_n = c->d_ovf_n;
     p.ovf_cap = c->ovf_cap;
     p.L = c->L;
@@ -1084,7 +1101,7 @@ void counts_free(ldgpu_counts* c) {
     if (!c) return;
     if (c->ctx) (void)hipSetDevice(c->ctx->device);
     for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_size, (void*)c->d_ovf_keys,
-                    (void*)c->d_ovf_lang, (void*)c->d_ovf_n})
+                    (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt, (void*)c->d_ovf_n})
         if (p) (void)hipFree(p);
     delete c;
 }
@@ -1141,7 +1158,7 @@ int after_batch(ldgpu_counts* c) {
     if (novf > 0) {
         CountParams p = count_params(c);
         HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream));
-        HIP_TRY(launch_counts_add(p, c->d_ovf_keys, nullptr, c->d_ovf_lang, novf, c->ctx->stream));
+        HIP_TRY(launch_counts_add(p, c->d_ovf_keys, nullptr, c->d_ovf_lang, c->d_ovf_cnt, novf, c->ctx->stream));
         unsigned int again = 0;
         HIP_TRY(hipMemcpyAsync(&again, c->d_ovf_n, sizeof again, hipMemcpyDeviceToHost, c->ctx->stream));
         HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
@@ -1169,18 +1186,21 @@ constexpr uint32_t kOvfMax = 1u << 27;
 
 int ensure_ovf(ldgpu_counts* c, int64_t windows) {
     const uint64_t want = std::min<uint64_t>(kOvfMax, next_pow2((uint64_t)std::max<int64_t>(windows, 1)));
-    if (want <= c->ovf_cap && c->d_ovf_keys && c->d_ovf_lang) return LDGPU_OK;
+    if (want <= c->ovf_cap && c->d_ovf_keys && c->d_ovf_lang && c->d_ovf_cnt) return LDGPU_OK;
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
     auto drop = [&] {
         if (c->d_ovf_keys) (void)hipFree(c->d_ovf_keys);
         if (c->d_ovf_lang) (void)hipFree(c->d_ovf_lang);
+        if (c->d_ovf_cnt) (void)hipFree(c->d_ovf_cnt);
         c->d_ovf_keys = nullptr;
         c->d_ovf_lang = nullptr;
+        c->d_ovf_cnt = nullptr;
         c->ovf_cap = 0;
     };
     auto take = [&](uint64_t n) {
         hipError_t e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * n);
         if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * n);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_cnt, sizeof(unsigned long long) * n);
         if (e == hipSuccess) c->ovf_cap = (uint32_t)n;
         else drop();
         return e;
@@ -1193,11 +1213,140 @@ int ensure_ovf(ldgpu_counts* c, int64_t windows) {
     return LDGPU_OK;
 }
 
+// FIT v2 batches: at most kBatchWindows windows (~200 MB of corpus at grams
+// 1-5), so the record scratch (8 B per window for the emit records, 8 B per
+// record for the buckets, <= 12 B per record of reduce output) stays within
+// ~20 GB of HBM, and a batch's distinct (gram, language) pairs per bucket stay
+// within the reduce LDS table.
+constexpr int64_t kBatchWindows = 1ll << 30;
+
+int count_launch_v2(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                    const int32_t* d_lang, int64_t n_docs, const int64_t* h_off) {
+    ldgpu_ctx* x = c->ctx;
+    hipStream_t st = x->stream;
+    const int grid_a = std::max(kSplits, (c->ctx->cus / kSplits) * kSplits);
+    if (int rc = ensure_ovf(c, 1 << 20)) return rc;
+    std::vector<int64_t> meta(3 * (size_t)(grid_a + 1));
+    std::vector<uint32_t> cnt3((size_t)kQ * kQ * kSplits);
+    std::vector<uint64_t> p2off((size_t)kQ * kQ * kSplits), boff((size_t)kQ * kQ + 1);
+    auto win_of = [&](int64_t d) { return doc_windows(c, h_off[d + 1] - h_off[d]); };
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0, W = 0;
+        while (d1 < n_docs) {
+            const int64_t w = win_of(d1);
+            if (d1 > d0 && W + w > c->batch_windows) break;
+            W += w;
+            ++d1;
+        }
+        // emit workgroups: document ranges balanced by windows; a workgroup's
+        // record region holds its windows (records <= windows), its block
+        // directory windows / 4096 + 2 blocks (every block but its last holds
+        // more than kBlkRecs - kRoundRecs records)
+        int64_t* wg_doc = meta.data();
+        int64_t* wg_rec = wg_doc + grid_a + 1;
+        int64_t* wg_dir = wg_rec + grid_a + 1;
+        int64_t d = d0, acc = 0, dirs = 0;
+        for (int k = 0; k < grid_a; ++k) {
+            const int64_t start_d = d, start_acc = acc, target = W * (k + 1) / grid_a;
+            while (d < d1 && acc < target) acc += win_of(d++);
+            wg_doc[k] = start_d - d0;
+            wg_rec[k] = start_acc;
+            wg_dir[k] = dirs;
+            dirs += (acc - start_acc) / (kBlkRecs - kRoundRecs) + 2;
+        }
+        wg_doc[grid_a] = d1 - d0;
+        wg_rec[grid_a] = W;
+        wg_dir[grid_a] = dirs;
+        HIP_TRY(x->f_wg.ensure(sizeof(int64_t) * meta.size()));
+        HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(W, 1)));
+        HIP_TRY(x->f_bstart.ensure(sizeof(int64_t) * (size_t)dirs));
+        HIP_TRY(x->f_bhdr.ensure(sizeof(uint32_t) * kHdr * (size_t)dirs));
+        HIP_TRY(x->f_nblk.ensure(sizeof(int32_t) * (size_t)grid_a));
+        HIP_TRY(x->f_cnt3.ensure(sizeof(uint32_t) * cnt3.size()));
+        HIP_TRY(hipMemcpyAsync(x->f_wg.p, meta.data(), sizeof(int64_t) * meta.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(x->f_cnt3.p, 0, sizeof(uint32_t) * cnt3.size(), st));
+        PartParams pp{};
+        pp.bytes = d_bytes;
+        pp.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+        pp.offsets = d_offsets + d0;
+        pp.doc_lang = d_lang + d0;
+        pp.L = c->L;
+        pp.nG = c->nG;
+        for (int i = 0; i < c->nG; ++i) pp.G[i] = c->G[i];
+        pp.lb = c->lb;
+        pp.cb = c->cb;
+        pp.grid_a = grid_a;
+        pp.wg_doc = (const int64_t*)x->f_wg.p;
+        pp.wg_rec = pp.wg_doc + grid_a + 1;
+        pp.wg_dir = pp.wg_rec + grid_a + 1;
+        pp.rec = (uint64_t*)x->f_rec.p;
+        pp.blk_start = (int64_t*)x->f_bstart.p;
+        pp.blk_hdr = (uint32_t*)x->f_bhdr.p;
+        pp.nblk = (int32_t*)x->f_nblk.p;
+        pp.cnt3 = (uint32_t*)x->f_cnt3.p;
+        pp.direct = count_params(c);
+        HIP_TRY(launch_emit(pp, st));
+        HIP_TRY(hipMemcpyAsync(cnt3.data(), x->f_cnt3.p, sizeof(uint32_t) * cnt3.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = after_batch(c)) return rc;  // direct adds (a count too large for a record) that overflowed
+        // exact bucket offsets: (q1, q2) major, emit group minor
+        uint64_t off = 0;
+        for (int q = 0; q < kQ * kQ; ++q) {
+            boff[q] = off;
+            for (int s = 0; s < kSplits; ++s) {
+                p2off[(size_t)q * kSplits + s] = off;
+                off += cnt3[(size_t)q * kSplits + s];
+            }
+        }
+        boff[(size_t)kQ * kQ] = off;
+        const int64_t R = (int64_t)off;
+        HIP_TRY(x->f_p2.ensure(sizeof(uint64_t) * p2off.size()));
+        HIP_TRY(x->f_boff.ensure(sizeof(uint64_t) * boff.size()));
+        HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(R, 1)));
+        HIP_TRY(x->f_okl.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(R, 1)));
+        HIP_TRY(x->f_ocnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(R, 1)));
+        HIP_TRY(x->f_on.ensure(sizeof(unsigned long long)));
+        HIP_TRY(hipMemcpyAsync(x->f_p2.p, p2off.data(), sizeof(uint64_t) * p2off.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(x->f_boff.p, boff.data(), sizeof(uint64_t) * boff.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(x->f_on.p, 0, sizeof(unsigned long long), st));
+        pp.p2off = (const uint64_t*)x->f_p2.p;
+        pp.rec2 = (uint64_t*)x->f_rec2.p;
+        pp.boff = (const uint64_t*)x->f_boff.p;
+        pp.out_kl = (uint64_t*)x->f_okl.p;
+        pp.out_cnt = (uint32_t*)x->f_ocnt.p;
+        pp.out_n = (unsigned long long*)x->f_on.p;
+        if (R > 0) {
+            HIP_TRY(launch_part2(pp, st));
+            HIP_TRY(launch_reduce(pp, st));
+        }
+        unsigned long long E = 0;
+        HIP_TRY(hipMemcpyAsync(&E, x->f_on.p, sizeof E, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if ((int64_t)E > R) return fail(LDGPU_EDEVICE, "fit reduce: %llu entries from %lld records", E, (long long)R);
+        // room for every entry as a new key: load <= 1/2, so the merge's
+        // probes never reach the overflow list in practice (it still catches them)
+        if (2 * (c->size + E) > c->cap) {
+            if (int rc = grow(c, next_pow2(2 * (c->size + E)))) return rc;
+        }
+        if (int rc = ensure_ovf(c, (int64_t)E)) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+        HIP_TRY(launch_merge(pp, count_params(c), (int64_t)E, st));
+        if (int rc = after_batch(c)) return rc;
+        d0 = d1;
+    }
+    return LDGPU_OK;
+}
+
 // Count documents [0, n_docs) of d_offsets / d_lang (h_off: the same offsets on
 // the host, used to plan sub-launches of at most ovf_cap windows each, so the
 // overflow list can never lose an entry).
 int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                  const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
+    if (c->v2) {
+        if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
+        return count_launch_v2(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off);
+    }
     int64_t total = 0;
     for (int64_t d = 0; d < n_docs; ++d) total += doc_windows(c, h_off[d + 1] - h_off[d]);
     if (int rc = ensure_ovf(c, total)) return rc;
@@ -1250,11 +1399,28 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
     c->nG = n_grams;
     for (int i = 0; i < n_grams; ++i) c->G[i] = gram_lengths[i];
     c->cap = next_pow2(std::max<int64_t>(1 << 12, 2 * std::max<int64_t>(capacity_hint, 0)));
+    // FIT v2 when a (gram, language, count) record fits 64 bits with >= 8
+    // count bits: 8 max(G) + 1 sentinel-key bits + ceil(log2 L) language bits
+    {
+        int maxg = 0;
+        for (int i = 0; i < n_grams; ++i) maxg = std::max(maxg, gram_lengths[i]);
+        c->lb = (uint32_t)std::max(1, log2u((uint64_t)n_langs));
+        const int cb = 64 - (8 * maxg + 1) - (int)c->lb;
+        c->cb = (uint32_t)std::max(cb, 0);
+        c->v2 = cb >= 8 && !diag_env("LDGPU_FIT_LEGACY");
+        c->batch_windows = kBatchWindows;
+        if (const char* bw = diag_env("LDGPU_FIT_BATCH_WINDOWS")) c->batch_windows = std::max(1ll, atoll(bw));
+        if (c->v2 && fit2_prepare() != hipSuccess) {  // dynamic-LDS limits of this device's kernels
+            (void)hipGetLastError();
+            c->v2 = false;
+        }
+    }
     int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
     hipError_t e = hipSuccess;
     if (!rc) e = hipMalloc((void**)&c->d_size, sizeof(unsigned long long));
     if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
     if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
+    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
     if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_n, sizeof(unsigned int));
     if (!rc && e == hipSuccess) e = hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), ctx->stream);
     if (!rc && e == hipSuccess) e = hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), ctx->stream);
@@ -1275,6 +1441,7 @@ extern "C" int ldgpu_counts_destroy(ldgpu_counts* c) {
 extern "C" int ldgpu_count_device(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                                   const int32_t* d_doc_lang, int64_t n_docs, void* stream) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (c->comm) return fail(LDGPU_EINVAL, "the count table is merged (ldgpu_counts_merge): it takes no more counts");
     if (n_docs < 0) return fail(LDGPU_EINVAL, "n_docs < 0");
     if (n_docs > 0 && (!d_offsets || !d_doc_lang || (n_bytes > 0 && !d_bytes)))
         return fail(LDGPU_EINVAL, "device pointer is NULL");
@@ -1293,6 +1460,7 @@ extern "C" int ldgpu_count_device(ldgpu_counts* c, const uint8_t* d_bytes, int64
 extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang,
                            int64_t n_docs) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (c->comm) return fail(LDGPU_EINVAL, "the count table is merged (ldgpu_counts_merge): it takes no more counts");
     if (int rc = check_offsets(offsets, n_docs)) return rc;
     if (n_docs == 0) return ok();
     if (!doc_lang) return fail(LDGPU_EINVAL, "doc_lang is NULL");
@@ -1391,6 +1559,25 @@ extern "C" int ldgpu_counts_size(ldgpu_counts* c, int64_t* n_grams, int64_t* key
     return ok();
 }
 
+extern "C" int ldgpu_counts_stats(ldgpu_counts* c, int64_t* n_grams, int64_t* n_pairs, int64_t* total) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    unsigned long long* d = nullptr;
+    unsigned long long h[2] = {0, 0};
+    HIP_TRY(hipMalloc((void**)&d, sizeof h));
+    hipError_t e = hipMemsetAsync(d, 0, sizeof h, c->ctx->stream);
+    if (e == hipSuccess) e = launch_stats(count_params(c), c->cap, d, c->ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "counts_stats: %s", hipGetErrorString(e));
+    if (n_grams) *n_grams = (int64_t)c->size;
+    if (n_pairs) *n_pairs = (int64_t)h[0];
+    if (total) *total = (int64_t)h[1];
+    return ok();
+}
+
 extern "C" int ldgpu_counts_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t* key_offsets, int64_t* counts_out) {
     if (!c || !key_offsets || !counts_out) return fail(LDGPU_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
@@ -1406,6 +1593,7 @@ extern "C" int ldgpu_counts_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t*
 extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_bytes, const int64_t* key_offsets,
                                 const int64_t* counts_in) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (c->comm) return fail(LDGPU_EINVAL, "the count table is merged (ldgpu_counts_merge): it takes no more counts");
     if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
     if (n == 0) return ok();
     if (!key_bytes || !key_offsets || !counts_in) return fail(LDGPU_EINVAL, "NULL argument");
@@ -1431,7 +1619,7 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     if (e == hipSuccess)
         e = hipMemcpyAsync(d_c, counts_in, (size_t)n * c->L * sizeof(int64_t), hipMemcpyHostToDevice, c->ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream);
-    if (e == hipSuccess) e = launch_counts_add(count_params(c), d_k, d_c, nullptr, n, c->ctx->stream);
+    if (e == hipSuccess) e = launch_counts_add(count_params(c), d_k, d_c, nullptr, nullptr, n, c->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
     (void)hipFree(d_k);
     if (d_c) (void)hipFree(d_c);
@@ -1469,6 +1657,7 @@ extern "C" int ldgpu_counts_export_device(ldgpu_counts* c, int64_t capacity, uin
 extern "C" int ldgpu_counts_add_device(ldgpu_counts* c, int64_t n, const uint64_t* d_keys, const int64_t* d_counts,
                                        void* stream) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (c->comm) return fail(LDGPU_EINVAL, "the count table is merged (ldgpu_counts_merge): it takes no more counts");
     if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
     if (n == 0) return ok();
     if (!d_keys || !d_counts) return fail(LDGPU_EINVAL, "device pointer is NULL");
@@ -1480,7 +1669,7 @@ extern "C" int ldgpu_counts_add_device(ldgpu_counts* c, int64_t n, const uint64_
         if (int rc = grow(c, next_pow2(4 * (c->size + n) + 16))) return rc;
     }
     HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream));
-    HIP_TRY(launch_counts_add(count_params(c), d_keys, reinterpret_cast<const unsigned long long*>(d_counts), nullptr,
+    HIP_TRY(launch_counts_add(count_params(c), d_keys, reinterpret_cast<const unsigned long long*>(d_counts), nullptr, nullptr,
                               n, c->ctx->stream));
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
     if (int rc = after_batch(c)) return rc;
@@ -1488,28 +1677,43 @@ extern "C" int ldgpu_counts_add_device(ldgpu_counts* c, int64_t n, const uint64_
 }
 
 namespace {
-// Host build of the table from the full count table (used when some language
-// has fewer than K present grams: the zero-valued fill needs every gram).
-int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
-    std::vector<uint64_t> keys;
-    std::vector<unsigned long long> cnt;
-    if (int rc = counts_pull(c, keys, cnt)) return rc;
-    const int L = c->L;
+// device scratch freed on scope exit
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() {
+        for (void* x : p)
+            if (x) (void)hipFree(x);
+    }
+    template <typename T>
+    hipError_t alloc(T** out, size_t n) {
+        void* x = nullptr;
+        hipError_t e = hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) p.push_back(x);
+        *out = (T*)x;
+        return e;
+    }
+};
+
+// filterTopGrams (LanguageDetector.scala:100-132) over a presence table --
+// keys sorted by (length, bytes), masks[n][S] -- into the cached table:
+// per language the present grams by class k ascending, then (when fewer than
+// K are present) zero-valued grams; ties by the (length, bytes) order.
+int table_from_presence(ldgpu_counts* c, const std::vector<uint64_t>& keys, const std::vector<uint64_t>& masks,
+                        int32_t K, int64_t* n_rows, int64_t* key_bytes) {
+    const int L = c->L, S = (L + 63) / 64;
     const size_t n = keys.size();
-    // presence class k_g = #languages with the gram; v_l = log(1 + [l]/k)
+    auto has = [&](size_t i, int l) { return (masks[i * S + l / 64] >> (l % 64)) & 1ull; };
     std::vector<int> kg(n, 0);
     for (size_t i = 0; i < n; ++i)
-        for (int l = 0; l < L; ++l) kg[i] += cnt[i * L + l] > 0;
+        for (int s = 0; s < S; ++s) kg[i] += __builtin_popcountll(masks[i * S + s]);
     std::vector<double> w(L + 1, 0.0);
     for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
-    // per language: count per class, then the threshold class and how many of
-    // it to take (keys are already in (length, bytes) order = the tie-break)
     std::vector<uint8_t> chosen(n, 0);
     if (K > 0) {
         std::vector<int64_t> per((size_t)L * (L + 1), 0);
         for (size_t i = 0; i < n; ++i)
             for (int l = 0; l < L; ++l)
-                if (cnt[i * L + l]) per[(size_t)l * (L + 1) + kg[i]]++;
+                if (has(i, l)) per[(size_t)l * (L + 1) + kg[i]]++;
         std::vector<int> kstar(L, L + 1);
         std::vector<int64_t> need(L, 0), absent_need(L, 0);
         for (int l = 0; l < L; ++l) {
@@ -1528,7 +1732,7 @@ int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_byt
         std::vector<int64_t> taken(L, 0), absent_taken(L, 0);
         for (size_t i = 0; i < n; ++i) {
             for (int l = 0; l < L; ++l) {
-                if (cnt[i * L + l]) {
+                if (has(i, l)) {
                     if (kg[i] < kstar[l]) {
                         chosen[i] = 1;
                     } else if (kg[i] == kstar[l] && taken[l] < need[l]) {
@@ -1543,16 +1747,12 @@ int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_byt
         }
     }
     std::vector<uint64_t> out_keys;
-    const int S = (L + 63) / 64;
     c->tbl_masks.clear();
     c->tbl_vals.clear();
     for (size_t i = 0; i < n; ++i) {
         if (!chosen[i]) continue;
         out_keys.push_back(keys[i]);
-        c->tbl_masks.resize(c->tbl_masks.size() + S, 0);
-        uint64_t* mk = &c->tbl_masks[c->tbl_masks.size() - S];
-        for (int l = 0; l < L; ++l)
-            if (cnt[i * L + l]) mk[l / 64] |= 1ull << (l % 64);
+        c->tbl_masks.insert(c->tbl_masks.end(), masks.begin() + i * S, masks.begin() + (i + 1) * S);
         c->tbl_vals.push_back(w[kg[i]]);
     }
     int64_t nb = 0;
@@ -1566,30 +1766,244 @@ int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_byt
     return LDGPU_OK;
 }
 
+// Host build from the full count table (used when some language has fewer
+// than K present grams: the zero-valued fill needs every gram).
+int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
+    std::vector<uint64_t> keys;
+    std::vector<unsigned long long> cnt;
+    if (int rc = counts_pull(c, keys, cnt)) return rc;
+    const int L = c->L, S = (L + 63) / 64;
+    std::vector<uint64_t> masks(keys.size() * S, 0);
+    for (size_t i = 0; i < keys.size(); ++i)
+        for (int l = 0; l < L; ++l)
+            if (cnt[i * L + l]) masks[i * S + l / 64] |= 1ull << (l % 64);
+    return table_from_presence(c, keys, masks, K, n_rows, key_bytes);
+}
+}  // namespace
 
-// Device build (SURVEY §8f "next" #3): presence masks, k and the
-// (language, k) histogram on the device; the host picks each language's
-// threshold class; the device flags the grams below it and emits the
-// threshold-class candidates; the host resolves their (length, bytes) order.
-// Only the chosen grams (<= L*K) and the candidates cross PCIe.
-struct DevBufs {
-    std::vector<void*> p;
-    ~DevBufs() {
-        for (void* x : p)
-            if (x) (void)hipFree(x);
-    }
-    template <typename T>
-    hipError_t alloc(T** out, size_t n) {
-        void* x = nullptr;
-        hipError_t e = hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T));
-        if (e == hipSuccess) p.push_back(x);
-        *out = (T*)x;
-        return e;
-    }
+// ------------------------------------------------------------ communicators
+struct ldgpu_comm {
+    ldgpu_ctx* ctx = nullptr;
+    int rank = 0, world = 1;
+    ncclComm_t nccl = nullptr;   // RCCL transport, else the host callbacks
+    ldgpu_host_coll host{};
 };
 
+#define NCCL_TRY(expr)                                                                             \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess) return fail(LDGPU_EDEVICE, "%s: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
+namespace {
+// all-gather of `bytes` host bytes per rank into out[world * bytes]
+int comm_allgather_host(ldgpu_comm* m, const void* send, int64_t bytes, void* out) {
+    if (m->world == 1) {
+        if (bytes) memcpy(out, send, (size_t)bytes);
+        return LDGPU_OK;
+    }
+    if (!m->nccl) {
+        if (m->host.allgather(m->host.user, send, bytes, out)) return fail(LDGPU_EDEVICE, "host all-gather failed");
+        return LDGPU_OK;
+    }
+    hipStream_t st = m->ctx->stream;
+    DevBufs db;
+    uint8_t *d_s, *d_r;
+    HIP_TRY(db.alloc(&d_s, (size_t)bytes));
+    HIP_TRY(db.alloc(&d_r, (size_t)bytes * m->world));
+    HIP_TRY(hipMemcpyAsync(d_s, send, (size_t)bytes, hipMemcpyHostToDevice, st));
+    NCCL_TRY(ncclAllGather(d_s, d_r, (size_t)bytes, ncclUint8, m->nccl, st));
+    HIP_TRY(hipMemcpyAsync(out, d_r, (size_t)bytes * m->world, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return LDGPU_OK;
+}
+
+// variable-size all-gather of host blobs (sizes first, then padded blobs)
+int comm_allgatherv_host(ldgpu_comm* m, const std::vector<uint8_t>& mine, std::vector<std::vector<uint8_t>>& all) {
+    const int W = m->world;
+    int64_t n = (int64_t)mine.size();
+    std::vector<int64_t> ns(W);
+    if (int rc = comm_allgather_host(m, &n, sizeof n, ns.data())) return rc;
+    const int64_t mx = std::max<int64_t>(1, *std::max_element(ns.begin(), ns.end()));
+    std::vector<uint8_t> pad((size_t)mx, 0), buf((size_t)mx * W);
+    if (n) memcpy(pad.data(), mine.data(), (size_t)n);
+    if (int rc = comm_allgather_host(m, pad.data(), mx, buf.data())) return rc;
+    all.assign(W, {});
+    for (int r = 0; r < W; ++r) all[r].assign(buf.begin() + (size_t)r * mx, buf.begin() + (size_t)r * mx + ns[r]);
+    return LDGPU_OK;
+}
+
+// all-to-all of device buffers: block r of d_send (sb[r] bytes) goes to rank
+// r, block r of d_recv (rb[r] bytes) comes from rank r
+int comm_alltoallv_dev(ldgpu_comm* m, const uint8_t* d_send, const std::vector<int64_t>& sb, uint8_t* d_recv,
+                       const std::vector<int64_t>& rb) {
+    const int W = m->world;
+    hipStream_t st = m->ctx->stream;
+    std::vector<int64_t> os(W + 1, 0), orr(W + 1, 0);
+    for (int r = 0; r < W; ++r) {
+        os[r + 1] = os[r] + sb[r];
+        orr[r + 1] = orr[r] + rb[r];
+    }
+    if (m->nccl) {
+        NCCL_TRY(ncclGroupStart());
+        for (int r = 0; r < W; ++r) {
+            if (sb[r]) NCCL_TRY(ncclSend(d_send + os[r], (size_t)sb[r], ncclUint8, r, m->nccl, st));
+            if (rb[r]) NCCL_TRY(ncclRecv(d_recv + orr[r], (size_t)rb[r], ncclUint8, r, m->nccl, st));
+        }
+        NCCL_TRY(ncclGroupEnd());
+        HIP_TRY(hipStreamSynchronize(st));
+        return LDGPU_OK;
+    }
+    std::vector<uint8_t> hs((size_t)std::max<int64_t>(os[W], 1)), hr((size_t)std::max<int64_t>(orr[W], 1));
+    if (os[W]) HIP_TRY(hipMemcpyAsync(hs.data(), d_send, (size_t)os[W], hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (W == 1) {
+        hr = hs;
+    } else if (m->host.alltoallv(m->host.user, hs.data(), sb.data(), hr.data(), rb.data())) {
+        return fail(LDGPU_EDEVICE, "host all-to-all failed");
+    }
+    if (orr[W]) HIP_TRY(hipMemcpyAsync(d_recv, hr.data(), (size_t)orr[W], hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return LDGPU_OK;
+}
+
+template <typename T>
+void put(std::vector<uint8_t>& b, const T* p, size_t n) {
+    const uint8_t* q = reinterpret_cast<const uint8_t*>(p);
+    b.insert(b.end(), q, q + n * sizeof(T));
+}
+}  // namespace
+
+extern "C" int ldgpu_comm_unique_id(uint8_t* out_id) {
+    if (!out_id) return fail(LDGPU_EINVAL, "out_id is NULL");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    memcpy(out_id, &id, LDGPU_COMM_ID_BYTES);
+    return ok();
+}
+
+extern "C" int ldgpu_comm_create_rccl(ldgpu_ctx* ctx, const uint8_t* id, int32_t rank, int32_t world,
+                                      ldgpu_comm** out) {
+    if (!ctx || !id || !out) return fail(LDGPU_EINVAL, "NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return fail(LDGPU_EINVAL, "rank %d outside world %d", rank, world);
+    HIP_TRY(hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, LDGPU_COMM_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    NCCL_TRY(ncclCommInitRank(&comm, world, uid, rank));
+    auto* m = new ldgpu_comm();
+    m->ctx = ctx;
+    m->rank = rank;
+    m->world = world;
+    m->nccl = comm;
+    *out = m;
+    return ok();
+}
+
+extern "C" int ldgpu_comm_create_host(ldgpu_ctx* ctx, int32_t rank, int32_t world, const ldgpu_host_coll* coll,
+                                      ldgpu_comm** out) {
+    if (!ctx || !coll || !out) return fail(LDGPU_EINVAL, "NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return fail(LDGPU_EINVAL, "rank %d outside world %d", rank, world);
+    if (world > 1 && (!coll->allgather || !coll->alltoallv)) return fail(LDGPU_EINVAL, "host collectives are NULL");
+    auto* m = new ldgpu_comm();
+    m->ctx = ctx;
+    m->rank = rank;
+    m->world = world;
+    m->host = *coll;
+    *out = m;
+    return ok();
+}
+
+extern "C" int ldgpu_comm_destroy(ldgpu_comm* m) {
+    if (!m) return ok();
+    if (m->nccl) (void)ncclCommDestroy(m->nccl);
+    delete m;
+    return ok();
+}
+
+// Owner exchange: every rank partitions its table by owner, one
+// all-to-all moves each rank's keys and count rows to their owners, and each
+// rank rebuilds its table from what it received: the global counts of the
+// grams it owns (integer sums: bit-exact in any order).
+extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
+    if (!c || !m) return fail(LDGPU_EINVAL, "NULL argument");
+    if (c->comm) return fail(LDGPU_EINVAL, "the count table is already merged");
+    if (m->ctx != c->ctx) return fail(LDGPU_EINVAL, "communicator and count table belong to different contexts");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    const int W = m->world, L = c->L;
+    hipStream_t st = c->ctx->stream;
+    const int64_t n = (int64_t)c->size;
+    DevBufs db;
+    unsigned long long *d_nof, *d_cur, *d_rows, *d_rrows;
+    uint64_t *d_keys, *d_rkeys;
+    HIP_TRY(db.alloc(&d_nof, W));
+    HIP_TRY(db.alloc(&d_cur, W));
+    HIP_TRY(db.alloc(&d_keys, n));
+    HIP_TRY(db.alloc(&d_rows, (size_t)n * L));
+    HIP_TRY(hipMemsetAsync(d_nof, 0, sizeof(unsigned long long) * W, st));
+    HIP_TRY(launch_owner_count(count_params(c), c->cap, (uint32_t)W, d_nof, st));
+    std::vector<unsigned long long> nof(W), cur(W);
+    HIP_TRY(hipMemcpyAsync(nof.data(), d_nof, sizeof(unsigned long long) * W, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int64_t> send_n(W);
+    unsigned long long acc = 0;
+    for (int r = 0; r < W; ++r) {
+        cur[r] = acc;
+        acc += nof[r];
+        send_n[r] = (int64_t)nof[r];
+    }
+    if ((int64_t)acc != n) return fail(LDGPU_EDEVICE, "merge: %llu grams partitioned, %lld held", acc, (long long)n);
+    HIP_TRY(hipMemcpyAsync(d_cur, cur.data(), sizeof(unsigned long long) * W, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_owner_scatter(count_params(c), c->cap, (uint32_t)W, d_cur, d_keys, d_rows, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int64_t> all((size_t)W * W);
+    if (int rc = comm_allgather_host(m, send_n.data(), sizeof(int64_t) * W, all.data())) return rc;
+    std::vector<int64_t> recv_n(W);
+    int64_t R = 0;
+    for (int r = 0; r < W; ++r) R += recv_n[r] = all[(size_t)r * W + m->rank];
+    HIP_TRY(db.alloc(&d_rkeys, R));
+    HIP_TRY(db.alloc(&d_rrows, (size_t)R * L));
+    std::vector<int64_t> sb(W), rb(W);
+    for (int r = 0; r < W; ++r) {
+        sb[r] = send_n[r] * 8;
+        rb[r] = recv_n[r] * 8;
+    }
+    if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_keys, sb, (uint8_t*)d_rkeys, rb)) return rc;
+    for (int r = 0; r < W; ++r) {
+        sb[r] *= L;
+        rb[r] *= L;
+    }
+    if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_rows, sb, (uint8_t*)d_rrows, rb)) return rc;
+    // the owned shard, rebuilt: the same key arrives from several ranks
+    (void)hipFree(c->d_keys);
+    (void)hipFree(c->d_counts);
+    c->d_keys = nullptr;
+    c->d_counts = nullptr;
+    c->cap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
+    if (int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts)) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+    c->size = 0;
+    HIP_TRY(launch_counts_add(count_params(c), d_rkeys, d_rrows, nullptr, nullptr, R, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = after_batch(c)) return rc;
+    c->comm = m;
+    c->tbl_valid = false;
+    return ok();
+}
+
+namespace {
+// Device build (SURVEY §8f "next" #3): presence masks, k and the (language,
+// k) histogram on the device; the host picks each language's threshold
+// class; the device flags the grams below it and resolves the threshold
+// class's (length, bytes) ties.  Only the chosen grams (<= L*K) cross PCIe.
+// On a merged table (c->comm) the histogram is summed over the ranks, the
+// ties are resolved against the ranks' candidate prefixes, and the chosen
+// rows of every rank are gathered: every rank builds the same global table.
 int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes, bool* fallback) {
     *fallback = false;
+    ldgpu_comm* cm = c->comm;
     const int L = c->L, S = (L + 63) / 64;
     const int64_t n = (int64_t)c->size;
     hipStream_t st = c->ctx->stream;
@@ -1612,25 +2026,63 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if ((int64_t)got != n) return fail(LDGPU_EDEVICE, "presence: %llu grams, %lld expected", got, (long long)n);
+    std::vector<int64_t> ghist(hist.begin(), hist.end());  // global (summed over ranks)
+    if (cm && cm->world > 1) {
+        std::vector<int64_t> mine(ghist), allh(ghist.size() * cm->world);
+        if (int rc = comm_allgather_host(cm, mine.data(), (int64_t)(sizeof(int64_t) * mine.size()), allh.data()))
+            return rc;
+        for (size_t i = 0; i < ghist.size(); ++i) {
+            ghist[i] = 0;
+            for (int r = 0; r < cm->world; ++r) ghist[i] += allh[(size_t)r * ghist.size() + i];
+        }
+    }
 
     std::vector<int32_t> kstar(L, L + 1), need(L, 0);
-    uint64_t cand_cap = 0;
+    uint64_t cand_cap = 0;  // this rank's candidates
     for (int l = 0; l < L; ++l) {
         int64_t acc = 0;
         for (int k = 1; k <= L; ++k) {
-            const int64_t ck = hist[(size_t)l * (L + 1) + k];
+            const int64_t ck = ghist[(size_t)l * (L + 1) + k];
             if (acc + ck >= K) {
                 kstar[l] = k;
                 need[l] = (int32_t)(K - acc);
-                if (need[l] > 0) cand_cap += (uint64_t)ck;
+                if (need[l] > 0) cand_cap += (uint64_t)hist[(size_t)l * (L + 1) + k];
                 break;
             }
             acc += ck;
         }
-        if (kstar[l] == L + 1 && acc < K) {
-            *fallback = true;  // zero-valued fill needed: every gram takes part
-            return LDGPU_OK;
+        if (kstar[l] == L + 1 && acc < K) *fallback = true;  // zero-valued fill: every gram takes part
+    }
+    if (*fallback) {
+        if (!cm) return LDGPU_OK;  // the host build from the count table
+        // merged table: gather every rank's presence rows, select on the host
+        std::vector<uint64_t> hk(n), hm((size_t)n * S);
+        if (n) {
+            HIP_TRY(hipMemcpyAsync(hk.data(), d_keys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(hm.data(), d_masks, sizeof(uint64_t) * n * S, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
         }
+        std::vector<uint8_t> blob;
+        put(blob, hk.data(), hk.size());
+        put(blob, hm.data(), hm.size());
+        std::vector<std::vector<uint8_t>> all;
+        if (int rc = comm_allgatherv_host(cm, blob, all)) return rc;
+        std::vector<std::pair<uint64_t, std::pair<int, size_t>>> order;
+        std::vector<const uint64_t*> rk(cm->world), rm(cm->world);
+        for (int r = 0; r < cm->world; ++r) {
+            const size_t nr = all[r].size() / (8 * (1 + S));
+            rk[r] = reinterpret_cast<const uint64_t*>(all[r].data());
+            rm[r] = rk[r] + nr;
+            for (size_t i = 0; i < nr; ++i) order.push_back({sort_key(rk[r][i]), {r, i}});
+        }
+        std::sort(order.begin(), order.end());
+        std::vector<uint64_t> keys(order.size()), masks(order.size() * S);
+        for (size_t j = 0; j < order.size(); ++j) {
+            keys[j] = rk[order[j].second.first][order[j].second.second];
+            memcpy(&masks[j * S], rm[order[j].second.first] + order[j].second.second * S, 8 * S);
+        }
+        *fallback = false;
+        return table_from_presence(c, keys, masks, K, n_rows, key_bytes);
     }
     int32_t *d_kstar, *d_need, *d_cl;
     uint8_t* d_chosen;
@@ -1654,7 +2106,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     if (cn != cand_cap) return fail(LDGPU_EDEVICE, "select: %u candidates, %llu expected", cn,
                                     (unsigned long long)cand_cap);
     // per language: the need[l] smallest (length, bytes) keys of its threshold
-    // class, picked on the device (candidates of language l form segment l)
+    // class (candidates of language l form segment l once sorted)
     std::vector<int64_t> seg(L + 1, 0);
     for (int l = 0; l < L; ++l)
         seg[l + 1] = seg[l] + (need[l] > 0 && kstar[l] <= L ? (int64_t)hist[(size_t)l * (L + 1) + kstar[l]] : 0);
@@ -1663,7 +2115,54 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     int64_t* d_seg;
     HIP_TRY(db.alloc(&d_seg, L + 1));
     HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), sizeof(int64_t) * (L + 1), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_topk_candidates((int64_t)cn, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, st));
+    if (!cm || cm->world == 1) {
+        HIP_TRY(launch_topk_candidates((int64_t)cn, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, nullptr, st));
+    } else {
+        // each rank's need[l] smallest candidates can hold the global ones:
+        // gather those prefixes, the need[l]-th smallest key of language l is
+        // its threshold, and every rank takes its candidates at or below it
+        uint64_t *d_sk, *d_thr;
+        HIP_TRY(db.alloc(&d_sk, cn));
+        HIP_TRY(db.alloc(&d_thr, L));
+        HIP_TRY(launch_topk_candidates((int64_t)cn, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, d_sk, st));
+        std::vector<int64_t> take(L, 0);
+        int64_t tot = 0;
+        for (int l = 0; l < L; ++l) tot += take[l] = std::min<int64_t>(need[l], seg[l + 1] - seg[l]);
+        std::vector<uint64_t> pre((size_t)std::max<int64_t>(tot, 1));
+        int64_t at = 0;
+        for (int l = 0; l < L; ++l) {
+            if (take[l])
+                HIP_TRY(hipMemcpyAsync(pre.data() + at, d_sk + seg[l], sizeof(uint64_t) * take[l],
+                                       hipMemcpyDeviceToHost, st));
+            at += take[l];
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<uint8_t> blob;
+        put(blob, take.data(), take.size());
+        put(blob, pre.data(), (size_t)tot);
+        std::vector<std::vector<uint8_t>> all;
+        if (int rc = comm_allgatherv_host(cm, blob, all)) return rc;
+        std::vector<std::vector<uint64_t>> per(L);
+        for (int r = 0; r < cm->world; ++r) {
+            const int64_t* tk = reinterpret_cast<const int64_t*>(all[r].data());
+            const uint64_t* ks = reinterpret_cast<const uint64_t*>(tk + L);
+            for (int l = 0; l < L; ++l) {
+                per[l].insert(per[l].end(), ks, ks + tk[l]);
+                ks += tk[l];
+            }
+        }
+        std::vector<uint64_t> thr(L, 0);
+        for (int l = 0; l < L; ++l) {
+            if (need[l] <= 0) continue;
+            if ((int64_t)per[l].size() < need[l])
+                return fail(LDGPU_EDEVICE, "top-K: %zu candidates of language %d, %d needed", per[l].size(), l,
+                            need[l]);
+            std::nth_element(per[l].begin(), per[l].begin() + (need[l] - 1), per[l].end());
+            thr[l] = per[l][need[l] - 1];
+        }
+        HIP_TRY(hipMemcpyAsync(d_thr, thr.data(), sizeof(uint64_t) * L, hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_mark_threshold((int64_t)cn, d_cl, d_ck, d_ci, d_thr, d_chosen, st));
+    }
     const int64_t cap_out = std::min<int64_t>(n, (int64_t)L * std::max<int32_t>(K, 0));
     uint64_t *d_ok, *d_om;
     int32_t* d_okk;
@@ -1684,6 +2183,27 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         HIP_TRY(hipMemcpyAsync(om.data(), d_om, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(okk.data(), d_okk, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (cm && cm->world > 1) {  // every rank's chosen rows
+        std::vector<uint8_t> blob;
+        put(blob, ok.data(), ok.size());
+        put(blob, om.data(), om.size());
+        put(blob, okk.data(), okk.size());
+        std::vector<std::vector<uint8_t>> all;
+        if (int rc = comm_allgatherv_host(cm, blob, all)) return rc;
+        ok.clear();
+        om.clear();
+        okk.clear();
+        for (int r = 0; r < cm->world; ++r) {
+            const size_t nr = all[r].size() / (8 + 8 * S + 4);
+            const uint64_t* k = reinterpret_cast<const uint64_t*>(all[r].data());
+            const uint64_t* mk = k + nr;
+            const int32_t* kk = reinterpret_cast<const int32_t*>(mk + nr * S);
+            ok.insert(ok.end(), k, k + nr);
+            om.insert(om.end(), mk, mk + nr * S);
+            okk.insert(okk.end(), kk, kk + nr);
+        }
+        m = ok.size();
     }
     std::vector<double> w(L + 1, 0.0);
     for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
@@ -1712,12 +2232,25 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
 }  // namespace
 
 // computeProbabilities + filterTopGrams (LanguageDetector.scala:75-132).
+// On a merged table: collective (every rank of the communicator calls it).
 extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    if (K <= 0 || c->size == 0) {
+    // a merged table takes the device path on every rank (its collectives
+    // must match), even for K <= 0 or an empty shard
+    if (!c->comm && (K <= 0 || c->size == 0)) {
         if (int rc = fit_table_host(c, K, n_rows, key_bytes)) return rc;
+        return ok();
+    }
+    if (K <= 0) {
+        c->tbl_masks.clear();
+        c->tbl_vals.clear();
+        c->tbl_bytes.assign(1, 0);
+        c->tbl_off.assign(1, 0);
+        c->tbl_valid = true;
+        if (n_rows) *n_rows = 0;
+        if (key_bytes) *key_bytes = 0;
         return ok();
     }
     bool fallback = false;

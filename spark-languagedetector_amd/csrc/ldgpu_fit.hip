@@ -35,7 +35,7 @@ __device__ __forceinline__ uint32_t ld_dw(const uint32_t* w, int64_t i, int64_t 
 }
 
 // find-or-insert; returns the slot or -1 when the probe limit is reached
-__device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key) {
+__device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key, bool& new_key) {
     uint64_t s = mix64(key) >> p.shift;
     for (int probe = 0; probe < kMaxProbe; ++probe) {
         uint64_t k = __hip_atomic_load(&p.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -44,7 +44,7 @@ __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t
             const unsigned long long old =
                 atomicCAS(reinterpret_cast<unsigned long long*>(&p.keys[s]), 0ull, (unsigned long long)key);
             if (old == 0ull) {
-                atomicAdd(p.size, 1ull);
+                new_key = true;
                 return (int64_t)s;
             }
             if (old == key) return (int64_t)s;
@@ -52,6 +52,13 @@ __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t
         s = (s + 1) & p.mask;
     }
     return -1;
+}
+
+// the table's distinct-key counter: one atomic per ballot of the lanes calling
+// together (a single same-address atomic per new key would serialise)
+__device__ __forceinline__ void count_new_keys(const CountParams& p, bool new_key) {
+    const uint64_t m = __ballot(new_key);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(p.size, (unsigned long long)__popcll(m));
 }
 
 // Diagnostics build only (tools/build_variant.sh ... -DLDGPU_FIT_ABLATE=n):
@@ -63,21 +70,21 @@ __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t
 
 __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
     if (LDGPU_FIT_ABLATE & 2) return;
-    const int64_t s = find_or_insert(p, key);
+    bool new_key = false;
+    const int64_t s = find_or_insert(p, key, new_key);
+    count_new_keys(p, new_key);
     if (s >= 0) {
         if (LDGPU_FIT_ABLATE & 4)  // timing probe: a 32-bit add on the counter's low word
             atomicAdd(reinterpret_cast<unsigned int*>(&p.counts[(size_t)s * p.L + lang]), (unsigned int)c);
         else if (!(LDGPU_FIT_ABLATE & 1))
             atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
     } else {
-        // overflow: one entry per unit count -- an LDS flush (1-gram
-        // histogram, 2-/3-byte hash) passes c > 1 and repeats the entry c times
-        for (unsigned long long r = 0; r < c; ++r) {
-            const unsigned int at = atomicAdd(p.ovf_n, 1u);
-            if (at < p.ovf_cap) {
-                p.ovf_keys[at] = key;
-                p.ovf_lang[at] = lang;
-            }
+        // overflow (probe limit): the host grows the table and re-adds the entry
+        const unsigned int at = atomicAdd(p.ovf_n, 1u);
+        if (at < p.ovf_cap) {
+            p.ovf_keys[at] = key;
+            p.ovf_lang[at] = lang;
+            p.ovf_cnt[at] = c;
         }
     }
 }
@@ -182,21 +189,45 @@ __global__ __launch_bounds__(kCountWaves * 64) void count_kernel(const CountPara
 }
 
 __global__ void counts_add_kernel(const CountParams p, const uint64_t* keys, const unsigned long long* rows,
-                                  const int32_t* lang_of, int64_t n) {
+                                  const int32_t* lang_of, const unsigned long long* cnt_of, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t s = find_or_insert(p, keys[i]);
+    bool new_key = false;
+    const int64_t s = find_or_insert(p, keys[i], new_key);
+    count_new_keys(p, new_key);
     if (s < 0) {
         atomicAdd(p.ovf_n, 1u);  // cannot happen after a grow; reported as table full
         return;
     }
     if (lang_of) {
-        atomicAdd(&p.counts[(size_t)s * p.L + lang_of[i]], 1ull);
+        atomicAdd(&p.counts[(size_t)s * p.L + lang_of[i]], cnt_of ? cnt_of[i] : 1ull);
     } else {
         for (int l = 0; l < p.L; ++l) {
             const unsigned long long c = rows[(size_t)i * p.L + l];
             if (c) atomicAdd(&p.counts[(size_t)s * p.L + l], c);
         }
+    }
+}
+
+// table statistics: [0] distinct (gram, language) pairs, [1] sum of counts
+__global__ void stats_kernel(const CountParams p, uint64_t cap, unsigned long long* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long pairs = 0, total = 0;
+    if (i < cap && p.keys[i] != kEmpty) {
+        for (int l = 0; l < p.L; ++l) {
+            const unsigned long long c = p.counts[i * p.L + l];
+            pairs += c != 0ull;
+            total += c;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        pairs += __shfl_xor(pairs, o);
+        total += __shfl_xor(total, o);
+    }
+    if ((threadIdx.x & 63) == 0 && (pairs | total)) {
+        atomicAdd(&out[0], pairs);
+        atomicAdd(&out[1], total);
     }
 }
 
@@ -241,10 +272,16 @@ hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream) {
 }
 
 hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const unsigned long long* rows,
-                             const int32_t* lang_of, int64_t n, hipStream_t stream) {
+                             const int32_t* lang_of, const unsigned long long* cnt_of, int64_t n,
+                             hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(counts_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, p, keys, rows,
-                       lang_of, n);
+                       lang_of, cnt_of, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_stats(const CountParams& p, uint64_t cap, unsigned long long* out, hipStream_t stream) {
+    hipLaunchKernelGGL(stats_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out);
     return hipGetLastError();
 }
 
@@ -401,7 +438,61 @@ __global__ void cand_mark_kernel(int64_t n, const uint32_t* lang_sorted, const u
     if (i - seg_start[l] < (int64_t)need[l]) chosen[cand_idx[perm[i]]] = 1;
 }
 
+// ---- multi-GPU merge: owner partition of the table (ldgpu_counts_merge)
+__device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
+    return (uint32_t)(((mix64(key) & 0xffffffffull) * world) >> 32);
+}
+
+__global__ void owner_count_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* n_of) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap && p.keys[i] != kEmpty) atomicAdd(&n_of[owner_of(p.keys[i], world)], 1ull);
+}
+
+__global__ void owner_scatter_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                     uint64_t* out_keys, unsigned long long* out_rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || p.keys[i] == kEmpty) return;
+    const uint64_t key = p.keys[i];
+    const unsigned long long o = atomicAdd(&cursor[owner_of(key, world)], 1ull);
+    out_keys[o] = key;
+    for (int l = 0; l < p.L; ++l) out_rows[o * p.L + l] = p.counts[i * p.L + l];
+}
+
+// distributed top-K: a candidate is chosen when its (length, bytes) sort key
+// is at most its language's global threshold
+__global__ void mark_threshold_kernel(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key,
+                                      const uint32_t* cand_idx, const uint64_t* thr, uint8_t* chosen) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && cand_key[i] <= thr[cand_lang[i]]) chosen[cand_idx[i]] = 1;
+}
+
+__global__ void gather_u64_kernel(int64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
 }  // namespace
+
+hipError_t launch_owner_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL(owner_count_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap, world, n_of);
+    return hipGetLastError();
+}
+
+hipError_t launch_owner_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                uint64_t* out_keys, unsigned long long* out_rows, hipStream_t stream) {
+    hipLaunchKernelGGL(owner_scatter_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap, world,
+                       cursor, out_keys, out_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_mark_threshold(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key,
+                                 const uint32_t* cand_idx, const uint64_t* thr, uint8_t* chosen, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mark_threshold_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, cand_lang, cand_key,
+                       cand_idx, thr, chosen);
+    return hipGetLastError();
+}
 
 hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
                            int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream) {
@@ -428,7 +519,7 @@ hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const ui
 // picked on the host.  Synchronises `stream` before returning (scratch freed).
 hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const uint64_t* cand_key,
                                   const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
-                                  uint8_t* chosen, hipStream_t stream) {
+                                  uint8_t* chosen, uint64_t* sorted_keys, hipStream_t stream) {
     if (cn <= 0) return hipSuccess;
     const int n = (int)cn;
     uint64_t* key_out = nullptr;
@@ -458,7 +549,11 @@ hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const ui
     }
     if (e == hipSuccess)
         e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, 8, stream);
-    if (e == hipSuccess) {
+    if (e == hipSuccess && sorted_keys) {  // distributed: each language's sorted candidate keys, no marking
+        hipLaunchKernelGGL(gather_u64_kernel, dim3(grid_of(cn, 256)), dim3(256), 0, stream, cn, perm_a, cand_key,
+                           sorted_keys);
+        e = hipGetLastError();
+    } else if (e == hipSuccess) {
         hipLaunchKernelGGL(cand_mark_kernel, dim3(grid_of(cn, 256)), dim3(256), 0, stream, cn, lang_b, perm_a,
                            seg_start, need, cand_idx, chosen);
         e = hipGetLastError();
@@ -482,6 +577,579 @@ hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const u
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(gather_chosen_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, S, chosen, keys, masks,
                        ks, out_keys, out_masks, out_k, out_n);
+    return hipGetLastError();
+}
+
+}  // namespace ldgpu
+
+// ---------------------------------------------------------------------------
+// FIT v2: radix-partitioned record aggregation -- the north star's "LDS-
+// privatised histogram, then a sort / segmented-reduce merge into HBM count
+// tables", built so that the global table sees ONE add per distinct
+// (gram, language) per batch instead of one device-scope atomic per window
+// (which bounded the single-pass count_kernel above: ~2.7e9 random atomics
+// per GiB).  Per batch of documents:
+//   emit    one wave per document: 1-byte windows into a per-wave LDS
+//           histogram, 2-/3-byte windows into a per-wave LDS hash (both
+//           flushed per document / gram length as counted records), longer
+//           windows straight to records.  Records gather in a workgroup LDS
+//           block; a full block is counting-sorted by q1 in LDS and written
+//           once, coalesced, into the workgroup's own region with a header
+//           of q1 starts.  The workgroup also histograms (q1, q2).
+//   part2   bucket q1 of one emit group: the group's q1 runs (load-balanced
+//           over a wave) are re-scattered by q2 to exact, host-scanned
+//           offsets -- 4096 contiguous buckets (q1, q2).
+//   reduce  one workgroup per bucket: an LDS hash (kAggSlots entries) sums
+//           the counts of equal (gram, language) records; distinct entries
+//           go out as (kl, count).
+//   merge   each entry is one find-or-insert + one u64 add in the table.
+// Integer sums are order-independent: counts stay bit-exact.
+namespace ldgpu {
+namespace {
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t make_rec(uint64_t bytes, int klen, uint32_t lang, uint64_t c, uint32_t lb,
+                                             uint32_t cb) {
+    const uint64_t sent = (1ull << (8 * klen)) | bytes;
+    return (((sent << lb) | (uint64_t)lang) << cb) | c;
+}
+
+// the packed gram key (ldgpu_common.h) of a record's kl = record >> cb
+__device__ __forceinline__ uint64_t kl_key(uint64_t kl, uint32_t lb) {
+    const uint64_t sent = kl >> lb;
+    const int klen = (63 - __builtin_clzll(sent)) >> 3;
+    return (sent ^ (1ull << (8 * klen))) | ((uint64_t)klen << 56);
+}
+
+__device__ __forceinline__ uint32_t q1_of(uint64_t r, uint32_t cb) { return (uint32_t)(mix64(r >> cb) >> (64 - kQBits)); }
+__device__ __forceinline__ uint32_t q2_of(uint64_t r, uint32_t cb) {
+    return (uint32_t)(mix64(r >> cb) >> (64 - 2 * kQBits)) & (kQ - 1);
+}
+
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations
+// (lgkmcnt), not for its outstanding global loads -- __syncthreads() would
+// drain those too, and emit keeps the next step's window loads in flight
+// across the round barriers.  Global stores before it need not be visible to
+// the other waves (each flushed block is read by the next kernel only).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// wave inclusive scan (64 lanes)
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+struct EmitLds {
+    uint64_t blk[kBlkRecs];
+    uint32_t hist2[kQ * kQ];
+    uint32_t h1[kEmitWaves][256];
+    uint32_t k2[kEmitWaves][kH2];
+    uint32_t c2[kEmitWaves][kH2];
+    uint32_t pcnt[kQ];
+    uint32_t pfill[kQ];
+    uint32_t pstart[kQ + 1];
+    uint32_t blk_n;
+    uint32_t active;
+    uint32_t next_doc;
+};
+
+enum { kNextDoc = 0, kWin = 1, kHFlush = 2, kH1Flush = 3, kDone = 4 };
+
+// one wave's position in its current document (wave-uniform)
+struct WaveState {
+    int64_t b, len, p0;
+    int32_t lang, gi, phase, cursor;
+    uint32_t used1;
+    bool pf;                     // pw holds the words of the next WIN step (issued a round early)
+    uint32_t pw[4][3];
+};
+
+// append the lanes' records (kSub per lane) to the workgroup block with one
+// reservation (the round bound keeps it from overflowing); every lane of the
+// wave must be active
+constexpr int kSubW = 4;  // window positions (or flushed slots) per lane per step
+
+__device__ __forceinline__ void emit_recs(EmitLds& S, const bool (&has)[kSubW], const uint64_t (&r)[kSubW],
+                                          int lane) {
+    uint64_t m[kSubW];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSubW; ++k) {
+        m[k] = __ballot(has[k]);
+        tot += (uint32_t)__popcll(m[k]);
+    }
+    if (!tot) return;
+    uint32_t base = 0;
+    if (lane == 0) base = __hip_atomic_fetch_add(&S.blk_n, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __shfl(base, 0);
+#pragma unroll
+    for (int k = 0; k < kSubW; ++k) {
+        if (has[k]) S.blk[base + lane_rank(m[k])] = r[k];
+        base += (uint32_t)__popcll(m[k]);
+    }
+}
+
+__device__ __forceinline__ void next_gram(const PartParams& p, WaveState& w) {
+    w.gi += 1;
+    w.p0 = 0;
+    w.cursor = 0;
+    w.phase = w.gi < p.nG ? kWin : (w.used1 ? kH1Flush : kNextDoc);
+}
+
+// the dwords of the kSubW positions of a WIN step at (gi, p0)
+__device__ __forceinline__ void window_loads(const PartParams& p, const WaveState& w, int lane,
+                                             uint32_t (&pw)[4][3]) {
+    const int n = p.G[w.gi];
+    const int64_t nwin = n_windows(w.len, n);
+    const int klen = w.len < n ? (int)w.len : n;
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+#pragma unroll
+    for (int k = 0; k < kSubW; ++k) {
+        const int64_t pos = w.p0 + 64 * k + lane;
+        const int64_t a = w.b + (pos < nwin ? pos : 0);
+        const int64_t i = a >> 2;
+        pw[k][0] = ld_dw(W, i, p.last_dword);
+        pw[k][1] = ld_dw(W, i + 1, p.last_dword);
+        pw[k][2] = klen > 4 ? ld_dw(W, i + 2, p.last_dword) : 0u;
+    }
+}
+
+// One step of a wave: <= 64 kSubW windows or flushed slots, <= 64 kSubW
+// records.  The positions' loads are all issued before any is used.
+__device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveState& w, int wave, int lane,
+                                          int64_t d0, int64_t d1) {
+    const uint64_t cmax = p.cb >= 32 ? 0xffffffffull : ((1ull << p.cb) - 1ull);
+    uint32_t* h1 = S.h1[wave];
+    uint32_t* k2 = S.k2[wave];
+    uint32_t* c2 = S.c2[wave];
+    if (w.phase == kNextDoc) {
+        uint32_t k = 0;
+        if (lane == 0) k = __hip_atomic_fetch_add(&S.next_doc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int64_t d = d0 + (int64_t)__shfl(k, 0);
+        if (d >= d1) {
+            w.phase = kDone;
+            if (lane == 0) __hip_atomic_fetch_sub(&S.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+        const int lang = p.doc_lang[d];
+        if (lang < 0 || lang >= p.L) return;  // reduceGrams keeps supported languages only
+        const int64_t b = p.offsets[d];
+        const int64_t len = p.offsets[d + 1] - b;
+        if (len <= 0 || p.nG == 0) return;
+        w.b = b;
+        w.len = len;
+        w.lang = lang;
+        w.gi = 0;
+        w.p0 = 0;
+        w.cursor = 0;
+        w.used1 = 0;
+        w.pf = false;
+        w.phase = kWin;
+        // fall through: the document's first windows in this step
+    }
+    bool has[kSubW];
+    uint64_t r[kSubW];
+#pragma unroll
+    for (int k = 0; k < kSubW; ++k) {
+        has[k] = false;
+        r[k] = 0;
+    }
+    if (w.phase == kWin) {
+        const int n = p.G[w.gi];
+        const int64_t nwin = n_windows(w.len, n);
+        const int klen = w.len < n ? (int)w.len : n;
+        const uint32_t lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
+        const uint32_t himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
+        uint32_t lo[kSubW], hi[kSubW];
+        bool valid[kSubW];
+        if (!w.pf) window_loads(p, w, lane, w.pw);
+        w.pf = false;
+#pragma unroll
+        for (int k = 0; k < kSubW; ++k) {
+            const int64_t pos = w.p0 + 64 * k + lane;
+            valid[k] = pos < nwin;
+            const uint32_t sh = (uint32_t)((w.b + (valid[k] ? pos : 0)) & 3);
+            lo[k] = __builtin_amdgcn_alignbyte(w.pw[k][1], w.pw[k][0], sh) & lomask;
+            hi[k] = __builtin_amdgcn_alignbyte(w.pw[k][2], w.pw[k][1], sh) & himask;
+        }
+        if (klen == 1) {
+#pragma unroll
+            for (int k = 0; k < kSubW; ++k)
+                if (valid[k]) __hip_atomic_fetch_add(&h1[lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            w.used1 = 1;
+        } else if (klen <= 3) {
+#pragma unroll
+            for (int k = 0; k < kSubW; ++k) {
+                if (!valid[k]) continue;
+                const uint32_t tag = lo[k] | ((uint32_t)klen << 24);  // never 0
+                uint32_t slot = (uint32_t)(((uint64_t)(lo[k] * 0x9E3779B1u) * kH2) >> 32);
+                bool done = false;
+                for (int t = 0; t < kH2Probe && !done; ++t) {
+                    uint32_t cur = k2[slot];  // read first: most windows find their key
+                    if (cur == 0u) {
+                        const uint32_t old = atomicCAS(&k2[slot], 0u, tag);
+                        cur = old == 0u ? tag : old;
+                    }
+                    if (cur == tag) {
+                        __hip_atomic_fetch_add(&c2[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        done = true;
+                    }
+                    slot = slot + 1u == kH2 ? 0u : slot + 1u;
+                }
+                if (!done) {
+                    has[k] = true;
+                    r[k] = make_rec(lo[k], klen, (uint32_t)w.lang, 1, p.lb, p.cb);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSubW; ++k) {
+                has[k] = valid[k];
+                r[k] = make_rec(((uint64_t)hi[k] << 32) | lo[k], klen, (uint32_t)w.lang, 1, p.lb, p.cb);
+            }
+        }
+        emit_recs(S, has, r, lane);
+        w.p0 += 64 * kSubW;
+        if (w.p0 >= nwin) {
+            __builtin_amdgcn_wave_barrier();
+            if (klen == 2 || klen == 3) {
+                w.phase = kHFlush;
+                w.cursor = 0;
+            } else {
+                next_gram(p, w);
+            }
+        }
+        if (w.phase == kWin) {  // the next step's loads fly across the round barrier
+            window_loads(p, w, lane, w.pw);
+            w.pf = true;
+        }
+        return;
+    }
+    if (w.phase == kHFlush) {  // this gram length's 2-/3-byte keys, 64 kSubW slots a step
+#pragma unroll
+        for (int k = 0; k < kSubW; ++k) {
+            const int slot = w.cursor + 64 * k + lane;
+            if (slot >= (int)kH2) continue;
+            const uint32_t tag = k2[slot];
+            if (!tag) continue;
+            const uint32_t c = c2[slot];
+            k2[slot] = 0u;
+            c2[slot] = 0u;
+            const int kl = (int)(tag >> 24);
+            const uint32_t bytes = tag & 0xffffffu;
+            if (c <= cmax) {
+                has[k] = true;
+                r[k] = make_rec(bytes, kl, (uint32_t)w.lang, c, p.lb, p.cb);
+            } else {
+                add_count(p.direct, ((uint64_t)kl << 56) | bytes, w.lang, c);
+            }
+        }
+        emit_recs(S, has, r, lane);
+        w.cursor += 64 * kSubW;
+        if (w.cursor >= (int)kH2) {
+            __builtin_amdgcn_wave_barrier();
+            next_gram(p, w);
+            if (w.phase == kWin) {
+                window_loads(p, w, lane, w.pw);
+                w.pf = true;
+            }
+        }
+        return;
+    }
+    if (w.phase == kH1Flush) {  // the document's 1-byte keys (256 bins: one step)
+#pragma unroll
+        for (int k = 0; k < kSubW; ++k) {
+            const int bin = 64 * k + lane;
+            const uint32_t c = h1[bin];
+            if (!c) continue;
+            h1[bin] = 0u;
+            if (c <= cmax) {
+                has[k] = true;
+                r[k] = make_rec((uint64_t)bin, 1, (uint32_t)w.lang, c, p.lb, p.cb);
+            } else {
+                add_count(p.direct, (1ull << 56) | (uint64_t)bin, w.lang, c);
+            }
+        }
+        emit_recs(S, has, r, lane);
+        __builtin_amdgcn_wave_barrier();
+        w.used1 = 0;
+        w.phase = kNextDoc;
+    }
+}
+
+// Write the block: counting sort by q1 in LDS, scattered stores into the
+// block's own contiguous range (the lines fill in L2 and leave whole).
+__device__ __forceinline__ void flush_block(const PartParams& p, EmitLds& S, uint32_t n, int64_t rb, int64_t gid,
+                                            int tid) {
+    for (uint32_t i = tid; i < n; i += kEmitWaves * 64) {
+        const uint64_t h = mix64(S.blk[i] >> p.cb);
+        const uint32_t q1 = (uint32_t)(h >> (64 - kQBits));
+        const uint32_t q2 = (uint32_t)(h >> (64 - 2 * kQBits)) & (kQ - 1);
+        __hip_atomic_fetch_add(&S.pcnt[q1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&S.hist2[q1 * kQ + q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    lds_barrier();
+    if (tid < 64) {
+        const uint32_t v = S.pcnt[tid];
+        const uint32_t inc = wave_inclusive_scan(v, tid);
+        S.pstart[tid] = inc - v;
+        S.pfill[tid] = inc - v;
+        S.pcnt[tid] = 0u;
+        if (tid == 63) S.pstart[kQ] = inc;
+    }
+    lds_barrier();
+    for (uint32_t i = tid; i < n; i += kEmitWaves * 64) {
+        const uint64_t r = S.blk[i];
+        const uint32_t at =
+            __hip_atomic_fetch_add(&S.pfill[q1_of(r, p.cb)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        p.rec[rb + at] = r;
+    }
+    if (tid <= kQ) p.blk_hdr[(size_t)gid * kHdr + tid] = S.pstart[tid];
+    if (tid == 0) {
+        p.blk_start[gid] = rb;
+        S.blk_n = 0u;
+    }
+    lds_barrier();
+}
+
+__global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t emit_smem[];
+    EmitLds& S = *reinterpret_cast<EmitLds*>(emit_smem);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int bid = blockIdx.x;
+    const int64_t d0 = p.wg_doc[bid], d1 = p.wg_doc[bid + 1];
+    const int64_t rbase = p.wg_rec[bid], dbase = p.wg_dir[bid];
+    for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64) S.hist2[i] = 0u;
+    for (int i = lane; i < 256; i += 64) S.h1[wave][i] = 0u;
+    for (int i = lane; i < (int)kH2; i += 64) S.k2[wave][i] = S.c2[wave][i] = 0u;
+    if (tid < kQ) S.pcnt[tid] = 0u;
+    if (tid == 0) {
+        S.blk_n = 0u;
+        S.active = kEmitWaves;
+        S.next_doc = 0u;
+    }
+    lds_barrier();
+    WaveState w{};
+    w.phase = kNextDoc;
+    int64_t written = 0;
+    int64_t nb = 0;
+    for (;;) {
+        // a round: every live wave takes one step (<= 64 kSubW records, so the
+        // block, flushed above kBlkRecs - kRoundRecs, never overflows)
+        if (w.phase != kDone) emit_step(p, S, w, wave, lane, d0, d1);
+        lds_barrier();
+        const uint32_t n = S.blk_n;
+        const uint32_t act = S.active;
+        lds_barrier();  // every thread has read n / act before the next round moves them
+        if (n > (uint32_t)(kBlkRecs - kRoundRecs) || (act == 0u && n > 0u)) {
+            flush_block(p, S, n, rbase + written, dbase + nb, tid);
+            written += n;
+            ++nb;
+        }
+        if (act == 0u) break;
+    }
+    if (tid == 0) p.nblk[bid] = (int32_t)nb;
+    const int grp = bid / (p.grid_a / kSplits);
+    for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64)
+        if (S.hist2[i]) atomicAdd(&p.cnt3[i * kSplits + grp], S.hist2[i]);
+}
+
+struct Part2Lds {
+    uint32_t cur[kQ];
+    int32_t gpre[257];
+};
+
+__device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) {
+    return (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32));
+}
+
+__global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams p) {
+    __shared__ Part2Lds S;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t q1 = blockIdx.x / kSplits;
+    const int s = blockIdx.x % kSplits;
+    const int per = p.grid_a / kSplits;
+    const int w0 = s * per;
+    if (tid == 0) {
+        int32_t acc = 0;
+        for (int k = 0; k < per; ++k) {
+            S.gpre[k] = acc;
+            acc += p.nblk[w0 + k];
+        }
+        S.gpre[per] = acc;
+    }
+    if (tid < kQ) S.cur[tid] = 0u;
+    __syncthreads();
+    const int64_t tb = S.gpre[per];
+    for (int64_t u0 = (int64_t)wave * 64; u0 < tb; u0 += kEmitWaves * 64) {
+        const int64_t u = u0 + lane;
+        int64_t start = 0;
+        uint32_t len = 0;
+        if (u < tb) {
+            int lo = 0, hi = per;  // emit workgroup of unit u: largest k with gpre[k] <= u
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (S.gpre[mid] <= u) lo = mid;
+                else hi = mid;
+            }
+            const int64_t gid = p.wg_dir[w0 + lo] + (u - S.gpre[lo]);
+            const uint32_t a = p.blk_hdr[(size_t)gid * kHdr + q1];
+            const uint32_t e = p.blk_hdr[(size_t)gid * kHdr + q1 + 1];
+            start = p.blk_start[gid] + a;
+            len = e - a;
+        }
+        // the chunk's 64 runs, kR at a time: the wave loads the runs' records
+        // cooperatively (runs average kBlkRecs / kQ records), kR loads in flight
+        constexpr int kR = 8;
+        for (int i = 0; i < 64; i += kR) {
+            int64_t st[kR];
+            uint32_t ln[kR];
+            uint32_t lm = 0;
+#pragma unroll
+            for (int k = 0; k < kR; ++k) {
+                st[k] = rdlane_i64(start, i + k);
+                ln[k] = (uint32_t)__builtin_amdgcn_readlane((int)len, i + k);
+                lm = ln[k] > lm ? ln[k] : lm;
+            }
+            for (uint32_t j = lane; j < ((lm + 63u) & ~63u); j += 64) {
+                uint64_t r[kR];
+#pragma unroll
+                for (int k = 0; k < kR; ++k) r[k] = j < ln[k] ? p.rec[st[k] + j] : 0ull;
+#pragma unroll
+                for (int k = 0; k < kR; ++k) {
+                    if (j < ln[k]) {
+                        const uint32_t q2 = q2_of(r[k], p.cb);
+                        const uint32_t at =
+                            __hip_atomic_fetch_add(&S.cur[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        p.rec2[p.p2off[(q1 * kQ + q2) * kSplits + s] + at] = r[k];
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// distinct (kl, count) out: wave-aggregated append
+__device__ __forceinline__ void out_append(const PartParams& p, bool has, uint64_t kl, uint32_t c, int lane) {
+    const uint64_t m = __ballot(has);
+    if (!m) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(p.out_n, (unsigned long long)__popcll(m));
+    base = __shfl(base, 0);
+    if (has) {
+        const unsigned long long o = base + lane_rank(m);
+        p.out_kl[o] = kl;
+        p.out_cnt[o] = c;
+    }
+}
+
+__global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t red_smem[];
+    uint64_t* keys = reinterpret_cast<uint64_t*>(red_smem);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(keys + kAggSlots);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    for (int i = tid; i < kAggSlots; i += kEmitWaves * 64) {
+        keys[i] = 0ull;
+        cnt[i] = 0u;
+    }
+    __syncthreads();
+    const int64_t beg = (int64_t)p.boff[blockIdx.x], end = (int64_t)p.boff[blockIdx.x + 1];
+    const uint64_t cmask = p.cb >= 64 ? ~0ull : ((1ull << p.cb) - 1ull);
+    constexpr int kU = 8;  // records per lane in flight
+    for (int64_t i00 = beg + (int64_t)wave * 64 * kU; i00 < end; i00 += kEmitWaves * 64 * kU) {
+      uint64_t rr[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+          const int64_t i = i00 + 64 * u + lane;
+          rr[u] = i < end ? p.rec2[i] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const bool valid = i00 + 64 * u + lane < end;
+        uint64_t kl = 0, c = 0;
+        bool left = false;
+        if (valid) {
+            const uint64_t r = rr[u];
+            kl = r >> p.cb;  // never 0: the sentinel bit
+            c = r & cmask;
+            uint32_t slot = (uint32_t)(((uint64_t)(uint32_t)mix64(kl) * kAggSlots) >> 32);
+            left = true;
+            for (int t = 0; t < 32 && left; ++t) {
+                unsigned long long old = keys[slot];  // read first: most records find their key
+                if (old == 0ull)
+                    old = atomicCAS(reinterpret_cast<unsigned long long*>(&keys[slot]), 0ull, (unsigned long long)kl);
+                if (old == 0ull || old == kl) {
+                    __hip_atomic_fetch_add(&cnt[slot], (uint32_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    left = false;
+                }
+                slot = (slot + 1u) & (kAggSlots - 1u);
+            }
+        }
+        out_append(p, left, kl, (uint32_t)c, lane);  // no LDS room: the record goes out as it is
+      }
+    }
+    __syncthreads();
+    for (int i0 = wave * 64; i0 < kAggSlots; i0 += kEmitWaves * 64) {
+        const int i = i0 + lane;
+        const uint64_t kl = keys[i];
+        out_append(p, kl != 0ull, kl, cnt[i], lane);
+    }
+}
+
+__global__ void merge_kernel(const PartParams p, const CountParams c, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t kl = p.out_kl[i];
+    add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out_cnt[i]);
+}
+
+}  // namespace
+
+size_t emit_lds_bytes() { return sizeof(EmitLds); }
+size_t reduce_lds_bytes() { return (size_t)kAggSlots * (sizeof(uint64_t) + sizeof(uint32_t)); }
+
+hipError_t fit2_prepare() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&emit_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)emit_lds_bytes());
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&reduce_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes());
+    return e;
+}
+
+hipError_t launch_emit(const PartParams& p, hipStream_t stream) {
+    hipLaunchKernelGGL(emit_kernel, dim3(p.grid_a), dim3(kEmitWaves * 64), emit_lds_bytes(), stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_part2(const PartParams& p, hipStream_t stream) {
+    hipLaunchKernelGGL(part2_kernel, dim3(kQ * kSplits), dim3(kEmitWaves * 64), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(const PartParams& p, hipStream_t stream) {
+    hipLaunchKernelGGL(reduce_kernel, dim3(kQ * kQ), dim3(kEmitWaves * 64), reduce_lds_bytes(), stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(const PartParams& p, const CountParams& c, int64_t n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, p, c, n);
     return hipGetLastError();
 }
 

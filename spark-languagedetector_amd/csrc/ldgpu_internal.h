@@ -113,8 +113,9 @@ struct CountParams {
     uint32_t shift;             // slot = mix64(key) >> shift
     uint64_t mask;              // cap - 1
     unsigned long long* size;   // distinct keys inserted
-    uint64_t* ovf_keys;         // overflow (probe limit reached): key, lang
+    uint64_t* ovf_keys;         // overflow (probe limit reached): key, lang, count
     int32_t* ovf_lang;
+    unsigned long long* ovf_cnt;
     unsigned int* ovf_n;
     uint32_t ovf_cap;
     int32_t L;
@@ -128,11 +129,70 @@ constexpr int kMaxProbe = 128;
 hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream);
 // insert keys[i] with counts rows[i][L] (add) into the table; n entries
 hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const unsigned long long* rows,
-                             const int32_t* lang_of /*nullable: row is one count 1 at lang_of[i]*/,
-                             int64_t n, hipStream_t stream);
+                             const int32_t* lang_of /*nullable: row is one count cnt_of[i] at lang_of[i]*/,
+                             const unsigned long long* cnt_of, int64_t n, hipStream_t stream);
+
+// ---- FIT v2: radix-partitioned record aggregation (ldgpu_fit.hip) ----
+// A window (or a per-document LDS-aggregated group of equal windows) becomes
+// one 64-bit record  ((sentinel << lb | lang) << cb) | count  with sentinel =
+// 1 << 8 klen | key bytes (klen <= 7).  kl = record >> cb identifies the
+// (gram, language) pair; h = mix64(kl) routes it: q1 = h >> 58, q2 = bits
+// 52..57 (4096 buckets), slot = low 32 bits (LDS hash in a bucket).
+constexpr int kQBits = 6;
+constexpr int kQ = 1 << kQBits;                 // buckets per level
+constexpr int kBlkRecs = 8192;                  // records per emit block (LDS)
+constexpr int kRoundRecs = 4096;                // records one emit round can add (16 waves x 64 lanes x 4)
+constexpr int kHdr = 68;                        // u32 per block header (kQ + 1 used)
+constexpr int kEmitWaves = 16;
+constexpr int kAggSlots = 8192;                 // LDS hash entries per bucket (reduce)
+constexpr int kSplits = 4;                      // emit workgroup groups (part2 inputs)
+
+struct PartParams {
+    // corpus of the batch
+    const uint8_t* bytes;
+    int64_t last_dword;
+    const int64_t* offsets;
+    const int32_t* doc_lang;
+    int32_t L;
+    int32_t nG;
+    int32_t G[kMaxGramLengths];
+    uint32_t lb, cb;            // language / count bit widths of a record
+    // emit (phase A): workgroup w owns documents [wg_doc[w], wg_doc[w+1]),
+    // records [wg_rec[w], ...) (capacity: its windows) and block ids
+    // [wg_dir[w], ...); blocks are sorted by q1 with a kHdr header
+    int32_t grid_a;             // emit workgroups (a multiple of kSplits)
+    const int64_t* wg_doc;
+    const int64_t* wg_rec;
+    const int64_t* wg_dir;
+    uint64_t* rec;
+    int64_t* blk_start;         // [blocks] record offset of the block
+    uint32_t* blk_hdr;          // [blocks][kHdr] exclusive q1 starts (+ total)
+    int32_t* nblk;              // [grid_a] blocks written
+    uint32_t* cnt3;             // [kQ][kQ][kSplits] records per (q1, q2, emit group)
+    CountParams direct;         // global table: counts too large for a record
+    // part2: q1 bucket of emit group s -> q2 sub-buckets at exact offsets
+    const uint64_t* p2off;      // [kQ][kQ][kSplits]
+    uint64_t* rec2;
+    // reduce: bucket (q1, q2) = rec2[boff[b] .. boff[b+1]) -> distinct (kl, count)
+    const uint64_t* boff;       // [kQ * kQ + 1]
+    uint64_t* out_kl;
+    uint32_t* out_cnt;          // a batch counts < 2^32 windows
+    unsigned long long* out_n;
+};
+
+size_t emit_lds_bytes();
+size_t reduce_lds_bytes();
+hipError_t fit2_prepare();
+hipError_t launch_emit(const PartParams& p, hipStream_t stream);
+hipError_t launch_part2(const PartParams& p, hipStream_t stream);
+hipError_t launch_reduce(const PartParams& p, hipStream_t stream);
+// add the reduce output (kl, count) entries 0..n into the global table
+hipError_t launch_merge(const PartParams& p, const CountParams& c, int64_t n, hipStream_t stream);
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
 hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
                          hipStream_t stream);
+// out[0] += distinct (gram, language) pairs, out[1] += sum of all counts
+hipError_t launch_stats(const CountParams& p, uint64_t cap, unsigned long long* out, hipStream_t stream);
 // compact occupied slots: out_keys[i], out_counts[i][L]; *out_n = number written
 hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys,
                           unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
@@ -149,9 +209,20 @@ hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const ui
                          const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
                          uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream);
 // chosen[idx[i]] = 1
+// sorted_keys (nullable): instead of marking, write the candidates' sort keys
+// in (language, key) order (the distributed top-K takes each segment's prefix)
 hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const uint64_t* cand_key,
                                   const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
-                                  uint8_t* chosen, hipStream_t stream);
+                                  uint8_t* chosen, uint64_t* sorted_keys, hipStream_t stream);
+// chosen[cand_idx[i]] = 1 when cand_key[i] <= thr[cand_lang[i]]
+hipError_t launch_mark_threshold(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key,
+                                 const uint32_t* cand_idx, const uint64_t* thr, uint8_t* chosen, hipStream_t stream);
+// multi-GPU merge: n_of[r] += occupied slots owned by rank r; scatter them
+// (keys, count rows) to out at cursor[owner]++
+hipError_t launch_owner_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
+                              hipStream_t stream);
+hipError_t launch_owner_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                uint64_t* out_keys, unsigned long long* out_rows, hipStream_t stream);
 hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream);
 // gather the chosen grams: out_keys[m], out_masks[m][S], out_k[m]
 hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,

@@ -59,10 +59,16 @@ SIGNATURES = [
     ("ldgpu_count", ctypes.c_int, [_p, _p, _p, _p, _i64]),
     ("ldgpu_count_device", ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p]),
     ("ldgpu_counts_size", ctypes.c_int, [_p, _pi64, _pi64]),
+    ("ldgpu_counts_stats", ctypes.c_int, [_p, _pi64, _pi64, _pi64]),
     ("ldgpu_counts_export", ctypes.c_int, [_p, _p, _p, _p]),
     ("ldgpu_counts_add", ctypes.c_int, [_p, _i64, _p, _p, _p]),
     ("ldgpu_counts_export_device", ctypes.c_int, [_p, _i64, _p, _p, _pi64, _p]),
     ("ldgpu_counts_add_device", ctypes.c_int, [_p, _i64, _p, _p, _p]),
+    ("ldgpu_comm_unique_id", ctypes.c_int, [_p]),
+    ("ldgpu_comm_create_rccl", ctypes.c_int, [_p, _p, _i32, _i32, _pp]),
+    ("ldgpu_comm_create_host", ctypes.c_int, [_p, _i32, _i32, _p, _pp]),
+    ("ldgpu_comm_destroy", ctypes.c_int, [_p]),
+    ("ldgpu_counts_merge", ctypes.c_int, [_p, _p]),
     ("ldgpu_fit_table_size", ctypes.c_int, [_p, _i32, _pi64, _pi64]),
     ("ldgpu_fit_table_export", ctypes.c_int, [_p, _p, _p, _p]),
     ("ldgpu_fit_table_export_masks", ctypes.c_int, [_p, _p, _p, _p, _p]),
@@ -70,6 +76,18 @@ SIGNATURES = [
 
 _libs = {}
 _lock = threading.Lock()
+
+
+COMM_ID_BYTES = 128
+
+# ldgpu_host_coll (include/ldgpu.h): collectives over host memory supplied by
+# the caller (the FIT merge's host transport)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, _pi64, ctypes.c_void_p, _pi64)
+
+
+class HostColl(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
 class LdgpuError(RuntimeError):

@@ -150,9 +150,10 @@ class DeviceCounts(_Owner):
     """A (gram, language) -> count table on one GPU (computeGrams + reduceGrams)."""
 
     def __init__(self, n_langs: int, gram_lengths: Sequence[int], capacity_hint: int = 0,
-                 device: Optional[int] = None):
-        self.lib = _lib.load()
-        self.ctx = _lib.context(device)
+                 device: Optional[int] = None, variant: str = "product"):
+        """variant="diag": the diagnostics library (tests of alternative paths)."""
+        self.lib = _lib.load(variant=variant)
+        self.ctx = _lib.context(device, variant)
         self.device = device
         self.L = int(n_langs)
         self.gram_lengths = list(gram_lengths)
@@ -190,6 +191,24 @@ class DeviceCounts(_Owner):
         n = ctypes.c_int64()
         self._check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), None))
         return n.value
+
+    def stats(self) -> Dict[str, int]:
+        """Distinct grams, distinct (gram, language) pairs, total count."""
+        v = [ctypes.c_int64() for _ in range(3)]
+        self._check(self.lib.ldgpu_counts_stats(self.h, *[ctypes.byref(x) for x in v]))
+        return {"grams": v[0].value, "pairs": v[1].value, "total": v[2].value}
+
+    def export_arrays(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(key_bytes uint8, key_offsets int64 [n+1], counts int64 [n, L]),
+        sorted by (length, bytes): export() without per-key Python objects."""
+        n = ctypes.c_int64()
+        nb = ctypes.c_int64()
+        self._check(self.lib.ldgpu_counts_size(self.h, ctypes.byref(n), ctypes.byref(nb)))
+        kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        ko = np.zeros(n.value + 1, dtype=np.int64)
+        cnt = np.zeros((n.value, self.L), dtype=np.int64)
+        self._check(self.lib.ldgpu_counts_export(self.h, _ptr(kb), _ptr(ko), _ptr(cnt)))
+        return kb[:int(ko[-1])], ko, cnt
 
     def export(self) -> Tuple[List[bytes], np.ndarray]:
         """Distinct grams sorted by (length, bytes) and int64 counts [n, L]."""

@@ -1,7 +1,8 @@
-"""Multi-process paths (world size 2, gloo on 127.0.0.1): the FIT count merge
-(all_gather of key lists + all_reduce of dense counts) and sharded scoring.
-CPU tests feed the merge with the C oracle's per-shard counts; the gpu test
-runs the whole fit_distributed on cuda:0 from two ranks."""
+"""Multi-process paths (world size 2, gloo on 127.0.0.1): the FIT merge
+(owner exchange, ldgpu_counts_merge) and sharded scoring.  The CPU test runs
+the owner-exchange protocol on the C oracle's per-shard counts; the gpu tests
+run the library's merge + distributed top-K from two ranks on cuda:0 (host
+transport over gloo) and the RCCL transport at world size 1."""
 import os
 import socket
 import sys
@@ -47,7 +48,7 @@ def _merge_worker(rank, world, port, out_dir):
     sub_off = off[lo:hi + 1] - off[lo]
     sub = data[off[lo]:off[hi]]
     keys, cnt = OC.count(sub, sub_off, lang[lo:hi], 6, [1, 2, 3])
-    gk, gc = merge_counts(keys, cnt, 6)
+    gk, gc = merge_counts(keys, cnt, 6)   # this rank's owned grams, global counts
     np.save(os.path.join(out_dir, f"counts{rank}.npy"), gc)
     with open(os.path.join(out_dir, f"keys{rank}.bin"), "wb") as f:
         for k in gk:
@@ -67,13 +68,24 @@ def _read_keys(path):
 
 
 def test_merge_counts_two_ranks(tmp_path):
+    """The ranks' owned shards partition the global table: disjoint, every
+    gram on its owner (distributed.owner_of), counts equal to the oracle's
+    single-process counts."""
     import ldoracle_c as OC
+    from languagedetection.distributed import owner_of, packed_keys
     mp.spawn(_merge_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
     ls, (data, off, lang) = _corpus()
     keys, cnt = OC.count(data, off, lang, 6, [1, 2, 3])
+    got = {}
     for r in range(2):
-        assert _read_keys(os.path.join(tmp_path, f"keys{r}.bin")) == keys
-        assert np.array_equal(np.load(os.path.join(tmp_path, f"counts{r}.npy")), cnt)
+        rk = _read_keys(os.path.join(tmp_path, f"keys{r}.bin"))
+        rc = np.load(os.path.join(tmp_path, f"counts{r}.npy"))
+        assert (owner_of(packed_keys(rk), 2) == r).all()
+        for k, row in zip(rk, rc):
+            assert k not in got
+            got[k] = row
+    assert sorted(got, key=lambda k: (len(k), k)) == keys
+    assert np.array_equal(np.array([got[k] for k in keys]), cnt)
 
 
 def test_sort_keys_roundtrip_and_order():
@@ -87,33 +99,67 @@ def test_sort_keys_roundtrip_and_order():
     assert cover == [(0, 3), (3, 6), (6, 10)]
 
 
-def _fit_worker(rank, world, port, out_dir):
+def _fit_worker(rank, world, port, out_dir, K, grams, transport):
     dist = _init(rank, world, port)
     from languagedetection import synth
-    from languagedetection.distributed import fit_distributed, shard_range
+    from languagedetection.api import LanguageDetector
+    from languagedetection.distributed import Communicator, merge_counts_device, shard_range
     ls, (data, off, lang) = _corpus()
     rows = list(zip([ls.names[i] for i in lang], synth.texts(data, off)))
     lo, hi = shard_range(len(rows), rank, world)
-    table = fit_distributed(rows[lo:hi], ls.names, [1, 2, 3], 80, device=0)
+    local = LanguageDetector.count_grams(rows[lo:hi], grams, ls.names, device=0)
+    comm = Communicator(device=0, transport=transport)
+    merge_counts_device(local, comm)
+    keys, cnt = local.export()      # this rank's owned shard, global counts
+    table = local.fit_table(K)      # collective: the global table on every rank
+    local.close()
+    comm.close()
     import json
     with open(os.path.join(out_dir, f"table{rank}.json"), "w") as f:
-        json.dump({k.hex(): v for k, v in table.items()}, f)
+        json.dump({"table": {k.hex(): v for k, v in table.items()},
+                   "counts": {k.hex(): c.tolist() for k, c in zip(keys, cnt)}}, f)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-def test_fit_distributed_matches_single_process(tmp_path):
+def _check_fit(tmp_path, world, K, grams):
     import json
     import ldoracle as O
+    import ldoracle_c as OC
     from languagedetection import synth
-    mp.spawn(_fit_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
     ls, (data, off, lang) = _corpus()
     rows = list(zip([ls.names[i] for i in lang], synth.texts(data, off)))
-    expect = O.filter_top_grams(O.fit_probabilities(rows, ls.names, [1, 2, 3]), ls.names, 80)
-    for r in range(2):
-        got = {bytes.fromhex(k): v for k, v in json.load(open(os.path.join(tmp_path, f"table{r}.json"))).items()}
+    expect = O.filter_top_grams(O.fit_probabilities(rows, ls.names, grams), ls.names, K)
+    okeys, ocnt = OC.count(data, off, lang, 6, grams)
+    counts = {}
+    for r in range(world):
+        d = json.load(open(os.path.join(tmp_path, f"table{r}.json")))
+        got = {bytes.fromhex(k): v for k, v in d["table"].items()}
         assert got == expect
+        for k, c in d["counts"].items():
+            assert k not in counts      # owned shards are disjoint
+            counts[k] = c
+    assert len(counts) == len(okeys)
+    assert all(counts[k.hex()] == ocnt[i].tolist() for i, k in enumerate(okeys))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,grams", [(80, [1, 2, 3]), (5000, [2, 3])])
+def test_fit_distributed_matches_single_process(tmp_path, K, grams):
+    """Two ranks (cuda:0 each), host transport over gloo: the library's owner
+    exchange leaves disjoint shards with the oracle's global counts, and the
+    distributed top-K gives every rank the oracle's table -- also with K above
+    some language's present grams (the zero-valued fill)."""
+    mp.spawn(_fit_worker, args=(2, free_port(), str(tmp_path), K, grams, "host"), nprocs=2, join=True)
+    _check_fit(tmp_path, 2, K, grams)
+
+
+@pytest.mark.gpu
+def test_fit_merge_rccl_transport_world1(tmp_path):
+    """The RCCL transport (ncclCommInitRank, grouped ncclSend/ncclRecv,
+    ncclAllGather) at world size 1, the only size one GPU allows."""
+    mp.spawn(_fit_worker, args=(1, free_port(), str(tmp_path), 80, [1, 2, 3], "rccl"), nprocs=1, join=True)
+    _check_fit(tmp_path, 1, 80, [1, 2, 3])
 
 
 def _score_worker(rank, world, port, out_dir):

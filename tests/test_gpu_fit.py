@@ -232,3 +232,38 @@ def test_config3_shape_counts_and_table():
     expect = _topk_table_from_counts(okeys, ocnt, L, K)
     assert table.keys() == expect.keys()
     assert all(table[g] == expect[g] for g in expect)
+
+
+@pytest.mark.parametrize("variant,env", [
+    ("product", {}),                                         # FIT v2: one batch
+    ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v2: many small batches
+    ("diag", {"LDGPU_FIT_LEGACY": "1"}),                     # single-pass count_kernel
+])
+@pytest.mark.parametrize("L,grams", [(20, [1, 2, 3, 4, 5]), (100, [1, 2, 6]), (256, [3, 1, 3]), (2, [5, 4])])
+def test_count_paths_match_oracle(L, grams, variant, env, monkeypatch):
+    """Both counting paths, bit-exact against the C restatement: the radix-
+    partitioned record path (FIT v2: records of (gram, language, count),
+    bucketed twice, LDS-aggregated) in one and in many batches, and the
+    single-pass kernel.  (100, [1, 2, 6]) leaves a record 8 count bits, so
+    hot 1-/2-grams of the long repetitive documents exceed a record's count
+    and take the direct global add; unsupported labels (-1) are skipped."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(L + len(grams))
+    ls = synth.make_languages(L, seed=L + 7)
+    data, off, lang = synth.generate(ls, 900, 0, 900, seed=L + 8)
+    docs = [bytes(data[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
+    docs += [b"a" * 3000, b"ab" * 1500, b"abc" * 700, b"", b"x", b"xy"]
+    dl = np.concatenate([lang, rng.integers(0, L, size=6).astype(np.int32)])
+    dl[::29] = -1
+    d, o = encoding.pack(docs)
+    counts = DeviceCounts(L, grams, variant=variant)
+    counts.count(d, o, dl)
+    counts.count(d[:int(o[300])], o[:301], dl[:300])   # a second call accumulates
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(d, o, dl, L, grams)
+    okeys2, ocnt2 = OC.count(d[:int(o[300])], o[:301], dl[:300], L, grams)
+    extra = dict(zip(okeys2, ocnt2))
+    expect = np.array([ocnt[i] + extra.get(k, 0) for i, k in enumerate(okeys)])
+    assert keys == okeys
+    assert np.array_equal(cnt, expect)

@@ -3,6 +3,7 @@ every counter (tools/pmc_profile.sh)."""
 import csv
 import glob
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -15,7 +16,7 @@ def main(out):
                 k = row.get("Kernel_Name", "?")
                 acc[k][row["Counter_Name"]].append((row.get("Dispatch_Id"), float(row["Counter_Value"])))
     for k, cs in acc.items():
-        if "score_kernel" not in k and "count_kernel" not in k:
+        if not re.search(os.environ.get("KERNELS", "score_kernel|count_kernel|emit_kernel|part2_kernel|reduce_kernel|merge_kernel"), k):
             continue
         print(k[:100])
         for c, vals in sorted(cs.items()):
