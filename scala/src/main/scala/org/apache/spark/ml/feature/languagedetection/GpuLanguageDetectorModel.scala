@@ -1,0 +1,193 @@
+package org.apache.spark.ml.feature.languagedetection
+
+import org.apache.hadoop.fs.Path
+import org.apache.spark.internal.Logging
+import org.apache.spark.ml.Model
+import org.apache.spark.ml.param.ParamMap
+import org.apache.spark.ml.param.shared.{HasInputCol, HasOutputCol}
+import org.apache.spark.ml.util._
+import org.apache.spark.sql.types.{StringType, StructType}
+import org.apache.spark.sql.{DataFrame, Dataset, Row, SaveMode}
+import org.json4s.JsonDSL._
+import org.json4s.{DefaultFormats, JArray, JString}
+
+/**
+  * Drop-in for the reference's LanguageDetectorModel (same package, class
+  * name, constructors, public vals -- including the `gramLenghts` spelling --
+  * params and defaults; LanguageDetectorModel.scala:168-243).  Scoring runs on
+  * the executor's GPU through libldgpu.so: transform broadcasts the table once
+  * as flat arrays, and every partition is packed into pinned direct buffers
+  * and scored in batches (ldgpu_score), instead of one Scala detect call per
+  * row.  Labels and scores are the reference's: the library reproduces the
+  * fp64 left fold of BLAS.axpy and breeze's first-maximum argmax.
+  */
+class LanguageDetectorModel(override val uid: String,
+                            val gramProbabilities: Map[Seq[Byte], Array[Double]],
+                            val gramLenghts: Seq[Int],
+                            val supportedLanguages: Seq[String])
+  extends Model[LanguageDetectorModel] with HasInputCol with HasOutputCol with Logging with MLWritable {
+
+  def this(gramProbabilities: Map[Seq[Byte], Array[Double]], gramLengths: Seq[Int], languages: Seq[String]) =
+    this(Identifiable.randomUID("LanguageDetectorModel"), gramProbabilities, gramLengths, languages)
+
+  setDefault(inputCol -> "fulltext", outputCol -> "lang")
+
+  def setInputCol(value: String): this.type = set(inputCol, value)
+  def setOutputCol(value: String): this.type = set(outputCol, value)
+
+  /** documents and bytes per ldgpu_score call (one pipelined call per batch) */
+  var batchDocs: Int = 1 << 20
+  var batchBytes: Int = 64 << 20
+
+  override def transformSchema(schema: StructType): StructType = {
+    val inputType = schema($(inputCol)).dataType
+    require(inputType.sameType(StringType), s"Input type must be StringType but got $inputType.")
+    SchemaUtils.appendColumn(schema, $(outputCol), StringType, nullable = true)
+  }
+
+  override def copy(extra: ParamMap): LanguageDetectorModel = {
+    val m = new LanguageDetectorModel(uid, gramProbabilities, gramLenghts, supportedLanguages)
+    copyValues(m, extra).setParent(parent)
+  }
+
+  override def transform(dataset: Dataset[_]): DataFrame = {
+    val schema = transformSchema(dataset.schema)
+    val spark = dataset.sparkSession
+    val table = spark.sparkContext.broadcast(PackedTable.of(gramProbabilities, supportedLanguages.length))
+    val grams = gramLenghts.toArray
+    val langs = supportedLanguages.toArray
+    val col = $(inputCol)
+    val nDocs = batchDocs
+    val nBytes = batchBytes
+    val rows = dataset.toDF().rdd.mapPartitions { it =>
+      if (!it.hasNext) Iterator.empty
+      else {
+        val model = LdgpuNative.model(table.id, table.value, grams)
+        val batch = new DocBatch(LdgpuNative.context(), nDocs, nBytes)
+        val pending = new java.util.ArrayList[Row](math.min(nDocs, 1 << 16))
+        new Iterator[Row] {
+          private var out: Iterator[Row] = Iterator.empty
+          private var idx = -1
+          private var open = true
+          // the next batch of rows: packed, scored in one ldgpu_score call
+          private def fill(): Unit = {
+            batch.clear()
+            pending.clear()
+            while (it.hasNext && !batch.full) {
+              val row = it.next()
+              if (idx < 0) idx = row.fieldIndex(col)
+              batch.addScore(row.getString(idx))
+              pending.add(row)
+            }
+            LdgpuNative.check(LdgpuNative.score(model, batch.bytes, batch.offsets, batch.n.toLong, batch.labels, null))
+            val scored = new Array[Row](batch.n)
+            var i = 0
+            while (i < batch.n) {
+              scored(i) = Row.fromSeq(pending.get(i).toSeq :+ langs(batch.label(i)))
+              i += 1
+            }
+            out = scored.iterator
+          }
+          override def hasNext: Boolean = {
+            if (!out.hasNext && it.hasNext) fill()
+            if (!out.hasNext && open) {
+              batch.close()
+              open = false
+            }
+            out.hasNext
+          }
+          override def next(): Row = {
+            if (!hasNext) throw new NoSuchElementException
+            out.next()
+          }
+        }
+      }
+    }
+    spark.createDataFrame(rows, schema)
+  }
+
+  override def write: MLWriter = new LanguageDetectorModel.LanguageDetectorModelWriter(this)
+}
+
+object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
+
+  override def read: MLReader[LanguageDetectorModel] = new LanguageDetectorModelReader
+  override def load(path: String): LanguageDetectorModel = super.load(path)
+
+  /**
+    * detect(Array[Byte], ...) (LanguageDetectorModel.scala:131-156): one
+    * document through a transient device table.  For many documents use
+    * transform, which keeps the table on the GPU and scores in batches.
+    */
+  def detect(text: Array[Byte], probabilityMap: Map[Seq[Byte], Array[Double]], supportedLanguages: Seq[String],
+             gramLengths: Seq[Int]): String = {
+    val ctx = LdgpuNative.context()
+    val model = PackedTable.of(probabilityMap, supportedLanguages.length).upload(ctx, gramLengths.toArray)
+    try {
+      val bytes = LdgpuNative.direct(text.length.toLong + 16)
+      bytes.put(text).flip()
+      val offsets = LdgpuNative.direct(16)
+      offsets.putLong(0, 0L)
+      offsets.putLong(8, text.length.toLong)
+      val label = LdgpuNative.direct(4)
+      LdgpuNative.check(LdgpuNative.score(model, bytes, offsets, 1L, label, null))
+      supportedLanguages(label.getInt(0))
+    } finally {
+      LdgpuNative.modelDestroy(model)
+    }
+  }
+
+  /** detect(String, ...) (:158-165): the low byte of every UTF-16 unit */
+  def detect(text: String, probabilityMap: Map[Seq[Byte], Array[Double]], supportedLanguages: Seq[String],
+             gramLengths: Seq[Int]): String =
+    detect(text.toCharArray.map(_.toByte), probabilityMap, supportedLanguages, gramLengths)
+
+  /**
+    * The reference's on-disk layout (:27-60): metadata JSON, probabilities
+    * (_1 array<tinyint>, _2 array<double>), supportedLanguages and gramLengths
+    * (`value`).  The metadata also carries "languageOrder": the reference's
+    * reader collects supportedLanguages without an ordering key (:82-87), so a
+    * multi-part dataset can come back permuted; this reader uses the pin, the
+    * reference's reader ignores the extra top-level field.
+    */
+  class LanguageDetectorModelWriter(instance: LanguageDetectorModel) extends MLWriter with Logging {
+    override protected def saveImpl(path: String): Unit = {
+      val spark = sparkSession
+      import spark.implicits._
+      DefaultParamsWriter.saveMetadata(instance, path, sc,
+        extraMetadata = Some("languageOrder" -> instance.supportedLanguages.toList))
+      spark.createDataset(instance.gramProbabilities.toSeq).write.mode(SaveMode.Overwrite)
+        .parquet(new Path(path, "probabilities").toString)
+      spark.createDataset(instance.supportedLanguages).coalesce(1).write.mode(SaveMode.Overwrite)
+        .parquet(new Path(path, "supportedLanguages").toString)
+      spark.createDataset(instance.gramLenghts).coalesce(1).write.mode(SaveMode.Overwrite)
+        .parquet(new Path(path, "gramLengths").toString)
+    }
+  }
+
+  class LanguageDetectorModelReader extends MLReader[LanguageDetectorModel] {
+    private val className = classOf[LanguageDetectorModel].getName
+
+    override def load(path: String): LanguageDetectorModel = {
+      val spark = sparkSession
+      import spark.implicits._
+      val metadata = DefaultParamsReader.loadMetadata(path, sc, className)
+      val probabilities = spark.read.parquet(new Path(path, "probabilities").toString)
+        .as[(Seq[Byte], Array[Double])].collect().toMap
+      val stored = spark.read.parquet(new Path(path, "supportedLanguages").toString).as[String].collect().toSeq
+      implicit val formats: DefaultFormats.type = DefaultFormats
+      val languages = metadata.metadata \ "languageOrder" match {
+        case JArray(values) =>
+          val pinned = values.collect { case JString(s) => s }
+          require(pinned.sorted == stored.sorted,
+            s"metadata languageOrder $pinned does not match the supportedLanguages dataset $stored")
+          pinned
+        case _ => stored
+      }
+      val grams = spark.read.parquet(new Path(path, "gramLengths").toString).as[Int].collect().toSeq
+      val model = new LanguageDetectorModel(metadata.uid, probabilities, grams, languages)
+      DefaultParamsReader.getAndSetParams(model, metadata)
+      model
+    }
+  }
+}
