@@ -204,18 +204,18 @@ def host_path(model, data, off, acc_labels):
 
 
 def traffic_from_profiles(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes, if they
-    were collected for this exact workload (tools/pmc_traffic.py)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        d = json.load(open(p))
-    except Exception:
-        return None
-    if d.get("workload_key") != workload_key:
-        return None
-    return d.get("traffic_bytes_per_launch")
+    """HBM bytes per launch (per count, for FIT) from the committed rocprofv3
+    PMC passes (profiles/pmc_traffic*.json), if they were collected for this
+    exact workload (tools/pmc_traffic.py, tools/pmc_profile.sh)."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload_key") == workload_key:
+            return d.get("traffic_bytes_per_launch")
+    return None
 
 
 def fit_main(args, world, rank, local, dev, backend):

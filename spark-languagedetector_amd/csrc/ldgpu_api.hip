@@ -1306,24 +1306,33 @@ int count_launch_v2(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(R, 1)));
         HIP_TRY(x->f_okl.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(R, 1)));
         HIP_TRY(x->f_ocnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(R, 1)));
-        HIP_TRY(x->f_on.ensure(sizeof(unsigned long long)));
+        HIP_TRY(x->f_on.ensure(sizeof(uint32_t) * kQ * kQ + sizeof(uint64_t) * (kQ * kQ + 1)));
         HIP_TRY(hipMemcpyAsync(x->f_p2.p, p2off.data(), sizeof(uint64_t) * p2off.size(), hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(x->f_boff.p, boff.data(), sizeof(uint64_t) * boff.size(), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemsetAsync(x->f_on.p, 0, sizeof(unsigned long long), st));
         pp.p2off = (const uint64_t*)x->f_p2.p;
         pp.rec2 = (uint64_t*)x->f_rec2.p;
         pp.boff = (const uint64_t*)x->f_boff.p;
         pp.out_kl = (uint64_t*)x->f_okl.p;
         pp.out_cnt = (uint32_t*)x->f_ocnt.p;
-        pp.out_n = (unsigned long long*)x->f_on.p;
+        pp.nout = (uint32_t*)x->f_on.p;
+        pp.epre = (const uint64_t*)((const uint8_t*)x->f_on.p + sizeof(uint32_t) * kQ * kQ);
+        std::vector<uint32_t> nout((size_t)kQ * kQ, 0u);
         if (R > 0) {
             HIP_TRY(launch_part2(pp, st));
             HIP_TRY(launch_reduce(pp, st));
+            HIP_TRY(hipMemcpyAsync(nout.data(), pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
         }
-        unsigned long long E = 0;
-        HIP_TRY(hipMemcpyAsync(&E, x->f_on.p, sizeof E, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        if ((int64_t)E > R) return fail(LDGPU_EDEVICE, "fit reduce: %llu entries from %lld records", E, (long long)R);
+        // the merge's entry order: buckets' outputs back to back
+        std::vector<uint64_t> epre((size_t)kQ * kQ + 1, 0);
+        for (int b = 0; b < kQ * kQ; ++b) {
+            if (nout[b] > boff[b + 1] - boff[b])
+                return fail(LDGPU_EDEVICE, "fit reduce: bucket %d wrote %u entries from %llu records", b, nout[b],
+                            (unsigned long long)(boff[b + 1] - boff[b]));
+            epre[b + 1] = epre[b] + nout[b];
+        }
+        const unsigned long long E = epre[(size_t)kQ * kQ];
+        HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
         // room for every entry as a new key: load <= 1/2, so the merge's
         // probes never reach the overflow list in practice (it still catches them)
         if (2 * (c->size + E) > c->cap) {

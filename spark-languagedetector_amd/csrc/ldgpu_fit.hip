@@ -785,25 +785,41 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveS
                 if (valid[k]) __hip_atomic_fetch_add(&h1[lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             w.used1 = 1;
         } else if (klen <= 3) {
+            // the kSubW positions probe together: one LDS round trip per
+            // probe step for all of them (most find their key at once)
+            uint32_t tag[kSubW], slot[kSubW];
+            bool pend[kSubW];
 #pragma unroll
             for (int k = 0; k < kSubW; ++k) {
-                if (!valid[k]) continue;
-                const uint32_t tag = lo[k] | ((uint32_t)klen << 24);  // never 0
-                uint32_t slot = (uint32_t)(((uint64_t)(lo[k] * 0x9E3779B1u) * kH2) >> 32);
-                bool done = false;
-                for (int t = 0; t < kH2Probe && !done; ++t) {
-                    uint32_t cur = k2[slot];  // read first: most windows find their key
-                    if (cur == 0u) {
-                        const uint32_t old = atomicCAS(&k2[slot], 0u, tag);
-                        cur = old == 0u ? tag : old;
+                tag[k] = lo[k] | ((uint32_t)klen << 24);  // never 0
+                slot[k] = (uint32_t)(((uint64_t)(lo[k] * 0x9E3779B1u) * kH2) >> 32);
+                pend[k] = valid[k];
+            }
+            for (int t = 0; t < kH2Probe; ++t) {
+                uint32_t cur[kSubW];
+#pragma unroll
+                for (int k = 0; k < kSubW; ++k) cur[k] = pend[k] ? k2[slot[k]] : 0u;
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < kSubW; ++k) {
+                    if (!pend[k]) continue;
+                    if (cur[k] == 0u) {
+                        const uint32_t old = atomicCAS(&k2[slot[k]], 0u, tag[k]);
+                        cur[k] = old == 0u ? tag[k] : old;
                     }
-                    if (cur == tag) {
-                        __hip_atomic_fetch_add(&c2[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        done = true;
+                    if (cur[k] == tag[k]) {
+                        __hip_atomic_fetch_add(&c2[slot[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        pend[k] = false;
+                    } else {
+                        slot[k] = slot[k] + 1u == kH2 ? 0u : slot[k] + 1u;
+                        any = true;
                     }
-                    slot = slot + 1u == kH2 ? 0u : slot + 1u;
                 }
-                if (!done) {
+                if (!__ballot(any)) break;
+            }
+#pragma unroll
+            for (int k = 0; k < kSubW; ++k) {
+                if (pend[k]) {  // no slot: the window goes out as a record
                     has[k] = true;
                     r[k] = make_rec(lo[k], klen, (uint32_t)w.lang, 1, p.lb, p.cb);
                 }
@@ -1042,15 +1058,19 @@ __global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams
     }
 }
 
-// distinct (kl, count) out: wave-aggregated append
-__device__ __forceinline__ void out_append(const PartParams& p, bool has, uint64_t kl, uint32_t c, int lane) {
+// distinct (kl, count) out: bucket b writes its entries from boff[b] on (it
+// has at most as many as records), through a workgroup-local counter -- one
+// global counter for every bucket's appends would serialise ~0.5M atomics
+// per batch on one address
+__device__ __forceinline__ void out_append(const PartParams& p, uint32_t* n_out, int64_t base, bool has, uint64_t kl,
+                                           uint32_t c, int lane) {
     const uint64_t m = __ballot(has);
     if (!m) return;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(p.out_n, (unsigned long long)__popcll(m));
-    base = __shfl(base, 0);
+    uint32_t at = 0;
+    if (lane == 0) at = __hip_atomic_fetch_add(n_out, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    at = __shfl(at, 0);
     if (has) {
-        const unsigned long long o = base + lane_rank(m);
+        const int64_t o = base + at + lane_rank(m);
         p.out_kl[o] = kl;
         p.out_cnt[o] = c;
     }
@@ -1060,6 +1080,7 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
     extern __shared__ __attribute__((aligned(16))) uint8_t red_smem[];
     uint64_t* keys = reinterpret_cast<uint64_t*>(red_smem);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(keys + kAggSlots);
+    uint32_t* n_out = cnt + kAggSlots;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -1067,61 +1088,82 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
         keys[i] = 0ull;
         cnt[i] = 0u;
     }
+    if (tid == 0) *n_out = 0u;
     __syncthreads();
     const int64_t beg = (int64_t)p.boff[blockIdx.x], end = (int64_t)p.boff[blockIdx.x + 1];
     const uint64_t cmask = p.cb >= 64 ? ~0ull : ((1ull << p.cb) - 1ull);
-    constexpr int kU = 8;  // records per lane in flight
+    constexpr int kU = 8;  // records per lane in flight; their probes advance together
     for (int64_t i00 = beg + (int64_t)wave * 64 * kU; i00 < end; i00 += kEmitWaves * 64 * kU) {
-      uint64_t rr[kU];
+        uint64_t kl[kU];
+        uint32_t c[kU], slot[kU];
+        bool pend[kU];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-          const int64_t i = i00 + 64 * u + lane;
-          rr[u] = i < end ? p.rec2[i] : 0ull;
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const bool valid = i00 + 64 * u + lane < end;
-        uint64_t kl = 0, c = 0;
-        bool left = false;
-        if (valid) {
-            const uint64_t r = rr[u];
-            kl = r >> p.cb;  // never 0: the sentinel bit
-            c = r & cmask;
-            uint32_t slot = (uint32_t)(((uint64_t)(uint32_t)mix64(kl) * kAggSlots) >> 32);
-            left = true;
-            for (int t = 0; t < 32 && left; ++t) {
-                unsigned long long old = keys[slot];  // read first: most records find their key
-                if (old == 0ull)
-                    old = atomicCAS(reinterpret_cast<unsigned long long*>(&keys[slot]), 0ull, (unsigned long long)kl);
-                if (old == 0ull || old == kl) {
-                    __hip_atomic_fetch_add(&cnt[slot], (uint32_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    left = false;
-                }
-                slot = (slot + 1u) & (kAggSlots - 1u);
-            }
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i00 + 64 * u + lane;
+            const uint64_t r = i < end ? p.rec2[i] : 0ull;
+            pend[u] = i < end;
+            kl[u] = r >> p.cb;  // never 0 for a record: the sentinel bit
+            c[u] = (uint32_t)(r & cmask);
+            slot[u] = (uint32_t)(((uint64_t)(uint32_t)mix64(kl[u]) * kAggSlots) >> 32);
         }
-        out_append(p, left, kl, (uint32_t)c, lane);  // no LDS room: the record goes out as it is
-      }
+        for (int t = 0; t < 32; ++t) {
+            uint64_t cur[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) cur[u] = pend[u] ? keys[slot[u]] : 0ull;  // read first: most records find their key
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                if (!pend[u]) continue;
+                if (cur[u] == 0ull) {
+                    const unsigned long long old =
+                        atomicCAS(reinterpret_cast<unsigned long long*>(&keys[slot[u]]), 0ull, (unsigned long long)kl[u]);
+                    cur[u] = old == 0ull ? kl[u] : old;
+                }
+                if (cur[u] == kl[u]) {
+                    __hip_atomic_fetch_add(&cnt[slot[u]], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pend[u] = false;
+                } else {
+                    slot[u] = (slot[u] + 1u) & (kAggSlots - 1u);
+                    any = true;
+                }
+            }
+            if (!__ballot(any)) break;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)  // no LDS room: the record goes out as it is
+            out_append(p, n_out, beg, pend[u], kl[u], c[u], lane);
     }
     __syncthreads();
     for (int i0 = wave * 64; i0 < kAggSlots; i0 += kEmitWaves * 64) {
         const int i = i0 + lane;
-        const uint64_t kl = keys[i];
-        out_append(p, kl != 0ull, kl, cnt[i], lane);
+        const uint64_t k = keys[i];
+        out_append(p, n_out, beg, k != 0ull, k, cnt[i], lane);
     }
+    __syncthreads();
+    if (tid == 0) p.nout[blockIdx.x] = *n_out;
 }
 
-__global__ void merge_kernel(const PartParams p, const CountParams c, int64_t n) {
+// entry i of the batch (buckets' outputs in bucket order, prefix epre) ->
+// bucket b = the last with epre[b] <= i, stored at boff[b] + (i - epre[b])
+__global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const CountParams c, int64_t n) {
+    __shared__ uint64_t pre[kQ * kQ + 1];
+    for (int i = threadIdx.x; i <= kQ * kQ; i += blockDim.x) pre[i] = p.epre[i];
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint64_t kl = p.out_kl[i];
-    add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out_cnt[i]);
+    int lo = 0;
+#pragma unroll
+    for (int step = 2048; step >= 1; step >>= 1)
+        if (lo + step <= kQ * kQ && pre[lo + step] <= (uint64_t)i) lo += step;
+    const int64_t at = (int64_t)p.boff[lo] + (i - (int64_t)pre[lo]);
+    const uint64_t kl = p.out_kl[at];
+    add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out_cnt[at]);
 }
 
 }  // namespace
 
 size_t emit_lds_bytes() { return sizeof(EmitLds); }
-size_t reduce_lds_bytes() { return (size_t)kAggSlots * (sizeof(uint64_t) + sizeof(uint32_t)); }
+size_t reduce_lds_bytes() { return (size_t)kAggSlots * (sizeof(uint64_t) + sizeof(uint32_t)) + 16; }
 
 hipError_t fit2_prepare() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&emit_kernel),
@@ -1149,7 +1191,7 @@ hipError_t launch_reduce(const PartParams& p, hipStream_t stream) {
 
 hipError_t launch_merge(const PartParams& p, const CountParams& c, int64_t n, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, p, c, n);
+    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, stream, p, c, n);
     return hipGetLastError();
 }
 

@@ -173,11 +173,13 @@ struct PartParams {
     // part2: q1 bucket of emit group s -> q2 sub-buckets at exact offsets
     const uint64_t* p2off;      // [kQ][kQ][kSplits]
     uint64_t* rec2;
-    // reduce: bucket (q1, q2) = rec2[boff[b] .. boff[b+1]) -> distinct (kl, count)
+    // reduce: bucket (q1, q2) = rec2[boff[b] .. boff[b+1]) -> distinct (kl,
+    // count) entries at out[boff[b] ..] (at most one per record), nout[b] of them
     const uint64_t* boff;       // [kQ * kQ + 1]
     uint64_t* out_kl;
     uint32_t* out_cnt;          // a batch counts < 2^32 windows
-    unsigned long long* out_n;
+    uint32_t* nout;             // [kQ * kQ]
+    const uint64_t* epre;       // merge: exclusive prefix of nout [kQ * kQ + 1]
 };
 
 size_t emit_lds_bytes();
