@@ -1276,6 +1276,7 @@ int count_launch_v2(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         for (int i = 0; i < c->nG; ++i) pp.G[i] = c->G[i];
         pp.lb = c->lb;
         pp.cb = c->cb;
+        if (const char* ab = diag_env("LDGPU_FIT_EMIT_ABLATE")) pp.ablate = atoi(ab);
         pp.grid_a = grid_a;
         pp.wg_doc = (const int64_t*)x->f_wg.p;
         pp.wg_rec = pp.wg_doc + grid_a + 1;

@@ -607,6 +607,8 @@ hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const u
 namespace ldgpu {
 namespace {
 
+__device__ __forceinline__ bool emit_ablated(const PartParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -646,12 +648,20 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
     return v;
 }
 
+// emit's per-wave LDS table of a document's 2-byte windows: 1024 packed
+// slots (16-bit key, 16-bit count), so a document's few hundred distinct
+// 2-grams probe short chains; documents of 64 Ki bytes or more skip it (a
+// count must stay below 0xffff)
+constexpr uint32_t kK2 = 1024;
+constexpr uint32_t kK2Empty = 0xffffffffu;
+constexpr int kK2Probe = 16;
+constexpr int64_t kK2MaxDoc = 0xffff;
+
 struct EmitLds {
     uint64_t blk[kBlkRecs];
     uint32_t hist2[kQ * kQ];
     uint32_t h1[kEmitWaves][256];
-    uint32_t k2[kEmitWaves][kH2];
-    uint32_t c2[kEmitWaves][kH2];
+    uint32_t k2[kEmitWaves][kK2];      // per-document 2-gram counts: key << 16 | count, kK2Empty = free
     uint32_t pcnt[kQ];
     uint32_t pfill[kQ];
     uint32_t pstart[kQ + 1];
@@ -728,7 +738,6 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveS
     const uint64_t cmax = p.cb >= 32 ? 0xffffffffull : ((1ull << p.cb) - 1ull);
     uint32_t* h1 = S.h1[wave];
     uint32_t* k2 = S.k2[wave];
-    uint32_t* c2 = S.c2[wave];
     if (w.phase == kNextDoc) {
         uint32_t k = 0;
         if (lane == 0) k = __hip_atomic_fetch_add(&S.next_doc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -784,18 +793,17 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveS
             for (int k = 0; k < kSubW; ++k)
                 if (valid[k]) __hip_atomic_fetch_add(&h1[lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             w.used1 = 1;
-        } else if (klen <= 3) {
+        } else if (klen == 2 && w.len < kK2MaxDoc && !emit_ablated(p, 1)) {
             // the kSubW positions probe together: one LDS round trip per
             // probe step for all of them (most find their key at once)
-            uint32_t tag[kSubW], slot[kSubW];
+            uint32_t slot[kSubW];
             bool pend[kSubW];
 #pragma unroll
             for (int k = 0; k < kSubW; ++k) {
-                tag[k] = lo[k] | ((uint32_t)klen << 24);  // never 0
-                slot[k] = (uint32_t)(((uint64_t)(lo[k] * 0x9E3779B1u) * kH2) >> 32);
+                slot[k] = (uint32_t)(((uint64_t)(lo[k] * 0x9E3779B1u) * kK2) >> 32);
                 pend[k] = valid[k];
             }
-            for (int t = 0; t < kH2Probe; ++t) {
+            for (int t = 0; t < kK2Probe; ++t) {
                 uint32_t cur[kSubW];
 #pragma unroll
                 for (int k = 0; k < kSubW; ++k) cur[k] = pend[k] ? k2[slot[k]] : 0u;
@@ -803,15 +811,17 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveS
 #pragma unroll
                 for (int k = 0; k < kSubW; ++k) {
                     if (!pend[k]) continue;
-                    if (cur[k] == 0u) {
-                        const uint32_t old = atomicCAS(&k2[slot[k]], 0u, tag[k]);
-                        cur[k] = old == 0u ? tag[k] : old;
+                    if (cur[k] == kK2Empty &&
+                        atomicCAS(&k2[slot[k]], kK2Empty, (lo[k] << 16) | 1u) == kK2Empty) {
+                        pend[k] = false;  // inserted with count 1
+                        continue;
                     }
-                    if (cur[k] == tag[k]) {
-                        __hip_atomic_fetch_add(&c2[slot[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (cur[k] == kK2Empty) cur[k] = k2[slot[k]];  // lost the race: see who won
+                    if ((cur[k] >> 16) == lo[k]) {
+                        __hip_atomic_fetch_add(&k2[slot[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         pend[k] = false;
                     } else {
-                        slot[k] = slot[k] + 1u == kH2 ? 0u : slot[k] + 1u;
+                        slot[k] = (slot[k] + 1u) & (kK2 - 1u);
                         any = true;
                     }
                 }
@@ -831,11 +841,15 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveS
                 r[k] = make_rec(((uint64_t)hi[k] << 32) | lo[k], klen, (uint32_t)w.lang, 1, p.lb, p.cb);
             }
         }
+        if (emit_ablated(p, 4)) {
+#pragma unroll
+            for (int k = 0; k < kSubW; ++k) has[k] = false;
+        }
         emit_recs(S, has, r, lane);
         w.p0 += 64 * kSubW;
         if (w.p0 >= nwin) {
             __builtin_amdgcn_wave_barrier();
-            if (klen == 2 || klen == 3) {
+            if (klen == 2 && w.len < kK2MaxDoc && !emit_ablated(p, 1)) {
                 w.phase = kHFlush;
                 w.cursor = 0;
             } else {
@@ -848,28 +862,24 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveS
         }
         return;
     }
-    if (w.phase == kHFlush) {  // this gram length's 2-/3-byte keys, 64 kSubW slots a step
+    if (w.phase == kHFlush) {  // this gram length's 2-byte keys, 64 kSubW slots a step
 #pragma unroll
         for (int k = 0; k < kSubW; ++k) {
-            const int slot = w.cursor + 64 * k + lane;
-            if (slot >= (int)kH2) continue;
-            const uint32_t tag = k2[slot];
-            if (!tag) continue;
-            const uint32_t c = c2[slot];
-            k2[slot] = 0u;
-            c2[slot] = 0u;
-            const int kl = (int)(tag >> 24);
-            const uint32_t bytes = tag & 0xffffffu;
+            const uint32_t slot = (uint32_t)w.cursor + 64u * k + lane;
+            const uint32_t v = k2[slot];
+            if (v == kK2Empty) continue;
+            k2[slot] = kK2Empty;
+            const uint32_t c = v & 0xffffu;
             if (c <= cmax) {
                 has[k] = true;
-                r[k] = make_rec(bytes, kl, (uint32_t)w.lang, c, p.lb, p.cb);
+                r[k] = make_rec(v >> 16, 2, (uint32_t)w.lang, c, p.lb, p.cb);
             } else {
-                add_count(p.direct, ((uint64_t)kl << 56) | bytes, w.lang, c);
+                add_count(p.direct, (2ull << 56) | (uint64_t)(v >> 16), w.lang, c);
             }
         }
         emit_recs(S, has, r, lane);
         w.cursor += 64 * kSubW;
-        if (w.cursor >= (int)kH2) {
+        if (w.cursor >= (int)kK2) {
             __builtin_amdgcn_wave_barrier();
             next_gram(p, w);
             if (w.phase == kWin) {
@@ -925,7 +935,7 @@ __device__ __forceinline__ void flush_block(const PartParams& p, EmitLds& S, uin
         const uint64_t r = S.blk[i];
         const uint32_t at =
             __hip_atomic_fetch_add(&S.pfill[q1_of(r, p.cb)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        p.rec[rb + at] = r;
+        if (!emit_ablated(p, 2)) p.rec[rb + at] = r;
     }
     if (tid <= kQ) p.blk_hdr[(size_t)gid * kHdr + tid] = S.pstart[tid];
     if (tid == 0) {
@@ -946,7 +956,7 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartPara
     const int64_t rbase = p.wg_rec[bid], dbase = p.wg_dir[bid];
     for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64) S.hist2[i] = 0u;
     for (int i = lane; i < 256; i += 64) S.h1[wave][i] = 0u;
-    for (int i = lane; i < (int)kH2; i += 64) S.k2[wave][i] = S.c2[wave][i] = 0u;
+    for (int i = lane; i < (int)kK2; i += 64) S.k2[wave][i] = kK2Empty;
     if (tid < kQ) S.pcnt[tid] = 0u;
     if (tid == 0) {
         S.blk_n = 0u;

@@ -140,7 +140,7 @@ hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const u
 // 52..57 (4096 buckets), slot = low 32 bits (LDS hash in a bucket).
 constexpr int kQBits = 6;
 constexpr int kQ = 1 << kQBits;                 // buckets per level
-constexpr int kBlkRecs = 8192;                  // records per emit block (LDS)
+constexpr int kBlkRecs = 6144;                  // records per emit block (LDS); flushed above 2048
 constexpr int kRoundRecs = 4096;                // records one emit round can add (16 waves x 64 lanes x 4)
 constexpr int kHdr = 68;                        // u32 per block header (kQ + 1 used)
 constexpr int kEmitWaves = 16;
@@ -157,6 +157,9 @@ struct PartParams {
     int32_t nG;
     int32_t G[kMaxGramLengths];
     uint32_t lb, cb;            // language / count bit widths of a record
+    int32_t ablate;             // diagnostics build only (LDGPU_FIT_EMIT_ABLATE; compiled out otherwise):
+                                // bit 0 2-byte windows skip the LDS table (records instead), bit 1 the
+                                // block flush skips its global stores, bit 2 no records at all
     // emit (phase A): workgroup w owns documents [wg_doc[w], wg_doc[w+1]),
     // records [wg_rec[w], ...) (capacity: its windows) and block ids
     // [wg_dir[w], ...); blocks are sorted by q1 with a kHdr header
