@@ -544,6 +544,20 @@ __device__ __forceinline__ int count_sb(const uint64_t (&m)[kSub]) {
 template <bool STAGED>
 __device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc& src, int32_t p0, int lane,
                                              Windows& x) {
+    if constexpr (STAGED) {
+        // the four positions of a lane are 64 B apart: one byte shift, and
+        // their dwords at immediate offsets from one address
+        const uint32_t a = (uint32_t)(src.base + p0) + (uint32_t)lane;
+        const uint32_t sh = a & 3u;
+        const uint32_t* w = src.lds + (a >> 2);
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            const uint32_t w0 = w[16 * k], w1 = w[16 * k + 1], w2 = w[16 * k + 2];
+            x.lo[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            x.hi[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
         uint32_t w0, w1, w2, sh;
@@ -557,7 +571,7 @@ __device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc&
 // a key (exact bitmaps: never a false positive) names its one language in
 // LDS, and its count is added there -- no queue, no verification.  Windows of
 // the last sub-block past nw are masked per lane.
-template <int N>
+template <int N, bool FULL>
 __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                              const Windows& x, int32_t nw, int lane) {
     const uint8_t* l1 = reinterpret_cast<const uint8_t*>(img + p.direct_off);
@@ -571,23 +585,27 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 #pragma unroll
         for (int k = 0; k < kSub; ++k) lang[k] = l1[x.lo[k] & 0xffu];
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) hit[k] = lang[k] != 0xffu && 64 * k + lane < nw;
+        for (int k = 0; k < kSub; ++k) hit[k] = lang[k] != 0xffu;
     } else {
-        uint32_t w[kSub], idx[kSub], base[kSub];
+        uint32_t w[kSub], base[kSub];
 #pragma unroll
         for (int k = 0; k < kSub; ++k) {
-            idx[k] = (x.lo[k] >> 5) & 2047u;
-            w[k] = img[kBmp1Words + idx[k]];
-            base[k] = b2[idx[k]];
+            const uint32_t idx = __builtin_amdgcn_ubfe(x.lo[k], 5, 11);
+            w[k] = img[kBmp1Words + idx];
+            base[k] = b2[idx];
         }
 #pragma unroll
         for (int k = 0; k < kSub; ++k) {
-            const uint32_t b = x.lo[k] & 31u;
-            hit[k] = ((w[k] >> b) & 1u) && 64 * k + lane < nw;
+            // bit (lo & 31) of the word; the offset / width operands of v_bfe
+            // take their low 5 bits, so no masking
+            hit[k] = __builtin_amdgcn_ubfe(w[k], x.lo[k], 1) != 0u;
             // rank of the key among the 2-byte keys (in range for every lane)
-            lang[k] = l2[base[k] + __builtin_popcount(w[k] & ((1u << b) - 1u))];
+            lang[k] = l2[base[k] + __builtin_popcount(__builtin_amdgcn_ubfe(w[k], 0, x.lo[k]))];
         }
     }
+    // FULL: more than 192 windows, so only the last sub-block is cut
+#pragma unroll
+    for (int k = FULL ? kSub - 1 : 0; k < kSub; ++k) hit[k] = hit[k] && 64 * k + lane < nw;
 #pragma unroll
     for (int k = 0; k < kSub; ++k)
         if (hit[k]) __hip_atomic_fetch_add(&cnt[lang[k]], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -613,9 +631,10 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                             const DocSrc& src, uint32_t dummy_a) {
     if (!((p.fast_mask >> N) & 1u)) return;
+    if (ablated(p, N <= 2 ? 8 : 16)) return;
     if constexpr (N <= 2) {
         if (p.direct_words) {
-            direct_count<N>(p, wl, img, x, len - N + 1, lane);
+            direct_count<N, FULL>(p, wl, img, x, len - N + 1, lane);
             return;
         }
     }
