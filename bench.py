@@ -214,7 +214,7 @@ def traffic_from_profiles(workload_key):
         except Exception:
             continue
         if d.get("workload_key") == workload_key:
-            return d.get("traffic_bytes_per_launch")
+            return d
     return None
 
 
@@ -303,7 +303,8 @@ def fit_main(args, world, rank, local, dev, backend):
         "windows_counted_exactly_once": windows_ok,
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
-                     "traffic": traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}"),
+                     "traffic": (traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}") or {}
+                                 ).get("traffic_bytes_per_launch"),
                      "kernel": "count (emit + part2 + reduce + merge)", "count_ms": round(count_s * 1e3, 3),
                      "algorithmic_bytes_per_count": int(algo)},
     }
@@ -436,8 +437,11 @@ def main():
                     f":K={args.profile_size}")
     if args.config == 2:
         workload_key = f"score:docs={n_docs}:bytes={args.doc_min}:L={args.langs}:G={args.grams}:K={args.profile_size}"
+    prof = traffic_from_profiles(workload_key) or {}
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(workload_key),
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": prof.get("traffic_bytes_per_launch"),
+                # TCC hit / (hit + miss) of the same launch (tools/pmc_traffic.sh)
+                "l2_hit_rate": (prof.get("l2") or {}).get("hit_rate"), "workload_key": workload_key,
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "lookups_per_s": round(windows / (kernel_ms * 1e-3), 1)}
 

@@ -346,6 +346,7 @@ struct ldgpu_model {
     int count_sign = 0;        // mode 3: sign of the shared value
     uint32_t direct_off = 0, direct_words = 0;  // mode 3: direct tables in the image (ScoreParams)
     bool count_int_argmax = false;  // mode 3: label = first max of the counts (monotone fold)
+    bool pack_ok = false;           // mode 3: short documents may be scored in packs (score_pack)
     int32_t* d_err = nullptr;
     unsigned long long* d_stats = nullptr;  // LDGPU_STATS diagnostics (printed at destroy)
 };
@@ -799,6 +800,16 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     if (e == hipSuccess) e = upload(&m->d_fold, fold, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
     m->lds_bytes = score_lds_bytes(S, m->mode, image_words);
+    // packs of short documents need kPackDocs counter blocks per wave: only
+    // when that keeps the workgroups per CU (the prepared LDS limit is then
+    // the packed size; a launch without packing asks for less)
+    if (m->mode == 3 && m->count_int_argmax && !diag_env("LDGPU_NO_PACK")) {
+        const size_t packed = score_lds_bytes(S, 3, image_words, true);
+        if (packed <= 163840 && 163840 / packed >= 163840 / m->lds_bytes) {
+            m->pack_ok = true;
+            m->lds_bytes = packed;
+        }
+    }
     int resident = 0;
     if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->lds_bytes, &resident);
     // persistent grid = what is resident; never more workgroups than the LDS admits
@@ -811,9 +822,9 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     }
     if (diag_env("LDGPU_DEBUG"))
         fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d direct=%u slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
-                        "resident_api=%d wg_per_cu=%d\n",
+                        "resident_api=%d wg_per_cu=%d pack=%d\n",
                 (long long)nk, m->mode, m->direct_words, S, (unsigned long long)bwords, (int)m->lds_filter, m->lds_bytes, resident,
-                m->wg_per_cu);
+                m->wg_per_cu, (int)m->pack_ok);
     if (e != hipSuccess) {
         model_free(m);
         return fail(e == hipErrorOutOfMemory ? LDGPU_ENOMEM : LDGPU_EDEVICE, "model upload: %s",
@@ -876,6 +887,9 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.count_sign = m->count_sign;
     // counts stay below 2^24: c <= windows of a document <= len * n_grams
     p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;
+    // packs of short documents (labels only; the kernel packs documents of
+    // maxg..128 bytes)
+    p.pack = m->pack_ok && !d_scores && mean < 192.0;
     p.err = d_err;
     p.stats = m->d_stats;
     p.L = m->L;

@@ -61,6 +61,9 @@ struct ScoreParams {
     // base2[2048] u16 (rank of each 2-byte bitmap word), lang2[n2] u8
     uint32_t direct_off;
     uint32_t direct_words;      // 0: no direct tables
+    // count mode: consecutive short documents are scored in packs
+    // (score_pack; the hit area holds kPackDocs counter blocks)
+    int32_t pack;
 };
 
 // Launch configuration of the score kernel.
@@ -82,18 +85,23 @@ constexpr int kBufWords = kBufBytes / 4 + 4;
 constexpr int kMaxLdsBloomLog2 = 14;       // bloom words in LDS up to 64 KiB
 constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
 
+// documents per pack of short documents (count mode, score_pack)
+constexpr uint32_t kPackDocs = 4;
+
 // per-wave hit area (u32 words): ordered modes hold 64 verified hits of
 // (S + 2) / 2 uint4 each; count mode (3) holds the probe's 64 dummy-store
-// words and the 64 S per-language counters
-constexpr uint32_t hit_area_words(int slices, int mode) {
-    return mode == 3 ? 64u * (1u + (uint32_t)slices) : 64u * 4u * (((uint32_t)slices + 2u) / 2u);
+// words and the 64 S u32 per-language counters (packing: kPackDocs blocks of
+// 64 S u16 counters)
+constexpr uint32_t hit_area_words(int slices, int mode, bool pack = false) {
+    return mode == 3 ? 64u * (1u + (pack ? kPackDocs / 2u : 1u) * (uint32_t)slices)
+                     : 64u * 4u * (((uint32_t)slices + 2u) / 2u);
 }
 
 // bytes of dynamic LDS the score kernel needs; image_words = the filter image
 // staged in LDS (bitmaps, the bloom when it fits, direct tables)
-inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words) {
-    return (size_t)image_words * 4u +
-           (size_t)kScoreWaves * (kQueueCap * 4u + hit_area_words(slices, mode) * 4u + 2u * kBufWords * 4u + 64u * 4u);
+inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool pack = false) {
+    return (size_t)image_words * 4u + (size_t)kScoreWaves * (kQueueCap * 4u + hit_area_words(slices, mode, pack) * 4u +
+                                                              2u * kBufWords * 4u + 64u * 4u);
 }
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values

@@ -90,6 +90,17 @@ struct WaveLds {
 // which take the probe's dummy stores (append_sb); hit_area_words(S, 3).
 __device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return reinterpret_cast<uint32_t*>(w.hits) + 64; }
 
+// counter idx += inc: u32 counters, or (PACK: packed short documents) u16
+// counters two to a word -- a document of a pack has at most 256 windows per
+// gram length, so no count carries into its neighbour
+template <bool PACK>
+__device__ __forceinline__ void count_inc(uint32_t* cnt, uint32_t idx, uint32_t inc) {
+    if constexpr (PACK)
+        __hip_atomic_fetch_add(&cnt[idx >> 1], inc << ((idx & 1u) << 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        __hip_atomic_fetch_add(&cnt[idx], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Where a document's bytes are read from: the wave's LDS buffer (staged
 // group: byte `base` of the buffer) or global memory (byte `base` of p.bytes).
 struct DocSrc {
@@ -197,7 +208,10 @@ __device__ __forceinline__ bool bucket_find(const Bucket* b, uint64_t key, uint6
 
 // weighted (MODE 3 fast path, distinct gram lengths): a hit of a k-byte key
 // counts p.mult[k] times (k's multiplicity in gramLengths).
-template <int S, int MODE, bool STAGED, bool KEYED>
+// PACK (MODE 3, packed short documents, score_pack): an entry's position is
+// its low 8 bits and bits 8..9 name the document of the pack, whose (u16)
+// counter block it counts into.
+template <int S, int MODE, bool STAGED, bool KEYED, bool PACK = false>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
                                       double (&acc)[S], int lane, bool weighted = false) {
     __builtin_amdgcn_wave_barrier();
@@ -208,12 +222,14 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         uint64_t m0 = 0;
         uint32_t lang1 = 0xffffffffu;  // count mode: the row's one language (Slot::pad)
         uint32_t inc = 1;
+        uint32_t coff = 0;  // PACK: the document's counter block
         if (j < qn) {
             const uint32_t e = w.queue[j];
             const int klen = (int)(e >> kPosBits);
             if (MODE == 3 && weighted) inc = p.mult[klen];
+            if (PACK) coff = ((e >> 8) & (kPackDocs - 1u)) * 64u * S;
             uint32_t w0, w1, w2, sh;
-            window_words<STAGED>(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
+            window_words<STAGED>(p, src, (int64_t)(e & (PACK ? 255u : (1u << kPosBits) - 1u)), w0, w1, w2, sh);
             const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
                                  __builtin_amdgcn_alignbyte(w1, w0, sh);
             const uint64_t key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
@@ -270,9 +286,9 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             // uniform-value table: order-free per-language hit counts (the
             // score is the fold of that many adds of the one value, applied
             // at the end of the document: count_scores)
-            if (S > 1 && good && lang1 != 0xffffffffu) {
+            if (good && lang1 != 0xffffffffu) {
                 // single-language row: no mask words to read (no extra lines)
-                __hip_atomic_fetch_add(&count_area(w)[lang1], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                count_inc<PACK>(count_area(w), coff + lang1, inc);
             } else if (good) {
                 uint32_t* cnt = count_area(w);
 #pragma unroll
@@ -282,7 +298,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                     while (mm) {
                         const int l = __builtin_ctzll(mm);
                         mm &= mm - 1;
-                        __hip_atomic_fetch_add(&cnt[64 * s + l], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        count_inc<PACK>(cnt, coff + 64 * s + l, inc);
                     }
                 }
             }
@@ -379,9 +395,8 @@ __device__ __forceinline__ void count_scores(const ScoreParams& p, const WaveLds
 // maximum of the scores is the first maximum of c (value > 0), of -c
 // (value < 0) or index 0 (value 0).  One integer DPP max over
 // (key << 8 | 255 - l); clears the counters.
-template <int S>
-__device__ __forceinline__ int count_argmax(const ScoreParams& p, const WaveLds& w, int lane) {
-    uint32_t* cnt = count_area(w);
+template <int S, typename C = uint32_t>
+__device__ __forceinline__ int count_argmax(const ScoreParams& p, C* cnt, int lane) {
     uint32_t best = 0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -440,29 +455,34 @@ __device__ __forceinline__ uint64_t lanes_below(int32_t n) {  // n in [1, 64]
     return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
 }
 
+// the filter word and bit position of sub-block k's window
+template <int KIND>
+__device__ __forceinline__ void filter_word(const uint32_t* img, uint32_t sh, uint32_t mul, const FWords& f,
+                                            const Windows& x, int k, uint32_t& w, uint32_t& bit) {
+    if constexpr (KIND == 1) {
+        w = img[(x.lo[k] >> 5) & 7u];
+        bit = x.lo[k];
+    } else if constexpr (KIND == 2) {
+        w = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
+        bit = x.lo[k];
+    } else if constexpr (KIND == 3) {
+        w = f.w3[k];
+        bit = mulhi24(__builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh), mul);
+    } else {  // KIND 4, keyed bloom: sh = key length, mul = unused
+        const uint32_t lo = sh >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * sh)) - 1u);
+        const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh - 4))) - 1u);
+        const uint32_t h = kb_hash(lo, hi, sh);
+        w = f.gb[h >> f.gshift];
+        bit = h >> (f.gshift - 5);
+    }
+}
+
 template <int KIND, int NSB>
 __device__ __forceinline__ void test_len(const uint32_t* img, uint32_t sh, uint32_t mul, const FWords& f,
                                          const Windows& x, int32_t nw, uint64_t (&m)[kSub]) {
     uint32_t w[NSB], bit[NSB];
 #pragma unroll
-    for (int k = 0; k < NSB; ++k) {
-        if constexpr (KIND == 1) {
-            w[k] = img[(x.lo[k] >> 5) & 7u];
-            bit[k] = x.lo[k];
-        } else if constexpr (KIND == 2) {
-            w[k] = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
-            bit[k] = x.lo[k];
-        } else if constexpr (KIND == 3) {
-            w[k] = f.w3[k];
-            bit[k] = mulhi24(__builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh), mul);
-        } else {  // KIND 4, keyed bloom: sh = key length, mul = unused
-            const uint32_t lo = sh >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * sh)) - 1u);
-            const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh - 4))) - 1u);
-            const uint32_t h = kb_hash(lo, hi, sh);
-            w[k] = f.gb[h >> f.gshift];
-            bit[k] = h >> (f.gshift - 5);
-        }
-    }
+    for (int k = 0; k < NSB; ++k) filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
 #pragma unroll
     for (int k = 0; k < NSB; ++k) {
         const uint32_t c = __builtin_amdgcn_ubfe(w[k], bit[k], 1);
@@ -571,9 +591,16 @@ __device__ __forceinline__ void load_windows(const ScoreParams& p, const DocSrc&
 // a key (exact bitmaps: never a false positive) names its one language in
 // LDS, and its count is added there -- no queue, no verification.  Windows of
 // the last sub-block past nw are masked per lane.
-template <int N, bool FULL>
+// PACK: position k of the lane is valid while N <= rem[k] (bytes to the end of
+// its document) and counts into its document's block (tb[k] >> 8).
+struct PackPos {
+    int32_t rem[kSub];  // bytes from the position to the end of its document (<= 0: none)
+    uint32_t tb[kSub];  // document index << 8 | position in the pack
+};
+
+template <int N, bool FULL, int S = 1, bool PACK = false>
 __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
-                                             const Windows& x, int32_t nw, int lane) {
+                                             const Windows& x, int32_t nw, int lane, const PackPos* pk = nullptr) {
     const uint8_t* l1 = reinterpret_cast<const uint8_t*>(img + p.direct_off);
     const uint16_t* b2 = reinterpret_cast<const uint16_t*>(img + p.direct_off + 64);
     const uint8_t* l2 = reinterpret_cast<const uint8_t*>(img + p.direct_off + 64 + 1024);
@@ -603,12 +630,20 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
             lang[k] = l2[base[k] + __builtin_popcount(__builtin_amdgcn_ubfe(w[k], 0, x.lo[k]))];
         }
     }
-    // FULL: more than 192 windows, so only the last sub-block is cut
+    if constexpr (PACK) {
 #pragma unroll
-    for (int k = FULL ? kSub - 1 : 0; k < kSub; ++k) hit[k] = hit[k] && 64 * k + lane < nw;
+        for (int k = 0; k < kSub; ++k) {
+            hit[k] = hit[k] && pk->rem[k] >= N;
+            lang[k] += (pk->tb[k] >> 8) * 64u * S;
+        }
+    } else {
+        // FULL: more than 192 windows, so only the last sub-block is cut
+#pragma unroll
+        for (int k = FULL ? kSub - 1 : 0; k < kSub; ++k) hit[k] = hit[k] && 64 * k + lane < nw;
+    }
 #pragma unroll
     for (int k = 0; k < kSub; ++k)
-        if (hit[k]) __hip_atomic_fetch_add(&cnt[lang[k]], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (hit[k]) count_inc<PACK>(cnt, lang[k], inc);
 }
 
 // Count-mode fast path, gram length N (straight-line code for N = 1..7, so
@@ -626,14 +661,18 @@ __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds&
     if (!ablated(p, 1)) flush<S, 3, STAGED, KEYED>(p, wl, qn, src, acc, lane, true);
 }
 
+// fm: p.fast_mask, bit kFmDirect = direct tables present (one SGPR, see
+// probe_count_all)
+constexpr int kFmDirect = 16;
+
 template <int N, bool FULL, int S, bool STAGED, bool KEYED>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
-                                            const DocSrc& src, uint32_t dummy_a) {
-    if (!((p.fast_mask >> N) & 1u)) return;
+                                            const DocSrc& src, uint32_t dummy_a, uint32_t fm) {
+    if (!((fm >> N) & 1u)) return;
     if (ablated(p, N <= 2 ? 8 : 16)) return;
     if constexpr (N <= 2) {
-        if (p.direct_words) {
+        if ((fm >> kFmDirect) & 1u) {
             direct_count<N, FULL>(p, wl, img, x, len - N + 1, lane);
             return;
         }
@@ -656,13 +695,105 @@ template <bool FULL, int S, bool STAGED, bool KEYED>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                                 const DocSrc& src, uint32_t dummy_a) {
-    probe_count<1, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<2, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<3, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<4, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<5, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<6, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
-    probe_count<7, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a);
+    // the per-length switches as bits of one SGPR, re-read per document (the
+    // compiler otherwise hoists seven lane-mask booleans out of the document
+    // loop and spills them to VGPR lanes: two v_readlane per test)
+    uint32_t fm = __builtin_amdgcn_readfirstlane(p.fast_mask | (p.direct_words ? 1u << kFmDirect : 0u));
+    asm volatile("" : "+s"(fm));
+    probe_count<1, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<2, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<3, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<4, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<5, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<6, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<7, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+}
+
+// Packed short documents (count mode): up to kPackDocs consecutive documents
+// of maxg..256 bytes, 256 bytes in all, share one superblock laid over their
+// contiguous bytes -- position j is byte j of the pack.  A window is a window
+// of the reference (LanguageDetectorModel.scala:139-144, all full-length as
+// len >= maxg) iff it ends inside its own document: N <= rem (bytes from j to
+// that document's end).  Hits count into the document's own counter block;
+// each document's label is its block's count argmax.  Three 64-B documents
+// per wave-pass instead of one: the lanes a lone short document leaves idle
+// do the next documents' windows.
+template <int N, int S, bool KEYED>
+__device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                           const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
+                                           const DocSrc& src, uint32_t dummy_a, uint32_t fm) {
+    if (!((fm >> N) & 1u)) return;
+    if constexpr (N <= 2) {
+        if ((fm >> kFmDirect) & 1u) {
+            direct_count<N, false, S, true>(p, wl, img, x, 0, lane, &pk);
+            return;
+        }
+    }
+    constexpr int KIND = N < 3 ? N : (KEYED ? 4 : 3);
+    constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
+    uint64_t m[kSub];
+    uint32_t w[kSub], bit[kSub];
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) m[k] = __ballot(__builtin_amdgcn_ubfe(w[k], bit[k], 1) != 0u && pk.rem[k] >= N);
+    if (qn + count_sb(m) > kQueueCap) {
+        double acc[S];  // unused in count mode
+        flush<S, 3, true, KEYED, true>(p, wl, qn, src, acc, lane, true);
+        qn = 0;
+    }
+    const uint32_t qbase = (uint32_t)(uintptr_t)wl.queue;
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        if (m[k]) {
+            const uint32_t off =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
+            const uint32_t a = select_by_mask(m[k], qbase + 4u * ((uint32_t)qn + off), dummy_a);
+            *(lds_u32*)(size_t)a = ((uint32_t)N << kPosBits) | pk.tb[k];
+            qn += __popcll(m[k]);
+        }
+    }
+}
+
+// One pack: documents [i, i + nd) of the staged group, ends e1 < e2 < e3 <=
+// tot relative to the pack's first byte (unused ends = tot); labels to
+// wl.labels[i ..).
+template <int S, bool KEYED>
+__device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                        const uint32_t* bloom, const DocSrc& src, int32_t e1, int32_t e2,
+                                        int32_t e3, int32_t tot, int nd, int i, int lane) {
+    Windows x;
+    load_windows<true>(p, src, 0, lane, x);
+    FWords f;
+    load_fwords<KEYED>(p, bloom, x, f);
+    PackPos pk;
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const int32_t j = 64 * k + lane;
+        const uint32_t d = (uint32_t)(j >= e1) + (uint32_t)(j >= e2) + (uint32_t)(j >= e3);
+        const int32_t end = j < e1 ? e1 : (j < e2 ? e2 : (j < e3 ? e3 : tot));
+        pk.rem[k] = end - j;
+        pk.tb[k] = (d << 8) | (uint32_t)j;
+    }
+    uint32_t fm = __builtin_amdgcn_readfirstlane(p.fast_mask | (p.direct_words ? 1u << kFmDirect : 0u));
+    asm volatile("" : "+s"(fm));
+    const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
+    int qn = 0;
+    probe_pack<1, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    probe_pack<2, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    probe_pack<3, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    probe_pack<4, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    probe_pack<5, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    probe_pack<6, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    probe_pack<7, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    if (qn) {
+        double acc[S];
+        flush<S, 3, true, KEYED, true>(p, wl, qn, src, acc, lane, true);
+    }
+    for (int q = 0; q < nd; ++q) {
+        const int lab = count_argmax<S>(p, reinterpret_cast<uint16_t*>(count_area(wl)) + q * 64 * S, lane);
+        if (lane == 0) wl.labels[i + q] = lab;
+    }
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
@@ -749,7 +880,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     if (ablated(p, 1)) qn = 0;
     if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
-        if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, wl, lane);
+        if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
         count_scores<S>(p, wl, acc, lane);
     }
 
@@ -840,15 +971,14 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     const uint32_t* bloom = FLDS ? lds + kBloomBase : p.filter + kBloomBase;
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
-    constexpr uint32_t kHitW = hit_area_words(S, MODE);
+    const uint32_t kHitW = hit_area_words(S, MODE, MODE == 3 && p.pack);
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap + wave * kHitW);
     wl.buf = lds + img_words + kScoreWaves * (kQueueCap + kHitW) + wave * 2 * kBufWords;
     wl.labels = lds + img_words + kScoreWaves * (kQueueCap + kHitW + 2 * kBufWords) + wave * 64;
 
     if constexpr (MODE == 3) {
         uint32_t* cnt = count_area(wl);
-#pragma unroll
-        for (int s = 0; s < S; ++s) cnt[64 * s + lane] = 0;
+        for (int s = 0; s < S * (p.pack ? (int)kPackDocs / 2 : 1); ++s) cnt[64 * s + lane] = 0;
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -895,12 +1025,36 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
         }
         __builtin_amdgcn_wave_barrier();
         if (staged) {
-            for (int i = 0; i < cnt; ++i) {
+            for (int i = 0; i < cnt;) {
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{cur, b - s0};
+                if constexpr (MODE == 3) {
+                    // a pack of consecutive short documents (score_pack);
+                    // p.pack is set only without score output, with count
+                    // argmax and fast lengths
+                    if (p.pack && len >= p.maxg && len <= 128) {
+                        int32_t e[kPackDocs];
+                        e[0] = (int32_t)len;
+                        int nd = 1;
+                        while (nd < kPackDocs && i + nd < cnt) {
+                            const int64_t l2 = rdlane_i64(offv, i + nd + 1) - rdlane_i64(offv, i + nd);
+                            if (l2 < p.maxg || e[nd - 1] + l2 > 64 * kSub) break;
+                            e[nd] = e[nd - 1] + (int32_t)l2;
+                            ++nd;
+                        }
+                        if (nd > 1) {
+                            const int32_t tot = e[nd - 1];
+                            score_pack<S, !FLDS>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
+                                                 nd > 3 ? e[2] : tot, tot, nd, i, lane);
+                            i += nd;
+                            continue;
+                        }
+                    }
+                }
                 const int lab = score_doc<S, MODE, true, !FLDS>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
+                ++i;
             }
         } else {
             for (int i = 0; i < cnt; ++i) {
@@ -923,7 +1077,8 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
 
 template <int S, int MODE, bool FLDS>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
-    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words);
+    const size_t lds =
+        score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words, MODE == 3 && p.pack);
     hipLaunchKernelGGL((score_kernel<S, MODE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }

@@ -183,6 +183,64 @@ def test_single_language_keys_direct_tables(L, grams, direct, monkeypatch):
     assert m.info()["mode"] == 2
 
 
+def _single_language_table(rng, L, grams, alphabet, n_keys, v):
+    table = {}
+    for _ in range(n_keys):
+        n = int(rng.choice(grams))
+        row = [0.0] * L
+        row[int(rng.integers(0, L))] = v
+        table[bytes(rng.choice(alphabet, size=n))] = row
+    return table
+
+
+@pytest.mark.parametrize("L,grams,single", [
+    (20, [1, 2, 3, 4, 5], True), (100, [1, 2, 3, 4, 5], True), (100, [2, 1, 2, 3], False),
+    (255, [1, 2, 7], True), (3, [3, 5], False), (130, [1, 2, 3, 4, 5, 6, 7], False),
+])
+def test_packed_short_documents(L, grams, single):
+    """Count mode, labels only (transform): consecutive documents of
+    maxg..128 bytes share one 256-position superblock (score_pack), each with
+    its own counters; windows must not cross a document boundary.  Lengths
+    straddle every case: shorter than maxg (partial windows, general path),
+    packs of 2..4, a document that does not fit the open pack, > 128."""
+    rng = np.random.default_rng(L * 5 + len(grams) + int(single))
+    alphabet = np.frombuffer(b"abcdefghij ", dtype=np.uint8)
+    v = math.log(2.0)
+    table = (_single_language_table(rng, L, grams, alphabet, 900, v) if single
+             else _random_table(rng, L, 600, grams, alphabet, True, uniform=v))
+    lens = rng.integers(0, 100, size=3000)
+    lens[:16] = [0, 1, 2, 7, 8, 64, 64, 64, 64, 63, 65, 128, 129, 256, 40, 40]
+    lens[1000:1100] = rng.integers(max(grams), 70, size=100)
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = DeviceModel(table, L, grams)
+    labels, _ = m.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(labels, ol), np.nonzero(labels != ol)[0][:10]
+    assert m.info()["mode"] == 2
+
+
+def test_packed_path_taken(monkeypatch, capfd):
+    """The diagnostics library reports whether a model packs short documents;
+    LDGPU_NO_PACK turns packing off and the labels stay the same."""
+    rng = np.random.default_rng(3)
+    alphabet = np.frombuffer(b"abcdefghij ", dtype=np.uint8)
+    L, grams = 100, [1, 2, 3, 4, 5]
+    table = _single_language_table(rng, L, grams, alphabet, 900, math.log(2.0))
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in rng.integers(20, 90, size=2000)]
+    data, off = encoding.pack(docs)
+    monkeypatch.setenv("LDGPU_DEBUG", "1")
+    packed = DeviceModel(table, L, grams, variant="diag")
+    assert "pack=1" in capfd.readouterr().err
+    a, _ = packed.score(data, off, want_scores=False)
+    monkeypatch.setenv("LDGPU_NO_PACK", "1")
+    plain = DeviceModel(table, L, grams, variant="diag")
+    assert "pack=0" in capfd.readouterr().err
+    b, _ = plain.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(a, ol) and np.array_equal(b, ol)
+
+
 def test_long_documents_and_hot_keys():
     """Every 1-gram in the table: every window hits, so the per-wave candidate
     queue flushes many times per document (order must survive the flushes)."""

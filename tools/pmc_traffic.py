@@ -32,6 +32,12 @@ def main(out):
         xs = kernel_values(os.path.join(out, name), ctr)
         # last dispatch = a timed launch (warm table, warm caches as in the bench)
         res[name] = xs[-1] * 1024.0 if xs else None
+    # L2 hit rate of the same (last, timed) launch: TCC requests that hit
+    hits = kernel_values(os.path.join(out, "l2_real"), "TCC_HIT_sum")
+    miss = kernel_values(os.path.join(out, "l2_real"), "TCC_MISS_sum")
+    l2 = None
+    if hits and miss and hits[-1] + miss[-1] > 0:
+        l2 = {"hits": hits[-1], "misses": miss[-1], "hit_rate": round(hits[-1] / (hits[-1] + miss[-1]), 4)}
     real = json.load(open(os.path.join(out, "fetch_real.json")))
     cfg = real["config"]
     n_docs, doc_b = cfg["docs_per_gpu"], cfg["doc_bytes"]
@@ -42,11 +48,13 @@ def main(out):
     traffic = None
     if f_read and f_write:
         traffic = res["fetch_real"] * f_read + res["write_real"] * f_write
-    wl = (f"score:docs={n_docs}:bytes={doc_b}:L={cfg['languages']}:G={','.join(map(str, cfg['gram_lengths']))}"
-          f":K={cfg['profile_size']}")
+    wl = real["roofline"].get("workload_key") or (
+        f"score:docs={n_docs}:bytes={doc_b}:L={cfg['languages']}:G={','.join(map(str, cfg['gram_lengths']))}"
+        f":K={cfg['profile_size']}")
     doc = {"workload_key": wl, "counters_bytes": res, "known_cal_read": known_read, "known_cal_write": known_write,
            "read_factor": f_read, "write_factor": f_write,
            "traffic_bytes_per_launch": round(traffic) if traffic else None,
+           "l2": l2,
            "algorithmic_bytes_per_launch": real["roofline"]["algorithmic_bytes_per_launch"],
            "note": "FETCH_SIZE/WRITE_SIZE (KiB) x 1024, calibrated on an empty-table launch of the same kernel"}
     with open(os.path.join(out, "pmc_traffic.json"), "w") as f:

@@ -2,7 +2,8 @@
 # HBM traffic of the SCORE kernel from PMC counters (MI355X_MICROARCH.md §HBM):
 # FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes (never combined with
 # tracing), each over the real workload and over an empty-table calibration run
-# whose bytes are known exactly (documents + offsets read, labels written).
+# whose bytes are known exactly (documents + offsets read, labels written),
+# plus the L2 (TCC) hit / miss counts of the real workload.
 # Writes $OUT/pmc_traffic.json (copy it to profiles/ to have bench.py report it).
 # Usage: tools/pmc_traffic.sh <outdir> [bench args...]
 set -u
@@ -22,4 +23,5 @@ run fetch_real FETCH_SIZE "$@"
 run write_real WRITE_SIZE "$@"
 run fetch_cal FETCH_SIZE --empty-table "$@"
 run write_cal WRITE_SIZE --empty-table "$@"
+run l2_real "TCC_HIT_sum TCC_MISS_sum" "$@"
 python3 tools/pmc_traffic.py "$OUT"
