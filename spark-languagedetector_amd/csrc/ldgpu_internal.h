@@ -45,7 +45,7 @@ struct ScoreParams {
     int32_t ablate;             // diagnostics build only (LDGPU_ABLATE; compiled out otherwise): bit 0 skip
                                 // verify/accumulate, bit 1 skip probe, bit 2 skip the hit replay, bit 3
                                 // skip count-mode 1-/2-byte direct counts, bit 4 skip count-mode >= 3-byte
-                                // tests
+                                // tests, bit 5 skip the count argmax (labels 0)
     int32_t nG;
     int32_t G[kMaxGramLengths];
     // fast path (documents of maxg..256 bytes: every window full-length):

@@ -718,11 +718,37 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
 // each document's label is its block's count argmax.  Three 64-B documents
 // per wave-pass instead of one: the lanes a lone short document leaves idle
 // do the next documents' windows.
+// keyed Bloom hash of sub-block k's N-byte window (filter_word, KIND 4)
+template <int N>
+__device__ __forceinline__ uint32_t keyed_hash(const Windows& x, int k) {
+    const uint32_t lo = N >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * N)) - 1u);
+    const uint32_t hi = N <= 4 ? 0u : x.hi[k] & ((1u << (8 * (N - 4))) - 1u);
+    return kb_hash(lo, hi, (uint32_t)N);
+}
+
+// keyed Bloom (global memory): the words of lengths 3..2+kPreN are loaded
+// before the first test, so a pack waits one L2 round trip, not one per
+// length; the tests recompute the bit position (VALU is cheap next to the
+// latency).  Longer lengths load at their test (registers).
+constexpr int kPreN = 3;
+
+template <int N>
+__device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x, uint32_t fm, uint32_t (&kw)[kPreN][kSub]) {
+    if constexpr (N - 3 < kPreN) {
+        if ((fm >> N) & 1u) {
+#pragma unroll
+            for (int k = 0; k < kSub; ++k) kw[N - 3][k] = f.gb[keyed_hash<N>(x, k) >> f.gshift];
+        }
+    }
+}
+
 template <int N, int S, bool KEYED>
 __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
-                                           const DocSrc& src, uint32_t dummy_a, uint32_t fm) {
+                                           const DocSrc& src, uint32_t dummy_a, uint32_t fm,
+                                           const uint32_t (&kw)[kPreN][kSub]) {
     if (!((fm >> N) & 1u)) return;
+    if (ablated(p, N <= 2 ? 8 : 16)) return;
     if constexpr (N <= 2) {
         if ((fm >> kFmDirect) & 1u) {
             direct_count<N, false, S, true>(p, wl, img, x, 0, lane, &pk);
@@ -734,7 +760,14 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
     uint64_t m[kSub];
     uint32_t w[kSub], bit[kSub];
 #pragma unroll
-    for (int k = 0; k < kSub; ++k) filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
+    for (int k = 0; k < kSub; ++k) {
+        if constexpr (KIND == 4 && N - 3 < kPreN) {
+            w[k] = kw[N - 3][k];
+            bit[k] = keyed_hash<N>(x, k) >> (f.gshift - 5);
+        } else {
+            filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
+        }
+    }
 #pragma unroll
     for (int k = 0; k < kSub; ++k) m[k] = __ballot(__builtin_amdgcn_ubfe(w[k], bit[k], 1) != 0u && pk.rem[k] >= N);
     if (qn + count_sb(m) > kQueueCap) {
@@ -779,18 +812,26 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
     asm volatile("" : "+s"(fm));
     const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
     int qn = 0;
-    probe_pack<1, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
-    probe_pack<2, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
-    probe_pack<3, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
-    probe_pack<4, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
-    probe_pack<5, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
-    probe_pack<6, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
-    probe_pack<7, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm);
+    if (ablated(p, 2)) fm = 0;
+    uint32_t kw[kPreN][kSub];
+    if constexpr (KEYED) {
+        keyed_preload<3>(f, x, fm, kw);
+        keyed_preload<4>(f, x, fm, kw);
+        keyed_preload<5>(f, x, fm, kw);
+    }
+    probe_pack<1, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<2, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<3, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<4, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<5, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<6, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<7, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    if (ablated(p, 1)) qn = 0;
     if (qn) {
         double acc[S];
         flush<S, 3, true, KEYED, true>(p, wl, qn, src, acc, lane, true);
     }
-    for (int q = 0; q < nd; ++q) {
+    for (int q = 0; q < (ablated(p, 32) ? 0 : nd); ++q) {
         const int lab = count_argmax<S>(p, reinterpret_cast<uint16_t*>(count_area(wl)) + q * 64 * S, lane);
         if (lane == 0) wl.labels[i + q] = lab;
     }
@@ -880,6 +921,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     if (ablated(p, 1)) qn = 0;
     if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
+        if (ablated(p, 32)) return 0;
         if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
         count_scores<S>(p, wl, acc, lane);
     }
@@ -955,7 +997,9 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
     r0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0));
 }
 
-template <int S, int MODE, bool FLDS>
+// PACK (count mode only): a separate instantiation with the pack path, so the
+// pack path's registers never burden the single-document kernels
+template <int S, int MODE, bool FLDS, bool PACK = false>
 __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
@@ -971,14 +1015,15 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     const uint32_t* bloom = FLDS ? lds + kBloomBase : p.filter + kBloomBase;
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
-    const uint32_t kHitW = hit_area_words(S, MODE, MODE == 3 && p.pack);
+    constexpr uint32_t kHitW = hit_area_words(S, MODE, PACK);
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap + wave * kHitW);
     wl.buf = lds + img_words + kScoreWaves * (kQueueCap + kHitW) + wave * 2 * kBufWords;
     wl.labels = lds + img_words + kScoreWaves * (kQueueCap + kHitW + 2 * kBufWords) + wave * 64;
 
     if constexpr (MODE == 3) {
         uint32_t* cnt = count_area(wl);
-        for (int s = 0; s < S * (p.pack ? (int)kPackDocs / 2 : 1); ++s) cnt[64 * s + lane] = 0;
+#pragma unroll
+        for (int s = 0; s < S * (PACK ? (int)kPackDocs / 2 : 1); ++s) cnt[64 * s + lane] = 0;
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -1029,11 +1074,11 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{cur, b - s0};
-                if constexpr (MODE == 3) {
+                if constexpr (PACK) {
                     // a pack of consecutive short documents (score_pack);
-                    // p.pack is set only without score output, with count
+                    // packing runs only without score output, with count
                     // argmax and fast lengths
-                    if (p.pack && len >= p.maxg && len <= 128) {
+                    if (len >= p.maxg && len <= 128) {
                         int32_t e[kPackDocs];
                         e[0] = (int32_t)len;
                         int nd = 1;
@@ -1077,18 +1122,37 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
 
 template <int S, int MODE, bool FLDS>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
-    const size_t lds =
-        score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words, MODE == 3 && p.pack);
+    const bool pack = MODE == 3 && p.pack;
+    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words, pack);
+    if constexpr (MODE == 3) {
+        if (pack) {
+            hipLaunchKernelGGL((score_kernel<S, MODE, FLDS, true>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((score_kernel<S, MODE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
 
-template <int S, int MODE, bool FLDS>
-hipError_t prepare_t(size_t lds, int* blocks) {
-    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, FLDS>);
+template <int S, int MODE, bool FLDS, bool PACK = false>
+hipError_t prepare_k(size_t lds, int* blocks) {
+    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, FLDS, PACK>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, kScoreWaves * 64, lds);
+}
+
+// count mode prepares both instantiations (single documents, packs); the
+// resident workgroups are the smaller of the two
+template <int S, int MODE, bool FLDS>
+hipError_t prepare_t(size_t lds, int* blocks) {
+    hipError_t e = prepare_k<S, MODE, FLDS>(lds, blocks);
+    if constexpr (MODE == 3) {
+        int b2 = 0;
+        if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, true>(lds, &b2);
+        if (e == hipSuccess) *blocks = std::min(*blocks, b2);
+    }
+    return e;
 }
 
 template <int MODE, bool FLDS>

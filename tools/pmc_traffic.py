@@ -45,18 +45,33 @@ def main(out):
     known_write = 4 * n_docs
     f_read = known_read / res["fetch_cal"] if res["fetch_cal"] else None
     f_write = known_write / res["write_cal"] if res["write_cal"] else None
+    # The empty-table run is the launch's streaming part (documents, offsets),
+    # which FETCH_SIZE counts at half (factor f_read, ~2).  What the real run
+    # fetches beyond it is table / Bloom gathers: random loads, which
+    # FETCH_SIZE counts at one 64-B request each (profiles/r02_gather_cal.json,
+    # tools/gather_cal.hip: factor g_read ~1) -- the streaming factor must not
+    # be applied to them.
+    g_read = 1.0
+    cal = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r02_gather_cal.json")
+    if os.path.exists(cal):
+        fpg = json.load(open(cal)).get("fetch_per_gather_B")
+        if fpg:
+            g_read = 64.0 / fpg
     traffic = None
     if f_read and f_write:
-        traffic = res["fetch_real"] * f_read + res["write_real"] * f_write
+        stream_part = min(res["fetch_cal"], res["fetch_real"])
+        gather_part = res["fetch_real"] - stream_part
+        traffic = stream_part * f_read + gather_part * g_read + res["write_real"] * f_write
     wl = real["roofline"].get("workload_key") or (
         f"score:docs={n_docs}:bytes={doc_b}:L={cfg['languages']}:G={','.join(map(str, cfg['gram_lengths']))}"
         f":K={cfg['profile_size']}")
     doc = {"workload_key": wl, "counters_bytes": res, "known_cal_read": known_read, "known_cal_write": known_write,
-           "read_factor": f_read, "write_factor": f_write,
+           "read_factor": f_read, "gather_read_factor": g_read, "write_factor": f_write,
            "traffic_bytes_per_launch": round(traffic) if traffic else None,
            "l2": l2,
            "algorithmic_bytes_per_launch": real["roofline"]["algorithmic_bytes_per_launch"],
-           "note": "FETCH_SIZE/WRITE_SIZE (KiB) x 1024, calibrated on an empty-table launch of the same kernel"}
+           "note": "FETCH_SIZE/WRITE_SIZE (KiB) x 1024; the streaming part calibrated on an empty-table launch of "
+                   "the same kernel, the remainder (random gathers) at the gather calibration's factor"}
     with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps(doc, indent=1))
