@@ -52,7 +52,7 @@ enum ldgpu_status {
 /* Device-path limits: gram lengths 1..LDGPU_MAX_GRAM (a key packs into one
  * u64: 7 payload bytes + a length byte), 1..LDGPU_MAX_LANGS languages. */
 #define LDGPU_MAX_GRAM 7
-#define LDGPU_MAX_LANGS 256
+#define LDGPU_MAX_LANGS 4096
 #define LDGPU_MAX_GRAM_LENGTHS 32
 
 const char* ldgpu_version(void);

@@ -349,6 +349,9 @@ struct ldgpu_model {
     bool pack_ok = false;           // mode 3: short documents may be scored in packs (score_pack)
     int32_t* d_err = nullptr;
     unsigned long long* d_stats = nullptr;  // LDGPU_STATS diagnostics (printed at destroy)
+    // L > kBlockLangs: one sub-model per block of kBlockLangs languages
+    // (model_build_blocked); this model then holds no table of its own
+    std::vector<ldgpu_model*> blocks;
 };
 
 // mode 3 fold table: fold[c] = ((0.0 + v) + v) ... c times
@@ -357,6 +360,7 @@ constexpr uint32_t kFoldMax = 8191;
 namespace {
 void model_free(ldgpu_model* m) {
     if (!m) return;
+    for (ldgpu_model* b : m->blocks) model_free(b);
     if (m->ctx) (void)hipSetDevice(m->ctx->device);
     if (m->d_stats) {
         unsigned long long st[2] = {0, 0};
@@ -574,8 +578,72 @@ extern "C" int ldgpu_model_create_masks(ldgpu_ctx* ctx, int64_t n_rows, const ui
 }
 
 namespace {
+// L > kBlockLangs: the languages are scored in blocks of kBlockLangs, one
+// sub-model per block holding that block's columns and only the keys with a
+// nonzero entry there (a zero row adds exact zeros: no effect); wrong-length
+// rows stay in every block so a hit still fails.  A document's label is the
+// first maximum over the blocks' maxima (launch_combine_blocks).
+int model_build_blocked(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                        ParsedTable& t, ldgpu_model** out) {
+    const int64_t nk = (int64_t)t.keys.size();
+    const int S = (n_langs + 63) / 64;
+    const int nb = (n_langs + kBlockLangs - 1) / kBlockLangs;
+    auto* m = new ldgpu_model();
+    m->ctx = ctx;
+    m->L = n_langs;
+    m->nG = n_grams;
+    for (int i = 0; i < n_grams; ++i) m->G[i] = gram_lengths[i];
+    m->slices = S;
+    m->dense = t.dense;
+    m->n_keys = nk;
+    for (int b = 0; b < nb; ++b) {
+        const int l0 = b * kBlockLangs, lb = std::min(kBlockLangs, n_langs - l0);
+        const int w0 = l0 / 64, sb = (lb + 63) / 64;
+        ParsedTable tb;
+        tb.dense = t.dense;
+        for (int64_t i = 0; i < nk; ++i) {
+            bool any = t.bad[i] != 0;
+            if (t.dense) {
+                for (int l = 0; l < lb && !any; ++l) any = t.drows[(size_t)i * n_langs + l0 + l] != 0.0;
+            } else {
+                for (int w = 0; w < sb && !any; ++w) any = t.masks[(size_t)i * S + w0 + w] != 0;
+            }
+            if (!any) continue;
+            tb.keys.push_back(t.keys[i]);
+            tb.bad.push_back(t.bad[i]);
+            if (t.dense) {
+                tb.drows.insert(tb.drows.end(), t.drows.begin() + (size_t)i * n_langs + l0,
+                                t.drows.begin() + (size_t)i * n_langs + l0 + lb);
+            } else {
+                for (int w = 0; w < sb; ++w) tb.masks.push_back(t.masks[(size_t)i * S + w0 + w]);
+                tb.vals.push_back(t.vals[i]);
+            }
+        }
+        ldgpu_model* sub = nullptr;
+        if (int rc = model_build(ctx, lb, gram_lengths, n_grams, tb, &sub)) {
+            model_free(m);
+            return rc;
+        }
+        m->blocks.push_back(sub);
+        m->has_bad |= sub->has_bad;
+        m->device_bytes += sub->device_bytes;
+        m->slot_cap += sub->slot_cap;
+    }
+    m->mode = m->blocks[0]->mode;
+    m->filter_log2 = m->blocks[0]->filter_log2;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
+    if (e != hipSuccess) {
+        model_free(m);
+        return fail(LDGPU_EDEVICE, "model upload: %s", hipGetErrorString(e));
+    }
+    *out = m;
+    return ok();
+}
+
 int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ParsedTable& t,
                 ldgpu_model** out) {
+    if (n_langs > kBlockLangs) return model_build_blocked(ctx, n_langs, gram_lengths, n_grams, t, out);
     const int64_t nk = (int64_t)t.keys.size();
     const int S = (n_langs + 63) / 64;
     const bool dense = t.dense;
@@ -854,9 +922,33 @@ extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_
 
 namespace {
 int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
-                 int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st) {
+                 int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st, double* d_best = nullptr,
+                 int block = 0, int64_t score_stride = 0) {
     if (n_docs == 0) return LDGPU_OK;
+    if (!m->blocks.empty()) {
+        // one launch per language block (block labels and maxima in stream-
+        // ordered scratch), then the first maximum across blocks
+        const int nb = (int)m->blocks.size();
+        int32_t* lab = nullptr;
+        double* best = nullptr;
+        HIP_TRY(hipMallocAsync((void**)&lab, sizeof(int32_t) * (size_t)nb * n_docs, st));
+        HIP_TRY(hipMallocAsync((void**)&best, sizeof(double) * (size_t)nb * n_docs, st));
+        int rc = LDGPU_OK;
+        for (int b = 0; b < nb && !rc; ++b)
+            rc = score_launch(m->blocks[b], d_bytes, n_bytes, d_offsets, n_docs, lab + (size_t)b * n_docs,
+                              d_scores ? d_scores + (size_t)b * kBlockLangs : nullptr, d_err, st,
+                              best + (size_t)b * n_docs, b, m->L);
+        hipError_t e = rc ? hipSuccess : launch_combine_blocks(n_docs, nb, lab, best, d_labels, st);
+        (void)hipFreeAsync(lab, st);
+        (void)hipFreeAsync(best, st);
+        if (rc) return rc;
+        HIP_TRY(e);
+        return LDGPU_OK;
+    }
     ScoreParams p{};
+    p.best = d_best;
+    p.block = block;
+    p.score_stride = score_stride;
     p.bytes = d_bytes;
     p.n_bytes = n_bytes;
     p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
@@ -889,7 +981,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;
     // packs of short documents (labels only; the kernel packs documents of
     // maxg..128 bytes)
-    p.pack = m->pack_ok && !d_scores && mean < 192.0;
+    p.pack = m->pack_ok && !d_scores && !d_best && mean < 192.0;
     p.err = d_err;
     p.stats = m->d_stats;
     p.L = m->L;
@@ -1076,6 +1168,13 @@ struct ldgpu_counts {
     int32_t* d_ovf_lang = nullptr;
     unsigned long long* d_ovf_cnt = nullptr;
     unsigned int* d_ovf_n = nullptr;
+    // second overflow list (allocated at the first overflow): re-inserting a
+    // list after a grow may overflow again, into this one
+    uint64_t* d_ovf2_keys = nullptr;
+    int32_t* d_ovf2_lang = nullptr;
+    unsigned long long* d_ovf2_cnt = nullptr;
+    unsigned int* d_ovf2_n = nullptr;
+    uint32_t ovf2_cap = 0;
     uint32_t ovf_cap = 1u << 20;  // windows per sub-launch; grown per call up to kOvfMax
     uint64_t size = 0;
     // FIT v2 (radix-partitioned records, ldgpu_fit.hip): the record format
@@ -1115,7 +1214,8 @@ void counts_free(ldgpu_counts* c) {
     if (!c) return;
     if (c->ctx) (void)hipSetDevice(c->ctx->device);
     for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_size, (void*)c->d_ovf_keys,
-                    (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt, (void*)c->d_ovf_n})
+                    (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt, (void*)c->d_ovf_n, (void*)c->d_ovf2_keys,
+                    (void*)c->d_ovf2_lang, (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
         if (p) (void)hipFree(p);
     delete c;
 }
@@ -1166,19 +1266,62 @@ int after_batch(ldgpu_counts* c) {
     if (novf > c->ovf_cap)  // cannot happen: sub-launches hold <= ovf_cap windows
         return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost)", novf);
     c->size = size;
-    if (2 * (size + novf) > c->cap || novf > 0) {
-        if (int rc = grow(c, next_pow2(4 * (size + novf) + 16))) return rc;
+    if (novf == 0) {
+        if (2 * size > c->cap) {
+            if (int rc = grow(c, next_pow2(4 * size + 16))) return rc;
+        }
+        c->tbl_valid = false;
+        return LDGPU_OK;
     }
-    if (novf > 0) {
+    // Windows whose key found no slot are on the overflow list: grow, then
+    // re-insert them (into the other list when they overflow again) until
+    // none is left.  The list counts windows, duplicates included, not new
+    // keys, so it never sizes the table: the table doubles per round.
+    if (!c->d_ovf2_keys || c->ovf2_cap < c->ovf_cap) {
+        HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+        for (void* q : {(void*)c->d_ovf2_keys, (void*)c->d_ovf2_lang, (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
+            if (q) (void)hipFree(q);
+        c->d_ovf2_keys = nullptr;
+        c->d_ovf2_lang = nullptr;
+        c->d_ovf2_cnt = nullptr;
+        c->d_ovf2_n = nullptr;
+        c->ovf2_cap = 0;
+        hipError_t e = hipMalloc((void**)&c->d_ovf2_keys, sizeof(uint64_t) * c->ovf_cap);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_lang, sizeof(int32_t) * c->ovf_cap);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_cnt, sizeof(unsigned long long) * c->ovf_cap);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_n, sizeof(unsigned int));
+        if (e != hipSuccess) return fail(LDGPU_ENOMEM, "overflow list: %s", hipGetErrorString(e));
+        c->ovf2_cap = c->ovf_cap;
+    }
+    uint64_t* src_k = c->d_ovf_keys;
+    int32_t* src_l = c->d_ovf_lang;
+    unsigned long long* src_c = c->d_ovf_cnt;
+    uint64_t* dst_k = c->d_ovf2_keys;
+    int32_t* dst_l = c->d_ovf2_lang;
+    unsigned long long* dst_c = c->d_ovf2_cnt;
+    unsigned int* dst_n = c->d_ovf2_n;
+    unsigned int* src_n = c->d_ovf_n;
+    uint64_t target = next_pow2(std::max<uint64_t>(2 * c->cap, 4 * size + 16));
+    for (unsigned int n = novf; n > 0;) {
+        if (int rc = grow(c, target)) return rc;
         CountParams p = count_params(c);
-        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream));
-        HIP_TRY(launch_counts_add(p, c->d_ovf_keys, nullptr, c->d_ovf_lang, c->d_ovf_cnt, novf, c->ctx->stream));
+        p.ovf_keys = dst_k;
+        p.ovf_lang = dst_l;
+        p.ovf_cnt = dst_c;
+        p.ovf_n = dst_n;
+        HIP_TRY(hipMemsetAsync(dst_n, 0, sizeof(unsigned int), c->ctx->stream));
+        HIP_TRY(launch_counts_add(p, src_k, nullptr, src_l, src_c, n, c->ctx->stream));
         unsigned int again = 0;
-        HIP_TRY(hipMemcpyAsync(&again, c->d_ovf_n, sizeof again, hipMemcpyDeviceToHost, c->ctx->stream));
+        HIP_TRY(hipMemcpyAsync(&again, dst_n, sizeof again, hipMemcpyDeviceToHost, c->ctx->stream));
         HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
         HIP_TRY(hipStreamSynchronize(c->ctx->stream));
-        if (again) return fail(LDGPU_ENOMEM, "count table overflow after growing");
         c->size = size;
+        n = again;
+        std::swap(src_k, dst_k);
+        std::swap(src_l, dst_l);
+        std::swap(src_c, dst_c);
+        std::swap(src_n, dst_n);
+        target = 2 * c->cap;
     }
     c->tbl_valid = false;
     return LDGPU_OK;
@@ -2140,7 +2283,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(db.alloc(&d_seg, L + 1));
     HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), sizeof(int64_t) * (L + 1), hipMemcpyHostToDevice, st));
     if (!cm || cm->world == 1) {
-        HIP_TRY(launch_topk_candidates((int64_t)cn, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, nullptr, st));
+        HIP_TRY(launch_topk_candidates((int64_t)cn, L, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, nullptr, st));
     } else {
         // each rank's need[l] smallest candidates can hold the global ones:
         // gather those prefixes, the need[l]-th smallest key of language l is
@@ -2148,7 +2291,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         uint64_t *d_sk, *d_thr;
         HIP_TRY(db.alloc(&d_sk, cn));
         HIP_TRY(db.alloc(&d_thr, L));
-        HIP_TRY(launch_topk_candidates((int64_t)cn, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, d_sk, st));
+        HIP_TRY(launch_topk_candidates((int64_t)cn, L, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, d_sk, st));
         std::vector<int64_t> take(L, 0);
         int64_t tot = 0;
         for (int l = 0; l < L; ++l) tot += take[l] = std::min<int64_t>(need[l], seg[l + 1] - seg[l]);

@@ -196,7 +196,15 @@ __global__ void counts_add_kernel(const CountParams p, const uint64_t* keys, con
     const int64_t s = find_or_insert(p, keys[i], new_key);
     count_new_keys(p, new_key);
     if (s < 0) {
-        atomicAdd(p.ovf_n, 1u);  // cannot happen after a grow; reported as table full
+        // no slot: entries of the (key, language, count) form go to the
+        // overflow list (re-inserted after a grow, after_batch); a row form
+        // entry is reported as table full
+        const unsigned int at = atomicAdd(p.ovf_n, 1u);
+        if (lang_of && at < p.ovf_cap) {
+            p.ovf_keys[at] = keys[i];
+            p.ovf_lang[at] = lang_of[i];
+            p.ovf_cnt[at] = cnt_of ? cnt_of[i] : 1ull;
+        }
         return;
     }
     if (lang_of) {
@@ -514,14 +522,17 @@ hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const ui
 // Threshold-class tie resolution on the device (filterTopGrams' take(K),
 // LanguageDetector.scala:113-119, under the build's (length, bytes) tie rule):
 // two stable LSD radix sorts -- by sort_key (59 bits), then by language
-// (8 bits) -- leave each language's candidates contiguous and in tie order.
+// (ceil(log2 L) bits) -- leave each language's candidates contiguous and in
+// tie order.
 // Sort keys are unique per gram, so this picks exactly the set nth_element
 // picked on the host.  Synchronises `stream` before returning (scratch freed).
-hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const uint64_t* cand_key,
+hipError_t launch_topk_candidates(int64_t cn, int L, const int32_t* cand_lang, const uint64_t* cand_key,
                                   const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
                                   uint8_t* chosen, uint64_t* sorted_keys, hipStream_t stream) {
     if (cn <= 0) return hipSuccess;
     const int n = (int)cn;
+    int lbits = 1;
+    while ((1 << lbits) < L) ++lbits;
     uint64_t* key_out = nullptr;
     uint32_t *perm_a = nullptr, *perm_b = nullptr, *lang_a = nullptr, *lang_b = nullptr;
     void* tmp = nullptr;
@@ -529,7 +540,7 @@ hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const ui
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp1, cand_key, key_out, perm_a, perm_b, n, 0, 59,
                                                       stream);
     if (e == hipSuccess)
-        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, 8, stream);
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, lbits, stream);
     if (e == hipSuccess) e = hipMalloc((void**)&key_out, sizeof(uint64_t) * cn);
     if (e == hipSuccess) e = hipMalloc((void**)&perm_a, sizeof(uint32_t) * cn);
     if (e == hipSuccess) e = hipMalloc((void**)&perm_b, sizeof(uint32_t) * cn);
@@ -548,7 +559,7 @@ hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const ui
         e = hipGetLastError();
     }
     if (e == hipSuccess)
-        e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, 8, stream);
+        e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp2, lang_a, lang_b, perm_b, perm_a, n, 0, lbits, stream);
     if (e == hipSuccess && sorted_keys) {  // distributed: each language's sorted candidate keys, no marking
         hipLaunchKernelGGL(gather_u64_kernel, dim3(grid_of(cn, 256)), dim3(256), 0, stream, cn, perm_a, cand_key,
                            sorted_keys);

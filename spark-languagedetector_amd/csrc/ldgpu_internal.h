@@ -64,7 +64,17 @@ struct ScoreParams {
     // count mode: consecutive short documents are scored in packs
     // (score_pack; the hit area holds kPackDocs counter blocks)
     int32_t pack;
+    // language blocks (L > kBlockLangs: one launch per block of languages,
+    // ldgpu_api.hip): per document this block's maximum score (block 0 with
+    // a NaN first score: +inf, the reference keeps index 0), the block index
+    // (the NaN-first rule is block 0's only) and the scores' row stride
+    double* best;
+    int32_t block;
+    int64_t score_stride;       // 0: L
 };
+
+// languages per block of a blocked model (L > kBlockLangs)
+constexpr int kBlockLangs = 256;
 
 // Launch configuration of the score kernel.
 #ifndef LDGPU_SCORE_WAVES
@@ -108,6 +118,10 @@ inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool p
 // (fma accumulate), 2 = dense fp64 rows, 3 = mask rows sharing one finite
 // value (per-language hit counts); lds_bloom = bloom staged in LDS
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream);
+// label[i] = the first block maximum over nb language blocks (block b's
+// labels / maxima at lab + b n, best + b n)
+hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out,
+                                 hipStream_t stream);
 // sets the dynamic-LDS limit and returns the resident workgroups per CU
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu);
 
@@ -226,7 +240,7 @@ hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const ui
 // chosen[idx[i]] = 1
 // sorted_keys (nullable): instead of marking, write the candidates' sort keys
 // in (language, key) order (the distributed top-K takes each segment's prefix)
-hipError_t launch_topk_candidates(int64_t cn, const int32_t* cand_lang, const uint64_t* cand_key,
+hipError_t launch_topk_candidates(int64_t cn, int L, const int32_t* cand_lang, const uint64_t* cand_key,
                                   const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
                                   uint8_t* chosen, uint64_t* sorted_keys, hipStream_t stream);
 // chosen[cand_idx[i]] = 1 when cand_key[i] <= thr[cand_lang[i]]

@@ -922,7 +922,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
         if (ablated(p, 32)) return 0;
-        if (!p.scores && len <= p.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
+        if (!p.scores && !p.best && len <= p.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
         count_scores<S>(p, wl, acc, lane);
     }
 
@@ -946,9 +946,14 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             found = true;
         }
     }
-    if (__builtin_isnan(rdlaned(acc[0], 0))) label = 0;
+    // breeze keeps index 0 when the first score is NaN (NaN never compares
+    // greater); in a language block other than the first, a NaN is just
+    // never the maximum
+    const bool nan_first = p.block == 0 && __builtin_isnan(rdlaned(acc[0], 0));
+    if (nan_first) label = 0;
+    if (p.best && lane == 0) p.best[doc] = nan_first ? __builtin_inf() : M;
     if (p.scores) {
-        double* out = p.scores + doc * (int64_t)p.L;
+        double* out = p.scores + doc * (p.score_stride ? p.score_stride : (int64_t)p.L);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int l = s * 64 + lane;
@@ -1187,7 +1192,32 @@ hipError_t prepare_m(int slices, bool lds_bloom, size_t lds, int* blocks) {
     return lds_bloom ? prepare_s<MODE, true>(slices, lds, blocks) : prepare_s<MODE, false>(slices, lds, blocks);
 }
 
+// first maximum across language blocks: block maxima compared with '>' in
+// block order, as breeze's argmax compares scores in language order
+__global__ void combine_blocks_kernel(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t l = lab[i];
+    double m = best[i];
+    for (int b = 1; b < nb; ++b) {
+        const double v = best[(int64_t)b * n + i];
+        if (v > m) {
+            m = v;
+            l = kBlockLangs * b + lab[(int64_t)b * n + i];
+        }
+    }
+    out[i] = l;
+}
+
 }  // namespace
+
+hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out,
+                                 hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(combine_blocks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, nb, lab, best,
+                       out);
+    return hipGetLastError();
+}
 
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream) {
     switch (mode) {

@@ -28,7 +28,7 @@ LDGPU_EDEVICE = 4
 LDGPU_EUNSUPPORTED = 5
 LDGPU_ENODEV = 6
 MAX_GRAM = 7
-MAX_LANGS = 256
+MAX_LANGS = 4096
 
 _p = ctypes.c_void_p
 _pp = ctypes.POINTER(ctypes.c_void_p)

@@ -64,7 +64,8 @@ def test_validation_order_kat():
 
 
 @pytest.mark.parametrize("L,grams,n_docs", [(3, [1, 2, 3], 300), (20, [1, 2, 3, 4, 5], 2000),
-                                            (70, [7, 1, 4, 4], 1500), (200, [1, 2, 3], 1200)])
+                                            (70, [7, 1, 4, 4], 1500), (200, [1, 2, 3], 1200),
+                                            (300, [1, 2, 3, 4], 1500)])
 def test_counts_match_c_oracle(L, grams, n_docs):
     ls = synth.make_languages(L, seed=L)
     data, off, lang = synth.generate(ls, n_docs, 0, 700, seed=L + 1)
@@ -202,6 +203,34 @@ def _topk_table_from_counts(keys, cnt, L, K):
         order = np.lexsort((idx, -v))
         chosen[order[:K]] = True
     return {keys[i]: [float(w[i]) if pres[i, l] else 0.0 for l in range(L)] for i in np.nonzero(chosen)[0]}
+
+
+def test_fit_and_score_more_than_256_languages():
+    """L > 256: FIT counts / top-K unchanged in form (mask words ceil(L/64)),
+    and the model scores in language blocks of 256 (one launch per block,
+    first maximum across blocks): labels and fp64 scores bit-identical to the
+    oracle, dense-built and mask-built, labels-only too."""
+    from languagedetection.runtime import DeviceModel
+    L, grams, K = 300, [1, 2, 3], 25
+    ls = synth.make_languages(L, seed=77)
+    data, off, lang = synth.generate(ls, 8 * L, 50, 300, seed=78)
+    counts = DeviceCounts(L, grams)
+    counts.count(data, off, lang)
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(data, off, lang, L, grams)
+    assert keys == okeys and np.array_equal(cnt, ocnt)
+    dense = counts.fit_table(K)
+    assert dense == _topk_table_from_counts(okeys, ocnt, L, K)
+    kb, ko, masks, vals = counts.fit_table_masks(K)
+    counts.close()
+    sdata, soff, _ = synth.generate(ls, 3000, 0, 300, seed=79)
+    ol, osc = OC.Table(dense, L).score(grams, sdata, soff, want_scores=True, nthreads=8)
+    for m in (DeviceModel(dense, L, grams), DeviceModel.from_masks(kb, ko, masks, vals, L, grams)):
+        labels, scores = m.score(sdata, soff, want_scores=True)
+        assert np.array_equal(labels, ol)
+        assert np.array_equal(scores.view(np.uint64), osc.view(np.uint64))
+        only, _ = m.score(sdata, soff, want_scores=False)
+        assert np.array_equal(only, ol)
 
 
 def test_config3_shape_counts_and_table():

@@ -241,6 +241,42 @@ def test_packed_path_taken(monkeypatch, capfd):
     assert np.array_equal(a, ol) and np.array_equal(b, ol)
 
 
+@pytest.mark.parametrize("L", [257, 300, 520])
+@pytest.mark.parametrize("form", ["count", "mask", "dense"])
+def test_language_blocks(L, form):
+    """More than 256 languages: one launch per block of 256 languages, the
+    label the first maximum across the blocks' maxima (ties keep the earlier
+    block).  Uniform-value tables make cross-block ties common."""
+    rng = np.random.default_rng(L + len(form))
+    alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+    grams = [1, 2, 3, 4]
+    if form == "dense":
+        table = _random_table(rng, L, 300, grams, alphabet, False)
+    else:
+        table = _random_table(rng, L, 300, grams, alphabet, True, uniform=math.log(2.0) if form == "count" else None)
+    lens = rng.integers(0, 300, size=800)
+    lens[:6] = [0, 1, 2, 40, 64, 256]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, grams, data, off)
+    labels, _ = m.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(labels, ol)
+
+
+def test_language_blocks_nan_and_inf():
+    """NaN / inf rows across blocks: a NaN first score keeps label 0 (block 0
+    only); a NaN in a later block never wins; +inf in a later block wins."""
+    L = 300
+    nan, inf = float("nan"), float("inf")
+    row = lambda pairs: [pairs.get(l, 0.0) for l in range(L)]
+    table = {b"a": row({0: nan, 5: 1.0}), b"b": row({256: nan, 3: 2.0}), b"c": row({290: inf, 1: 5.0}),
+             b"d": row({260: 7.0, 2: 7.0}), b"e": row({280: 9.0})}
+    docs = [b"a", b"b", b"c", b"d", b"e", b"ab", b"bc", b"de", b"", b"zz"]
+    data, off = encoding.pack(docs)
+    check_parity(table, L, [1], data, off)
+
+
 def test_long_documents_and_hot_keys():
     """Every 1-gram in the table: every window hits, so the per-wave candidate
     queue flushes many times per document (order must survive the flushes)."""
