@@ -661,6 +661,30 @@ __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds&
     if (!ablated(p, 1)) flush<S, 3, STAGED, KEYED>(p, wl, qn, src, acc, lane, true);
 }
 
+// keyed Bloom hash of sub-block k's N-byte window (filter_word, KIND 4)
+template <int N>
+__device__ __forceinline__ uint32_t keyed_hash(const Windows& x, int k) {
+    const uint32_t lo = N >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * N)) - 1u);
+    const uint32_t hi = N <= 4 ? 0u : x.hi[k] & ((1u << (8 * (N - 4))) - 1u);
+    return kb_hash(lo, hi, (uint32_t)N);
+}
+
+// keyed Bloom (global memory): the words of lengths 3..2+kPreN are loaded
+// before the first test, so a pack waits one L2 round trip, not one per
+// length; the tests recompute the bit position (VALU is cheap next to the
+// latency).  Longer lengths load at their test (registers).
+constexpr int kPreN = 3;
+
+template <int N>
+__device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x, uint32_t fm, uint32_t (&kw)[kPreN][kSub]) {
+    if constexpr (N - 3 < kPreN) {
+        if ((fm >> N) & 1u) {
+#pragma unroll
+            for (int k = 0; k < kSub; ++k) kw[N - 3][k] = f.gb[keyed_hash<N>(x, k) >> f.gshift];
+        }
+    }
+}
+
 // fm: p.fast_mask, bit kFmDirect = direct tables present (one SGPR, see
 // probe_count_all)
 constexpr int kFmDirect = 16;
@@ -680,10 +704,11 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
     constexpr int KIND = N < 3 ? N : (KEYED ? 4 : 3);
     constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
     uint64_t m[kSub];
-    if constexpr (FULL)
+    if constexpr (FULL) {
         test_len<KIND, 4>(img, sh, mul, f, x, len - N + 1, m);
-    else
+    } else {
         test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
+    }
     if (qn + count_sb(m) > kQueueCap) {
         flush_count<S, STAGED, KEYED>(p, wl, qn, src, lane);
         qn = 0;
@@ -718,30 +743,6 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
 // each document's label is its block's count argmax.  Three 64-B documents
 // per wave-pass instead of one: the lanes a lone short document leaves idle
 // do the next documents' windows.
-// keyed Bloom hash of sub-block k's N-byte window (filter_word, KIND 4)
-template <int N>
-__device__ __forceinline__ uint32_t keyed_hash(const Windows& x, int k) {
-    const uint32_t lo = N >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * N)) - 1u);
-    const uint32_t hi = N <= 4 ? 0u : x.hi[k] & ((1u << (8 * (N - 4))) - 1u);
-    return kb_hash(lo, hi, (uint32_t)N);
-}
-
-// keyed Bloom (global memory): the words of lengths 3..2+kPreN are loaded
-// before the first test, so a pack waits one L2 round trip, not one per
-// length; the tests recompute the bit position (VALU is cheap next to the
-// latency).  Longer lengths load at their test (registers).
-constexpr int kPreN = 3;
-
-template <int N>
-__device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x, uint32_t fm, uint32_t (&kw)[kPreN][kSub]) {
-    if constexpr (N - 3 < kPreN) {
-        if ((fm >> N) & 1u) {
-#pragma unroll
-            for (int k = 0; k < kSub; ++k) kw[N - 3][k] = f.gb[keyed_hash<N>(x, k) >> f.gshift];
-        }
-    }
-}
-
 template <int N, int S, bool KEYED>
 __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
