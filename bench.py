@@ -299,6 +299,7 @@ def fit_main(args, world, rank, local, dev, backend):
                    "parallelism": f"dp{world} (corpus sharded; owner-exchange merge + distributed top-K)"},
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
                      for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
+        "count_s_per_step": [round(float(p[0].get("count_s", 0.0)), 4) for p in parts],
         "count_windows_per_s": round(windows / count_s, 1),
         "windows_counted_exactly_once": windows_ok,
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -193,7 +193,54 @@ struct ldgpu_ctx {
     // context's count tables under `mu` and kept between fits: multi-GB
     // allocations per fit would cost more than the counting itself
     DevBuf f_rec, f_rec2, f_bstart, f_bhdr, f_nblk, f_cnt3, f_wg, f_p2, f_boff, f_okl, f_ocnt, f_on;
+    // device blocks of destroyed / grown count tables and overflow lists,
+    // reused by exact size: a Spark executor fits partition after partition,
+    // and freeing and re-mapping ~10 GB per fit stalls the allocator
+    std::mutex cache_mu;
+    std::vector<std::pair<size_t, void*>> cache;
+    size_t cache_bytes = 0;
 };
+
+namespace {
+constexpr size_t kCacheMaxBytes = 96ull << 30;
+constexpr size_t kCacheMaxBlocks = 32;
+
+hipError_t cache_alloc(ldgpu_ctx* c, void** p, size_t bytes) {
+    {
+        std::lock_guard<std::mutex> g(c->cache_mu);
+        for (size_t i = 0; i < c->cache.size(); ++i) {
+            if (c->cache[i].first == bytes) {
+                *p = c->cache[i].second;
+                c->cache_bytes -= bytes;
+                c->cache.erase(c->cache.begin() + (std::ptrdiff_t)i);
+                return hipSuccess;
+            }
+        }
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory) {  // give the cache back to the device and retry
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(c->cache_mu);
+        for (auto& b : c->cache) (void)hipFree(b.second);
+        c->cache.clear();
+        c->cache_bytes = 0;
+        e = hipMalloc(p, bytes);
+    }
+    return e;
+}
+
+void cache_free(ldgpu_ctx* c, void* p, size_t bytes) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(c->cache_mu);
+    c->cache.emplace_back(bytes, p);
+    c->cache_bytes += bytes;
+    while (!c->cache.empty() && (c->cache_bytes > kCacheMaxBytes || c->cache.size() > kCacheMaxBlocks)) {
+        (void)hipFree(c->cache.front().second);
+        c->cache_bytes -= c->cache.front().first;
+        c->cache.erase(c->cache.begin());
+    }
+}
+}  // namespace
 
 namespace {
 void pipe_destroy(ScorePipe* pp) {
@@ -287,6 +334,7 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
                       &c->f_boff, &c->f_okl, &c->f_ocnt, &c->f_on})
         b->release();
     for (ScorePipe* pp : c->pipes) pipe_destroy(pp);
+    for (auto& b : c->cache) (void)hipFree(b.second);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return ok();
@@ -1212,19 +1260,32 @@ CountParams count_params(const ldgpu_counts* c) {
 
 void counts_free(ldgpu_counts* c) {
     if (!c) return;
-    if (c->ctx) (void)hipSetDevice(c->ctx->device);
-    for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_size, (void*)c->d_ovf_keys,
-                    (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt, (void*)c->d_ovf_n, (void*)c->d_ovf2_keys,
-                    (void*)c->d_ovf2_lang, (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
+    if (c->ctx) {
+        (void)hipSetDevice(c->ctx->device);
+        // table and overflow lists back to the context's cache (no kernel
+        // uses them once the stream drained)
+        (void)hipStreamSynchronize(c->ctx->stream);
+        cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
+        cache_free(c->ctx, c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
+        cache_free(c->ctx, c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
+        cache_free(c->ctx, c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
+    } else {
+        for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_ovf_keys, (void*)c->d_ovf_lang,
+                        (void*)c->d_ovf_cnt})
+            if (p) (void)hipFree(p);
+    }
+    for (void* p : {(void*)c->d_size, (void*)c->d_ovf_n, (void*)c->d_ovf2_keys, (void*)c->d_ovf2_lang,
+                    (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
         if (p) (void)hipFree(p);
     delete c;
 }
 
 int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, unsigned long long** counts) {
-    HIP_TRY(hipMalloc((void**)keys, cap * sizeof(uint64_t)));
-    hipError_t e = hipMalloc((void**)counts, cap * (size_t)c->L * sizeof(unsigned long long));
+    HIP_TRY(cache_alloc(c->ctx, (void**)keys, cap * sizeof(uint64_t)));
+    hipError_t e = cache_alloc(c->ctx, (void**)counts, cap * (size_t)c->L * sizeof(unsigned long long));
     if (e != hipSuccess) {
-        (void)hipFree(*keys);
+        cache_free(c->ctx, *keys, cap * sizeof(uint64_t));
         *keys = nullptr;
         return fail(LDGPU_ENOMEM, "count table of %llu slots: %s", (unsigned long long)cap, hipGetErrorString(e));
     }
@@ -1248,8 +1309,8 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
     CountParams to = count_params(&tmp);
     HIP_TRY(launch_rehash(from, to, c->cap, c->ctx->stream));
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
-    (void)hipFree(c->d_keys);
-    (void)hipFree(c->d_counts);
+    cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
+    cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
     c->d_keys = nk;
     c->d_counts = nc;
     c->cap = new_cap;
@@ -1273,11 +1334,13 @@ int after_batch(ldgpu_counts* c) {
         c->tbl_valid = false;
         return LDGPU_OK;
     }
-    // Windows whose key found no slot are on the overflow list: grow, then
-    // re-insert them (into the other list when they overflow again) until
-    // none is left.  The list counts windows, duplicates included, not new
-    // keys, so it never sizes the table: the table doubles per round.
-    if (!c->d_ovf2_keys || c->ovf2_cap < c->ovf_cap) {
+    // Entries whose key found no slot are on the overflow list: grow, then
+    // re-insert them (into the second list when they overflow again) until
+    // none is left.  The list may count windows, duplicates included (count
+    // kernel), or distinct records (FIT v2 merge), so it sizes the first grow
+    // only within 8x the table; later rounds double.  The second list needs
+    // room for at most this list's entries.
+    if (!c->d_ovf2_keys || c->ovf2_cap < novf) {
         HIP_TRY(hipStreamSynchronize(c->ctx->stream));
         for (void* q : {(void*)c->d_ovf2_keys, (void*)c->d_ovf2_lang, (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
             if (q) (void)hipFree(q);
@@ -1286,12 +1349,12 @@ int after_batch(ldgpu_counts* c) {
         c->d_ovf2_cnt = nullptr;
         c->d_ovf2_n = nullptr;
         c->ovf2_cap = 0;
-        hipError_t e = hipMalloc((void**)&c->d_ovf2_keys, sizeof(uint64_t) * c->ovf_cap);
-        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_lang, sizeof(int32_t) * c->ovf_cap);
-        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_cnt, sizeof(unsigned long long) * c->ovf_cap);
+        hipError_t e = hipMalloc((void**)&c->d_ovf2_keys, sizeof(uint64_t) * novf);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_lang, sizeof(int32_t) * novf);
+        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_cnt, sizeof(unsigned long long) * novf);
         if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf2_n, sizeof(unsigned int));
         if (e != hipSuccess) return fail(LDGPU_ENOMEM, "overflow list: %s", hipGetErrorString(e));
-        c->ovf2_cap = c->ovf_cap;
+        c->ovf2_cap = novf;
     }
     uint64_t* src_k = c->d_ovf_keys;
     int32_t* src_l = c->d_ovf_lang;
@@ -1301,7 +1364,9 @@ int after_batch(ldgpu_counts* c) {
     unsigned long long* dst_c = c->d_ovf2_cnt;
     unsigned int* dst_n = c->d_ovf2_n;
     unsigned int* src_n = c->d_ovf_n;
-    uint64_t target = next_pow2(std::max<uint64_t>(2 * c->cap, 4 * size + 16));
+    uint32_t dst_cap = c->ovf2_cap, src_cap = c->ovf_cap;
+    uint64_t target = std::min<uint64_t>(next_pow2(4 * (size + (uint64_t)novf) + 16), 8 * c->cap);
+    target = std::max<uint64_t>(target, 2 * c->cap);
     for (unsigned int n = novf; n > 0;) {
         if (int rc = grow(c, target)) return rc;
         CountParams p = count_params(c);
@@ -1309,6 +1374,7 @@ int after_batch(ldgpu_counts* c) {
         p.ovf_lang = dst_l;
         p.ovf_cnt = dst_c;
         p.ovf_n = dst_n;
+        p.ovf_cap = dst_cap;
         HIP_TRY(hipMemsetAsync(dst_n, 0, sizeof(unsigned int), c->ctx->stream));
         HIP_TRY(launch_counts_add(p, src_k, nullptr, src_l, src_c, n, c->ctx->stream));
         unsigned int again = 0;
@@ -1321,6 +1387,7 @@ int after_batch(ldgpu_counts* c) {
         std::swap(src_l, dst_l);
         std::swap(src_c, dst_c);
         std::swap(src_n, dst_n);
+        std::swap(src_cap, dst_cap);
         target = 2 * c->cap;
     }
     c->tbl_valid = false;
@@ -1346,18 +1413,18 @@ int ensure_ovf(ldgpu_counts* c, int64_t windows) {
     if (want <= c->ovf_cap && c->d_ovf_keys && c->d_ovf_lang && c->d_ovf_cnt) return LDGPU_OK;
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
     auto drop = [&] {
-        if (c->d_ovf_keys) (void)hipFree(c->d_ovf_keys);
-        if (c->d_ovf_lang) (void)hipFree(c->d_ovf_lang);
-        if (c->d_ovf_cnt) (void)hipFree(c->d_ovf_cnt);
+        cache_free(c->ctx, c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
+        cache_free(c->ctx, c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
+        cache_free(c->ctx, c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
         c->d_ovf_keys = nullptr;
         c->d_ovf_lang = nullptr;
         c->d_ovf_cnt = nullptr;
         c->ovf_cap = 0;
     };
     auto take = [&](uint64_t n) {
-        hipError_t e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * n);
-        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * n);
-        if (e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_cnt, sizeof(unsigned long long) * n);
+        hipError_t e = cache_alloc(c->ctx, (void**)&c->d_ovf_keys, sizeof(uint64_t) * n);
+        if (e == hipSuccess) e = cache_alloc(c->ctx, (void**)&c->d_ovf_lang, sizeof(int32_t) * n);
+        if (e == hipSuccess) e = cache_alloc(c->ctx, (void**)&c->d_ovf_cnt, sizeof(unsigned long long) * n);
         if (e == hipSuccess) c->ovf_cap = (uint32_t)n;
         else drop();
         return e;
@@ -1585,9 +1652,10 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
     int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
     hipError_t e = hipSuccess;
     if (!rc) e = hipMalloc((void**)&c->d_size, sizeof(unsigned long long));
-    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
-    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
-    if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
+    if (!rc && e == hipSuccess) e = cache_alloc(c->ctx, (void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
+    if (!rc && e == hipSuccess) e = cache_alloc(c->ctx, (void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
+    if (!rc && e == hipSuccess)
+        e = cache_alloc(c->ctx, (void**)&c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
     if (!rc && e == hipSuccess) e = hipMalloc((void**)&c->d_ovf_n, sizeof(unsigned int));
     if (!rc && e == hipSuccess) e = hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), ctx->stream);
     if (!rc && e == hipSuccess) e = hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), ctx->stream);
@@ -2143,8 +2211,8 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     }
     if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_rows, sb, (uint8_t*)d_rrows, rb)) return rc;
     // the owned shard, rebuilt: the same key arrives from several ranks
-    (void)hipFree(c->d_keys);
-    (void)hipFree(c->d_counts);
+    cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
+    cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
     c->d_keys = nullptr;
     c->d_counts = nullptr;
     c->cap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
