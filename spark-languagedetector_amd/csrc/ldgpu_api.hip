@@ -778,8 +778,21 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
          !use_buckets; m->slot_cap *= 2) {
         const int slog = log2u(m->slot_cap);
         const uint64_t cmask = m->slot_cap - 1;
-        auto pos1 = [&](uint64_t k) { return mix64(k) >> (64 - slog); };
-        auto pos2 = [&](uint64_t k) { return mix64(k) & cmask; };
+        (void)cmask;
+        if (slog > 32) {
+            delete m;
+            return fail(LDGPU_ENOMEM, "key table: more than 2^32 slots");
+        }
+        auto pos1 = [&](uint64_t k) {
+            uint32_t h1, h2;
+            slot_hash((uint32_t)k, (uint32_t)(k >> 32), h1, h2);
+            return slog ? (uint64_t)(h1 >> (32 - slog)) : 0ull;
+        };
+        auto pos2 = [&](uint64_t k) {
+            uint32_t h1, h2;
+            slot_hash((uint32_t)k, (uint32_t)(k >> 32), h1, h2);
+            return slog ? (uint64_t)(h2 >> (32 - slog)) : 0ull;
+        };
         slots.assign(m->slot_cap, Slot{kEmpty, 0, 0xffffffffu, 0.0, 0});
         bool ok_all = true;
         for (int64_t i = 0; i < nk && ok_all; ++i) {
@@ -1013,6 +1026,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     const uint64_t n_index = m->d_buckets ? m->n_buckets : m->slot_cap;
     p.slot_shift = (uint32_t)(64 - log2u(n_index));
     p.slot_mask = n_index - 1;
+    p.slot_shift32 = (uint32_t)(32 - log2u(n_index));  // cuckoo slots: slot_hash
     p.filter = m->d_filter;
     p.bloom_shift = (uint32_t)(32 - m->filter_log2);
     p.bloom_words = (uint32_t)((uint64_t)1 << m->filter_log2);

@@ -92,6 +92,19 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t k) {
     return k;
 }
 
+// Cuckoo slot positions of the score table (Slot, 2 choices): two 32-bit
+// hashes of 24-bit multiplies over bytes 0..2, 3..5 and (6, length) --
+// full-rate VALU ops, where mix64's 64-bit multiplies are multi-pass -- whose
+// top bits depend on every key bit; slot 1 = h1 >> (32 - log2 cap), slot 2 =
+// h2 >> (32 - log2 cap).  (lo, hi = the key's two 32-bit halves)
+__host__ __device__ __forceinline__ void slot_hash(uint32_t lo, uint32_t hi, uint32_t& h1, uint32_t& h2) {
+    const uint32_t a = lo & 0xffffffu;
+    const uint32_t b = (lo >> 24) | (hi << 8);
+    const uint32_t c = hi >> 16;
+    h1 = mul24(a, 0x9E3779u) ^ mul24(b, 0x85EBCAu) ^ mul24(c ^ (a >> 12), 0xC2B2AFu);
+    h2 = mul24(b ^ (c << 8), 0x27D4EBu) ^ mul24(a, 0x165667u) ^ mul24(c ^ (b >> 12), 0xD3A265u);
+}
+
 __host__ __device__ __forceinline__ int key_len(uint64_t key) { return (int)(key >> 56); }
 
 inline uint64_t pack_key_host(const uint8_t* p, int len) {

@@ -26,8 +26,9 @@ struct ScoreParams {
     double* scores;             // nullable [n_docs][L]
     const Slot* slots;          // open-addressed key -> row table (modes 0-2)
     const Bucket* buckets;      // count mode: bucketed key -> (row, language) table; slot_shift/mask index it
-    uint32_t slot_shift;        // slot = mix64(key) >> slot_shift
+    uint32_t slot_shift;        // bucket = mix64(key) >> slot_shift (or & slot_mask)
     uint64_t slot_mask;
+    uint32_t slot_shift32;      // cuckoo slot = h1 (h2) >> slot_shift32 of slot_hash
     const uint32_t* filter;     // image: bmp1 | bmp2 | bloom (ldgpu_common.h)
     uint32_t bloom_words;       // power of two
     uint32_t bloom_shift;       // bloom word = hash >> bloom_shift (>= 10)

@@ -233,8 +233,8 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
                                  __builtin_amdgcn_alignbyte(w1, w0, sh);
             const uint64_t key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
-            const uint64_t h = mix64(key);
             if (MODE == 3 && KEYED && p.buckets) {  // (buckets only for tables beyond the caches)
+                const uint64_t h = mix64(key);
                 // 4-slot buckets, one 64-B line each: the key is in its primary
                 // bucket, or -- only if that bucket's overflow flag is set -- in
                 // its secondary one (Bucket, ldgpu_common.h)
@@ -253,7 +253,9 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                 // the second slot's loads behind the first one's key test), so
                 // a candidate costs one L2 round trip, not three.
                 const u32x4* sl = reinterpret_cast<const u32x4*>(p.slots);
-                const uint64_t ia = h >> p.slot_shift, ic = h & p.slot_mask;
+                uint32_t h1, h2;
+                slot_hash((uint32_t)key, (uint32_t)(key >> 32), h1, h2);
+                const uint64_t ia = h1 >> p.slot_shift32, ic = h2 >> p.slot_shift32;
                 u32x4 a0 = sl[2 * ia], a1 = sl[2 * ia + 1], c0 = sl[2 * ic], c1 = sl[2 * ic + 1];
                 asm volatile("" : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1));
                 const bool ha = ((((uint64_t)a0.y) << 32) | a0.x) == key;
