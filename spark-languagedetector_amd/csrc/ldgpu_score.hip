@@ -549,7 +549,9 @@ __device__ __forceinline__ void append_sb(uint32_t* queue, uint32_t dummy_a, int
         if (m[k]) {
             const uint32_t off =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            const uint32_t a = select_by_mask(m[k], qbase + 4u * ((uint32_t)qn + off), dummy_a);
+            // the queue's next free word as one scalar: a single v_lshl_add
+            const uint32_t qb = __builtin_amdgcn_readfirstlane(qbase + 4u * (uint32_t)qn);
+            const uint32_t a = select_by_mask(m[k], (off << 2) + qb, dummy_a);
             *(lds_u32*)(size_t)a = tag0 + 64u * k;
             qn += __popcll(m[k]);
         }
@@ -613,8 +615,9 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
     if constexpr (N == 1) {
 #pragma unroll
         for (int k = 0; k < kSub; ++k) lang[k] = l1[x.lo[k] & 0xffu];
+        // (a zero-extended byte: 0xff is its only value >= 0xff)
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) hit[k] = lang[k] != 0xffu;
+        for (int k = 0; k < kSub; ++k) hit[k] = lang[k] < 0xffu;
     } else {
         uint32_t w[kSub], base[kSub];
 #pragma unroll
@@ -784,7 +787,8 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
         if (m[k]) {
             const uint32_t off =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            const uint32_t a = select_by_mask(m[k], qbase + 4u * ((uint32_t)qn + off), dummy_a);
+            const uint32_t qb = __builtin_amdgcn_readfirstlane(qbase + 4u * (uint32_t)qn);
+            const uint32_t a = select_by_mask(m[k], (off << 2) + qb, dummy_a);
             *(lds_u32*)(size_t)a = ((uint32_t)N << kPosBits) | pk.tb[k];
             qn += __popcll(m[k]);
         }
