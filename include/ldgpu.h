@@ -49,9 +49,13 @@ enum ldgpu_status {
     LDGPU_ENODEV = 6         /* no HIP device */
 };
 
-/* Device-path limits: gram lengths 1..LDGPU_MAX_GRAM (a key packs into one
- * u64: 7 payload bytes + a length byte), 1..LDGPU_MAX_LANGS languages. */
-#define LDGPU_MAX_GRAM 7
+/* Device-path limits.  SCORE: gram lengths 1..LDGPU_MAX_GRAM (keys of up to
+ * 7 bytes pack into one u64, 7 payload bytes + a length byte; keys of 8..15
+ * bytes into two words, in a table of their own).  FIT counting: gram lengths
+ * 1..LDGPU_MAX_FIT_GRAM.  1..LDGPU_MAX_LANGS languages (SCORE scores more than
+ * 256 in blocks of 256 languages). */
+#define LDGPU_MAX_GRAM 15      /* SCORE tables: keys of 8..15 bytes take two words */
+#define LDGPU_MAX_FIT_GRAM 7   /* FIT counting: one-word keys */
 #define LDGPU_MAX_LANGS 4096
 #define LDGPU_MAX_GRAM_LENGTHS 32
 

@@ -135,16 +135,16 @@ void par_memcpy(void* dst, const void* src, size_t n) {
     for (auto& x : th) x.join();
 }
 
-int check_grams(const int32_t* G, int32_t nG) {
+int check_grams(const int32_t* G, int32_t nG, int max_len = kMaxGram) {
     if (nG < 0 || nG > LDGPU_MAX_GRAM_LENGTHS)
         return fail(LDGPU_EINVAL, "number of gram lengths %d outside [0, %d]", nG, LDGPU_MAX_GRAM_LENGTHS);
     if (nG > 0 && !G) return fail(LDGPU_EINVAL, "gram_lengths is NULL");
     for (int i = 0; i < nG; ++i) {
         if (G[i] <= 0)
             return fail(LDGPU_EINVAL, "requirement failed: size=%d and step=1, but both must be positive", G[i]);
-        if (G[i] > LDGPU_MAX_GRAM)
+        if (G[i] > max_len)
             return fail(LDGPU_EUNSUPPORTED, "gram length %d exceeds the device path's limit of %d bytes", G[i],
-                        LDGPU_MAX_GRAM);
+                        max_len);
     }
     return LDGPU_OK;
 }
@@ -384,6 +384,8 @@ struct ldgpu_model {
     int ablate = 0;           // diagnostics build only: LDGPU_ABLATE
     size_t device_bytes = 0;
     Slot* d_slots = nullptr;
+    WideSlot* d_wslots = nullptr;  // wide keys (8..15 bytes), nullptr: none
+    uint64_t wslot_cap = 0;
     Bucket* d_buckets = nullptr;  // count mode key table
     uint64_t n_buckets = 0;
     uint32_t* d_filter = nullptr;
@@ -416,7 +418,7 @@ void model_free(ldgpu_model* m) {
             fprintf(stderr, "[ldgpu] stats: candidates verified %llu, hits %llu\n", st[0], st[1]);
         (void)hipFree(m->d_stats);
     }
-    for (void* p : {(void*)m->d_slots, (void*)m->d_buckets, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
+    for (void* p : {(void*)m->d_slots, (void*)m->d_wslots, (void*)m->d_buckets, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
                     (void*)m->d_fold, (void*)m->d_err})
         if (p) (void)hipFree(p);
     delete m;
@@ -439,7 +441,8 @@ namespace {
 // be hit, are dropped), per key a wrong-length flag, and either mask form
 // (masks [n][S], vals [n]) or dense fp64 rows [n][L].
 struct ParsedTable {
-    std::vector<uint64_t> keys;
+    std::vector<uint64_t> keys;          // one-word keys (<= 7 bytes), rows [0, keys.size())
+    std::vector<uint64_t> wlo, whi;      // wide keys (8..15 bytes), rows keys.size() + j
     std::vector<uint8_t> bad;
     bool dense = false;
     std::vector<uint64_t> masks;
@@ -454,18 +457,43 @@ int check_model_args(ldgpu_ctx* ctx, ldgpu_model** out, int64_t n_rows, int32_t 
         return fail(LDGPU_EUNSUPPORTED, "%d languages exceed the device path's limit of %d", n_langs,
                     LDGPU_MAX_LANGS);
     if (n_rows < 0) return fail(LDGPU_EINVAL, "n_rows < 0");
-    return check_grams(gram_lengths, n_grams);
+    return check_grams(gram_lengths, n_grams, kMaxWideGram);  // SCORE tables: two-word keys up to 15 bytes
 }
 
-// unique keys -> source row index (later duplicates win)
+// unique keys -> source row index (later duplicates win); wide keys (8..15
+// bytes) into wlo / whi with their rows after the one-word keys' rows
+struct PairHash {
+    size_t operator()(const std::pair<uint64_t, uint64_t>& k) const { return (size_t)mix64(k.first ^ mix64(k.second)); }
+};
+
 int unique_keys(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets, int maxg,
-                std::vector<uint64_t>& keys, std::vector<int64_t>& src_row) {
+                std::vector<uint64_t>& keys, std::vector<int64_t>& src_row, std::vector<uint64_t>* wlo = nullptr,
+                std::vector<uint64_t>* whi = nullptr) {
     std::unordered_map<uint64_t, int64_t> idx;
     idx.reserve((size_t)n_rows * 2 + 1);
+    std::unordered_map<std::pair<uint64_t, uint64_t>, int64_t, PairHash> widx;
+    std::vector<int64_t> wrow;
     for (int64_t r = 0; r < n_rows; ++r) {
         const int64_t len = key_offsets[r + 1] - key_offsets[r];
         if (len < 0) return fail(LDGPU_EINVAL, "key_offsets decrease at row %lld", (long long)r);
         if (len == 0 || len > maxg) continue;
+        if (len > kMaxGram) {
+            if (!wlo) continue;
+            const uint8_t* b = key_bytes + key_offsets[r];
+            uint64_t lo = 0, hi = (uint64_t)len << 56;
+            for (int i = 0; i < 8; ++i) lo |= (uint64_t)b[i] << (8 * i);
+            for (int i = 8; i < len; ++i) hi |= (uint64_t)b[i] << (8 * (i - 8));
+            auto it = widx.find({lo, hi});
+            if (it == widx.end()) {
+                widx.emplace(std::make_pair(lo, hi), (int64_t)wlo->size());
+                wlo->push_back(lo);
+                whi->push_back(hi);
+                wrow.push_back(r);
+            } else {
+                wrow[it->second] = r;
+            }
+            continue;
+        }
         const uint64_t k = pack_key_host(key_bytes + key_offsets[r], (int)len);
         auto it = idx.find(k);
         if (it == idx.end()) {
@@ -476,6 +504,7 @@ int unique_keys(int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_off
             src_row[it->second] = r;
         }
     }
+    src_row.insert(src_row.end(), wrow.begin(), wrow.end());
     return LDGPU_OK;
 }
 
@@ -554,9 +583,10 @@ extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t*
     if (n_rows > 0 && (!key_bytes || !key_offsets || !rows)) return fail(LDGPU_EINVAL, "table pointer is NULL");
     ParsedTable t;
     std::vector<int64_t> src_row;
-    if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row))
+    if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row,
+                             &t.wlo, &t.whi))
         return rc;
-    const int64_t nk = (int64_t)t.keys.size();
+    const int64_t nk = (int64_t)src_row.size();  // rows: one-word keys, then wide keys
     const int S = (n_langs + 63) / 64;
     t.bad.resize(nk);
     for (int64_t i = 0; i < nk; ++i) t.bad[i] = row_ok && !row_ok[src_row[i]];
@@ -607,9 +637,10 @@ extern "C" int ldgpu_model_create_masks(ldgpu_ctx* ctx, int64_t n_rows, const ui
         return fail(LDGPU_EINVAL, "table pointer is NULL");
     ParsedTable t;
     std::vector<int64_t> src_row;
-    if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row))
+    if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row,
+                             &t.wlo, &t.whi))
         return rc;
-    const int64_t nk = (int64_t)t.keys.size();
+    const int64_t nk = (int64_t)src_row.size();  // rows: one-word keys, then wide keys
     const int S = (n_langs + 63) / 64;
     t.bad.assign(nk, 0);
     t.masks.resize((size_t)nk * S);
@@ -633,7 +664,8 @@ namespace {
 // first maximum over the blocks' maxima (launch_combine_blocks).
 int model_build_blocked(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
                         ParsedTable& t, ldgpu_model** out) {
-    const int64_t nk = (int64_t)t.keys.size();
+    const int64_t nn = (int64_t)t.keys.size();
+    const int64_t nk = nn + (int64_t)t.wlo.size();  // rows: one-word keys, then wide keys
     const int S = (n_langs + 63) / 64;
     const int nb = (n_langs + kBlockLangs - 1) / kBlockLangs;
     auto* m = new ldgpu_model();
@@ -657,7 +689,12 @@ int model_build_blocked(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_len
                 for (int w = 0; w < sb && !any; ++w) any = t.masks[(size_t)i * S + w0 + w] != 0;
             }
             if (!any) continue;
-            tb.keys.push_back(t.keys[i]);
+            if (i < nn) {
+                tb.keys.push_back(t.keys[i]);
+            } else {
+                tb.wlo.push_back(t.wlo[i - nn]);
+                tb.whi.push_back(t.whi[i - nn]);
+            }
             tb.bad.push_back(t.bad[i]);
             if (t.dense) {
                 tb.drows.insert(tb.drows.end(), t.drows.begin() + (size_t)i * n_langs + l0,
@@ -692,7 +729,9 @@ int model_build_blocked(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_len
 int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ParsedTable& t,
                 ldgpu_model** out) {
     if (n_langs > kBlockLangs) return model_build_blocked(ctx, n_langs, gram_lengths, n_grams, t, out);
-    const int64_t nk = (int64_t)t.keys.size();
+    const int64_t nn = (int64_t)t.keys.size();        // one-word keys: rows [0, nn)
+    const int64_t nw = (int64_t)t.wlo.size();         // wide keys: rows [nn, nn + nw)
+    const int64_t nk = nn + nw;
     const int S = (n_langs + 63) / 64;
     const bool dense = t.dense;
     std::vector<uint64_t>& keys = t.keys;
@@ -761,9 +800,9 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // so most lookups read ONE HBM line instead of two slots; cache-resident
     // tables keep the two independent slot loads (one dependent step less)
     // (such a table's bloom never fits LDS: the keyed kernels, which alone read buckets)
-    const bool use_buckets = m->mode == 3 && nk > (1 << 20);
+    const bool use_buckets = m->mode == 3 && nn > (1 << 20);
     if (use_buckets) {
-        for (m->n_buckets = next_pow2(std::max<uint64_t>(16, (uint64_t)nk / 3 + 1));; m->n_buckets *= 2) {
+        for (m->n_buckets = next_pow2(std::max<uint64_t>(16, (uint64_t)nn / 3 + 1));; m->n_buckets *= 2) {
             if (bucket_place(keys, masks, S, t.bad, m->n_buckets, buckets)) break;
             if (m->n_buckets >= (1ull << 32)) {
                 delete m;
@@ -774,7 +813,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         for (int64_t i = 0; i < nk; ++i) m->has_bad |= t.bad[i] != 0;
     }
     for (m->slot_cap = use_buckets ? m->slot_cap
-                                   : next_pow2(std::max<uint64_t>(16, (uint64_t)(2.5 * (double)nk) + 1));
+                                   : next_pow2(std::max<uint64_t>(16, (uint64_t)(2.5 * (double)nn) + 1));
          !use_buckets; m->slot_cap *= 2) {
         const int slog = log2u(m->slot_cap);
         const uint64_t cmask = m->slot_cap - 1;
@@ -795,7 +834,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         };
         slots.assign(m->slot_cap, Slot{kEmpty, 0, 0xffffffffu, 0.0, 0});
         bool ok_all = true;
-        for (int64_t i = 0; i < nk && ok_all; ++i) {
+        for (int64_t i = 0; i < nn && ok_all; ++i) {
             Slot cur{keys[i], (uint32_t)i, 0xffffffffu, 0.0, 0};
             if (!dense) {
                 cur.val = vals[i];
@@ -836,18 +875,72 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         }
     }
 
+    // wide keys (8..15 bytes): their own 2-choice cuckoo table (WideSlot), rows
+    // nn + j of the row arrays
+    std::vector<WideSlot> wslots;
+    if (nw > 0) {
+        for (m->wslot_cap = next_pow2(std::max<uint64_t>(16, (uint64_t)(2.5 * (double)nw) + 1));;
+             m->wslot_cap *= 2) {
+            const int wlog = log2u(m->wslot_cap);
+            if (wlog > 32) {
+                delete m;
+                return fail(LDGPU_ENOMEM, "wide key table: more than 2^32 slots");
+            }
+            auto wpos = [&](const WideSlot& w, int which) {
+                uint32_t h1, h2;
+                wide_hash(w.lo, w.hi, h1, h2);
+                return (uint64_t)((which ? h2 : h1) >> (32 - wlog));
+            };
+            wslots.assign(m->wslot_cap, WideSlot{0, 0, 0, 0xffffffffu, {0, 0}});
+            bool ok_all = true;
+            for (int64_t j = 0; j < nw && ok_all; ++j) {
+                const int64_t i = nn + j;
+                WideSlot cur{t.wlo[j], t.whi[j], (uint32_t)i, 0xffffffffu, {0, 0}};
+                if (!dense) {
+                    int bits = 0;
+                    for (int sidx = 0; sidx < S; ++sidx) {
+                        const uint64_t w = masks[(size_t)i * S + sidx];
+                        if (w && !bits) cur.lang1 = 64u * (uint32_t)sidx + (uint32_t)__builtin_ctzll(w);
+                        bits += __builtin_popcountll(w);
+                    }
+                    if (bits != 1) cur.lang1 = 0xffffffffu;
+                }
+                if (t.bad[i]) {
+                    cur.row |= kBadRow;
+                    m->has_bad = true;
+                }
+                uint64_t at = wpos(cur, 0);
+                if (wslots[at].hi != 0 && wslots[wpos(cur, 1)].hi == 0) at = wpos(cur, 1);
+                bool placed = false;
+                for (int step = 0; step < 2000; ++step) {
+                    if (wslots[at].hi == 0) {  // (hi holds the length: never 0 in a key)
+                        wslots[at] = cur;
+                        placed = true;
+                        break;
+                    }
+                    std::swap(cur, wslots[at]);
+                    const uint64_t a = wpos(cur, 0), b = wpos(cur, 1);
+                    at = at == a ? b : a;
+                }
+                ok_all = placed;
+            }
+            if (ok_all) break;
+        }
+    }
+
     // filter image: exact bitmaps of the 1- and 2-byte keys, then the prefix
     // Bloom filter of the longer ones (ldgpu_common.h).  The bloom is staged
     // in LDS up to 64 KiB, else read from global memory (L2 / Infinity Cache).
     // ~2 keys per 32-bit word (one bit each) keeps false positives at a few
     // percent: they only cost verification lanes (~1 VALU op each, batched 64
     // at a time), while LDS costs resident workgroups.
-    int64_t n_long = 0;
-    for (int64_t i = 0; i < nk; ++i) {
+    int64_t n_long = nw;
+    for (int64_t i = 0; i < nn; ++i) {
         const int kl = key_len(keys[i]);
         m->len_mask |= 1u << kl;
         n_long += kl >= 3;
     }
+    for (int64_t j = 0; j < nw; ++j) m->len_mask |= 1u << key_len(t.whi[j]);
     double kpw = 2.5;
     if (const char* s = diag_env("LDGPU_BLOOM_KPW")) kpw = std::max(0.05, atof(s));  // tuning experiments only
     uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
@@ -856,17 +949,19 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     m->filter_log2 = log2u(bwords);
     const uint32_t bshift = 32u - (uint32_t)m->filter_log2;
     std::vector<uint32_t> filter(kBloomBase + bwords, 0u);
-    for (int64_t i = 0; i < nk; ++i) {
-        const int kl = key_len(keys[i]);
+    for (int64_t i = 0; i < nn + nw; ++i) {
+        // a wide key's filter bits: its first seven bytes and its length
+        const int kl = i < nn ? key_len(keys[i]) : key_len(t.whi[i - nn]);
+        const uint64_t kw = i < nn ? keys[i] : t.wlo[i - nn];
         if (kl == 1) {
-            const uint32_t b0 = (uint32_t)(keys[i] & 0xff);
+            const uint32_t b0 = (uint32_t)(kw & 0xff);
             filter[b0 >> 5] |= 1u << (b0 & 31);
         } else if (kl == 2) {
-            const uint32_t b01 = (uint32_t)(keys[i] & 0xffff);
+            const uint32_t b01 = (uint32_t)(kw & 0xffff);
             filter[kBmp1Words + (b01 >> 5)] |= 1u << (b01 & 31);
         } else {
-            const uint32_t lo = (uint32_t)keys[i];
-            const uint32_t hi = (uint32_t)(keys[i] >> 32) & ((1u << (8 * std::max(0, kl - 4))) - 1u);
+            const uint32_t lo = (uint32_t)kw;
+            const uint32_t hi = (uint32_t)(kw >> 32) & ((1u << (8 * std::min(3, std::max(0, kl - 4)))) - 1u);
             if (m->lds_filter) {  // prefix bloom
                 const uint32_t b = pf_bit(kl, lo, hi);
                 filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (b & 31u);
@@ -884,7 +979,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     if (m->mode == 3 && m->lds_filter && n_langs <= 255 && !diag_env("LDGPU_NO_DIRECT")) {
         std::vector<uint8_t> lang1(256, 0xff), lang2of(65536, 0xff);
         bool ok = true;
-        for (int64_t i = 0; i < nk && ok; ++i) {
+        for (int64_t i = 0; i < nn && ok; ++i) {
             const int kl = key_len(keys[i]);
             if (kl > 2) continue;
             int bits = 0, lang = 0;
@@ -921,6 +1016,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
 
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = upload(&m->d_slots, slots, &m->device_bytes);
+    if (e == hipSuccess && nw > 0) e = upload(&m->d_wslots, wslots, &m->device_bytes);
     if (e == hipSuccess && use_buckets) e = upload(&m->d_buckets, buckets, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_filter, filter, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_masks, masks, &m->device_bytes);
@@ -1027,6 +1123,8 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.slot_shift = (uint32_t)(64 - log2u(n_index));
     p.slot_mask = n_index - 1;
     p.slot_shift32 = (uint32_t)(32 - log2u(n_index));  // cuckoo slots: slot_hash
+    p.wslots = m->d_wslots;
+    p.wslot_shift32 = m->d_wslots ? (uint32_t)(32 - log2u(m->wslot_cap)) : 0u;
     p.filter = m->d_filter;
     p.bloom_shift = (uint32_t)(32 - m->filter_log2);
     p.bloom_words = (uint32_t)((uint64_t)1 << m->filter_log2);
@@ -1849,9 +1947,9 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     std::vector<uint64_t> keys(n);
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = key_offsets[i + 1] - key_offsets[i];
-        if (len < 1 || len > LDGPU_MAX_GRAM)
+        if (len < 1 || len > LDGPU_MAX_FIT_GRAM)
             return fail(LDGPU_EINVAL, "key %lld has length %lld outside [1, %d]", (long long)i, (long long)len,
-                        LDGPU_MAX_GRAM);
+                        LDGPU_MAX_FIT_GRAM);
         keys[i] = pack_key_host(key_bytes + key_offsets[i], (int)len);
     }
     std::lock_guard<std::mutex> lock(c->ctx->mu);

@@ -7,6 +7,11 @@
 // keys (LanguageDetector.scala:26, LanguageDetectorModel.scala:132), including
 // the length (a partial window "ab" of a 2-byte document at n=3 IS the 2-gram
 // "ab").  key 0 never occurs (klen >= 1) and marks an empty hash slot.
+//
+// Wide keys (SCORE tables only, klen 8..kMaxWideGram): two u64 words,
+//     lo = b0 .. b7 (little-endian),  hi = b8 .. b(klen-1) | klen << 56
+// in a table of their own (WideSlot).  Their filter bits use the first
+// seven bytes and the length, as a 7-byte key's do.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -14,7 +19,8 @@
 
 namespace ldgpu {
 
-constexpr int kMaxGram = 7;
+constexpr int kMaxGram = 7;       // one-word keys; FIT counts up to this length
+constexpr int kMaxWideGram = 15;  // SCORE tables: two-word keys up to this length
 constexpr int kMaxLangs = 256;
 constexpr int kMaxGramLengths = 32;
 constexpr uint64_t kEmpty = 0;
@@ -78,8 +84,8 @@ constexpr uint32_t kBmp1Words = 8;
 constexpr uint32_t kBmp2Words = 2048;
 constexpr uint32_t kBloomBase = kBmp1Words + kBmp2Words;
 
-// Candidate queue entry: klen in the top 3 bits, window position below.
-constexpr uint32_t kPosBits = 29;
+// Candidate queue entry: klen in the top 4 bits, window position below.
+constexpr uint32_t kPosBits = 28;
 constexpr int64_t kMaxDocBytes = (int64_t)1 << kPosBits;
 
 // Slot hash for the device hash tables (splitmix64 finaliser).
@@ -103,6 +109,15 @@ __host__ __device__ __forceinline__ void slot_hash(uint32_t lo, uint32_t hi, uin
     const uint32_t c = hi >> 16;
     h1 = mul24(a, 0x9E3779u) ^ mul24(b, 0x85EBCAu) ^ mul24(c ^ (a >> 12), 0xC2B2AFu);
     h2 = mul24(b ^ (c << 8), 0x27D4EBu) ^ mul24(a, 0x165667u) ^ mul24(c ^ (b >> 12), 0xD3A265u);
+}
+
+// Cuckoo slot positions of the wide-key table: the two words folded into
+// slot_hash's input
+__host__ __device__ __forceinline__ void wide_hash(uint64_t lo, uint64_t hi, uint32_t& h1, uint32_t& h2) {
+    const uint32_t u0 = (uint32_t)hi, u1 = (uint32_t)(hi >> 32);
+    const uint32_t x0 = (uint32_t)lo ^ mul24(u0 ^ (u1 << 13), 0x5BD1E9u) ^ (u1 >> 19);
+    const uint32_t x1 = (uint32_t)(lo >> 32) ^ mul24((u0 >> 12) ^ u1, 0x873593u) ^ (u0 << 7);
+    slot_hash(x0, x1, h1, h2);
 }
 
 __host__ __device__ __forceinline__ int key_len(uint64_t key) { return (int)(key >> 56); }
@@ -140,6 +155,16 @@ struct alignas(16) Slot {
 };
 
 constexpr uint32_t kBadRow = 0x80000000u;
+
+// Slot of the wide-key table (32 B): the key's two words, row index (kBadRow
+// as in Slot) and the row's one language (or 0xffffffff); values and masks
+// are read from the row arrays.  lo = hi = 0 marks an empty slot.
+struct alignas(16) WideSlot {
+    uint64_t lo, hi;
+    uint32_t row;
+    uint32_t lang1;
+    uint32_t pad[2];
+};
 
 // Count-mode key table: 2-choice buckets of 4 slots, one 64-B line each.
 // p[i] = row | (the row's one language, or 0xffffffff) << 32.  A key goes

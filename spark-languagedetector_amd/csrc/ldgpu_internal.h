@@ -29,6 +29,8 @@ struct ScoreParams {
     uint32_t slot_shift;        // bucket = mix64(key) >> slot_shift (or & slot_mask)
     uint64_t slot_mask;
     uint32_t slot_shift32;      // cuckoo slot = h1 (h2) >> slot_shift32 of slot_hash
+    const WideSlot* wslots;     // wide keys (8..15 bytes), nullptr: none
+    uint32_t wslot_shift32;     // wide slot = h1 (h2) >> wslot_shift32 of wide_hash
     const uint32_t* filter;     // image: bmp1 | bmp2 | bloom (ldgpu_common.h)
     uint32_t bloom_words;       // power of two
     uint32_t bloom_shift;       // bloom word = hash >> bloom_shift (>= 10)
@@ -56,7 +58,7 @@ struct ScoreParams {
     int32_t n_fast;             // entries in gpack
     int32_t maxg;               // max(G)
     uint32_t fast_mask;         // count mode fast path: bit n = n is in G and some key has n bytes
-    uint8_t mult[8];            // count mode: multiplicity of n in G (the fast path tests n once)
+    uint8_t mult[16];           // count mode: multiplicity of n in G (the fast path tests n once)
     // count mode, direct tables (every 1-/2-byte key names one language):
     // image words [direct_off, + direct_words) = lang1[256] u8 (0xff: no key),
     // base2[2048] u16 (rank of each 2-byte bitmap word), lang2[n2] u8

@@ -127,6 +127,24 @@ __device__ __forceinline__ void window_words(const ScoreParams& p, const DocSrc&
     }
 }
 
+// the window's bytes [pos, pos + 16) as 5 words + byte shift (wide keys)
+template <bool STAGED>
+__device__ __forceinline__ void window_words5(const ScoreParams& p, const DocSrc& src, int64_t pos, uint32_t (&w)[5],
+                                              uint32_t& sh) {
+    const int64_t a = src.base + pos;
+    sh = (uint32_t)(a & 3);
+    if constexpr (STAGED) {
+        const uint32_t i = (uint32_t)(a >> 2);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) w[t] = src.lds[i + t];
+    } else {
+        const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+        const int64_t i = a >> 2;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) w[t] = ld_dw(W, i + t, p.last_dword);
+    }
+}
+
 // Max over the wave of a non-NaN double, by DPP row shifts / broadcasts (no
 // LDS traffic); the result is read from lane 63 and is wave-uniform.
 __device__ __forceinline__ double dpp_max_step_impl(double v, int olo, int ohi) {
@@ -206,12 +224,43 @@ __device__ __forceinline__ bool bucket_find(const Bucket* b, uint64_t key, uint6
     return true;
 }
 
+// A wide candidate (8..15 bytes): its own 2-choice table (WideSlot); value
+// and mask words from the row arrays.
+template <bool STAGED, int MODE, int S>
+__device__ __forceinline__ void wide_lookup(const ScoreParams& p, const DocSrc& src, int64_t pos, int klen,
+                                         uint32_t& row, uint32_t& lang1, double& v, uint64_t& m0) {
+    uint32_t w[5], sh;
+    window_words5<STAGED>(p, src, pos, w, sh);
+    const uint64_t lo = ((uint64_t)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32) |
+                        __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    const uint64_t hw = ((uint64_t)__builtin_amdgcn_alignbyte(w[4], w[3], sh) << 32) |
+                        __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+    const uint64_t hi = (klen == 8 ? 0ull : (hw & (~0ull >> (64 - 8 * (klen - 8))))) | ((uint64_t)klen << 56);
+    uint32_t h1, h2;
+    wide_hash(lo, hi, h1, h2);
+    const u32x4* sl = reinterpret_cast<const u32x4*>(p.wslots);
+    const uint64_t ia = h1 >> p.wslot_shift32, ic = h2 >> p.wslot_shift32;
+    u32x4 a0 = sl[2 * ia], a1 = sl[2 * ia + 1], c0 = sl[2 * ic], c1 = sl[2 * ic + 1];
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1));
+    const bool ha = ((((uint64_t)a0.y) << 32) | a0.x) == lo && ((((uint64_t)a0.w) << 32) | a0.z) == hi;
+    const bool hc = ((((uint64_t)c0.y) << 32) | c0.x) == lo && ((((uint64_t)c0.w) << 32) | c0.z) == hi;
+    if (ha || hc) {
+        const u32x4 s1 = ha ? a1 : c1;  // WideSlot: row, lang1
+        row = s1.x;
+        lang1 = s1.y;
+        if (MODE != 2 && !(row & kBadRow)) {
+            v = p.vals[row];
+            m0 = p.masks[(size_t)row * S];
+        }
+    }
+}
+
 // weighted (MODE 3 fast path, distinct gram lengths): a hit of a k-byte key
 // counts p.mult[k] times (k's multiplicity in gramLengths).
 // PACK (MODE 3, packed short documents, score_pack): an entry's position is
 // its low 8 bits and bits 8..9 name the document of the pack, whose (u16)
 // counter block it counts into.
-template <int S, int MODE, bool STAGED, bool KEYED, bool PACK = false>
+template <int S, int MODE, bool STAGED, bool KEYED, bool PACK = false, bool WIDE = false>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
                                       double (&acc)[S], int lane, bool weighted = false) {
     __builtin_amdgcn_wave_barrier();
@@ -228,8 +277,12 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             const int klen = (int)(e >> kPosBits);
             if (MODE == 3 && weighted) inc = p.mult[klen];
             if (PACK) coff = ((e >> 8) & (kPackDocs - 1u)) * 64u * S;
+            const int64_t pos = (int64_t)(e & (PACK ? 255u : (1u << kPosBits) - 1u));
+            if (WIDE && klen > kMaxGram) {  // (WIDE kernels: tables holding wide keys)
+                wide_lookup<STAGED, MODE, S>(p, src, pos, klen, row, lang1, v, m0);
+            } else {
             uint32_t w0, w1, w2, sh;
-            window_words<STAGED>(p, src, (int64_t)(e & (PACK ? 255u : (1u << kPosBits) - 1u)), w0, w1, w2, sh);
+            window_words<STAGED>(p, src, pos, w0, w1, w2, sh);
             const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
                                  __builtin_amdgcn_alignbyte(w1, w0, sh);
             const uint64_t key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
@@ -268,6 +321,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                     m0 = (((uint64_t)s1.w) << 32) | s1.z;
                 }
             }
+            }  // narrow key
         }
         const bool hit = row != 0xffffffffu;
         const bool bad = hit && (row & kBadRow);
@@ -472,7 +526,8 @@ __device__ __forceinline__ void filter_word(const uint32_t* img, uint32_t sh, ui
         bit = mulhi24(__builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh), mul);
     } else {  // KIND 4, keyed bloom: sh = key length, mul = unused
         const uint32_t lo = sh >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * sh)) - 1u);
-        const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh - 4))) - 1u);
+        // (a wide key hashes its first seven bytes)
+        const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh < 7 ? sh - 4 : 3))) - 1u);
         const uint32_t h = kb_hash(lo, hi, sh);
         w = f.gb[h >> f.gshift];
         bit = h >> (f.gshift - 5);
@@ -659,18 +714,18 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 // Count-mode verify of a full queue in the middle of a document's probe
 // (hit-dense tables: config 5's 10M keys); counts are order-free, so the
 // probe just continues.
-template <int S, bool STAGED, bool KEYED>
+template <int S, bool STAGED, bool KEYED, bool WIDE>
 __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds& wl, int qn, const DocSrc& src,
                                             int lane) {
     double acc[S];  // unused in count mode
-    if (!ablated(p, 1)) flush<S, 3, STAGED, KEYED>(p, wl, qn, src, acc, lane, true);
+    if (!ablated(p, 1)) flush<S, 3, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, true);
 }
 
 // keyed Bloom hash of sub-block k's N-byte window (filter_word, KIND 4)
 template <int N>
 __device__ __forceinline__ uint32_t keyed_hash(const Windows& x, int k) {
     const uint32_t lo = N >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * N)) - 1u);
-    const uint32_t hi = N <= 4 ? 0u : x.hi[k] & ((1u << (8 * (N - 4))) - 1u);
+    const uint32_t hi = N <= 4 ? 0u : x.hi[k] & ((1u << (8 * (N < 7 ? N - 4 : 3))) - 1u);
     return kb_hash(lo, hi, (uint32_t)N);
 }
 
@@ -694,7 +749,7 @@ __device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x,
 // probe_count_all)
 constexpr int kFmDirect = 16;
 
-template <int N, bool FULL, int S, bool STAGED, bool KEYED>
+template <int N, bool FULL, int S, bool STAGED, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                             const DocSrc& src, uint32_t dummy_a, uint32_t fm) {
@@ -715,13 +770,13 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
         test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
     }
     if (qn + count_sb(m) > kQueueCap) {
-        flush_count<S, STAGED, KEYED>(p, wl, qn, src, lane);
+        flush_count<S, STAGED, KEYED, WIDE>(p, wl, qn, src, lane);
         qn = 0;
     }
     append_sb(wl.queue, dummy_a, qn, m, N, 0, lane);
 }
 
-template <bool FULL, int S, bool STAGED, bool KEYED>
+template <bool FULL, int S, bool STAGED, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                                 const DocSrc& src, uint32_t dummy_a) {
@@ -730,13 +785,30 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
     // loop and spills them to VGPR lanes: two v_readlane per test)
     uint32_t fm = __builtin_amdgcn_readfirstlane(p.fast_mask | (p.direct_words ? 1u << kFmDirect : 0u));
     asm volatile("" : "+s"(fm));
-    probe_count<1, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<2, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<3, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<4, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<5, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<6, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<7, FULL, S, STAGED, KEYED>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<3, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<4, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<5, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<6, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    probe_count<7, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    // wide gram lengths 8..15: one loop, the length a scalar (their filter
+    // bits use the first seven bytes: the same two tests as length 7)
+    for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {
+        const int n = 8 + __builtin_ctz(wm);
+        const uint32_t sh = KEYED ? (uint32_t)n : pf_shift(n), mul = pf_mult(n);
+        constexpr int K3 = KEYED ? 4 : 3;
+        uint64_t m[kSub];
+        if constexpr (FULL)
+            test_len<K3, 4>(img, sh, mul, f, x, len - n + 1, m);
+        else
+            test_nsb<K3>(img, sh, mul, f, x, len - n + 1, m);
+        if (qn + count_sb(m) > kQueueCap) {
+            flush_count<S, STAGED, KEYED, WIDE>(p, wl, qn, src, lane);
+            qn = 0;
+        }
+        append_sb(wl.queue, dummy_a, qn, m, n, 0, lane);
+    }
 }
 
 // Packed short documents (count mode): up to kPackDocs consecutive documents
@@ -748,7 +820,7 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
 // each document's label is its block's count argmax.  Three 64-B documents
 // per wave-pass instead of one: the lanes a lone short document leaves idle
 // do the next documents' windows.
-template <int N, int S, bool KEYED>
+template <int N, int S, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
                                            const DocSrc& src, uint32_t dummy_a, uint32_t fm,
@@ -778,7 +850,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
     for (int k = 0; k < kSub; ++k) m[k] = __ballot(__builtin_amdgcn_ubfe(w[k], bit[k], 1) != 0u && pk.rem[k] >= N);
     if (qn + count_sb(m) > kQueueCap) {
         double acc[S];  // unused in count mode
-        flush<S, 3, true, KEYED, true>(p, wl, qn, src, acc, lane, true);
+        flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
         qn = 0;
     }
     const uint32_t qbase = (uint32_t)(uintptr_t)wl.queue;
@@ -798,7 +870,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
 // One pack: documents [i, i + nd) of the staged group, ends e1 < e2 < e3 <=
 // tot relative to the pack's first byte (unused ends = tot); labels to
 // wl.labels[i ..).
-template <int S, bool KEYED>
+template <int S, bool KEYED, bool WIDE>
 __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                         const uint32_t* bloom, const DocSrc& src, int32_t e1, int32_t e2,
                                         int32_t e3, int32_t tot, int nd, int i, int lane) {
@@ -826,17 +898,46 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
         keyed_preload<4>(f, x, fm, kw);
         keyed_preload<5>(f, x, fm, kw);
     }
-    probe_pack<1, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<2, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<3, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<4, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<5, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<6, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<7, S, KEYED>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<3, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<4, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<5, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<6, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {  // wide lengths 8..15
+        const int n = 8 + __builtin_ctz(wm);
+        constexpr int K3 = KEYED ? 4 : 3;
+        const uint32_t sh = KEYED ? (uint32_t)n : pf_shift(n), mul = pf_mult(n);
+        uint64_t m[kSub];
+        uint32_t w[kSub], bit[kSub];
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) filter_word<K3>(img, sh, mul, f, x, k, w[k], bit[k]);
+#pragma unroll
+        for (int k = 0; k < kSub; ++k)
+            m[k] = __ballot(__builtin_amdgcn_ubfe(w[k], bit[k], 1) != 0u && pk.rem[k] >= n);
+        if (qn + count_sb(m) > kQueueCap) {
+            double acc[S];
+            flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
+            qn = 0;
+        }
+        const uint32_t qbase = (uint32_t)(uintptr_t)wl.queue;
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            if (m[k]) {
+                const uint32_t off =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
+                const uint32_t qb = __builtin_amdgcn_readfirstlane(qbase + 4u * (uint32_t)qn);
+                const uint32_t a = select_by_mask(m[k], (off << 2) + qb, dummy_a);
+                *(lds_u32*)(size_t)a = ((uint32_t)n << kPosBits) | pk.tb[k];
+                qn += __popcll(m[k]);
+            }
+        }
+    }
     if (ablated(p, 1)) qn = 0;
     if (qn) {
         double acc[S];
-        flush<S, 3, true, KEYED, true>(p, wl, qn, src, acc, lane, true);
+        flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
     }
     for (int q = 0; q < (ablated(p, 32) ? 0 : nd); ++q) {
         const int lab = count_argmax<S>(p, reinterpret_cast<uint16_t*>(count_area(wl)) + q * 64 * S, lane);
@@ -845,7 +946,7 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
-template <int S, int MODE, bool STAGED, bool KEYED>
+template <int S, int MODE, bool STAGED, bool KEYED, bool WIDE>
 __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                           const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
                                           const DocSrc& src, int lane) {
@@ -871,9 +972,9 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             load_fwords<KEYED>(p, bloom, x, f);
             if constexpr (MODE == 3) {
                 if (len >= 192 + p.maxg)
-                    probe_count_all<true, S, STAGED, KEYED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
+                    probe_count_all<true, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
                 else
-                    probe_count_all<false, S, STAGED, KEYED>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
+                    probe_count_all<false, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
             }
             uint64_t gq = p.gpack[0];
             for (int gi = 0; gi < (MODE == 3 ? 0 : p.n_fast); ++gi) {
@@ -896,7 +997,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             }
             if (!general) {
                 if (ablated(p, 1)) qn = 0;
-                if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane, MODE == 3);
+                if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, MODE == 3);
             }
             qn = 0;
         }
@@ -918,7 +1019,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                 uint64_t m[kSub];
                 test_sb<false, KEYED>(img, g.klen, f, x, g.nwin - p0, m);
                 if (qn + count_sb(m) > kQueueCap) {
-                    flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
+                    flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
                     qn = 0;
                 }
                 append_sb(wl.queue, dummy_a, qn, m, g.klen, p0, lane);
@@ -926,7 +1027,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
         }
     }
     if (ablated(p, 1)) qn = 0;
-    if (qn) flush<S, MODE, STAGED, KEYED>(p, wl, qn, src, acc, lane);
+    if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
         if (ablated(p, 32)) return 0;
         if (!p.scores && !p.best && len <= p.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
@@ -1011,7 +1112,7 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
 
 // PACK (count mode only): a separate instantiation with the pack path, so the
 // pack path's registers never burden the single-document kernels
-template <int S, int MODE, bool FLDS, bool PACK = false>
+template <int S, int MODE, bool FLDS, bool PACK = false, bool WIDE = false>
 __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
@@ -1102,14 +1203,14 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                         }
                         if (nd > 1) {
                             const int32_t tot = e[nd - 1];
-                            score_pack<S, !FLDS>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
+                            score_pack<S, !FLDS, WIDE>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
                                                  nd > 3 ? e[2] : tot, tot, nd, i, lane);
                             i += nd;
                             continue;
                         }
                     }
                 }
-                const int lab = score_doc<S, MODE, true, !FLDS>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, true, !FLDS, WIDE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
                 ++i;
             }
@@ -1118,7 +1219,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{nullptr, b};
-                const int lab = score_doc<S, MODE, false, !FLDS>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, false, !FLDS, WIDE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
             }
         }
@@ -1132,23 +1233,30 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     if (lane < prev_cnt) p.labels[prev_g0 + lane] = (int32_t)wl.labels[lane];
 }
 
-template <int S, int MODE, bool FLDS>
-hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
+template <int S, int MODE, bool FLDS, bool WIDE>
+hipError_t launch_w(const ScoreParams& p, int grid, hipStream_t stream) {
     const bool pack = MODE == 3 && p.pack;
     const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words, pack);
     if constexpr (MODE == 3) {
         if (pack) {
-            hipLaunchKernelGGL((score_kernel<S, MODE, FLDS, true>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
+            hipLaunchKernelGGL((score_kernel<S, MODE, FLDS, true, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds,
+                               stream, p);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((score_kernel<S, MODE, FLDS>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
+    hipLaunchKernelGGL((score_kernel<S, MODE, FLDS, false, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
 
-template <int S, int MODE, bool FLDS, bool PACK = false>
+// tables with wide keys (8..15 bytes) run the WIDE instantiations
+template <int S, int MODE, bool FLDS>
+hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
+    return p.wslots ? launch_w<S, MODE, FLDS, true>(p, grid, stream) : launch_w<S, MODE, FLDS, false>(p, grid, stream);
+}
+
+template <int S, int MODE, bool FLDS, bool PACK = false, bool WIDE = false>
 hipError_t prepare_k(size_t lds, int* blocks) {
-    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, FLDS, PACK>);
+    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, FLDS, PACK, WIDE>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, kScoreWaves * 64, lds);
@@ -1159,9 +1267,13 @@ hipError_t prepare_k(size_t lds, int* blocks) {
 template <int S, int MODE, bool FLDS>
 hipError_t prepare_t(size_t lds, int* blocks) {
     hipError_t e = prepare_k<S, MODE, FLDS>(lds, blocks);
+    int b2 = 0;
+    if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, false, true>(lds, &b2);
+    if (e == hipSuccess) *blocks = std::min(*blocks, b2);
     if constexpr (MODE == 3) {
-        int b2 = 0;
         if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, true>(lds, &b2);
+        if (e == hipSuccess) *blocks = std::min(*blocks, b2);
+        if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, true, true>(lds, &b2);
         if (e == hipSuccess) *blocks = std::min(*blocks, b2);
     }
     return e;

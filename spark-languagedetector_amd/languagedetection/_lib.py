@@ -27,7 +27,8 @@ LDGPU_ENOMEM = 3
 LDGPU_EDEVICE = 4
 LDGPU_EUNSUPPORTED = 5
 LDGPU_ENODEV = 6
-MAX_GRAM = 7
+MAX_GRAM = 15  # SCORE tables (keys of 8..15 bytes take two words)
+MAX_FIT_GRAM = 7
 MAX_LANGS = 4096
 
 _p = ctypes.c_void_p

@@ -277,6 +277,39 @@ def test_language_blocks_nan_and_inf():
     check_parity(table, L, [1], data, off)
 
 
+@pytest.mark.parametrize("grams", [[8], [1, 3, 8, 12, 15], [15, 2, 9, 9], [5, 10]])
+@pytest.mark.parametrize("form", ["count", "mask", "dense"])
+def test_wide_keys(grams, form):
+    """Gram lengths 8..15: keys of 8..15 bytes take two words in a table of
+    their own; partial windows of documents shorter than n make keys of every
+    length up to n.  Labels and fp64 scores bit-identical to the oracle,
+    labels-only (count argmax, packs) too."""
+    rng = np.random.default_rng(sum(grams) * 7 + len(form))
+    alphabet = np.frombuffer(b"abc ", dtype=np.uint8)
+    L = 12
+    lens_k = sorted(set(grams) | {max(1, g - 3) for g in grams})
+    if form == "dense":
+        table = _random_table(rng, L, 500, lens_k, alphabet, False)
+    else:
+        table = _random_table(rng, L, 500, lens_k, alphabet, True, uniform=math.log(2.0) if form == "count" else None)
+    lens = rng.integers(0, 120, size=1500)
+    lens[:10] = [0, 1, 7, 8, 9, 14, 15, 16, 255, 256]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, grams, data, off)
+    labels, _ = m.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(labels, ol)
+
+
+def test_wide_keys_wrong_length_row():
+    """A wide key whose row has the wrong length fails only when hit."""
+    m = LanguageDetectorModel({"abcdefghij": [1.0], "xy": [0.0, 1.0]}, [2, 10], ["a", "b"])
+    assert m.predict_indices(["xyxy"])[0].tolist() == [1]
+    with pytest.raises(ValueError, match="requirement failed"):
+        m.predict_indices(["zzabcdefghijzz"])
+
+
 def test_long_documents_and_hot_keys():
     """Every 1-gram in the table: every window hits, so the per-wave candidate
     queue flushes many times per document (order must survive the flushes)."""
@@ -334,7 +367,7 @@ def test_invalid_arguments():
     with pytest.raises(ValueError, match="both must be positive"):
         DeviceModel({b"a": [1.0]}, 1, [0])
     with pytest.raises(NotImplementedError):
-        DeviceModel({b"a": [1.0]}, 1, [8])
+        DeviceModel({b"a": [1.0]}, 1, [16])  # SCORE keys: up to 15 bytes
     m = DeviceModel({b"a": [1.0]}, 1, [1])
     with pytest.raises(ValueError, match="offsets decrease"):
         m.score(np.zeros(8, dtype=np.uint8), np.array([0, 4, 2], dtype=np.int64))
