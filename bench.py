@@ -66,7 +66,7 @@ def parse():
     # SURVEY §8d shapes; explicit flags override
     preset = {2: dict(docs=10_000_000, doc_min=256, doc_max=256, langs=20, grams="1,2,3,4,5", profile_size=500,
                       train_docs=1000),
-              4: dict(docs=25_000_000, doc_min=32, doc_max=96, langs=100, grams="1,2,3,4,5", profile_size=1000,
+              4: dict(docs=125_000_000, doc_min=32, doc_max=96, langs=100, grams="1,2,3,4,5", profile_size=1000,
                       train_docs=300),
               5: dict(docs=10_000_000, doc_min=256, doc_max=256, langs=200, grams="1,2,3,4,5,6,7",
                       profile_size=50_000, train_docs=80)}[args.config]
