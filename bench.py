@@ -208,14 +208,26 @@ def traffic_from_profiles(workload_key):
     PMC passes (profiles/pmc_traffic*.json), if they were collected for this
     exact workload (tools/pmc_traffic.py, tools/pmc_profile.sh)."""
     import glob
+    import re
+    docs_re = re.compile(r":docs=(\d+):")
+    same_shape = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload_key") == workload_key:
+        k = d.get("workload_key") or ""
+        if k == workload_key:
             return d
-    return None
+        # the same score workload profiled over fewer documents: traffic
+        # scales with the documents (the table is read once per launch and
+        # is counted in the profiled launch's bytes, a slight overestimate)
+        a, b = docs_re.search(k), docs_re.search(workload_key)
+        if a and b and docs_re.sub(":", k) == docs_re.sub(":", workload_key):
+            scale = int(b.group(1)) / int(a.group(1))
+            same_shape = dict(d, traffic_bytes_per_launch=round(d["traffic_bytes_per_launch"] * scale),
+                              traffic_scaled_from=f"{os.path.basename(p)} ({a.group(1)} docs, x{scale:g})")
+    return same_shape
 
 
 def fit_main(args, world, rank, local, dev, backend):
@@ -443,6 +455,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": prof.get("traffic_bytes_per_launch"),
                 # TCC hit / (hit + miss) of the same launch (tools/pmc_traffic.sh)
                 "l2_hit_rate": (prof.get("l2") or {}).get("hit_rate"), "workload_key": workload_key,
+                "traffic_scaled_from": prof.get("traffic_scaled_from"),
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "lookups_per_s": round(windows / (kernel_ms * 1e-3), 1)}
 

@@ -49,13 +49,14 @@ enum ldgpu_status {
     LDGPU_ENODEV = 6         /* no HIP device */
 };
 
-/* Device-path limits.  SCORE: gram lengths 1..LDGPU_MAX_GRAM (keys of up to
- * 7 bytes pack into one u64, 7 payload bytes + a length byte; keys of 8..15
- * bytes into two words, in a table of their own).  FIT counting: gram lengths
- * 1..LDGPU_MAX_FIT_GRAM.  1..LDGPU_MAX_LANGS languages (SCORE scores more than
- * 256 in blocks of 256 languages). */
+/* Device-path limits.  Gram lengths 1..LDGPU_MAX_GRAM for SCORE tables and
+ * LDGPU_MAX_FIT_GRAM for FIT counting: keys of up to 7 bytes pack into one
+ * u64 (7 payload bytes + a length byte); keys of 8..15 bytes take two words,
+ * in a table of their own (SCORE and FIT alike; the multi-GPU FIT merge covers
+ * lengths 1..7).  1..LDGPU_MAX_LANGS languages (SCORE scores more than 256 in
+ * blocks of 256 languages). */
 #define LDGPU_MAX_GRAM 15      /* SCORE tables: keys of 8..15 bytes take two words */
-#define LDGPU_MAX_FIT_GRAM 7   /* FIT counting: one-word keys */
+#define LDGPU_MAX_FIT_GRAM 15  /* FIT counting: keys of 8..15 bytes in a two-word table */
 #define LDGPU_MAX_LANGS 4096
 #define LDGPU_MAX_GRAM_LENGTHS 32
 
@@ -121,7 +122,7 @@ int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets
  * given: NULL is HIP's null stream; ldgpu_ctx_stream() gives the context's).
  * d_bytes must be 4-byte aligned and n_bytes >= d_offsets[n_docs].
  * d_scores is nullable.  Offsets are trusted (validate with the host API);
- * documents must be shorter than 2^29 bytes (the host API checks this). */
+ * documents must be shorter than 2^28 bytes (the host API checks this). */
 int ldgpu_score_device(ldgpu_model* model, const uint8_t* d_bytes, int64_t n_bytes,
                        const int64_t* d_offsets, int64_t n_docs, int32_t* d_labels,
                        double* d_scores, void* stream);
@@ -164,7 +165,8 @@ int ldgpu_counts_add(ldgpu_counts* counts, int64_t n, const uint8_t* key_bytes,
 
 /* Device-resident forms of export / add (the multi-GPU merge keeps counts in
  * HBM and exchanges them with RCCL).  Keys are packed u64: bytes little-endian
- * in bits 0..55, length (1..7) in bits 56..63.  export_device writes the
+ * in bits 0..55, length (1..7) in bits 56..63 (a table holding grams of 8..15
+ * bytes fails export_device with LDGPU_EUNSUPPORTED: use ldgpu_counts_export).  export_device writes the
  * distinct grams (unordered) into caller buffers of `capacity` entries
  * (keys[capacity], counts[capacity][n_langs] int64) and their number to
  * *n_out; it fails with LDGPU_EINVAL if capacity is too small.  Both are

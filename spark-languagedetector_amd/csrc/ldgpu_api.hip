@@ -1320,6 +1320,10 @@ struct ldgpu_counts {
     ldgpu_ctx* ctx = nullptr;
     int32_t L = 0, nG = 0;
     int32_t G[kMaxGramLengths] = {};
+    // gramLengths split: one-word lengths (1..7: the count kernels) and wide
+    // lengths (8..15: wide_count_kernel), each in the caller's order
+    int32_t nGn = 0, Gn[kMaxGramLengths] = {};
+    int32_t nGw = 0, Gw[kMaxGramLengths] = {};
     uint64_t cap = 0;
     uint64_t* d_keys = nullptr;
     unsigned long long* d_counts = nullptr;
@@ -1343,6 +1347,16 @@ struct ldgpu_counts {
     uint32_t lb = 0, cb = 0;
     int64_t batch_windows = 0;  // kBatchWindows (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
     ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
+    // grams of 8..15 bytes: a two-word-key table of their own (ldgpu_fit.hip)
+    uint64_t wcap = 0, wsize = 0;
+    uint64_t* d_wlo = nullptr;
+    uint64_t* d_whi = nullptr;
+    unsigned long long* d_wcounts = nullptr;
+    unsigned long long* d_wsize = nullptr;
+    unsigned int* d_wfull = nullptr;
+    // the wide grams (lo, hi) in (length, bytes) order, as of the last
+    // counts_pull: key kWideTag << 56 | r of a pulled key list is wide[r]
+    std::vector<std::pair<uint64_t, uint64_t>> wide_sorted;
     // cached fit table (ldgpu_fit_table_size -> _export)
     bool tbl_valid = false;
     std::vector<uint8_t> tbl_bytes;
@@ -1365,13 +1379,15 @@ CountParams count_params(const ldgpu_counts* c) {
     p.ovf_n = c->d_ovf_n;
     p.ovf_cap = c->ovf_cap;
     p.L = c->L;
-    p.nG = c->nG;
-    for (int i = 0; i < c->nG; ++i) p.G[i] = c->G[i];
+    p.nG = c->nGn;
+    for (int i = 0; i < c->nGn; ++i) p.G[i] = c->Gn[i];
     return p;
 }
 
 void counts_free(ldgpu_counts* c) {
     if (!c) return;
+    for (void* p : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts, (void*)c->d_wsize, (void*)c->d_wfull})
+        if (p) (void)hipFree(p);
     if (c->ctx) {
         (void)hipSetDevice(c->ctx->device);
         // table and overflow lists back to the context's cache (no kernel
@@ -1509,7 +1525,7 @@ int after_batch(ldgpu_counts* c) {
 // windows the count kernel visits for a document of len bytes
 int64_t doc_windows(const ldgpu_counts* c, int64_t len) {
     int64_t w = 0;
-    for (int i = 0; i < c->nG; ++i) w += n_windows(len, c->G[i]);
+    for (int i = 0; i < c->nGn; ++i) w += n_windows(len, c->Gn[i]);
     return w;
 }
 
@@ -1608,8 +1624,8 @@ int count_launch_v2(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         pp.offsets = d_offsets + d0;
         pp.doc_lang = d_lang + d0;
         pp.L = c->L;
-        pp.nG = c->nG;
-        for (int i = 0; i < c->nG; ++i) pp.G[i] = c->G[i];
+        pp.nG = c->nGn;
+        for (int i = 0; i < c->nGn; ++i) pp.G[i] = c->Gn[i];
         pp.lb = c->lb;
         pp.cb = c->cb;
         if (const char* ab = diag_env("LDGPU_FIT_EMIT_ABLATE")) pp.ablate = atoi(ab);
@@ -1684,11 +1700,142 @@ int count_launch_v2(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     return LDGPU_OK;
 }
 
+// ---- grams of 8..15 bytes (wide_count_kernel, ldgpu_fit.hip)
+WideCountParams wide_params(const ldgpu_counts* c) {
+    WideCountParams p{};
+    p.klo = c->d_wlo;
+    p.khi = c->d_whi;
+    p.counts = c->d_wcounts;
+    p.shift = c->wcap ? (uint32_t)(64 - log2u(c->wcap)) : 63u;
+    p.mask = c->wcap ? c->wcap - 1 : 0;
+    p.size = c->d_wsize;
+    p.full = c->d_wfull;
+    p.L = c->L;
+    p.nG = c->nGw;
+    for (int i = 0; i < c->nGw; ++i) p.G[i] = c->Gw[i];
+    p.narrow = count_params(c);
+    return p;
+}
+
+// room for `extra` more wide keys at load <= 1/2 (so an insert's probe always
+// ends): allocate or grow (device rehash) the wide table
+int wide_ensure(ldgpu_counts* c, uint64_t extra) {
+    hipStream_t st = c->ctx->stream;
+    if (!c->d_wsize) {
+        HIP_TRY(hipMalloc((void**)&c->d_wsize, sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc((void**)&c->d_wfull, sizeof(unsigned int)));
+        HIP_TRY(hipMemsetAsync(c->d_wsize, 0, sizeof(unsigned long long), st));
+        HIP_TRY(hipMemsetAsync(c->d_wfull, 0, sizeof(unsigned int), st));
+    }
+    if (c->wcap && 2 * (c->wsize + extra) <= c->wcap) return LDGPU_OK;
+    const uint64_t cap = next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->wsize + extra)));
+    ldgpu_counts t;
+    t.L = c->L;
+    t.wcap = cap;
+    hipError_t e = hipMalloc((void**)&t.d_wlo, cap * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&t.d_whi, cap * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&t.d_wcounts, cap * (size_t)c->L * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_whi, 0, cap * sizeof(uint64_t), st);
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_wcounts, 0, cap * (size_t)c->L * sizeof(unsigned long long), st);
+    if (e == hipSuccess && c->wcap) e = launch_wide_rehash(wide_params(c), wide_params(&t), c->wcap, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        for (void* q : {(void*)t.d_wlo, (void*)t.d_whi, (void*)t.d_wcounts})
+            if (q) (void)hipFree(q);
+        return fail(LDGPU_ENOMEM, "wide count table of %llu slots: %s", (unsigned long long)cap, hipGetErrorString(e));
+    }
+    for (void* q : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts})
+        if (q) (void)hipFree(q);
+    c->d_wlo = t.d_wlo;
+    c->d_whi = t.d_whi;
+    c->d_wcounts = t.d_wcounts;
+    c->wcap = cap;
+    t.d_wlo = t.d_whi = nullptr;
+    t.d_wcounts = nullptr;
+    return LDGPU_OK;
+}
+
+// after a wide launch: the table's size, and no insert left without a slot
+int wide_after(ldgpu_counts* c) {
+    unsigned long long size = 0;
+    unsigned int full = 0;
+    HIP_TRY(hipMemcpyAsync(&size, c->d_wsize, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&full, c->d_wfull, sizeof full, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    if (full) return fail(LDGPU_EDEVICE, "wide count table: an insert found no slot");
+    c->wsize = size;
+    c->tbl_valid = false;
+    return LDGPU_OK;
+}
+
+// Count the wide gram lengths of documents [0, n_docs): sub-launches of at
+// most kWideLaunchWindows wide windows, the table grown for each up front;
+// partial windows shorter than 8 bytes go to the one-word table through its
+// overflow-safe insert (so the overflow list must hold them all).
+constexpr int64_t kWideLaunchWindows = 1ll << 25;
+
+int wide_count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                      const int32_t* d_lang, int64_t n_docs, const int64_t* h_off) {
+    hipStream_t st = c->ctx->stream;
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0, wide = 0, part = 0;
+        while (d1 < n_docs) {
+            const int64_t len = h_off[d1 + 1] - h_off[d1];
+            int64_t w = 0, q = 0;
+            for (int i = 0; i < c->nGw; ++i) {
+                if (len >= 8) w += n_windows(len, c->Gw[i]);
+                else if (len > 0) q += 1;
+            }
+            if (d1 > d0 && wide + w > kWideLaunchWindows) break;
+            wide += w;
+            part += q;
+            ++d1;
+        }
+        if (int rc = wide_ensure(c, (uint64_t)wide)) return rc;
+        if (int rc = ensure_ovf(c, std::max<int64_t>(part, 1))) return rc;
+        if (2 * (c->size + (uint64_t)part) > c->cap) {
+            if (int rc = grow(c, next_pow2(4 * (c->size + (uint64_t)part) + 16))) return rc;
+        }
+        WideCountParams p = wide_params(c);
+        p.bytes = d_bytes;
+        p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+        p.offsets = d_offsets + d0;
+        p.doc_lang = d_lang + d0;
+        p.n_docs = d1 - d0;
+        p.narrow.ovf_cap = c->ovf_cap;
+        const int64_t want = (p.n_docs + kCountWaves - 1) / kCountWaves;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->ctx->cus * 2));
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+        HIP_TRY(launch_wide_count(p, grid, st));
+        if (int rc = wide_after(c)) return rc;
+        if (int rc = after_batch(c)) return rc;  // the one-word keys of short documents
+        d0 = d1;
+    }
+    return LDGPU_OK;
+}
+
 // Count documents [0, n_docs) of d_offsets / d_lang (h_off: the same offsets on
 // the host, used to plan sub-launches of at most ovf_cap windows each, so the
-// overflow list can never lose an entry).
+// overflow list can never lose an entry): the one-word gram lengths, then the
+// wide ones.
+int count_launch_narrow(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                        const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st);
+
 int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                  const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
+    if (c->nGn > 0) {
+        if (int rc = count_launch_narrow(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, st)) return rc;
+    }
+    if (c->nGw > 0) {
+        if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
+        if (int rc = wide_count_launch(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off)) return rc;
+    }
+    return LDGPU_OK;
+}
+
+int count_launch_narrow(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                        const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
     if (c->v2) {
         if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
         return count_launch_v2(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off);
@@ -1737,19 +1884,25 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
     if (n_langs < 1 || n_langs > LDGPU_MAX_LANGS)
         return fail(n_langs < 1 ? LDGPU_EINVAL : LDGPU_EUNSUPPORTED, "n_langs %d outside [1, %d]", n_langs,
                     LDGPU_MAX_LANGS);
-    if (int rc = check_grams(gram_lengths, n_grams)) return rc;
+    if (int rc = check_grams(gram_lengths, n_grams, kMaxWideGram)) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
     auto* c = new ldgpu_counts();
     c->ctx = ctx;
     c->L = n_langs;
     c->nG = n_grams;
-    for (int i = 0; i < n_grams; ++i) c->G[i] = gram_lengths[i];
+    for (int i = 0; i < n_grams; ++i) {
+        c->G[i] = gram_lengths[i];
+        if (gram_lengths[i] <= kMaxGram)
+            c->Gn[c->nGn++] = gram_lengths[i];
+        else
+            c->Gw[c->nGw++] = gram_lengths[i];
+    }
     c->cap = next_pow2(std::max<int64_t>(1 << 12, 2 * std::max<int64_t>(capacity_hint, 0)));
     // FIT v2 when a (gram, language, count) record fits 64 bits with >= 8
     // count bits: 8 max(G) + 1 sentinel-key bits + ceil(log2 L) language bits
     {
         int maxg = 0;
-        for (int i = 0; i < n_grams; ++i) maxg = std::max(maxg, gram_lengths[i]);
+        for (int i = 0; i < c->nGn; ++i) maxg = std::max(maxg, c->Gn[i]);
         c->lb = (uint32_t)std::max(1, log2u((uint64_t)n_langs));
         const int cb = 64 - (8 * maxg + 1) - (int)c->lb;
         c->cb = (uint32_t)std::max(cb, 0);
@@ -1840,6 +1993,23 @@ extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t*
 }
 
 namespace {
+// device scratch freed on scope exit
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() {
+        for (void* x : p)
+            if (x) (void)hipFree(x);
+    }
+    template <typename T>
+    hipError_t alloc(T** out, size_t n) {
+        void* x = nullptr;
+        hipError_t e = hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) p.push_back(x);
+        *out = (T*)x;
+        return e;
+    }
+};
+
 // compacted host copy: keys + counts rows, sorted by (length, bytes)
 int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsigned long long>& cnt) {
     const uint64_t n = c->size;
@@ -1865,26 +2035,85 @@ int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsign
     if (e != hipSuccess) return fail(LDGPU_EDEVICE, "count export: %s", hipGetErrorString(e));
     if (got != n) return fail(LDGPU_EDEVICE, "count export: %llu slots occupied, %llu expected", got,
                               (unsigned long long)n);
-    std::vector<uint64_t> order(n);
     std::vector<std::pair<uint64_t, uint64_t>> sk(n);
     for (uint64_t i = 0; i < n; ++i) sk[i] = {sort_key(k[i]), i};
     std::sort(sk.begin(), sk.end());
-    keys.resize(n);
-    cnt.resize((size_t)n * c->L);
+    // the wide grams (8..15 bytes) after them, in (length, bytes) order, as
+    // stand-in keys kWideTag << 56 | rank (c->wide_sorted[rank])
+    const uint64_t nw = c->wsize;
+    std::vector<uint64_t> wlo(nw), whi(nw);
+    std::vector<unsigned long long> wc((size_t)nw * c->L);
+    if (nw) {
+        uint64_t *d_lo = nullptr, *d_hi = nullptr;
+        unsigned long long *d_wc = nullptr, *d_wn = nullptr;
+        hipError_t e2 = hipMalloc((void**)&d_lo, nw * sizeof(uint64_t));
+        if (e2 == hipSuccess) e2 = hipMalloc((void**)&d_hi, nw * sizeof(uint64_t));
+        if (e2 == hipSuccess) e2 = hipMalloc((void**)&d_wc, nw * c->L * sizeof(unsigned long long));
+        if (e2 == hipSuccess) e2 = hipMalloc((void**)&d_wn, sizeof(unsigned long long));
+        if (e2 == hipSuccess) e2 = hipMemsetAsync(d_wn, 0, sizeof(unsigned long long), c->ctx->stream);
+        if (e2 == hipSuccess) e2 = launch_wide_compact(wide_params(c), c->wcap, d_lo, d_hi, d_wc, d_wn, c->ctx->stream);
+        unsigned long long wgot = 0;
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(&wgot, d_wn, sizeof wgot, hipMemcpyDeviceToHost, c->ctx->stream);
+        if (e2 == hipSuccess)
+            e2 = hipMemcpyAsync(wlo.data(), d_lo, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->ctx->stream);
+        if (e2 == hipSuccess)
+            e2 = hipMemcpyAsync(whi.data(), d_hi, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->ctx->stream);
+        if (e2 == hipSuccess)
+            e2 = hipMemcpyAsync(wc.data(), d_wc, nw * c->L * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                c->ctx->stream);
+        if (e2 == hipSuccess) e2 = hipStreamSynchronize(c->ctx->stream);
+        for (void* p : {(void*)d_lo, (void*)d_hi, (void*)d_wc, (void*)d_wn})
+            if (p) (void)hipFree(p);
+        if (e2 != hipSuccess) return fail(LDGPU_EDEVICE, "wide count export: %s", hipGetErrorString(e2));
+        if (wgot != nw) return fail(LDGPU_EDEVICE, "wide count export: %llu slots occupied, %llu expected", wgot,
+                                    (unsigned long long)nw);
+    }
+    // (length, bytes) order of a wide key: length, then bytes 0..7, then 8..
+    auto be = [](uint64_t x) { return __builtin_bswap64(x); };
+    std::vector<uint64_t> word(nw);
+    for (uint64_t i = 0; i < nw; ++i) word[i] = i;
+    std::sort(word.begin(), word.end(), [&](uint64_t a, uint64_t b) {
+        const int la = key_len(whi[a]), lb = key_len(whi[b]);
+        if (la != lb) return la < lb;
+        if (wlo[a] != wlo[b]) return be(wlo[a]) < be(wlo[b]);
+        return be(whi[a] << 8) < be(whi[b] << 8);
+    });
+    c->wide_sorted.resize(nw);
+    keys.resize(n + nw);
+    cnt.resize((size_t)(n + nw) * c->L);
     for (uint64_t i = 0; i < n; ++i) {
         keys[i] = k[sk[i].second];
         memcpy(&cnt[(size_t)i * c->L], &cc[(size_t)sk[i].second * c->L], sizeof(unsigned long long) * c->L);
     }
+    for (uint64_t r = 0; r < nw; ++r) {
+        c->wide_sorted[r] = {wlo[word[r]], whi[word[r]]};
+        keys[n + r] = (kWideTag << 56) | r;
+        memcpy(&cnt[(size_t)(n + r) * c->L], &wc[(size_t)word[r] * c->L], sizeof(unsigned long long) * c->L);
+    }
     return LDGPU_OK;
 }
 
-void write_keys(const std::vector<uint64_t>& keys, uint8_t* key_bytes, int64_t* key_offsets) {
+// bytes of a pulled key (one-word, or a wide stand-in resolved through
+// c->wide_sorted): returns the length, writes the bytes when out != nullptr
+int gram_bytes(const ldgpu_counts* c, uint64_t k, uint8_t* out) {
+    if (key_len(k) < (int)kWideTag) {
+        const int len = key_len(k);
+        if (out)
+            for (int j = 0; j < len; ++j) out[j] = (uint8_t)(k >> (8 * j));
+        return len;
+    }
+    const auto& w = c->wide_sorted[k & ((1ull << 56) - 1)];
+    const int len = key_len(w.second);
+    if (out)
+        for (int j = 0; j < len; ++j) out[j] = (uint8_t)((j < 8 ? w.first : w.second) >> (8 * (j & 7)));
+    return len;
+}
+
+void write_keys(const ldgpu_counts* c, const std::vector<uint64_t>& keys, uint8_t* key_bytes, int64_t* key_offsets) {
     int64_t o = 0;
     key_offsets[0] = 0;
     for (size_t i = 0; i < keys.size(); ++i) {
-        const int len = key_len(keys[i]);
-        for (int j = 0; j < len; ++j) key_bytes[o + j] = (uint8_t)(keys[i] >> (8 * j));
-        o += len;
+        o += gram_bytes(c, keys[i], key_bytes + o);
         key_offsets[i + 1] = o;
     }
 }
@@ -1894,13 +2123,13 @@ extern "C" int ldgpu_counts_size(ldgpu_counts* c, int64_t* n_grams, int64_t* key
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    if (n_grams) *n_grams = (int64_t)c->size;
+    if (n_grams) *n_grams = (int64_t)(c->size + c->wsize);
     if (key_bytes) {
         std::vector<uint64_t> k;
         std::vector<unsigned long long> cc;
         if (int rc = counts_pull(c, k, cc)) return rc;
         int64_t s = 0;
-        for (uint64_t x : k) s += key_len(x);
+        for (uint64_t x : k) s += gram_bytes(c, x, nullptr);
         *key_bytes = s;
     }
     return ok();
@@ -1915,11 +2144,18 @@ extern "C" int ldgpu_counts_stats(ldgpu_counts* c, int64_t* n_grams, int64_t* n_
     HIP_TRY(hipMalloc((void**)&d, sizeof h));
     hipError_t e = hipMemsetAsync(d, 0, sizeof h, c->ctx->stream);
     if (e == hipSuccess) e = launch_stats(count_params(c), c->cap, d, c->ctx->stream);
+    if (e == hipSuccess && c->wcap) {  // the wide table, through the same kernel (hi != 0: occupied)
+        CountParams w{};
+        w.keys = c->d_whi;
+        w.counts = c->d_wcounts;
+        w.L = c->L;
+        e = launch_stats(w, c->wcap, d, c->ctx->stream);
+    }
     if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(LDGPU_EDEVICE, "counts_stats: %s", hipGetErrorString(e));
-    if (n_grams) *n_grams = (int64_t)c->size;
+    if (n_grams) *n_grams = (int64_t)(c->size + c->wsize);
     if (n_pairs) *n_pairs = (int64_t)h[0];
     if (total) *total = (int64_t)h[1];
     return ok();
@@ -1932,7 +2168,7 @@ extern "C" int ldgpu_counts_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t*
     std::vector<uint64_t> k;
     std::vector<unsigned long long> cc;
     if (int rc = counts_pull(c, k, cc)) return rc;
-    write_keys(k, key_bytes, key_offsets);
+    write_keys(c, k, key_bytes, key_offsets);
     for (size_t i = 0; i < cc.size(); ++i) counts_out[i] = (int64_t)cc[i];
     return ok();
 }
@@ -1944,16 +2180,54 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
     if (n == 0) return ok();
     if (!key_bytes || !key_offsets || !counts_in) return fail(LDGPU_EINVAL, "NULL argument");
-    std::vector<uint64_t> keys(n);
+    // one-word keys (1..7 bytes) and wide keys (8..15 bytes: two words)
+    std::vector<uint64_t> keys, wlo, whi;
+    std::vector<int64_t> narrow_rows, wide_rows;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = key_offsets[i + 1] - key_offsets[i];
         if (len < 1 || len > LDGPU_MAX_FIT_GRAM)
             return fail(LDGPU_EINVAL, "key %lld has length %lld outside [1, %d]", (long long)i, (long long)len,
                         LDGPU_MAX_FIT_GRAM);
-        keys[i] = pack_key_host(key_bytes + key_offsets[i], (int)len);
+        const uint8_t* kb = key_bytes + key_offsets[i];
+        if (len <= kMaxGram) {
+            keys.push_back(pack_key_host(kb, (int)len));
+            narrow_rows.push_back(i);
+        } else {
+            wlo.push_back((pack_key_host(kb, 8) & ((1ull << 56) - 1)) | ((uint64_t)kb[7] << 56));
+            whi.push_back((pack_key_host(kb + 8, (int)len - 8) & ((1ull << 56) - 1)) | ((uint64_t)len << 56));
+            wide_rows.push_back(i);
+        }
     }
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
+    if (!wide_rows.empty()) {
+        const int64_t nw = (int64_t)wide_rows.size();
+        if (int rc = wide_ensure(c, (uint64_t)nw)) return rc;
+        std::vector<int64_t> wrows((size_t)nw * c->L);
+        for (int64_t j = 0; j < nw; ++j)
+            memcpy(&wrows[(size_t)j * c->L], counts_in + (size_t)wide_rows[j] * c->L, sizeof(int64_t) * c->L);
+        DevBufs wb;
+        uint64_t *d_lo, *d_hi;
+        unsigned long long* d_r;
+        HIP_TRY(wb.alloc(&d_lo, nw));
+        HIP_TRY(wb.alloc(&d_hi, nw));
+        HIP_TRY(wb.alloc(&d_r, (size_t)nw * c->L));
+        HIP_TRY(hipMemcpyAsync(d_lo, wlo.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, c->ctx->stream));
+        HIP_TRY(hipMemcpyAsync(d_hi, whi.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, c->ctx->stream));
+        HIP_TRY(hipMemcpyAsync(d_r, wrows.data(), (size_t)nw * c->L * sizeof(int64_t), hipMemcpyHostToDevice,
+                               c->ctx->stream));
+        HIP_TRY(launch_wide_add(wide_params(c), d_lo, d_hi, d_r, nw, c->ctx->stream));
+        if (int rc = wide_after(c)) return rc;
+    }
+    if (keys.empty()) return ok();
+    std::vector<int64_t> nrows;
+    if ((int64_t)keys.size() != n) {
+        nrows.resize(keys.size() * (size_t)c->L);
+        for (size_t j = 0; j < keys.size(); ++j)
+            memcpy(&nrows[j * c->L], counts_in + (size_t)narrow_rows[j] * c->L, sizeof(int64_t) * c->L);
+        counts_in = nrows.data();
+        n = (int64_t)keys.size();
+    }
     if (2 * (c->size + (uint64_t)n) > c->cap) {
         if (int rc = grow(c, next_pow2(4 * (c->size + n) + 16))) return rc;
     }
@@ -1980,6 +2254,9 @@ extern "C" int ldgpu_counts_export_device(ldgpu_counts* c, int64_t capacity, uin
     if (!c || !n_out) return fail(LDGPU_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
+    if (c->wsize)
+        return fail(LDGPU_EUNSUPPORTED, "export_device: the table holds grams of 8..15 bytes, which have no packed "
+                                        "u64 form (use ldgpu_counts_export)");
     *n_out = (int64_t)c->size;
     if ((int64_t)c->size > capacity)
         return fail(LDGPU_EINVAL, "export_device: %llu grams exceed the capacity %lld", (unsigned long long)c->size,
@@ -2024,22 +2301,6 @@ extern "C" int ldgpu_counts_add_device(ldgpu_counts* c, int64_t n, const uint64_
 }
 
 namespace {
-// device scratch freed on scope exit
-struct DevBufs {
-    std::vector<void*> p;
-    ~DevBufs() {
-        for (void* x : p)
-            if (x) (void)hipFree(x);
-    }
-    template <typename T>
-    hipError_t alloc(T** out, size_t n) {
-        void* x = nullptr;
-        hipError_t e = hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T));
-        if (e == hipSuccess) p.push_back(x);
-        *out = (T*)x;
-        return e;
-    }
-};
 
 // filterTopGrams (LanguageDetector.scala:100-132) over a presence table --
 // keys sorted by (length, bytes), masks[n][S] -- into the cached table:
@@ -2103,10 +2364,10 @@ int table_from_presence(ldgpu_counts* c, const std::vector<uint64_t>& keys, cons
         c->tbl_vals.push_back(w[kg[i]]);
     }
     int64_t nb = 0;
-    for (uint64_t k : out_keys) nb += key_len(k);
+    for (uint64_t k : out_keys) nb += gram_bytes(c, k, nullptr);
     c->tbl_bytes.assign((size_t)std::max<int64_t>(nb, 1), 0);
     c->tbl_off.assign(out_keys.size() + 1, 0);
-    write_keys(out_keys, c->tbl_bytes.data(), c->tbl_off.data());
+    write_keys(c, out_keys, c->tbl_bytes.data(), c->tbl_off.data());
     c->tbl_valid = true;
     if (n_rows) *n_rows = (int64_t)out_keys.size();
     if (key_bytes) *key_bytes = nb;
@@ -2276,6 +2537,10 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     if (!c || !m) return fail(LDGPU_EINVAL, "NULL argument");
     if (c->comm) return fail(LDGPU_EINVAL, "the count table is already merged");
     if (m->ctx != c->ctx) return fail(LDGPU_EINVAL, "communicator and count table belong to different contexts");
+    // (every rank has the same gram lengths, so all ranks fail alike)
+    if (c->nGw > 0 || c->wsize > 0)
+        return fail(LDGPU_EUNSUPPORTED, "the multi-GPU merge covers gram lengths 1..%d; this table counts grams of "
+                                        "8..15 bytes", kMaxGram);
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
     const int W = m->world, L = c->L;
@@ -2570,7 +2835,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     for (uint64_t k : out_keys) nb += key_len(k);
     c->tbl_bytes.assign((size_t)std::max<int64_t>(nb, 1), 0);
     c->tbl_off.assign(out_keys.size() + 1, 0);
-    write_keys(out_keys, c->tbl_bytes.data(), c->tbl_off.data());
+    write_keys(c, out_keys, c->tbl_bytes.data(), c->tbl_off.data());
     c->tbl_valid = true;
     if (n_rows) *n_rows = (int64_t)m;
     if (key_bytes) *key_bytes = nb;
@@ -2586,7 +2851,9 @@ extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows,
     HIP_TRY(hipSetDevice(c->ctx->device));
     // a merged table takes the device path on every rank (its collectives
     // must match), even for K <= 0 or an empty shard
-    if (!c->comm && (K <= 0 || c->size == 0)) {
+    // (tables holding grams of 8..15 bytes take the host top-K over the
+    // pulled table, whose keys stay in (length, bytes) order)
+    if (!c->comm && (K <= 0 || c->size == 0 || c->wsize > 0)) {
         if (int rc = fit_table_host(c, K, n_rows, key_bytes)) return rc;
         return ok();
     }

@@ -8,10 +8,10 @@
 // the length (a partial window "ab" of a 2-byte document at n=3 IS the 2-gram
 // "ab").  key 0 never occurs (klen >= 1) and marks an empty hash slot.
 //
-// Wide keys (SCORE tables only, klen 8..kMaxWideGram): two u64 words,
+// Wide keys (klen 8..kMaxWideGram): two u64 words,
 //     lo = b0 .. b7 (little-endian),  hi = b8 .. b(klen-1) | klen << 56
-// in a table of their own (WideSlot).  Their filter bits use the first
-// seven bytes and the length, as a 7-byte key's do.
+// in a table of their own (SCORE: WideSlot, whose filter bits use the first
+// seven bytes and the length, as a 7-byte key's do; FIT: wide_count_kernel).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -19,8 +19,8 @@
 
 namespace ldgpu {
 
-constexpr int kMaxGram = 7;       // one-word keys; FIT counts up to this length
-constexpr int kMaxWideGram = 15;  // SCORE tables: two-word keys up to this length
+constexpr int kMaxGram = 7;       // one-word keys
+constexpr int kMaxWideGram = 15;  // two-word keys up to this length (SCORE tables, FIT counts)
 constexpr int kMaxLangs = 256;
 constexpr int kMaxGramLengths = 32;
 constexpr uint64_t kEmpty = 0;
@@ -128,10 +128,17 @@ inline uint64_t pack_key_host(const uint8_t* p, int len) {
     return k;
 }
 
+// Host-side stand-in for a FIT gram of 8..15 bytes among one-word keys:
+// kWideTag << 56 | its rank in the (length, bytes) order of the table's wide
+// grams.  It sorts after every one-word key (whose top byte is <= 7), so a
+// key list sorted by sort_key is in (length, bytes) order throughout.
+constexpr uint64_t kWideTag = 16;
+
 // (length, unsigned bytes) order of a packed key: length in the top byte,
 // the bytes big-endian below it (the build's top-K tie-break).
 __host__ __device__ __forceinline__ uint64_t sort_key(uint64_t key) {
     const int len = key_len(key);
+    if (len >= (int)kWideTag) return key;
     uint64_t s = (uint64_t)len << 56;
     for (int i = 0; i < len; ++i) s |= ((key >> (8 * i)) & 0xffull) << (48 - 8 * i);
     return s;

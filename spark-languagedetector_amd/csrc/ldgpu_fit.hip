@@ -1217,3 +1217,184 @@ hipError_t launch_merge(const PartParams& p, const CountParams& c, int64_t n, hi
 }
 
 }  // namespace ldgpu
+
+// ---------------------------------------------------------------------------
+// FIT of gram lengths 8..15 (computeGrams + reduceGrams, LanguageDetector.
+// scala:25-66, for windows too long for a one-word key).  Such windows count
+// into a table of two-word keys of their own -- lo = bytes 0..7, hi = bytes
+// 8.. | klen << 56 (ldgpu_common.h) -- with one u64 counter row per slot, as
+// the one-word table.  A wide gram length still makes one-word keys: the
+// partial window of a document shorter than 8 bytes (Scala sliding gives the
+// whole text), which goes to the one-word table.  One wave per document, a
+// lane per window; an insert claims its slot by a CAS on hi carrying a
+// "being written" bit, stores lo, then publishes hi, so a reader that finds
+// the bit waits for the key before comparing it.  The host keeps the table at
+// most half full (wide_ensure), so a probe always ends.
+namespace ldgpu {
+namespace {
+
+constexpr uint64_t kWidePending = 1ull << 63;  // never set in hi (klen <= 15 in bits 56..59)
+
+__device__ __forceinline__ uint64_t wide_slot(uint64_t lo, uint64_t hi) { return mix64(lo ^ mix64(hi)); }
+
+// find-or-insert of (lo, hi); -1 only if every slot is taken
+__device__ __forceinline__ int64_t wide_find_or_insert(const WideCountParams& p, uint64_t lo, uint64_t hi,
+                                                       bool& new_key) {
+    uint64_t s = wide_slot(lo, hi) >> p.shift;
+    for (uint64_t probe = 0; probe <= p.mask; ++probe) {
+        uint64_t h = __hip_atomic_load(&p.khi[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (h == kEmpty) {
+            const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&p.khi[s]), 0ull,
+                                                     (unsigned long long)(hi | kWidePending));
+            if (old == 0ull) {
+                __hip_atomic_store(&p.klo[s], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&p.khi[s], hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                new_key = true;
+                return (int64_t)s;
+            }
+            h = old;
+        }
+        // another lane's insert in flight: its lo is stored before hi is
+        // published (a lane of this wave wrote it above, before this loop)
+        while (h & kWidePending) h = __hip_atomic_load(&p.khi[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (h == hi && __hip_atomic_load(&p.klo[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo)
+            return (int64_t)s;
+        s = (s + 1) & p.mask;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void wide_add(const WideCountParams& p, uint64_t lo, uint64_t hi, int lang,
+                                         unsigned long long c) {
+    bool new_key = false;
+    const int64_t s = wide_find_or_insert(p, lo, hi, new_key);
+    const uint64_t m = __ballot(new_key);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(p.size, (unsigned long long)__popcll(m));
+    if (s >= 0)
+        atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
+    else
+        atomicOr(p.full, 1u);
+}
+
+__global__ __launch_bounds__(kCountWaves * 64) void wide_count_kernel(const WideCountParams p) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+    const int64_t stride = (int64_t)gridDim.x * kCountWaves;
+    for (int64_t doc = (int64_t)blockIdx.x * kCountWaves + wave; doc < p.n_docs; doc += stride) {
+        const int lang = p.doc_lang[doc];
+        if (lang < 0 || lang >= p.L) continue;  // reduceGrams keeps supported languages only
+        const int64_t b = p.offsets[doc];
+        const int64_t len = p.offsets[doc + 1] - b;
+        for (int gi = 0; gi < p.nG; ++gi) {
+            const int n = p.G[gi];
+            const int64_t nwin = n_windows(len, n);
+            const int klen = len < n ? (int)len : n;
+            for (int64_t p0 = 0; p0 < nwin; p0 += 64) {
+                const int64_t pos = p0 + lane;
+                if (pos >= nwin) continue;
+                const int64_t a = b + pos;
+                const int64_t i = a >> 2;
+                const uint32_t sh = (uint32_t)(a & 3);
+                uint32_t w[5];
+#pragma unroll
+                for (int t = 0; t < 5; ++t) w[t] = ld_dw(W, i + t, p.last_dword);
+                const uint64_t lo = ((uint64_t)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32) |
+                                    __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+                if (klen <= kMaxGram) {  // a short document's whole text: a one-word key
+                    add_count(p.narrow, (lo & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56), lang, 1ull);
+                    continue;
+                }
+                const uint64_t hw = ((uint64_t)__builtin_amdgcn_alignbyte(w[4], w[3], sh) << 32) |
+                                    __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+                const uint64_t hi =
+                    (klen == 8 ? 0ull : (hw & (~0ull >> (64 - 8 * (klen - 8))))) | ((uint64_t)klen << 56);
+                wide_add(p, lo, hi, lang, 1ull);
+            }
+        }
+    }
+}
+
+// grow: every occupied slot of `from` (keys unique) into `to`
+__global__ void wide_rehash_kernel(const WideCountParams from, const WideCountParams to, uint64_t from_cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= from_cap) return;
+    const uint64_t hi = from.khi[i];
+    if (hi == kEmpty) return;
+    const uint64_t lo = from.klo[i];
+    uint64_t s = wide_slot(lo, hi) >> to.shift;
+    while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.khi[s]), 0ull, (unsigned long long)hi) != 0ull)
+        s = (s + 1) & to.mask;
+    to.klo[s] = lo;
+    for (int l = 0; l < from.L; ++l) to.counts[(size_t)s * to.L + l] = from.counts[(size_t)i * from.L + l];
+}
+
+// ldgpu_counts_add of wide keys: rows[i][L] added at (lo[i], hi[i])
+__global__ void wide_add_kernel(const WideCountParams p, const uint64_t* lo, const uint64_t* hi,
+                                const unsigned long long* rows, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool new_key = false;
+    const int64_t s = i < n ? wide_find_or_insert(p, lo[i], hi[i], new_key) : -1;
+    const uint64_t m = __ballot(new_key);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(p.size, (unsigned long long)__popcll(m));
+    if (i >= n) return;
+    if (s < 0) {
+        atomicOr(p.full, 1u);
+        return;
+    }
+    for (int l = 0; l < p.L; ++l) {
+        const unsigned long long c = rows[(size_t)i * p.L + l];
+        if (c) atomicAdd(&p.counts[(size_t)s * p.L + l], c);
+    }
+}
+
+__global__ void wide_compact_kernel(const WideCountParams p, uint64_t cap, uint64_t* out_lo, uint64_t* out_hi,
+                                    unsigned long long* out_counts, unsigned long long* out_n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool occ = i < cap && p.khi[i] != kEmpty;
+    const uint64_t m = __ballot(occ);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    const int leader = __builtin_ctzll(m);
+    if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (!occ) return;
+    const unsigned long long o =
+        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    out_lo[o] = p.klo[i];
+    out_hi[o] = p.khi[i];
+    for (int l = 0; l < p.L; ++l) out_counts[o * p.L + l] = p.counts[i * p.L + l];
+}
+
+}  // namespace
+
+hipError_t launch_wide_count(const WideCountParams& p, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(wide_count_kernel, dim3(grid), dim3(kCountWaves * 64), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_rehash(const WideCountParams& from, const WideCountParams& to, uint64_t from_cap,
+                              hipStream_t stream) {
+    if (from_cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(wide_rehash_kernel, dim3((unsigned)((from_cap + 255) / 256)), dim3(256), 0, stream, from, to,
+                       from_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_add(const WideCountParams& p, const uint64_t* lo, const uint64_t* hi,
+                           const unsigned long long* rows, int64_t n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(wide_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, p, lo, hi, rows, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_compact(const WideCountParams& p, uint64_t cap, uint64_t* out_lo, uint64_t* out_hi,
+                               unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream) {
+    if (cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(wide_compact_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out_lo,
+                       out_hi, out_counts, out_n);
+    return hipGetLastError();
+}
+
+}  // namespace ldgpu

@@ -229,6 +229,36 @@ hipError_t launch_stats(const CountParams& p, uint64_t cap, unsigned long long* 
 hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys,
                           unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
 
+// ---- FIT of gram lengths 8..15 (ldgpu_fit.hip): a table of two-word keys
+// (lo = bytes 0..7, hi = bytes 8.. | klen << 56; hi = 0: empty slot) with a
+// u64 counter row per slot
+struct WideCountParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    int64_t last_dword;
+    const int64_t* offsets;
+    const int32_t* doc_lang;
+    int64_t n_docs;
+    uint64_t* klo;              // [cap]
+    uint64_t* khi;              // [cap]
+    unsigned long long* counts; // [cap][L]
+    uint32_t shift;             // slot = wide_slot(lo, hi) >> shift
+    uint64_t mask;              // cap - 1
+    unsigned long long* size;   // distinct keys inserted
+    unsigned int* full;         // set when an insert found no slot (the host keeps load <= 1/2)
+    int32_t L;
+    int32_t nG;                 // the wide gram lengths, in gramLengths order
+    int32_t G[kMaxGramLengths];
+    CountParams narrow;         // partial windows of documents shorter than 8 bytes: one-word keys
+};
+
+hipError_t launch_wide_count(const WideCountParams& p, int grid, hipStream_t stream);
+hipError_t launch_wide_rehash(const WideCountParams& from, const WideCountParams& to, uint64_t from_cap,
+                              hipStream_t stream);
+hipError_t launch_wide_add(const WideCountParams& p, const uint64_t* lo, const uint64_t* hi,
+                           const unsigned long long* rows, int64_t n, hipStream_t stream);
+hipError_t launch_wide_compact(const WideCountParams& p, uint64_t cap, uint64_t* out_lo, uint64_t* out_hi,
+                               unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
+
 // ---- device probability / top-K (computeProbabilities + filterTopGrams)
 // presence: compact occupied slots into keys[n], masks[n][S] (count > 0 per
 // language) and k[n] (= popcount), and histogram hist[l][k] over (gram, l).

@@ -66,7 +66,7 @@ struct Windows {
 };
 
 struct GramCtx {
-    int32_t nwin;  // windows of this gram length (docs < 2^29 bytes)
+    int32_t nwin;  // windows of this gram length (docs < 2^28 bytes)
     int32_t klen;  // key length: n, or len for a partial window
 };
 
@@ -248,7 +248,7 @@ __device__ __forceinline__ void wide_lookup(const ScoreParams& p, const DocSrc& 
         const u32x4 s1 = ha ? a1 : c1;  // WideSlot: row, lang1
         row = s1.x;
         lang1 = s1.y;
-        if (MODE != 2 && !(row & kBadRow)) {
+        if (MODE != 2 && MODE != 3 && !(row & kBadRow)) {
             v = p.vals[row];
             m0 = p.masks[(size_t)row * S];
         }
@@ -298,6 +298,22 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                 if (found) {
                     row = (uint32_t)pay;
                     lang1 = (uint32_t)(pay >> 32);
+                }
+            } else if constexpr (MODE == 3) {
+                // count mode reads only the slots' first halves (key, row,
+                // the row's one language): a multi-language row's mask words
+                // come from p.masks, and the value is the table's one value
+                const u32x4* sl = reinterpret_cast<const u32x4*>(p.slots);
+                uint32_t h1, h2;
+                slot_hash((uint32_t)key, (uint32_t)(key >> 32), h1, h2);
+                const uint64_t ia = h1 >> p.slot_shift32, ic = h2 >> p.slot_shift32;
+                u32x4 a0 = sl[2 * ia], c0 = sl[2 * ic];
+                asm volatile("" : "+v"(a0), "+v"(c0));
+                const bool ha = ((((uint64_t)a0.y) << 32) | a0.x) == key;
+                const bool hc = ((((uint64_t)c0.y) << 32) | c0.x) == key;
+                if (ha || hc) {
+                    row = ha ? a0.z : c0.z;
+                    lang1 = ha ? a0.w : c0.w;
                 }
             } else {
                 // 2-choice cuckoo table: the key is in one of two slots (or
@@ -349,8 +365,8 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
                 uint32_t* cnt = count_area(w);
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    // S = 1: the slot's mask word (buckets: S > 1 only reach here for multi-language rows)
-                    uint64_t mm = (S == 1 && !(KEYED && p.buckets)) ? m0 : p.masks[(size_t)row * S + s];
+                    // (a multi-language row: its mask words from the row arrays)
+                    uint64_t mm = p.masks[(size_t)row * S + s];
                     while (mm) {
                         const int l = __builtin_ctzll(mm);
                         mm &= mm - 1;
@@ -674,20 +690,20 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 #pragma unroll
         for (int k = 0; k < kSub; ++k) hit[k] = lang[k] < 0xffu;
     } else {
-        uint32_t w[kSub], base[kSub];
+        uint32_t w[kSub];
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            const uint32_t idx = __builtin_amdgcn_ubfe(x.lo[k], 5, 11);
-            w[k] = img[kBmp1Words + idx];
-            base[k] = b2[idx];
-        }
+        for (int k = 0; k < kSub; ++k) w[k] = img[kBmp1Words + __builtin_amdgcn_ubfe(x.lo[k], 5, 11)];
 #pragma unroll
         for (int k = 0; k < kSub; ++k) {
             // bit (lo & 31) of the word; the offset / width operands of v_bfe
             // take their low 5 bits, so no masking
             hit[k] = __builtin_amdgcn_ubfe(w[k], x.lo[k], 1) != 0u;
-            // rank of the key among the 2-byte keys (in range for every lane)
-            lang[k] = l2[base[k] + __builtin_popcount(__builtin_amdgcn_ubfe(w[k], 0, x.lo[k]))];
+            // the key's language by its rank among the 2-byte keys: read for
+            // hits only (a missing window costs one LDS read, not three)
+            lang[k] = 0;
+            if (hit[k])
+                lang[k] = l2[b2[__builtin_amdgcn_ubfe(x.lo[k], 5, 11)] +
+                             __builtin_popcount(__builtin_amdgcn_ubfe(w[k], 0, x.lo[k]))];
         }
     }
     if constexpr (PACK) {

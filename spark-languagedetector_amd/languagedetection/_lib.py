@@ -28,7 +28,7 @@ LDGPU_EDEVICE = 4
 LDGPU_EUNSUPPORTED = 5
 LDGPU_ENODEV = 6
 MAX_GRAM = 15  # SCORE tables (keys of 8..15 bytes take two words)
-MAX_FIT_GRAM = 7
+MAX_FIT_GRAM = 15  # FIT counting (grams of 8..15 bytes in a two-word table)
 MAX_LANGS = 4096
 
 _p = ctypes.c_void_p

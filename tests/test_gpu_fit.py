@@ -296,3 +296,75 @@ def test_count_paths_match_oracle(L, grams, variant, env, monkeypatch):
     expect = np.array([ocnt[i] + extra.get(k, 0) for i, k in enumerate(okeys)])
     assert keys == okeys
     assert np.array_equal(cnt, expect)
+
+
+def _wide_corpus(grams, L, seed):
+    rng = np.random.default_rng(seed)
+    alphabet = np.frombuffer(b"abcd ", dtype=np.uint8)
+    lens = rng.integers(0, 60, size=600)
+    lens[:12] = [0, 1, 2, 7, 8, 9, 11, 14, 15, 16, 17, 30]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    lang = rng.integers(0, L, size=len(docs)).astype(np.int32)
+    lang[::41] = -1
+    return data, off, lang
+
+
+@pytest.mark.parametrize("grams", [[8], [1, 3, 9, 12], [15, 2, 9, 9], [5, 10], [7, 8]])
+def test_wide_gram_counts_table_and_model(grams):
+    """Gram lengths 8..15 (computeGrams, LanguageDetector.scala:32-43, any n):
+    windows of 8..15 bytes count in a two-word-key table of their own; the
+    partial window of a document shorter than n is its whole text, so a wide
+    length also makes keys of every length below n (those under 8 bytes in
+    the one-word table).  Counts bit-exact against the C restatement over two
+    calls, the top-K table (host selection over the pulled table, ties by
+    (length, bytes)) equal to the rule applied to the oracle's counts, and the
+    model built from it scoring like the oracle."""
+    from languagedetection.runtime import DeviceModel
+    L = 5
+    data, off, lang = _wide_corpus(grams, L, sum(grams))
+    counts = DeviceCounts(L, grams, capacity_hint=16)
+    counts.count(data, off, lang)
+    counts.count(data[:int(off[100])], off[:101], lang[:100])   # a second call accumulates
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(data, off, lang, L, grams)
+    okeys2, ocnt2 = OC.count(data[:int(off[100])], off[:101], lang[:100], L, grams)
+    extra = dict(zip(okeys2, ocnt2))
+    expect = np.array([ocnt[i] + extra.get(k, 0) for i, k in enumerate(okeys)])
+    assert keys == okeys
+    assert np.array_equal(cnt, expect)
+    assert max(len(k) for k in keys) == max(grams) or max(grams) <= 7
+    st = counts.stats()
+    assert st == {"grams": len(okeys), "pairs": int((expect > 0).sum()), "total": int(expect.sum())}
+    for K in (20, 100000):   # 100000: every gram, zero-valued fill included
+        table = counts.fit_table(K)
+        assert table == _topk_table_from_counts(okeys, expect, L, K)
+    table = counts.fit_table(30)
+    counts.close()
+    sdata, soff, _ = _wide_corpus(grams, L, sum(grams) + 1)
+    ol, osc = OC.Table(table, L).score(grams, sdata, soff, want_scores=True, nthreads=8)
+    labels, scores = DeviceModel(table, L, grams).score(sdata, soff, want_scores=True)
+    assert np.array_equal(labels, ol)
+    assert np.array_equal(scores.view(np.uint64), osc.view(np.uint64))
+
+
+def test_wide_gram_counts_add_and_limits():
+    """ldgpu_counts_add takes keys of 1..15 bytes (wide ones into the two-word
+    table); the packed-u64 device export has no form for them and says so."""
+    L, grams = 4, [2, 9]
+    data, off, lang = _wide_corpus(grams, L, 5)
+    a = DeviceCounts(L, grams)
+    a.count(data, off, lang)
+    keys, cnt = a.export()
+    assert any(len(k) > 7 for k in keys)
+    b = DeviceCounts(L, [1])
+    b.add(keys[::2], cnt[::2])
+    b.add(keys, cnt)
+    k2, c2 = b.export()
+    extra = np.zeros_like(cnt)
+    extra[::2] = cnt[::2]
+    assert k2 == keys and np.array_equal(c2, cnt + extra)
+    with pytest.raises(NotImplementedError, match="8..15 bytes"):
+        a.export_device()
+    with pytest.raises(NotImplementedError):
+        DeviceCounts(L, [16])
