@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--no-alt-paths", action="store_true",
+                    help="skip timing the same table on the ordered mask-replay path (diagnostics library)")
     ap.add_argument("--empty-table", action="store_true", help="calibration: table with no keys")
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--mode", choices=["score", "fit"], default="score",
@@ -201,6 +203,38 @@ def host_path(model, data, off, acc_labels):
     pin.close()
     pout.close()
     return res
+
+
+def mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs, d_lab, stream):
+    """The same table forced onto the ordered mask-replay path (the general
+    path of any table whose rows do not share one value: verified hits replayed
+    in reference order, s_l = s_l + v per hit) through the diagnostics library
+    (LDGPU_NO_COUNT_MODE): its kernel time and whether its labels equal the
+    count-mode launch's.  Reported beside `value`, never as it."""
+    os.environ["LDGPU_NO_COUNT_MODE"] = "1"
+    try:
+        alt = DeviceModel.from_masks(*packed, args.langs, grams, device=local, variant="diag")
+    finally:
+        del os.environ["LDGPU_NO_COUNT_MODE"]
+    d_alt = torch.empty_like(d_lab)
+
+    def step():
+        alt.score_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), n_docs, d_alt.data_ptr(), 0, stream.cuda_stream)
+    for _ in range(max(1, args.warmup)):
+        step()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for s_, e_ in ev:
+        s_.record(stream)
+        step()
+        e_.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev]))
+    mode = alt.info()["mode"]
+    alt.close()
+    return {"table_mode": {0: "mask", 1: "mask, finite values (fma replay)", 2: "dense"}.get(mode, str(mode)),
+            "kernel_ms": round(ms, 4), "docs_per_s": round(n_docs / (ms * 1e-3), 1),
+            "labels_match_count_mode": bool(torch.equal(d_alt, d_lab)),
+            "library": "libldgpu_diag.so (LDGPU_NO_COUNT_MODE=1)"}
 
 
 def traffic_from_profiles(workload_key):
@@ -468,6 +502,9 @@ def main():
         dl = d_lab[:len(ol)].cpu().numpy()
         oracle_check = {"labels_match_oracle": bool(np.array_equal(dl, ol)), "docs_checked": int(len(ol)),
                         "mismatches": int((dl != ol).sum())}
+    alt = None
+    if rank == 0 and world == 1 and args.config == 2 and not args.no_alt_paths and not args.empty_table:
+        alt = mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs, d_lab, stream)
     host = None
     if rank == 0 and world == 1 and not args.no_host_path and not args.empty_table:
         host = host_path(model, data, off, acc_labels=d_lab.cpu().numpy())
@@ -504,6 +541,7 @@ def main():
         "labels_match_oracle": None if oracle_check is None else oracle_check["labels_match_oracle"],
         "oracle_check": oracle_check,
         "host_path": host,
+        "mask_replay_path": alt,
         "fit_setup": fit_info,
         "label_accuracy_vs_generator": acc,
     }

@@ -374,6 +374,7 @@ struct ldgpu_model {
     bool dense = false;
     int mode = 0;             // kernel mode: 0 mask, 1 mask + finite values, 2 dense, 3 mask + one finite value
     bool lds_filter = true;
+    bool kb_lines = false;   // keyed bloom in the line layout (kKbLineBytes)
     bool has_bad = false;
     int64_t n_keys = 0;
     uint64_t slot_cap = 0;
@@ -946,6 +947,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
     bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
     m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
+    m->kb_lines = !m->lds_filter && 4 * bwords > kKbLineBytes;
     m->filter_log2 = log2u(bwords);
     const uint32_t bshift = 32u - (uint32_t)m->filter_log2;
     std::vector<uint32_t> filter(kBloomBase + bwords, 0u);
@@ -965,9 +967,11 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
             if (m->lds_filter) {  // prefix bloom
                 const uint32_t b = pf_bit(kl, lo, hi);
                 filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (b & 31u);
-            } else {  // keyed bloom (kb_hash)
+            } else {  // keyed bloom (kb_hash; keys of >= 4 bytes in their position's line)
                 const uint32_t h = kb_hash(lo, hi, (uint32_t)kl);
-                filter[kBloomBase + (h >> bshift)] |= 1u << ((h >> (bshift - 5)) & 31u);
+                const bool ln = m->kb_lines && kl >= 4;
+                const uint32_t w = (ln ? kb_line16(lo, bshift) : 0u) + (h >> kb_sword(kl, m->kb_lines, bshift));
+                filter[kBloomBase + w] |= 1u << ((h >> kb_sbit(kl, m->kb_lines, bshift)) & 31u);
             }
         }
     }
@@ -1127,6 +1131,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.wslot_shift32 = m->d_wslots ? (uint32_t)(32 - log2u(m->wslot_cap)) : 0u;
     p.filter = m->d_filter;
     p.bloom_shift = (uint32_t)(32 - m->filter_log2);
+    p.kb_lines = m->kb_lines ? 1 : 0;
     p.bloom_words = (uint32_t)((uint64_t)1 << m->filter_log2);
     p.len_mask = m->len_mask;
     p.masks = m->d_masks;

@@ -77,6 +77,33 @@ __host__ __device__ __forceinline__ uint32_t kb_hash(uint32_t lo, uint32_t hi, u
     return mul24(a, 0x9E3779u) ^ mul24(b, 0x85EBCAu) ^ mul24(c ^ (a >> 12), 0xC2B2AFu);
 }
 
+// Keyed bloom, line layout (blooms beyond kKbLineBytes, ldgpu_internal.h):
+// every key of >= 4 bytes of one window position -- the lengths 4..15 that
+// start there -- sets its bit in ONE 64-B line (16 words) chosen by the
+// position's first four bytes, so one position's tests of every length >= 4
+// read one line of L2 / HBM instead of one line per length: word = line << 4
+// | h >> 28, bit = (h >> 23) mod 32 of h = kb_hash, line = kb_line(bytes
+// 0..3) >> (32 - (wlog - 4)).  Keys of 3 bytes, and every key of a smaller
+// keyed bloom, keep a word of their own: word = h >> (32 - wlog).
+__host__ __device__ __forceinline__ uint32_t kb_line(uint32_t lo) {
+    return mul24(lo, 0xB5297Au) ^ mul24(lo >> 8, 0x68E31Du);
+}
+// The bloom word of a key of klen >= 3 bytes with kb_hash h is
+// line16 + (h >> s_word), its bit (h >> s_bit) mod 32: in the line layout a
+// key of >= 4 bytes takes s_word = 28, s_bit = 23 and line16 = its position's
+// line << 4; a 3-byte key, or any key outside the line layout, s_word =
+// wshift (= 32 - wlog), s_bit = wshift - 5 and line16 = 0.  (Both shifts
+// are wave-uniform: one formula for every lane.)
+__host__ __device__ __forceinline__ uint32_t kb_sword(uint32_t klen, bool lines, uint32_t wshift) {
+    return lines && klen >= 4 ? 28u : wshift;
+}
+__host__ __device__ __forceinline__ uint32_t kb_sbit(uint32_t klen, bool lines, uint32_t wshift) {
+    return lines && klen >= 4 ? 23u : wshift - 5u;
+}
+__host__ __device__ __forceinline__ uint32_t kb_line16(uint32_t lo, uint32_t wshift) {
+    return (kb_line(lo) >> (wshift + 4)) << 4;
+}
+
 // Filter image (host-built, staged whole into LDS): a direct 256-bit bitmap
 // of the 1-byte keys, a direct 65536-bit bitmap of the 2-byte keys, then the
 // prefix Bloom words.

@@ -34,6 +34,7 @@ struct ScoreParams {
     const uint32_t* filter;     // image: bmp1 | bmp2 | bloom (ldgpu_common.h)
     uint32_t bloom_words;       // power of two
     uint32_t bloom_shift;       // bloom word = hash >> bloom_shift (>= 10)
+    int32_t kb_lines;           // keyed bloom in the line layout (kb_line16: blooms beyond kKbLineBytes)
     uint32_t len_mask;          // bit k set: the table holds keys of k bytes
     const uint64_t* masks;      // mask mode: [rows][S] language bitmasks
     const double* vals;         // mask mode: [rows] the row's one nonzero value
@@ -97,16 +98,20 @@ constexpr int kBufBytes = 1024;            // staged bytes of a document group p
 constexpr int kBufWords = kBufBytes / 4 + 4;
 constexpr int kMaxLdsBloomLog2 = 14;       // bloom words in LDS up to 64 KiB
 constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
+// keyed blooms of more than this many bytes take the line layout (every
+// length >= 4 of a position in one 64-B line): an XCD's 4 MiB L2 holds half of
+// one or less, so lines saved are HBM / Infinity Cache lines; a smaller bloom
+// stays L2-resident and keeps one word per key
+constexpr uint64_t kKbLineBytes = 2ull << 20;
 
 // documents per pack of short documents (count mode, score_pack)
 constexpr uint32_t kPackDocs = 4;
 
 // per-wave hit area (u32 words): ordered modes hold 64 verified hits of
-// (S + 2) / 2 uint4 each; count mode (3) holds the probe's 64 dummy-store
-// words and the 64 S u32 per-language counters (packing: kPackDocs blocks of
-// 64 S u16 counters)
+// (S + 2) / 2 uint4 each; count mode (3) holds the 64 S u32 per-language
+// counters (packing: kPackDocs blocks of 64 S u16 counters)
 constexpr uint32_t hit_area_words(int slices, int mode, bool pack = false) {
-    return mode == 3 ? 64u * (1u + (pack ? kPackDocs / 2u : 1u) * (uint32_t)slices)
+    return mode == 3 ? 64u * (pack ? kPackDocs / 2u : 1u) * (uint32_t)slices
                      : 64u * 4u * (((uint32_t)slices + 2u) / 2u);
 }
 

@@ -42,6 +42,12 @@ namespace {
 
 constexpr int kSub = 4;  // 64-position sub-blocks per superblock
 
+// tuning switch (build variants only): count mode issues its verify loads
+// before the direct 1-/2-byte counts and completes them after (probe_count_all)
+#ifndef LDGPU_SPLIT_VERIFY
+#define LDGPU_SPLIT_VERIFY 1
+#endif
+
 // timing ablations exist only in the diagnostics build (LDGPU_DIAG)
 __device__ __forceinline__ bool ablated(const ScoreParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
 
@@ -86,9 +92,8 @@ struct WaveLds {
     uint32_t* labels; // [64] labels of the current group
 };
 
-// MODE 3 per-language hit counters: after the first 64 words of the hit area,
-// which take the probe's dummy stores (append_sb); hit_area_words(S, 3).
-__device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return reinterpret_cast<uint32_t*>(w.hits) + 64; }
+// MODE 3 per-language hit counters: the wave's hit area; hit_area_words(S, 3).
+__device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return reinterpret_cast<uint32_t*>(w.hits); }
 
 // counter idx += inc: u32 counters, or (PACK: packed short documents) u16
 // counters two to a word -- a document of a pack has at most 256 windows per
@@ -255,6 +260,86 @@ __device__ __forceinline__ void wide_lookup(const ScoreParams& p, const DocSrc& 
     }
 }
 
+// Count mode, split verify of the queue's first 64 candidates (one-word keys,
+// cuckoo slots): verify_issue builds the keys and issues both slots' loads;
+// the caller does independent LDS work (the direct 1-/2-byte counts) while
+// they are in flight, and verify_complete compares and counts.  Counts are
+// order-free, so the result is flush's.
+struct VerifyIssue {
+    u32x4 a0, c0;   // first halves of the key's two cuckoo slots (Slot: key, row, language)
+    uint64_t key;
+    uint32_t inc;   // the key length's multiplicity in gramLengths
+    bool valid;
+};
+
+template <bool STAGED>
+__device__ __forceinline__ void verify_issue(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
+                                             int lane, VerifyIssue& v) {
+    __builtin_amdgcn_wave_barrier();
+    v.valid = lane < qn;
+    v.key = 0;
+    v.inc = 0;
+    v.a0 = v.c0 = u32x4{0u, 0u, 0u, 0u};
+    if (v.valid) {
+        const uint32_t e = w.queue[lane];
+        const int klen = (int)(e >> kPosBits);
+        v.inc = p.mult[klen];
+        uint32_t w0, w1, w2, sh;
+        window_words<STAGED>(p, src, (int64_t)(e & ((1u << kPosBits) - 1u)), w0, w1, w2, sh);
+        const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) |
+                             __builtin_amdgcn_alignbyte(w1, w0, sh);
+        v.key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
+        const u32x4* sl = reinterpret_cast<const u32x4*>(p.slots);
+        uint32_t h1, h2;
+        slot_hash((uint32_t)v.key, (uint32_t)(v.key >> 32), h1, h2);
+        v.a0 = sl[2 * (uint64_t)(h1 >> p.slot_shift32)];
+        v.c0 = sl[2 * (uint64_t)(h2 >> p.slot_shift32)];
+    }
+}
+
+template <int S>
+__device__ __forceinline__ void verify_complete(const ScoreParams& p, const WaveLds& w, const VerifyIssue& v) {
+    uint32_t row = 0xffffffffu, lang1 = 0xffffffffu;
+    if (v.valid) {
+        const bool ha = ((((uint64_t)v.a0.y) << 32) | v.a0.x) == v.key;
+        const bool hc = ((((uint64_t)v.c0.y) << 32) | v.c0.x) == v.key;
+        if (ha || hc) {
+            row = ha ? v.a0.z : v.c0.z;
+            lang1 = ha ? v.a0.w : v.c0.w;
+        }
+    }
+    const bool hit = row != 0xffffffffu;
+    const bool bad = hit && (row & kBadRow);
+    if (__ballot(bad)) {
+        if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1);
+    }
+    const bool good = hit && !bad;
+#ifdef LDGPU_STATS
+    if (p.stats) {
+        const int ng = __popcll(__ballot(good));
+        const int nv = __popcll(__ballot(v.valid));
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&p.stats[0], (unsigned long long)nv);
+            atomicAdd(&p.stats[1], (unsigned long long)ng);
+        }
+    }
+#endif
+    uint32_t* cnt = count_area(w);
+    if (good && lang1 != 0xffffffffu) {
+        count_inc<false>(cnt, lang1, v.inc);
+    } else if (good) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            uint64_t mm = p.masks[(size_t)row * S + s];
+            while (mm) {
+                const int l = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                count_inc<false>(cnt, 64 * s + l, v.inc);
+            }
+        }
+    }
+}
+
 // weighted (MODE 3 fast path, distinct gram lengths): a hit of a k-byte key
 // counts p.mult[k] times (k's multiplicity in gramLengths).
 // PACK (MODE 3, packed short documents, score_pack): an entry's position is
@@ -262,9 +347,9 @@ __device__ __forceinline__ void wide_lookup(const ScoreParams& p, const DocSrc& 
 // counter block it counts into.
 template <int S, int MODE, bool STAGED, bool KEYED, bool PACK = false, bool WIDE = false>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
-                                      double (&acc)[S], int lane, bool weighted = false) {
+                                      double (&acc)[S], int lane, bool weighted = false, int q_begin = 0) {
     __builtin_amdgcn_wave_barrier();
-    for (int q0 = 0; q0 < qn; q0 += 64) {
+    for (int q0 = q_begin; q0 < qn; q0 += 64) {
         const int j = q0 + lane;
         uint32_t row = 0xffffffffu;
         double v = 0.0;
@@ -493,9 +578,10 @@ __device__ __forceinline__ int count_argmax(const ScoreParams& p, C* cnt, int la
 // ldgpu_common.h) -- a big table's keys share few 3-byte prefixes, which
 // would saturate prefix words; gb / gshift locate that bloom.
 struct FWords {
-    uint32_t w3[kSub];
+    uint32_t w3[kSub];  // prefix bloom: the position's word; keyed line layout: its line << 4 (kb_line16)
     const uint32_t* gb;
     uint32_t gshift;
+    bool lines;         // keyed bloom in the line layout (ScoreParams::kb_lines)
 };
 
 template <bool KEYED>
@@ -504,8 +590,14 @@ __device__ __forceinline__ void load_fwords(const ScoreParams& p, const uint32_t
     if constexpr (KEYED) {
         f.gb = bloom;
         f.gshift = p.bloom_shift;
+        f.lines = p.kb_lines != 0;
+        if (f.lines) {  // (a scalar branch: the line hashes only for the line layout)
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) f.w3[k] = 0;
+            for (int k = 0; k < kSub; ++k) f.w3[k] = kb_line16(x.lo[k], p.bloom_shift);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSub; ++k) f.w3[k] = 0u;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < kSub; ++k) f.w3[k] = bloom[pf_word(x.lo[k], p.bloom_shift)];
@@ -545,8 +637,9 @@ __device__ __forceinline__ void filter_word(const uint32_t* img, uint32_t sh, ui
         // (a wide key hashes its first seven bytes)
         const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh < 7 ? sh - 4 : 3))) - 1u);
         const uint32_t h = kb_hash(lo, hi, sh);
-        w = f.gb[h >> f.gshift];
-        bit = h >> (f.gshift - 5);
+        // (f.w3 is 0 outside the line layout)
+        w = f.gb[(sh >= 4 ? f.w3[k] : 0u) + (h >> kb_sword(sh, f.lines, f.gshift))];
+        bit = h >> kb_sbit(sh, f.lines, f.gshift);
     }
 }
 
@@ -596,19 +689,12 @@ __device__ __forceinline__ void test_sb(const uint32_t* img, int klen, const FWo
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// per lane: bit `lane` of m ? a : b (one v_cndmask on the mask itself)
-__device__ __forceinline__ uint32_t select_by_mask(uint64_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-    return r;
-}
-
 // Append the candidates of one superblock to the queue in position order;
-// the caller guarantees room for every set bit.  Every lane stores (no exec
-// juggling): a candidate to its queue rank, the others to their own word of
-// the wave's hit area (idle while probing), at byte address dummy_a.
-__device__ __forceinline__ void append_sb(uint32_t* queue, uint32_t dummy_a, int& qn, const uint64_t (&m)[kSub],
-                                          int klen, int32_t p0, int lane) {
+// the caller guarantees room for every set bit.  Only the candidate lanes
+// store (exec = the ballot itself, one s_and_saveexec: no per-lane select),
+// each to the queue's next free word + its rank among them.
+__device__ __forceinline__ void append_sb(uint32_t* queue, int& qn, const uint64_t (&m)[kSub], int klen, int32_t p0,
+                                          int lane) {
     // opaque lane: the tags are then built here, not hoisted out of the
     // document loop as loop invariants (which the allocator spills)
     uint32_t l = (uint32_t)lane;
@@ -618,12 +704,10 @@ __device__ __forceinline__ void append_sb(uint32_t* queue, uint32_t dummy_a, int
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
         if (m[k]) {
-            const uint32_t off =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            // the queue's next free word as one scalar: a single v_lshl_add
-            const uint32_t qb = __builtin_amdgcn_readfirstlane(qbase + 4u * (uint32_t)qn);
-            const uint32_t a = select_by_mask(m[k], (off << 2) + qb, dummy_a);
-            *(lds_u32*)(size_t)a = tag0 + 64u * k;
+            // rank among the candidates + the queue's fill, in entries
+            const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], (uint32_t)qn));
+            if (__builtin_amdgcn_inverse_ballot_w64(m[k])) *(lds_u32*)(size_t)(qbase + 4u * at) = tag0 + 64u * k;
             qn += __popcll(m[k]);
         }
     }
@@ -672,6 +756,22 @@ struct PackPos {
     int32_t rem[kSub];  // bytes from the position to the end of its document (<= 0: none)
     uint32_t tb[kSub];  // document index << 8 | position in the pack
 };
+
+// append_sb for packs: an entry is klen << kPosBits | the pack tag (tb)
+__device__ __forceinline__ void append_pack(uint32_t* queue, int& qn, const uint64_t (&m)[kSub], uint32_t klen,
+                                            const PackPos& pk) {
+    const uint32_t qbase = (uint32_t)(uintptr_t)queue;
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        if (m[k]) {
+            const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], (uint32_t)qn));
+            if (__builtin_amdgcn_inverse_ballot_w64(m[k]))
+                *(lds_u32*)(size_t)(qbase + 4u * at) = (klen << kPosBits) | pk.tb[k];
+            qn += __popcll(m[k]);
+        }
+    }
+}
 
 template <int N, bool FULL, int S = 1, bool PACK = false>
 __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
@@ -756,7 +856,8 @@ __device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x,
     if constexpr (N - 3 < kPreN) {
         if ((fm >> N) & 1u) {
 #pragma unroll
-            for (int k = 0; k < kSub; ++k) kw[N - 3][k] = f.gb[keyed_hash<N>(x, k) >> f.gshift];
+            for (int k = 0; k < kSub; ++k)
+                kw[N - 3][k] = f.gb[(N >= 4 ? f.w3[k] : 0u) + (keyed_hash<N>(x, k) >> kb_sword(N, f.lines, f.gshift))];
         }
     }
 }
@@ -768,7 +869,7 @@ constexpr int kFmDirect = 16;
 template <int N, bool FULL, int S, bool STAGED, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
-                                            const DocSrc& src, uint32_t dummy_a, uint32_t fm) {
+                                            const DocSrc& src, uint32_t fm) {
     if (!((fm >> N) & 1u)) return;
     if (ablated(p, N <= 2 ? 8 : 16)) return;
     if constexpr (N <= 2) {
@@ -789,25 +890,32 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
         flush_count<S, STAGED, KEYED, WIDE>(p, wl, qn, src, lane);
         qn = 0;
     }
-    append_sb(wl.queue, dummy_a, qn, m, N, 0, lane);
+    append_sb(wl.queue, qn, m, N, 0, lane);
 }
 
 template <bool FULL, int S, bool STAGED, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
-                                                const DocSrc& src, uint32_t dummy_a) {
+                                                const DocSrc& src) {
     // the per-length switches as bits of one SGPR, re-read per document (the
     // compiler otherwise hoists seven lane-mask booleans out of the document
     // loop and spills them to VGPR lanes: two v_readlane per test)
     uint32_t fm = __builtin_amdgcn_readfirstlane(p.fast_mask | (p.direct_words ? 1u << kFmDirect : 0u));
     asm volatile("" : "+s"(fm));
-    probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<3, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<4, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<5, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<6, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
-    probe_count<7, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, dummy_a, fm);
+    // With direct tables the 1-/2-byte counts never touch the queue: the
+    // longer lengths are probed first, their first 64 candidates' slot loads
+    // issued, and the direct counts run while those loads are in flight
+    // (LDGPU_SPLIT_VERIFY; one-word keys in cuckoo slots only)
+    const bool split = LDGPU_SPLIT_VERIFY && !WIDE && !(KEYED && p.buckets) && ((fm >> kFmDirect) & 1u);
+    if (!split) {
+        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    }
+    probe_count<3, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    probe_count<4, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    probe_count<5, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    probe_count<6, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    probe_count<7, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
     // wide gram lengths 8..15: one loop, the length a scalar (their filter
     // bits use the first seven bytes: the same two tests as length 7)
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {
@@ -823,7 +931,22 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
             flush_count<S, STAGED, KEYED, WIDE>(p, wl, qn, src, lane);
             qn = 0;
         }
-        append_sb(wl.queue, dummy_a, qn, m, n, 0, lane);
+        append_sb(wl.queue, qn, m, n, 0, lane);
+    }
+    if (split) {
+        VerifyIssue v;
+        const bool pending = qn > 0 && !ablated(p, 1);
+        if (pending) verify_issue<STAGED>(p, wl, qn, src, lane, v);
+        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+        if (pending) {
+            verify_complete<S>(p, wl, v);
+            if (qn > 64) {
+                double acc[S];  // unused in count mode
+                flush<S, 3, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, true, 64);
+            }
+        }
+        qn = 0;
     }
 }
 
@@ -839,7 +962,7 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
 template <int N, int S, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
-                                           const DocSrc& src, uint32_t dummy_a, uint32_t fm,
+                                           const DocSrc& src, uint32_t fm,
                                            const uint32_t (&kw)[kPreN][kSub]) {
     if (!((fm >> N) & 1u)) return;
     if (ablated(p, N <= 2 ? 8 : 16)) return;
@@ -857,7 +980,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
     for (int k = 0; k < kSub; ++k) {
         if constexpr (KIND == 4 && N - 3 < kPreN) {
             w[k] = kw[N - 3][k];
-            bit[k] = keyed_hash<N>(x, k) >> (f.gshift - 5);
+            bit[k] = keyed_hash<N>(x, k) >> kb_sbit(N, f.lines, f.gshift);
         } else {
             filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
         }
@@ -869,18 +992,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
         flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
         qn = 0;
     }
-    const uint32_t qbase = (uint32_t)(uintptr_t)wl.queue;
-#pragma unroll
-    for (int k = 0; k < kSub; ++k) {
-        if (m[k]) {
-            const uint32_t off =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            const uint32_t qb = __builtin_amdgcn_readfirstlane(qbase + 4u * (uint32_t)qn);
-            const uint32_t a = select_by_mask(m[k], (off << 2) + qb, dummy_a);
-            *(lds_u32*)(size_t)a = ((uint32_t)N << kPosBits) | pk.tb[k];
-            qn += __popcll(m[k]);
-        }
-    }
+    append_pack(wl.queue, qn, m, (uint32_t)N, pk);
 }
 
 // One pack: documents [i, i + nd) of the staged group, ends e1 < e2 < e3 <=
@@ -905,7 +1017,6 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
     }
     uint32_t fm = __builtin_amdgcn_readfirstlane(p.fast_mask | (p.direct_words ? 1u << kFmDirect : 0u));
     asm volatile("" : "+s"(fm));
-    const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
     int qn = 0;
     if (ablated(p, 2)) fm = 0;
     uint32_t kw[kPreN][kSub];
@@ -914,13 +1025,13 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
         keyed_preload<4>(f, x, fm, kw);
         keyed_preload<5>(f, x, fm, kw);
     }
-    probe_pack<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<3, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<4, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<5, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<6, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
-    probe_pack<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<3, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<4, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<5, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<6, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {  // wide lengths 8..15
         const int n = 8 + __builtin_ctz(wm);
         constexpr int K3 = KEYED ? 4 : 3;
@@ -937,18 +1048,7 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
             flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
             qn = 0;
         }
-        const uint32_t qbase = (uint32_t)(uintptr_t)wl.queue;
-#pragma unroll
-        for (int k = 0; k < kSub; ++k) {
-            if (m[k]) {
-                const uint32_t off =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-                const uint32_t qb = __builtin_amdgcn_readfirstlane(qbase + 4u * (uint32_t)qn);
-                const uint32_t a = select_by_mask(m[k], (off << 2) + qb, dummy_a);
-                *(lds_u32*)(size_t)a = ((uint32_t)n << kPosBits) | pk.tb[k];
-                qn += __popcll(m[k]);
-            }
-        }
+        append_pack(wl.queue, qn, m, (uint32_t)n, pk);
     }
     if (ablated(p, 1)) qn = 0;
     if (qn) {
@@ -970,7 +1070,6 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
 #pragma unroll
     for (int s = 0; s < S; ++s) acc[s] = 0.0;
     int qn = 0;
-    const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
     bool general = !(len >= p.maxg && len <= 64 * kSub);
     if (!general) {
         // fast path: every window is full-length (klen = n) and one
@@ -988,9 +1087,9 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             load_fwords<KEYED>(p, bloom, x, f);
             if constexpr (MODE == 3) {
                 if (len >= 192 + p.maxg)
-                    probe_count_all<true, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
+                    probe_count_all<true, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src);
                 else
-                    probe_count_all<false, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src, dummy_a);
+                    probe_count_all<false, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src);
             }
             uint64_t gq = p.gpack[0];
             for (int gi = 0; gi < (MODE == 3 ? 0 : p.n_fast); ++gi) {
@@ -1009,7 +1108,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                     general = true;
                     break;
                 }
-                append_sb(wl.queue, dummy_a, qn, m, n, 0, lane);
+                append_sb(wl.queue, qn, m, n, 0, lane);
             }
             if (!general) {
                 if (ablated(p, 1)) qn = 0;
@@ -1038,7 +1137,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                     flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
                     qn = 0;
                 }
-                append_sb(wl.queue, dummy_a, qn, m, g.klen, p0, lane);
+                append_sb(wl.queue, qn, m, g.klen, p0, lane);
             }
         }
     }

@@ -22,7 +22,7 @@ for s in $ONLY; do
   case $s in
     c2)   step bench_c2 300 python -u bench.py --json-out "$OUT/bench_c2.json" ;;
     prof) step rocprof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof_c2" -o run \
-            -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-path
+            -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --no-alt-paths
           find "$OUT/prof_c2" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_c2.csv" \; ;;
     c4)   step bench_c4 400 python -u bench.py --config 4 --steps 10 --warmup 2 --json-out "$OUT/bench_c4.json" ;;
     c5)   step bench_c5 500 python -u bench.py --config 5 --steps 5 --warmup 1 --no-host-path --json-out "$OUT/bench_c5.json" ;;

@@ -15,7 +15,7 @@ run() {  # name counter extra-args...
   local name=$1 ctr=$2; shift 2
   echo "== $name ($ctr)"
   timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/$name" -o run -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path --json-out "$PWD/$OUT/$name.json" "$@" > "$OUT/$name.log" 2>&1
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path --no-alt-paths --json-out "$PWD/$OUT/$name.json" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/$name.log"; exit $rc; }
 }
