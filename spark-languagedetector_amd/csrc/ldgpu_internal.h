@@ -109,9 +109,10 @@ constexpr uint32_t kPackDocs = 4;
 
 // per-wave hit area (u32 words): ordered modes hold 64 verified hits of
 // (S + 2) / 2 uint4 each; count mode (3) holds the 64 S u32 per-language
-// counters (packing: kPackDocs blocks of 64 S u16 counters)
+// counters (packing: 64 words for the pack probe's non-candidate stores, then
+// kPackDocs blocks of 64 S u16 counters)
 constexpr uint32_t hit_area_words(int slices, int mode, bool pack = false) {
-    return mode == 3 ? 64u * (pack ? kPackDocs / 2u : 1u) * (uint32_t)slices
+    return mode == 3 ? (pack ? 64u + 64u * (kPackDocs / 2u) * (uint32_t)slices : 64u * (uint32_t)slices)
                      : 64u * 4u * (((uint32_t)slices + 2u) / 2u);
 }
 

@@ -90,10 +90,13 @@ struct WaveLds {
                       // (MODE 3: the document's per-language hit counters, count_area)
     uint32_t* buf;    // [2][kBufBytes / 4 + 4] staged bytes of document groups (double buffer)
     uint32_t* labels; // [64] labels of the current group
+    uint32_t* cnt;    // MODE 3: per-language hit counters (count_area)
 };
 
-// MODE 3 per-language hit counters: the wave's hit area; hit_area_words(S, 3).
-__device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return reinterpret_cast<uint32_t*>(w.hits); }
+// MODE 3 per-language hit counters: the wave's hit area -- in the packing
+// kernels after its first 64 words, which take the pack probe's non-candidate
+// stores (append_pack); hit_area_words(S, 3, pack).
+__device__ __forceinline__ uint32_t* count_area(const WaveLds& w) { return w.cnt; }
 
 // counter idx += inc: u32 counters, or (PACK: packed short documents) u16
 // counters two to a word -- a document of a pack has at most 256 windows per
@@ -757,17 +760,20 @@ struct PackPos {
     uint32_t tb[kSub];  // document index << 8 | position in the pack
 };
 
-// append_sb for packs: an entry is klen << kPosBits | the pack tag (tb)
+// append_sb for packs: an entry is klen << kPosBits | the pack tag (tb).
+// Every lane stores (measured faster here than an exec-masked store): a
+// candidate to its queue rank, the others to their own word at dummy_a.
 __device__ __forceinline__ void append_pack(uint32_t* queue, int& qn, const uint64_t (&m)[kSub], uint32_t klen,
-                                            const PackPos& pk) {
+                                            const PackPos& pk, uint32_t dummy_a) {
     const uint32_t qbase = (uint32_t)(uintptr_t)queue;
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
         if (m[k]) {
             const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], (uint32_t)qn));
-            if (__builtin_amdgcn_inverse_ballot_w64(m[k]))
-                *(lds_u32*)(size_t)(qbase + 4u * at) = (klen << kPosBits) | pk.tb[k];
+            uint32_t a;  // bit `lane` of m[k] ? queue word : dummy word (one v_cndmask on the mask)
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(a) : "v"(dummy_a), "v"(qbase + 4u * at), "s"(m[k]));
+            *(lds_u32*)(size_t)a = (klen << kPosBits) | pk.tb[k];
             qn += __popcll(m[k]);
         }
     }
@@ -962,7 +968,7 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
 template <int N, int S, bool KEYED, bool WIDE>
 __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
-                                           const DocSrc& src, uint32_t fm,
+                                           const DocSrc& src, uint32_t dummy_a, uint32_t fm,
                                            const uint32_t (&kw)[kPreN][kSub]) {
     if (!((fm >> N) & 1u)) return;
     if (ablated(p, N <= 2 ? 8 : 16)) return;
@@ -992,7 +998,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
         flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
         qn = 0;
     }
-    append_pack(wl.queue, qn, m, (uint32_t)N, pk);
+    append_pack(wl.queue, qn, m, (uint32_t)N, pk, dummy_a);
 }
 
 // One pack: documents [i, i + nd) of the staged group, ends e1 < e2 < e3 <=
@@ -1019,19 +1025,20 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
     asm volatile("" : "+s"(fm));
     int qn = 0;
     if (ablated(p, 2)) fm = 0;
+    const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
     uint32_t kw[kPreN][kSub];
     if constexpr (KEYED) {
         keyed_preload<3>(f, x, fm, kw);
         keyed_preload<4>(f, x, fm, kw);
         keyed_preload<5>(f, x, fm, kw);
     }
-    probe_pack<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
-    probe_pack<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
-    probe_pack<3, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
-    probe_pack<4, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
-    probe_pack<5, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
-    probe_pack<6, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
-    probe_pack<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, fm, kw);
+    probe_pack<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<3, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<4, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<5, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<6, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+    probe_pack<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {  // wide lengths 8..15
         const int n = 8 + __builtin_ctz(wm);
         constexpr int K3 = KEYED ? 4 : 3;
@@ -1048,7 +1055,7 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
             flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
             qn = 0;
         }
-        append_pack(wl.queue, qn, m, (uint32_t)n, pk);
+        append_pack(wl.queue, qn, m, (uint32_t)n, pk, dummy_a);
     }
     if (ablated(p, 1)) qn = 0;
     if (qn) {
@@ -1247,6 +1254,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap + wave * kHitW);
     wl.buf = lds + img_words + kScoreWaves * (kQueueCap + kHitW) + wave * 2 * kBufWords;
     wl.labels = lds + img_words + kScoreWaves * (kQueueCap + kHitW + 2 * kBufWords) + wave * 64;
+    wl.cnt = reinterpret_cast<uint32_t*>(wl.hits) + (PACK ? 64 : 0);
 
     if constexpr (MODE == 3) {
         uint32_t* cnt = count_area(wl);
