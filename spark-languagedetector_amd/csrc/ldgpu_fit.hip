@@ -346,18 +346,31 @@ __global__ void presence_kernel(const CountParams p, uint64_t cap, int S, uint64
             const uint32_t off =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             const unsigned long long o = base + off;
+            const unsigned long long* row = p.counts + i * L;
+            // the row's presence bits, 64 languages a word, 8 counters per
+            // batch of independent loads (no per-counter branch); then the
+            // (language, k) histogram from the bits -- the row is read once
             int k = 0;
             for (int s = 0; s < S; ++s) {
+                const int l0 = 64 * s, nl = min(64, L - l0);
                 uint64_t w = 0;
-                for (int b = 0; b < 64 && s * 64 + b < L; ++b)
-                    if (p.counts[i * L + s * 64 + b] != 0ull) w |= 1ull << b;
+                for (int b0 = 0; b0 < nl; b0 += 8) {
+                    unsigned long long v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = b0 + u < nl ? row[l0 + b0 + u] : 0ull;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) w |= (uint64_t)(v[u] != 0ull) << (b0 + u);
+                }
                 out_masks[o * S + s] = w;
                 k += __popcll(w);
             }
             out_keys[o] = p.keys[i];
             out_k[o] = k;
-            for (int l = 0; l < L; ++l) {
-                if (p.counts[i * L + l] != 0ull) {
+            for (int s = 0; s < S; ++s) {
+                uint64_t w = out_masks[o * S + s];
+                while (w) {
+                    const int l = 64 * s + __builtin_ctzll(w);
+                    w &= w - 1;
                     if (lds_hist)
                         atomicAdd(&lhist[l * (L + 1) + k], 1u);
                     else
