@@ -94,7 +94,7 @@ constexpr int kScoreWaves = LDGPU_SCORE_WAVES;  // waves per workgroup (768 thre
 #endif
 constexpr int kScoreMinWgPerCu = LDGPU_SCORE_MIN_WG;
 constexpr int kQueueCap = 288;             // candidate entries (u32) per wave (>= 256 + slack)
-constexpr int kBufBytes = 1024;            // staged bytes of a document group per wave
+constexpr int kBufBytes = 1024;            // staged bytes of a document group per wave (one 64 x 16-B LDS-DMA)
 constexpr int kBufWords = kBufBytes / 4 + 4;
 constexpr int kMaxLdsBloomLog2 = 14;       // bloom words in LDS up to 64 KiB
 constexpr int kMaxBloomLog2 = 22;          // bloom_shift >= 10
