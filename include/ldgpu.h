@@ -52,9 +52,8 @@ enum ldgpu_status {
 /* Device-path limits.  Gram lengths 1..LDGPU_MAX_GRAM for SCORE tables and
  * LDGPU_MAX_FIT_GRAM for FIT counting: keys of up to 7 bytes pack into one
  * u64 (7 payload bytes + a length byte); keys of 8..15 bytes take two words,
- * in a table of their own (SCORE and FIT alike; the multi-GPU FIT merge covers
- * lengths 1..7).  1..LDGPU_MAX_LANGS languages (SCORE scores more than 256 in
- * blocks of 256 languages). */
+ * in a table of their own (SCORE and FIT alike).  1..LDGPU_MAX_LANGS
+ * languages (SCORE scores more than 256 in blocks of 256 languages). */
 #define LDGPU_MAX_GRAM 15      /* SCORE tables: keys of 8..15 bytes take two words */
 #define LDGPU_MAX_FIT_GRAM 15  /* FIT counting: keys of 8..15 bytes in a two-word table */
 #define LDGPU_MAX_LANGS 4096
@@ -214,6 +213,9 @@ int ldgpu_comm_destroy(ldgpu_comm* comm);
  * merged table runs the global top-K through the communicator (a (language,
  * class) histogram all-reduce, an all-gather of each rank's tie candidates,
  * an all-gather of the chosen rows), and every rank exports the same table.
+ * Grams of 8..15 bytes (their own table) travel by an all-gather of every
+ * rank's entries instead, each rank keeping those it owns, and a merged table
+ * holding any takes the top-K over every rank's presence rows on the host.
  * Collective: every rank calls it.  Counting more documents into a merged
  * table is an error (LDGPU_EINVAL). */
 int ldgpu_counts_merge(ldgpu_counts* counts, ldgpu_comm* comm);

@@ -1354,6 +1354,7 @@ struct ldgpu_counts {
     ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
     // grams of 8..15 bytes: a two-word-key table of their own (ldgpu_fit.hip)
     uint64_t wcap = 0, wsize = 0;
+    bool merged_wide = false;   // merged table: some rank held wide grams (the same on every rank)
     uint64_t* d_wlo = nullptr;
     uint64_t* d_whi = nullptr;
     unsigned long long* d_wcounts = nullptr;
@@ -2015,6 +2016,49 @@ struct DevBufs {
     }
 };
 
+// the wide table's occupied slots (unordered): lo, hi, counts rows
+int wide_export(ldgpu_counts* c, std::vector<uint64_t>& wlo, std::vector<uint64_t>& whi,
+                std::vector<unsigned long long>& wc) {
+    const uint64_t nw = c->wsize;
+    wlo.assign(nw, 0);
+    whi.assign(nw, 0);
+    wc.assign((size_t)nw * c->L, 0);
+    if (!nw) return LDGPU_OK;
+    DevBufs wb;
+    uint64_t *d_lo, *d_hi;
+    unsigned long long *d_wc, *d_wn;
+    HIP_TRY(wb.alloc(&d_lo, nw));
+    HIP_TRY(wb.alloc(&d_hi, nw));
+    HIP_TRY(wb.alloc(&d_wc, (size_t)nw * c->L));
+    HIP_TRY(wb.alloc(&d_wn, 1));
+    hipStream_t st = c->ctx->stream;
+    HIP_TRY(hipMemsetAsync(d_wn, 0, sizeof(unsigned long long), st));
+    HIP_TRY(launch_wide_compact(wide_params(c), c->wcap, d_lo, d_hi, d_wc, d_wn, st));
+    unsigned long long got = 0;
+    HIP_TRY(hipMemcpyAsync(&got, d_wn, sizeof got, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(wlo.data(), d_lo, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(whi.data(), d_hi, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(wc.data(), d_wc, nw * c->L * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (got != nw)
+        return fail(LDGPU_EDEVICE, "wide count export: %llu slots occupied, %llu expected", got, (unsigned long long)nw);
+    return LDGPU_OK;
+}
+
+// the (length, bytes) order of wide keys: length, then bytes 0..7, then 8..
+std::vector<uint64_t> wide_order(const std::vector<uint64_t>& wlo, const std::vector<uint64_t>& whi) {
+    auto be = [](uint64_t x) { return __builtin_bswap64(x); };
+    std::vector<uint64_t> word(wlo.size());
+    for (uint64_t i = 0; i < word.size(); ++i) word[i] = i;
+    std::sort(word.begin(), word.end(), [&](uint64_t a, uint64_t b) {
+        const int la = key_len(whi[a]), lb = key_len(whi[b]);
+        if (la != lb) return la < lb;
+        if (wlo[a] != wlo[b]) return be(wlo[a]) < be(wlo[b]);
+        return be(whi[a] << 8) < be(whi[b] << 8);
+    });
+    return word;
+}
+
 // compacted host copy: keys + counts rows, sorted by (length, bytes)
 int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsigned long long>& cnt) {
     const uint64_t n = c->size;
@@ -2045,44 +2089,11 @@ int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsign
     std::sort(sk.begin(), sk.end());
     // the wide grams (8..15 bytes) after them, in (length, bytes) order, as
     // stand-in keys kWideTag << 56 | rank (c->wide_sorted[rank])
-    const uint64_t nw = c->wsize;
-    std::vector<uint64_t> wlo(nw), whi(nw);
-    std::vector<unsigned long long> wc((size_t)nw * c->L);
-    if (nw) {
-        uint64_t *d_lo = nullptr, *d_hi = nullptr;
-        unsigned long long *d_wc = nullptr, *d_wn = nullptr;
-        hipError_t e2 = hipMalloc((void**)&d_lo, nw * sizeof(uint64_t));
-        if (e2 == hipSuccess) e2 = hipMalloc((void**)&d_hi, nw * sizeof(uint64_t));
-        if (e2 == hipSuccess) e2 = hipMalloc((void**)&d_wc, nw * c->L * sizeof(unsigned long long));
-        if (e2 == hipSuccess) e2 = hipMalloc((void**)&d_wn, sizeof(unsigned long long));
-        if (e2 == hipSuccess) e2 = hipMemsetAsync(d_wn, 0, sizeof(unsigned long long), c->ctx->stream);
-        if (e2 == hipSuccess) e2 = launch_wide_compact(wide_params(c), c->wcap, d_lo, d_hi, d_wc, d_wn, c->ctx->stream);
-        unsigned long long wgot = 0;
-        if (e2 == hipSuccess) e2 = hipMemcpyAsync(&wgot, d_wn, sizeof wgot, hipMemcpyDeviceToHost, c->ctx->stream);
-        if (e2 == hipSuccess)
-            e2 = hipMemcpyAsync(wlo.data(), d_lo, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->ctx->stream);
-        if (e2 == hipSuccess)
-            e2 = hipMemcpyAsync(whi.data(), d_hi, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->ctx->stream);
-        if (e2 == hipSuccess)
-            e2 = hipMemcpyAsync(wc.data(), d_wc, nw * c->L * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                c->ctx->stream);
-        if (e2 == hipSuccess) e2 = hipStreamSynchronize(c->ctx->stream);
-        for (void* p : {(void*)d_lo, (void*)d_hi, (void*)d_wc, (void*)d_wn})
-            if (p) (void)hipFree(p);
-        if (e2 != hipSuccess) return fail(LDGPU_EDEVICE, "wide count export: %s", hipGetErrorString(e2));
-        if (wgot != nw) return fail(LDGPU_EDEVICE, "wide count export: %llu slots occupied, %llu expected", wgot,
-                                    (unsigned long long)nw);
-    }
-    // (length, bytes) order of a wide key: length, then bytes 0..7, then 8..
-    auto be = [](uint64_t x) { return __builtin_bswap64(x); };
-    std::vector<uint64_t> word(nw);
-    for (uint64_t i = 0; i < nw; ++i) word[i] = i;
-    std::sort(word.begin(), word.end(), [&](uint64_t a, uint64_t b) {
-        const int la = key_len(whi[a]), lb = key_len(whi[b]);
-        if (la != lb) return la < lb;
-        if (wlo[a] != wlo[b]) return be(wlo[a]) < be(wlo[b]);
-        return be(whi[a] << 8) < be(whi[b] << 8);
-    });
+    std::vector<uint64_t> wlo, whi;
+    std::vector<unsigned long long> wc;
+    if (int rc = wide_export(c, wlo, whi, wc)) return rc;
+    const uint64_t nw = wlo.size();
+    const std::vector<uint64_t> word = wide_order(wlo, whi);
     c->wide_sorted.resize(nw);
     keys.resize(n + nw);
     cnt.resize((size_t)(n + nw) * c->L);
@@ -2534,6 +2545,69 @@ extern "C" int ldgpu_comm_destroy(ldgpu_comm* m) {
     return ok();
 }
 
+namespace {
+uint32_t wide_owner(uint64_t lo, uint64_t hi, uint32_t world) {
+    return (uint32_t)(((mix64(lo ^ mix64(hi)) & 0xffffffffull) * world) >> 32);
+}
+
+// The merge's wide grams (8..15 bytes, their own table): every rank's entries
+// reach every rank over the host all-gather -- they are few next to the
+// one-word grams -- and each rank keeps, summed, those it owns.  Sets
+// c->merged_wide on every rank alike when any rank held one.
+int merge_wide(ldgpu_counts* c, ldgpu_comm* m) {
+    const int L = c->L;
+    std::vector<uint64_t> wlo, whi;
+    std::vector<unsigned long long> wc;
+    if (int rc = wide_export(c, wlo, whi, wc)) return rc;
+    std::vector<uint8_t> blob;
+    put(blob, wlo.data(), wlo.size());
+    put(blob, whi.data(), whi.size());
+    put(blob, wc.data(), wc.size());
+    std::vector<std::vector<uint8_t>> all;
+    if (int rc = comm_allgatherv_host(m, blob, all)) return rc;
+    std::vector<uint64_t> olo, ohi;
+    std::vector<unsigned long long> orows;
+    bool any = false;
+    for (int r = 0; r < m->world; ++r) {
+        const size_t nr = all[r].size() / (16 + 8 * (size_t)L);
+        any |= nr > 0;
+        const uint64_t* lo = reinterpret_cast<const uint64_t*>(all[r].data());
+        const uint64_t* hi = lo + nr;
+        const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(hi + nr);
+        for (size_t i = 0; i < nr; ++i) {
+            if (wide_owner(lo[i], hi[i], (uint32_t)m->world) != (uint32_t)m->rank) continue;
+            olo.push_back(lo[i]);
+            ohi.push_back(hi[i]);
+            orows.insert(orows.end(), rows + i * L, rows + (i + 1) * L);
+        }
+    }
+    c->merged_wide = any;
+    // this rank's wide table, rebuilt from the owned entries
+    for (void* q : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts})
+        if (q) (void)hipFree(q);
+    c->d_wlo = c->d_whi = nullptr;
+    c->d_wcounts = nullptr;
+    c->wcap = 0;
+    c->wsize = 0;
+    if (c->d_wsize) HIP_TRY(hipMemsetAsync(c->d_wsize, 0, sizeof(unsigned long long), c->ctx->stream));
+    const int64_t n = (int64_t)olo.size();
+    if (!n) return LDGPU_OK;
+    if (int rc = wide_ensure(c, (uint64_t)n)) return rc;
+    DevBufs wb;
+    uint64_t *d_lo, *d_hi;
+    unsigned long long* d_r;
+    HIP_TRY(wb.alloc(&d_lo, n));
+    HIP_TRY(wb.alloc(&d_hi, n));
+    HIP_TRY(wb.alloc(&d_r, (size_t)n * L));
+    hipStream_t st = c->ctx->stream;
+    HIP_TRY(hipMemcpyAsync(d_lo, olo.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_hi, ohi.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_r, orows.data(), (size_t)n * L * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_wide_add(wide_params(c), d_lo, d_hi, d_r, n, st));
+    return wide_after(c);
+}
+}  // namespace
+
 // Owner exchange: every rank partitions its table by owner, one
 // all-to-all moves each rank's keys and count rows to their owners, and each
 // rank rebuilds its table from what it received: the global counts of the
@@ -2542,10 +2616,6 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     if (!c || !m) return fail(LDGPU_EINVAL, "NULL argument");
     if (c->comm) return fail(LDGPU_EINVAL, "the count table is already merged");
     if (m->ctx != c->ctx) return fail(LDGPU_EINVAL, "communicator and count table belong to different contexts");
-    // (every rank has the same gram lengths, so all ranks fail alike)
-    if (c->nGw > 0 || c->wsize > 0)
-        return fail(LDGPU_EUNSUPPORTED, "the multi-GPU merge covers gram lengths 1..%d; this table counts grams of "
-                                        "8..15 bytes", kMaxGram);
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
     const int W = m->world, L = c->L;
@@ -2605,6 +2675,7 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     HIP_TRY(launch_counts_add(count_params(c), d_rkeys, d_rrows, nullptr, nullptr, R, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (int rc = after_batch(c)) return rc;
+    if (int rc = merge_wide(c, m)) return rc;
     c->comm = m;
     c->tbl_valid = false;
     return ok();
@@ -2670,6 +2741,9 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         }
         if (kstar[l] == L + 1 && acc < K) *fallback = true;  // zero-valued fill: every gram takes part
     }
+    // a merged table with wide grams (c->merged_wide, alike on every rank)
+    // selects on the host over every rank's presence rows, wide ones included
+    if (cm && c->merged_wide) *fallback = true;
     if (*fallback) {
         if (!cm) return LDGPU_OK;  // the host build from the count table
         // merged table: gather every rank's presence rows, select on the host
@@ -2697,6 +2771,36 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         for (size_t j = 0; j < order.size(); ++j) {
             keys[j] = rk[order[j].second.first][order[j].second.second];
             memcpy(&masks[j * S], rm[order[j].second.first] + order[j].second.second * S, 8 * S);
+        }
+        if (c->merged_wide) {  // every rank's wide grams after them, in (length, bytes) order
+            std::vector<uint64_t> wlo, whi;
+            std::vector<unsigned long long> wc;
+            if (int rc = wide_export(c, wlo, whi, wc)) return rc;
+            std::vector<uint64_t> wm(wlo.size() * S, 0);
+            for (size_t i = 0; i < wlo.size(); ++i)
+                for (int l = 0; l < L; ++l)
+                    if (wc[i * L + l]) wm[i * S + l / 64] |= 1ull << (l % 64);
+            std::vector<uint8_t> wblob;
+            put(wblob, wlo.data(), wlo.size());
+            put(wblob, whi.data(), whi.size());
+            put(wblob, wm.data(), wm.size());
+            std::vector<std::vector<uint8_t>> wall;
+            if (int rc = comm_allgatherv_host(cm, wblob, wall)) return rc;
+            std::vector<uint64_t> glo, ghi, gm;
+            for (int r = 0; r < cm->world; ++r) {
+                const size_t nr = wall[r].size() / (8 * (2 + (size_t)S));
+                const uint64_t* lo = reinterpret_cast<const uint64_t*>(wall[r].data());
+                glo.insert(glo.end(), lo, lo + nr);
+                ghi.insert(ghi.end(), lo + nr, lo + 2 * nr);
+                gm.insert(gm.end(), lo + 2 * nr, lo + 2 * nr + nr * S);
+            }
+            const std::vector<uint64_t> word = wide_order(glo, ghi);
+            c->wide_sorted.resize(word.size());
+            for (size_t r = 0; r < word.size(); ++r) {
+                c->wide_sorted[r] = {glo[word[r]], ghi[word[r]]};
+                keys.push_back((kWideTag << 56) | r);
+                masks.insert(masks.end(), gm.begin() + word[r] * S, gm.begin() + (word[r] + 1) * S);
+            }
         }
         *fallback = false;
         return table_from_presence(c, keys, masks, K, n_rows, key_bytes);

@@ -144,22 +144,25 @@ def _check_fit(tmp_path, world, K, grams):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,grams", [(80, [1, 2, 3]), (5000, [2, 3])])
+@pytest.mark.parametrize("K,grams", [(80, [1, 2, 3]), (5000, [2, 3]), (60, [2, 9]), (5000, [1, 8, 12])])
 def test_fit_distributed_matches_single_process(tmp_path, K, grams):
     """Two ranks (cuda:0 each), host transport over gloo: the library's owner
     exchange leaves disjoint shards with the oracle's global counts, and the
     distributed top-K gives every rank the oracle's table -- also with K above
-    some language's present grams (the zero-valued fill)."""
+    some language's present grams (the zero-valued fill), and with gram
+    lengths 8..15 (wide grams: every rank's entries all-gathered, each rank
+    keeping those it owns; the top-K over every rank's presence rows)."""
     mp.spawn(_fit_worker, args=(2, free_port(), str(tmp_path), K, grams, "host"), nprocs=2, join=True)
     _check_fit(tmp_path, 2, K, grams)
 
 
 @pytest.mark.gpu
-def test_fit_merge_rccl_transport_world1(tmp_path):
+@pytest.mark.parametrize("grams", [[1, 2, 3], [2, 9]])
+def test_fit_merge_rccl_transport_world1(tmp_path, grams):
     """The RCCL transport (ncclCommInitRank, grouped ncclSend/ncclRecv,
     ncclAllGather) at world size 1, the only size one GPU allows."""
-    mp.spawn(_fit_worker, args=(1, free_port(), str(tmp_path), 80, [1, 2, 3], "rccl"), nprocs=1, join=True)
-    _check_fit(tmp_path, 1, 80, [1, 2, 3])
+    mp.spawn(_fit_worker, args=(1, free_port(), str(tmp_path), 80, grams, "rccl"), nprocs=1, join=True)
+    _check_fit(tmp_path, 1, 80, grams)
 
 
 def _score_worker(rank, world, port, out_dir):
