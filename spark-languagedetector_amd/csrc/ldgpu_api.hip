@@ -203,7 +203,7 @@ struct ldgpu_ctx {
 
 namespace {
 constexpr size_t kCacheMaxBytes = 96ull << 30;
-constexpr size_t kCacheMaxBlocks = 32;
+constexpr size_t kCacheMaxBlocks = 64;
 
 hipError_t cache_alloc(ldgpu_ctx* c, void** p, size_t bytes) {
     {
@@ -1999,18 +1999,28 @@ extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t*
 }
 
 namespace {
-// device scratch freed on scope exit
+// device scratch freed on scope exit; with a context, the blocks come from
+// and go back to its cache (a fit's scratch has the same sizes fit after fit:
+// no hipMalloc / hipFree per call).  Blocks go back once the caller's work on
+// the context's stream is queued; later users of the stream run after it.
 struct DevBufs {
-    std::vector<void*> p;
+    ldgpu_ctx* ctx = nullptr;
+    std::vector<std::pair<void*, size_t>> p;
     ~DevBufs() {
-        for (void* x : p)
-            if (x) (void)hipFree(x);
+        for (auto& x : p) {
+            if (!x.first) continue;
+            if (ctx)
+                cache_free(ctx, x.first, x.second);
+            else
+                (void)hipFree(x.first);
+        }
     }
     template <typename T>
     hipError_t alloc(T** out, size_t n) {
         void* x = nullptr;
-        hipError_t e = hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T));
-        if (e == hipSuccess) p.push_back(x);
+        const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        hipError_t e = ctx ? cache_alloc(ctx, &x, bytes) : hipMalloc(&x, bytes);
+        if (e == hipSuccess) p.emplace_back(x, bytes);
         *out = (T*)x;
         return e;
     }
@@ -2696,6 +2706,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     const int64_t n = (int64_t)c->size;
     hipStream_t st = c->ctx->stream;
     DevBufs db;
+    db.ctx = c->ctx;
     uint64_t *d_keys, *d_masks;
     int32_t* d_k;
     unsigned long long* d_n;

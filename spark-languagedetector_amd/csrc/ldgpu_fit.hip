@@ -34,6 +34,39 @@ __device__ __forceinline__ uint32_t ld_dw(const uint32_t* w, int64_t i, int64_t 
     return w[i < last ? i : last];
 }
 
+// Block-level compaction: the block's occupied slots of one chunk get
+// consecutive output positions from ONE global atomic (a per-wave atomic on
+// the one counter serialises ~cap/64 of them at an L2 channel: 12.6 ms of a
+// 64M-slot table); returns this thread's output index (valid if occ).
+constexpr int kScanThreads = 1024;
+
+// grid of the grid-stride compaction kernels: up to 2048 blocks of kScanThreads
+unsigned scan_grid(uint64_t n) {
+    return (unsigned)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + kScanThreads - 1) / kScanThreads));
+}
+
+__device__ __forceinline__ unsigned long long block_compact(bool occ, unsigned long long* out_n, unsigned int* wcnt,
+                                                            unsigned long long* bbase) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m = __ballot(occ);
+    if (lane == 0) wcnt[wave] = (unsigned int)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int acc = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) {
+            const unsigned int c = wcnt[w];
+            wcnt[w] = acc;
+            acc += c;
+        }
+        *bbase = acc ? atomicAdd(out_n, (unsigned long long)acc) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long o = *bbase + wcnt[wave] +
+                                 __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    __syncthreads();  // wcnt / bbase are reused by the next chunk
+    return o;
+}
+
 // find-or-insert; returns the slot or -1 when the probe limit is reached
 __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key, bool& new_key) {
     uint64_t s = mix64(key) >> p.shift;
@@ -218,10 +251,12 @@ __global__ void counts_add_kernel(const CountParams p, const uint64_t* keys, con
 }
 
 // table statistics: [0] distinct (gram, language) pairs, [1] sum of counts
-__global__ void stats_kernel(const CountParams p, uint64_t cap, unsigned long long* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// (grid-stride, one pair of global atomics per block)
+__global__ __launch_bounds__(256) void stats_kernel(const CountParams p, uint64_t cap, unsigned long long* out) {
+    __shared__ unsigned long long red[2][4];
     unsigned long long pairs = 0, total = 0;
-    if (i < cap && p.keys[i] != kEmpty) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (p.keys[i] == kEmpty) continue;
         for (int l = 0; l < p.L; ++l) {
             const unsigned long long c = p.counts[i * p.L + l];
             pairs += c != 0ull;
@@ -233,9 +268,18 @@ __global__ void stats_kernel(const CountParams p, uint64_t cap, unsigned long lo
         pairs += __shfl_xor(pairs, o);
         total += __shfl_xor(total, o);
     }
-    if ((threadIdx.x & 63) == 0 && (pairs | total)) {
-        atomicAdd(&out[0], pairs);
-        atomicAdd(&out[1], total);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = pairs;
+        red[1][threadIdx.x >> 6] = total;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        const unsigned long long b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        if (a | b) {
+            atomicAdd(&out[0], a);
+            atomicAdd(&out[1], b);
+        }
     }
 }
 
@@ -254,22 +298,19 @@ __global__ void rehash_kernel(const CountParams from, const CountParams to, uint
     for (int l = 0; l < from.L; ++l) to.counts[(size_t)s * to.L + l] = from.counts[(size_t)i * from.L + l];
 }
 
-__global__ void compact_kernel(const CountParams p, uint64_t cap, uint64_t* out_keys,
-                               unsigned long long* out_counts, unsigned long long* out_n) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool occ = i < cap && p.keys[i] != kEmpty;
-    const uint64_t m = __ballot(occ);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    unsigned long long base = 0;
-    const int leader = __builtin_ctzll(m);
-    if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    if (!occ) return;
-    const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    const unsigned long long o = base + off;
-    out_keys[o] = p.keys[i];
-    for (int l = 0; l < p.L; ++l) out_counts[o * p.L + l] = p.counts[i * p.L + l];
+__global__ __launch_bounds__(kScanThreads) void compact_kernel(const CountParams p, uint64_t cap, uint64_t* out_keys,
+                                                               unsigned long long* out_counts,
+                                                               unsigned long long* out_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < cap; c0 += (uint64_t)gridDim.x * kScanThreads) {
+        const uint64_t i = c0 + threadIdx.x;
+        const bool occ = i < cap && p.keys[i] != kEmpty;
+        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
+        if (!occ) continue;
+        out_keys[o] = p.keys[i];
+        for (int l = 0; l < p.L; ++l) out_counts[o * p.L + l] = p.counts[i * p.L + l];
+    }
 }
 
 }  // namespace
@@ -289,7 +330,8 @@ hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const u
 }
 
 hipError_t launch_stats(const CountParams& p, uint64_t cap, unsigned long long* out, hipStream_t stream) {
-    hipLaunchKernelGGL(stats_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out);
+    hipLaunchKernelGGL(stats_kernel, dim3((unsigned)std::min<uint64_t>(4096, (cap + 255) / 256)), dim3(256), 0, stream,
+                       p, cap, out);
     return hipGetLastError();
 }
 
@@ -301,7 +343,7 @@ hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_
 
 hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys, unsigned long long* out_counts,
                           unsigned long long* out_n, hipStream_t stream) {
-    hipLaunchKernelGGL(compact_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out_keys,
+    hipLaunchKernelGGL(compact_kernel, dim3(scan_grid(cap)), dim3(kScanThreads), 0, stream, p, cap, out_keys,
                        out_counts, out_n);
     return hipGetLastError();
 }
@@ -324,58 +366,54 @@ hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys
 namespace ldgpu {
 namespace {
 
-__global__ void presence_kernel(const CountParams p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
-                                int32_t* out_k, unsigned long long* out_n, unsigned int* hist) {
+// grid-stride over the table in chunks of kScanThreads slots; the (language,
+// k) histogram in LDS (L <= 88), flushed once per block
+__global__ __launch_bounds__(kScanThreads) void presence_kernel(const CountParams p, uint64_t cap, int S,
+                                                                uint64_t* out_keys, uint64_t* out_masks,
+                                                                int32_t* out_k, unsigned long long* out_n,
+                                                                unsigned int* hist) {
     extern __shared__ unsigned int lhist[];
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
     const int L = p.L;
     const bool lds_hist = L <= 88;  // L * (L + 1) * 4 B <= 31 KiB
     if (lds_hist) {
         for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x) lhist[i] = 0u;
         __syncthreads();
     }
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool occ = i < cap && p.keys[i] != kEmpty;
-    const uint64_t m = __ballot(occ);
-    const int lane = threadIdx.x & 63;
-    if (m) {
-        unsigned long long base = 0;
-        const int leader = __builtin_ctzll(m);
-        if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
-        base = __shfl(base, leader);
-        if (occ) {
-            const uint32_t off =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const unsigned long long o = base + off;
-            const unsigned long long* row = p.counts + i * L;
-            // the row's presence bits, 64 languages a word, 8 counters per
-            // batch of independent loads (no per-counter branch); then the
-            // (language, k) histogram from the bits -- the row is read once
-            int k = 0;
-            for (int s = 0; s < S; ++s) {
-                const int l0 = 64 * s, nl = min(64, L - l0);
-                uint64_t w = 0;
-                for (int b0 = 0; b0 < nl; b0 += 8) {
-                    unsigned long long v[8];
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < cap; c0 += (uint64_t)gridDim.x * kScanThreads) {
+        const uint64_t i = c0 + threadIdx.x;
+        const bool occ = i < cap && p.keys[i] != kEmpty;
+        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
+        if (!occ) continue;
+        const unsigned long long* row = p.counts + i * L;
+        // the row's presence bits, 64 languages a word, 8 counters per batch of
+        // independent loads; then the histogram from the bits (one read of the row)
+        int k = 0;
+        for (int s = 0; s < S; ++s) {
+            const int l0 = 64 * s, nl = min(64, L - l0);
+            uint64_t w = 0;
+            for (int b0 = 0; b0 < nl; b0 += 8) {
+                unsigned long long v[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = b0 + u < nl ? row[l0 + b0 + u] : 0ull;
+                for (int u = 0; u < 8; ++u) v[u] = b0 + u < nl ? row[l0 + b0 + u] : 0ull;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) w |= (uint64_t)(v[u] != 0ull) << (b0 + u);
-                }
-                out_masks[o * S + s] = w;
-                k += __popcll(w);
+                for (int u = 0; u < 8; ++u) w |= (uint64_t)(v[u] != 0ull) << (b0 + u);
             }
-            out_keys[o] = p.keys[i];
-            out_k[o] = k;
-            for (int s = 0; s < S; ++s) {
-                uint64_t w = out_masks[o * S + s];
-                while (w) {
-                    const int l = 64 * s + __builtin_ctzll(w);
-                    w &= w - 1;
-                    if (lds_hist)
-                        atomicAdd(&lhist[l * (L + 1) + k], 1u);
-                    else
-                        atomicAdd(&hist[l * (L + 1) + k], 1u);
-                }
+            out_masks[o * S + s] = w;
+            k += __popcll(w);
+        }
+        out_keys[o] = p.keys[i];
+        out_k[o] = k;
+        for (int s = 0; s < S; ++s) {
+            uint64_t w = out_masks[o * S + s];
+            while (w) {
+                const int l = 64 * s + __builtin_ctzll(w);
+                w &= w - 1;
+                if (lds_hist)
+                    atomicAdd(&lhist[l * (L + 1) + k], 1u);
+                else
+                    atomicAdd(&hist[l * (L + 1) + k], 1u);
             }
         }
     }
@@ -416,24 +454,22 @@ __global__ void mark_kernel(const uint32_t* idx, int64_t n, uint8_t* chosen) {
     if (i < n) chosen[idx[i]] = 1;
 }
 
-__global__ void gather_chosen_kernel(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys,
-                                     const uint64_t* masks, const int32_t* ks, uint64_t* out_keys,
-                                     uint64_t* out_masks, int32_t* out_k, unsigned long long* out_n) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool c = j < n && chosen[j];
-    const uint64_t m = __ballot(c);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    unsigned long long base = 0;
-    const int leader = __builtin_ctzll(m);
-    if (lane == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    if (!c) return;
-    const unsigned long long o =
-        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    out_keys[o] = keys[j];
-    out_k[o] = ks[j];
-    for (int s = 0; s < S; ++s) out_masks[o * S + s] = masks[j * S + s];
+__global__ __launch_bounds__(kScanThreads) void gather_chosen_kernel(int64_t n, int S, const uint8_t* chosen,
+                                                                     const uint64_t* keys, const uint64_t* masks,
+                                                                     const int32_t* ks, uint64_t* out_keys,
+                                                                     uint64_t* out_masks, int32_t* out_k,
+                                                                     unsigned long long* out_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (int64_t c0 = (int64_t)blockIdx.x * kScanThreads; c0 < n; c0 += (int64_t)gridDim.x * kScanThreads) {
+        const int64_t j = c0 + threadIdx.x;
+        const bool c = j < n && chosen[j];
+        const unsigned long long o = block_compact(c, out_n, wcnt, &bbase);
+        if (!c) continue;
+        out_keys[o] = keys[j];
+        out_k[o] = ks[j];
+        for (int s = 0; s < S; ++s) out_masks[o * S + s] = masks[j * S + s];
+    }
 }
 
 unsigned grid_of(int64_t n, int b) { return (unsigned)std::max<int64_t>(1, (n + b - 1) / b); }
@@ -518,8 +554,8 @@ hipError_t launch_mark_threshold(int64_t n, const int32_t* cand_lang, const uint
 hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
                            int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream) {
     const size_t lds = p.L <= 88 ? (size_t)p.L * (p.L + 1) * 4 : 0;
-    hipLaunchKernelGGL(presence_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), lds, stream, p, cap, S, out_keys,
-                       out_masks, out_k, out_n, hist);
+    hipLaunchKernelGGL(presence_kernel, dim3(scan_grid(cap)), dim3(kScanThreads), lds, stream, p, cap, S, out_keys, out_masks,
+                       out_k, out_n, hist);
     return hipGetLastError();
 }
 
@@ -599,8 +635,8 @@ hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const u
                                 const int32_t* ks, uint64_t* out_keys, uint64_t* out_masks, int32_t* out_k,
                                 unsigned long long* out_n, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_chosen_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, S, chosen, keys, masks,
-                       ks, out_keys, out_masks, out_k, out_n);
+    hipLaunchKernelGGL(gather_chosen_kernel, dim3(scan_grid((uint64_t)n)), dim3(kScanThreads), 0, stream, n, S, chosen,
+                       keys, masks, ks, out_keys, out_masks, out_k, out_n);
     return hipGetLastError();
 }
 
