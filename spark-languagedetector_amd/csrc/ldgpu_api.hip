@@ -947,7 +947,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
     bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
     m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
-    m->kb_lines = !m->lds_filter && 4 * bwords > kKbLineBytes;
+    m->kb_lines = !m->lds_filter && (4 * bwords > kKbLineBytes || diag_env("LDGPU_KB_LINES"));  // (tests: any keyed bloom)
     m->filter_log2 = log2u(bwords);
     const uint32_t bshift = 32u - (uint32_t)m->filter_log2;
     std::vector<uint32_t> filter(kBloomBase + bwords, 0u);

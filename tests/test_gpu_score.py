@@ -571,3 +571,44 @@ def test_product_library_ignores_env_switches(monkeypatch):
     data, off = encoding.pack(docs)
     m = check_parity(table, 20, [1, 2, 3], data, off)
     assert m.info()["mode"] == 2
+
+
+@pytest.mark.parametrize("form,grams,doc_range", [
+    ("count", [1, 2, 3, 4, 5, 6, 7], (200, 256)),    # config-5 form: single documents
+    ("count", [1, 2, 3, 4, 5], (20, 90)),             # packs of short documents
+    ("mask", [2, 3, 5, 7], (0, 300)),                 # ordered replay, partial windows, long docs
+    ("count", [3, 9, 12], (0, 120)),                  # wide keys in their lines
+])
+def test_keyed_bloom_line_layout(form, grams, doc_range, monkeypatch):
+    """The keyed bloom's line layout (every key of >= 4 bytes of a window
+    position in one 64-B line; the product library takes it beyond 2 MiB, as
+    config 5's 16 MiB bloom): forced on a 60k-key table through the
+    diagnostics library (LDGPU_KB_LINES).  Labels and fp64 scores
+    bit-identical to the oracle, labels-only too; the product library's
+    word-per-key layout on the same table agrees."""
+    rng = np.random.default_rng(sum(grams) + doc_range[1])
+    L = 40
+    ls = synth.make_languages(L, seed=91)
+    data, off, _ = synth.generate(ls, 2500, doc_range[0], doc_range[1], seed=92 + len(grams))
+    raw = data.tobytes()
+    table = {}
+    while len(table) < 60000:
+        d = int(rng.integers(0, len(off) - 1))
+        n = int(rng.choice(grams))
+        ln = int(off[d + 1] - off[d])
+        if ln < n:
+            continue
+        p = int(rng.integers(0, ln - n + 1))
+        mask = rng.random(L) < 0.05
+        mask[int(rng.integers(0, L))] = True
+        v = math.log(2.0) if form == "count" else math.log(1.0 + 1.0 / int(mask.sum()))
+        table[raw[off[d] + p: off[d] + p + n]] = [v if b else 0.0 for b in mask]
+    monkeypatch.setenv("LDGPU_KB_LINES", "1")
+    m = check_parity(table, L, grams, data, off, variant="diag")
+    assert m.info()["filter_bits"] > 64 * 1024 * 8  # keyed (global) bloom
+    labels, _ = m.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(labels, ol)
+    monkeypatch.delenv("LDGPU_KB_LINES")
+    plain, _ = DeviceModel(table, L, grams).score(data, off, want_scores=False)
+    assert np.array_equal(plain, ol)

@@ -121,3 +121,23 @@ def test_product_library_reads_no_env_switches():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"LDGPU_" not in blob
     assert b"LDGPU_ABLATE" in open(_lib.DIAG_LIB_PATH, "rb").read()
+
+
+def test_bench_traffic_lookup_scales_profiled_launch():
+    """bench.py reports the committed PMC traffic of its exact workload, or of
+    the same workload profiled over fewer documents scaled to its own count
+    (roofline.traffic_scaled_from says so); another shape gets none."""
+    import importlib.util
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    prof = json.load(open(os.path.join(root, "profiles", "pmc_traffic_config5.json")))
+    key = prof["workload_key"]
+    assert bench.traffic_from_profiles(key)["traffic_bytes_per_launch"] == prof["traffic_bytes_per_launch"]
+    docs = int(key.split(":docs=")[1].split(":")[0])
+    scaled = bench.traffic_from_profiles(key.replace(f":docs={docs}:", f":docs={5 * docs}:"))
+    assert scaled["traffic_bytes_per_launch"] == round(5 * prof["traffic_bytes_per_launch"])
+    assert "x5" in scaled["traffic_scaled_from"]
+    assert bench.traffic_from_profiles(key.replace(":L=200:", ":L=201:")) is None
