@@ -43,8 +43,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, choices=[2, 4, 5], default=2,
-                    help="BASELINE.json config: 2 = headline (default), 4 = short text, 5 = large profile")
+    ap.add_argument("--config", type=int, choices=[1, 2, 4, 5], default=2,
+                    help="BASELINE.json config: 2 = headline (default), 4 = short text, 5 = large profile, "
+                         "1 = the reference's own CPU-sized case (3 languages, 10k documents)")
     ap.add_argument("--docs", type=int, default=None, help="documents per GPU")
     ap.add_argument("--doc-bytes", type=int, default=None, help="fixed document length (sets min = max)")
     ap.add_argument("--doc-min", type=int, default=None)
@@ -66,7 +67,9 @@ def parse():
     ap.add_argument("--fit-bytes", type=int, default=1 << 30, help="fit mode: corpus bytes per GPU")
     args = ap.parse_args()
     # SURVEY §8d shapes; explicit flags override
-    preset = {2: dict(docs=10_000_000, doc_min=256, doc_max=256, langs=20, grams="1,2,3,4,5", profile_size=500,
+    preset = {1: dict(docs=10_000, doc_min=128, doc_max=384, langs=3, grams="1,2,3", profile_size=1000,
+                      train_docs=1000),
+              2: dict(docs=10_000_000, doc_min=256, doc_max=256, langs=20, grams="1,2,3,4,5", profile_size=500,
                       train_docs=1000),
               4: dict(docs=125_000_000, doc_min=32, doc_max=96, langs=100, grams="1,2,3,4,5", profile_size=1000,
                       train_docs=300),
@@ -512,7 +515,8 @@ def main():
     total_docs = n_docs * world * args.steps
     doc_desc = f"{args.doc_min} B" if args.doc_min == args.doc_max else f"U[{args.doc_min},{args.doc_max}] B"
     if args.config != 2:
-        line_note = {4: "config 4 is quoted on 1B docs over 8 GPUs (1.25e8 per GPU); --docs sets this run's count",
+        line_note = {1: "config 1: the reference's CPU-sized case (SURVEY §8d), timed beside its CPU restatement",
+                     4: "config 4 is quoted on 1B docs over 8 GPUs (1.25e8 per GPU); --docs sets this run's count",
                      5: "config 5: table of up to L*K rows far beyond LDS: bloom in L2/MALL, slots in HBM"}[args.config]
     else:
         line_note = None
