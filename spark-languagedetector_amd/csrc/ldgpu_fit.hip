@@ -9,17 +9,21 @@
 // row of L u64 counters per slot (keys[cap], counts[cap][L]).  Integer atomics
 // are order-independent, so the counts are bit-exact whatever the schedule.
 //
-// Kernel structure (one wave per document, persistent grid): lanes = 64
-// consecutive window positions of one gram length.  1-gram windows (the
-// hottest keys: every document hits ' ', 'e', ...) are first aggregated in a
-// per-wave 256-bin LDS histogram and flushed once per document, so the global
-// atomics on those rows drop from one per byte to one per distinct byte per
-// document; 2- and 3-byte keys likewise go through a per-wave LDS hash (kH2
-// slots, flushed after each gram length; a key that finds no slot goes global).  Longer keys insert straight into the global table: find-or-CAS
-// the key (relaxed agent-scope loads, device-scope CAS), then one u64 atomic
-// add on the (slot, lang) counter.  An insert that exceeds kMaxProbe probes
-// appends (key, lang) to an overflow list that the host re-inserts after
-// growing the table.
+// Two counting paths share the table: FIT v2 (emit / part2 / reduce /
+// merge, below: radix-partitioned record aggregation, one table add per
+// distinct (gram, language) per batch -- the path every table whose
+// (gram, language, count) record fits 64 bits takes) and the single-pass
+// count_kernel here (tables whose record does not fit, e.g. 7-byte grams with
+// hundreds of languages; diagnostics builds force it: LDGPU_FIT_LEGACY).  count_kernel:
+// one wave per document, lanes = 64 consecutive window positions of one gram
+// length; 1-gram windows aggregated in a per-wave 256-bin LDS histogram, 2-
+// and 3-byte keys in a per-wave LDS hash (kH2 slots, flushed after each gram
+// length; a key that finds no slot goes global), longer keys straight into
+// the global table: find-or-CAS the key (relaxed agent-scope loads,
+// device-scope CAS), then one u64 atomic add on the (slot, lang) counter.  An
+// insert that exceeds kMaxProbe probes appends (key, lang, count) to an
+// overflow list that the host re-inserts after growing the table.  Gram
+// lengths 8..15 count in a table of two-word keys of their own (end of file).
 #include <algorithm>
 
 #include <hipcub/hipcub.hpp>

@@ -8,31 +8,34 @@
 //       if table contains window: s = s + row   (daxpy, a = 1.0)     :145-149
 //   label = argmax(s), first maximum (breeze)                       :154
 //
-// Structure (one wave per document, persistent grid, next document's bytes
-// prefetched into registers while the current one is scored):
+// Structure (one wave per document, persistent grid; each wave's groups of
+// consecutive documents staged into its LDS by double-buffered LDS-DMA):
 //   probe      a superblock = 256 window positions, 4 per lane at stride 64.
-//              Each lane loads the 8 bytes at each of its positions once
-//              (dword loads + v_alignbyte) and, once per superblock, the
-//              filter words those positions need: the 1-byte and 2-byte
-//              exact-bitmap words and the prefix-Bloom word chosen by the
-//              position's first three bytes (shared by every key length
-//              >= 3, ldgpu_common.h).  Each gram length n then tests one bit
-//              of a word already in a register (a 24-bit multiply and a bit
-//              extract), and a ballot appends the candidates to a per-wave LDS
-//              queue with mbcnt, so the queue is in reference order: n outer,
-//              position inner.
-//   verify     64 queued keys at a time probe the global open-addressed table
-//              (32-B slots carrying key, row, value and mask word 0).
-//   accumulate hits are replayed in queue order; lane l owns language l
-//              (slices of 64 for L > 64) and does s_l = s_l + row_l, so every
-//              s_l sees exactly the reference's sequence of fp64 adds: scores
-//              are bit-identical, not just within tolerance.  Mask-form rows
-//              (all nonzeros equal: every fit-produced row) add v or skip
-//              (x + 0.0 == x because s never is -0.0).
-//   argmax     lane-local over slices, then a 6-step xor-shuffle reduction on
-//              (value, index) with the breeze rule.
+//              Each lane reads the 8 bytes at each of its positions once
+//              (LDS words + v_alignbyte) and, once per superblock, the
+//              prefix-Bloom word chosen by each position's first three bytes
+//              (shared by every key length >= 3, ldgpu_common.h); a table
+//              whose bloom exceeds LDS uses the keyed bloom in global memory
+//              instead.  Each gram length n then tests one bit of a word (a
+//              24-bit multiply and a bit extract), and a ballot appends the
+//              candidates to a per-wave LDS queue with mbcnt, so the queue is
+//              in reference order: n outer, position inner.
+//   verify     64 queued keys at a time probe the global table (2-choice
+//              cuckoo slots, 4-slot buckets for big count-mode tables, a
+//              two-word table for keys of 8..15 bytes).
+//   accumulate count mode (every row one shared value): per-language hit
+//              counts in LDS (order-free; 1-/2-byte keys counted straight from
+//              LDS direct tables, and the verify loads of the longer keys
+//              issued before those direct counts), scores = a host-built fold
+//              table.  Other mask tables: hits replayed in queue order, lane l
+//              owns language l (slices of 64 for L > 64) and does s_l = s_l +
+//              v or + 0.0; dense tables: s_l = s_l + row_l.  Every s_l sees
+//              exactly the reference's sequence of fp64 adds: scores are
+//              bit-identical, not just within tolerance.
+//   argmax     DPP wave max, then the first index holding it (breeze rule).
 // Documents of max(G)..256 bytes take a fast path (all windows full-length,
-// one superblock); shorter (partial windows) and longer ones loop n outer,
+// one superblock); in count mode consecutive short ones share a superblock
+// (packs).  Shorter documents (partial windows) and longer ones loop n outer,
 // superblocks inner.
 #include "ldgpu_internal.h"
 
