@@ -1113,9 +1113,10 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.bytes = d_bytes;
     p.n_bytes = n_bytes;
     p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
-    // documents per staged group: the mean document (+ 16 B alignment slack) fits kBufBytes
+    // documents per staged group: at most 63 (the lanes holding a group's
+    // offsets); the kernel takes as many as fit the staging buffer
+    p.group = 63;
     const double mean = (double)n_bytes / (double)std::max<int64_t>(n_docs, 1);
-    p.group = (int32_t)std::max<int64_t>(1, std::min<int64_t>(63, (int64_t)((kBufBytes - 16) / std::max(mean, 1.0))));
     p.offsets = d_offsets;
     p.n_docs = n_docs;
     p.labels = d_labels;

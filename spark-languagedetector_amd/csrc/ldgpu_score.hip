@@ -1292,9 +1292,14 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
         // previous group's label store has drained
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        const int64_t g1 = min(g0 + (int64_t)G, dend);
-        const int cnt = (int)(g1 - g0);
+        // this group: as many consecutive whole documents as the staging
+        // buffer holds from s0 (at least one; offsets never decrease, so
+        // the lanes that fit are a prefix)
         const int64_t s0 = rdlane_i64(offv, 0) & ~(int64_t)15;
+        const int lim = (int)min((int64_t)G, dend - g0);
+        const int fl = (int)fresh_lane();
+        const int cnt = max(1, (int)__popcll(__ballot(fl >= 1 && fl <= lim && offv - s0 <= (int64_t)kBufBytes)));
+        const int64_t g1 = g0 + cnt;
         const int64_t send = rdlane_i64(offv, cnt);
         const bool staged = send - s0 <= kBufBytes;
         uint32_t* const cur = par ? buf1 : buf0;
