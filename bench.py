@@ -100,7 +100,7 @@ def build_table(args, ls, device):
     counts.close()
     n = len(ko) - 1
     table = None
-    if n * args.langs <= 50_000_000:
+    if n * args.langs <= 1_000_000:  # larger tables reach the CPU baseline as the packed arrays
         b = kb.tobytes()
         table = {}
         for i in range(n):
@@ -128,12 +128,18 @@ def host_cores() -> int:
         return int(os.cpu_count() or 1)
 
 
-def cpu_baseline(args, table, grams, data, off):
-    """The oracle's C restatement (kind 'port'), on rank 0, bounded sample."""
+def cpu_baseline(args, table, grams, data, off, packed=None):
+    """The oracle's C restatement (kind 'port'), on rank 0, bounded sample.
+    The table comes as a {gram: row} dict, or (tables too large for one, as
+    config 5's 10M rows x 200 languages) as the packed mask-form arrays."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ldoracle_c as OC
     threads = host_cores()
-    t = OC.Table(table, args.langs)
+    if table:
+        t = OC.Table(table, args.langs)
+    else:
+        kb, ko, masks, vals = packed
+        t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals, args.langs)
     probe = min(20_000, len(off) - 1)
     t0 = time.perf_counter()
     t.score(grams, data, off[:probe + 1], nthreads=threads)
@@ -424,6 +430,7 @@ def main():
         return fit_main(args, world, rank, local, dev, backend)
 
     ls = synth.make_languages(args.langs)
+    packed = None
     if args.empty_table:
         table, grams, fit_info = {}, [int(x) for x in args.grams.split(",")], {}
         model = DeviceModel(table, args.langs, grams, device=local)
@@ -472,7 +479,7 @@ def main():
         elapsed = float(t.item())
 
     # labels sanity (synthetic docs carry their generating language)
-    acc = float((d_lab[:pool].cpu().numpy() == plang[:n_docs][:pool]).mean()) if table else None
+    acc = float((d_lab[:pool].cpu().numpy() == plang[:n_docs][:pool]).mean()) if (table or packed) else None
 
     info = model.info()
     doc_b = n_bytes / max(n_docs, 1)                      # mean document bytes
@@ -498,8 +505,8 @@ def main():
 
     cpu = None
     oracle_check = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and table:
-        cpu, ol = cpu_baseline(args, table, grams, data, off)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and (table or packed):
+        cpu, ol = cpu_baseline(args, table, grams, data, off, packed)
         # the timed kernel's own labels (the last step's) against the oracle's
         # on the CPU sample: the exact code path the value measures
         dl = d_lab[:len(ol)].cpu().numpy()

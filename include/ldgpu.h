@@ -108,6 +108,22 @@ int ldgpu_model_destroy(ldgpu_model* model);
 int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
                      int64_t* table_slots, int64_t* filter_bits, int64_t* device_bytes);
 
+/* The device layout the model's scoring kernel takes (bit set = in use), so a
+ * caller (and the parity tests) can tell which product path scores it:
+ * the window filter (LDS prefix Bloom, or a keyed bloom in L2 / Infinity Cache,
+ * one word per key or one 64-B line per window position), the key table
+ * (cuckoo slots, or 4-slot buckets for count-mode tables beyond 2^20 keys),
+ * packs of short documents (labels-only count mode). */
+#define LDGPU_LAYOUT_LDS_BLOOM          0x01
+#define LDGPU_LAYOUT_KEYED_BLOOM        0x02
+#define LDGPU_LAYOUT_KEYED_BLOOM_LINES  0x04
+#define LDGPU_LAYOUT_BUCKETS            0x08
+#define LDGPU_LAYOUT_WIDE_KEYS          0x10
+#define LDGPU_LAYOUT_DIRECT             0x20
+#define LDGPU_LAYOUT_PACKS              0x40
+#define LDGPU_LAYOUT_LANG_BLOCKS        0x80
+int ldgpu_model_layout(const ldgpu_model* model, int32_t* flags);
+
 /* Host buffers in, host buffers out; synchronous.  out_scores is nullable
  * ([n_docs][n_langs] fp64).  out_labels[d] is the index into the supported
  * languages of argmax(scores of d): first maximum, all-zero -> 0.  Chunks of

@@ -1081,6 +1081,22 @@ extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_
     return ok();
 }
 
+extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
+    if (!m || !flags) return fail(LDGPU_EINVAL, "model/flags is NULL");
+    const ldgpu_model* b = m->blocks.empty() ? m : m->blocks[0];  // blocks share one layout
+    int32_t f = 0;
+    if (b->lds_filter) f |= LDGPU_LAYOUT_LDS_BLOOM;
+    if (!b->lds_filter && !b->kb_lines) f |= LDGPU_LAYOUT_KEYED_BLOOM;
+    if (b->kb_lines) f |= LDGPU_LAYOUT_KEYED_BLOOM_LINES;
+    if (b->d_buckets) f |= LDGPU_LAYOUT_BUCKETS;
+    if (b->d_wslots) f |= LDGPU_LAYOUT_WIDE_KEYS;
+    if (b->direct_words) f |= LDGPU_LAYOUT_DIRECT;
+    if (b->pack_ok) f |= LDGPU_LAYOUT_PACKS;
+    if (!m->blocks.empty()) f |= LDGPU_LAYOUT_LANG_BLOCKS;
+    *flags = f;
+    return ok();
+}
+
 namespace {
 int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
                  int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st, double* d_best = nullptr,
@@ -1258,15 +1274,10 @@ int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_
         }
         return LDGPU_OK;
     };
-    int64_t d0 = 0;
-    int k = 0;
-    int rc = LDGPU_OK;
-    while (d0 < n_docs && rc == LDGPU_OK) {
-        int64_t d1 = d0 + 1;
-        while (d1 < n_docs && d1 - d0 < kChunkDocs && offsets[d1 + 1] - offsets[d0] <= kChunkBytes) ++d1;
+    // one chunk's copies and launch on stage st; an error returns without
+    // leaving the loop's drain behind (the caller breaks, then drains)
+    auto issue = [&](ScoreStage& st, int64_t d0, int64_t d1) -> int {
         const int64_t nd = d1 - d0, b0 = offsets[d0], nb = offsets[d1] - b0;
-        ScoreStage& st = pp->stage[k & 1];
-        if ((rc = retire(st))) break;
         HIP_TRY(st.bytes.ensure((size_t)nb + 16));
         HIP_TRY(st.offsets.ensure(sizeof(int64_t) * (nd + 1)));
         HIP_TRY(st.labels.ensure(sizeof(int32_t) * nd));
@@ -1282,10 +1293,10 @@ int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_
         }
         if (nb) HIP_TRY(hipMemcpyAsync(st.bytes.p, src, nb, hipMemcpyHostToDevice, st.stream));
         HIP_TRY(hipMemcpyAsync(st.offsets.p, ho, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, st.stream));
-        if ((rc = score_launch(m, (const uint8_t*)st.bytes.p, nb, (const int64_t*)st.offsets.p, nd,
-                               (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, pp->d_err,
-                               st.stream)))
-            break;
+        if (int r = score_launch(m, (const uint8_t*)st.bytes.p, nb, (const int64_t*)st.offsets.p, nd,
+                                 (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, pp->d_err,
+                                 st.stream))
+            return r;
         int32_t* lab_dst = out_labels + d0;
         double* sc_dst = out_scores ? out_scores + d0 * m->L : nullptr;
         if (!pinned_out) {
@@ -1304,15 +1315,45 @@ int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_
         st.d0 = d0;
         st.nd = nd;
         st.busy = true;
+        return LDGPU_OK;
+    };
+    // diagnostics build: fail after issuing this many chunks (error-path tests)
+    const char* fail_at = diag_env("LDGPU_FAIL_CHUNK");
+    int64_t d0 = 0;
+    int k = 0;
+    int rc = LDGPU_OK;
+    while (d0 < n_docs && rc == LDGPU_OK) {
+        int64_t d1 = d0 + 1;
+        while (d1 < n_docs && d1 - d0 < kChunkDocs && offsets[d1 + 1] - offsets[d0] <= kChunkBytes) ++d1;
+        ScoreStage& st = pp->stage[k & 1];
+        if ((rc = retire(st))) break;
+        if (fail_at && k == atoi(fail_at)) {
+            rc = fail(LDGPU_EDEVICE, "injected failure at chunk %d (LDGPU_FAIL_CHUNK)", k);
+            break;
+        }
+        if ((rc = issue(st, d0, d1))) break;
         d0 = d1;
         ++k;
     }
-    // drain in chunk order (also after an error, so no copy outlives the call)
-    for (int i = 0; i < 2; ++i) {
-        const int r = retire(pp->stage[(k + i) & 1]);
-        if (!rc) rc = r;
+    // drain: every copy this call queued (also a half-issued chunk's, after an
+    // error) completes before the call returns, in chunk order; a stage is
+    // idle when the pipeline goes back to the pool
+    for (auto& st : pp->stage) {
+        const hipError_t e = hipStreamSynchronize(st.stream);
+        if (!rc && e != hipSuccess) rc = fail(LDGPU_EDEVICE, "score pipeline: %s", hipGetErrorString(e));
     }
-    if (rc) return rc;
+    for (int i = 0; i < 2; ++i) {
+        ScoreStage& st = pp->stage[(k + i) & 1];
+        if (rc) {
+            st.busy = false;  // the call failed: its outputs are undefined
+            continue;
+        }
+        rc = retire(st);
+    }
+    if (rc) {
+        (void)hipMemset(pp->d_err, 0, sizeof(int32_t));  // no stale row error for the pipeline's next call
+        return rc;
+    }
     if (m->has_bad) {
         for (auto& st : pp->stage) HIP_TRY(hipStreamSynchronize(st.stream));
         if (int r = check_row_error(m, pp->d_err, pp->stage[0].stream)) return r;

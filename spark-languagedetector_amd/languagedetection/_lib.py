@@ -30,6 +30,9 @@ LDGPU_ENODEV = 6
 MAX_GRAM = 15  # SCORE tables (keys of 8..15 bytes take two words)
 MAX_FIT_GRAM = 15  # FIT counting (grams of 8..15 bytes in a two-word table)
 MAX_LANGS = 4096
+# ldgpu_model_layout flags
+LAYOUT_FLAGS = {"lds_bloom": 0x01, "keyed_bloom": 0x02, "keyed_bloom_lines": 0x04, "buckets": 0x08,
+                "wide_keys": 0x10, "direct": 0x20, "packs": 0x40, "lang_blocks": 0x80}
 
 _p = ctypes.c_void_p
 _pp = ctypes.POINTER(ctypes.c_void_p)
@@ -53,6 +56,7 @@ SIGNATURES = [
     ("ldgpu_model_create_masks", ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _i32, _p, _i32, _pp]),
     ("ldgpu_model_destroy", ctypes.c_int, [_p]),
     ("ldgpu_model_info", ctypes.c_int, [_p, _pi32, _pi64, _pi64, _pi64, _pi64]),
+    ("ldgpu_model_layout", ctypes.c_int, [_p, _pi32]),
     ("ldgpu_score", ctypes.c_int, [_p, _p, _p, _i64, _p, _p]),
     ("ldgpu_score_device", ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _p, _p]),
     ("ldgpu_counts_create", ctypes.c_int, [_p, _i32, _p, _i32, _i64, _pp]),

@@ -111,8 +111,11 @@ class DeviceModel(_Owner):
         mode = ctypes.c_int32()
         vals = [ctypes.c_int64() for _ in range(4)]
         self._check(self.lib.ldgpu_model_info(self.h, ctypes.byref(mode), *[ctypes.byref(v) for v in vals]))
+        flags = ctypes.c_int32()
+        self._check(self.lib.ldgpu_model_layout(self.h, ctypes.byref(flags)))
         return {"mode": mode.value, "n_keys": vals[0].value, "table_slots": vals[1].value,
-                "filter_bits": vals[2].value, "device_bytes": vals[3].value}
+                "filter_bits": vals[2].value, "device_bytes": vals[3].value,
+                "layout": sorted(k for k, b in _lib.LAYOUT_FLAGS.items() if flags.value & b)}
 
     def score(self, data: np.ndarray, offsets: np.ndarray, want_scores: bool = False,
               out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, Optional[np.ndarray]]:

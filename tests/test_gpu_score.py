@@ -446,6 +446,113 @@ def test_config4_shape_parity_short_docs_100_langs():
     assert m.info()["mode"] in (0, 2)
 
 
+def test_config4_timed_kernel_labels_only_packs():
+    """The kernel config 4's bench times: a GPU-fitted K=1000 table of ~100k
+    rows at L=100 (every chosen gram in one presence class: count mode) whose
+    keyed bloom (256 KiB) is read from L2, scored labels-only, so U[32,96]-byte
+    documents go through the packs of short documents (score_pack).  The
+    product library's layout flags name that path; labels equal the C
+    oracle's on every document."""
+    from languagedetection.runtime import DeviceCounts
+    L, grams = 100, [1, 2, 3, 4, 5]
+    ls = synth.make_languages(L)
+    lang = np.repeat(np.arange(L, dtype=np.int32), 300)
+    tdata, toff, tlang = synth.generate(ls, len(lang), 200, 2000, seed=synth.SEED_BASE + 100, doc_lang=lang)
+    c = DeviceCounts(L, grams, capacity_hint=1 << 20)
+    c.count(tdata, toff, tlang)
+    kb, ko, masks, vals = c.fit_table_masks(1000)
+    c.close()
+    assert len(ko) - 1 > 64 * 1024 * 2.5 / 4  # a bloom beyond LDS
+    m = DeviceModel.from_masks(kb, ko, masks, vals, L, grams)
+    info = m.info()
+    assert info["mode"] == 2, info
+    assert "keyed_bloom" in info["layout"] and "packs" in info["layout"], info
+    data, off, _ = synth.generate(ls, 60000, 32, 96, seed=synth.SEED_BASE + 4)
+    t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals, L)
+    ol, _ = t.score(grams, data, off, want_scores=False, nthreads=8)
+    lab, _ = m.score(data, off, want_scores=False)
+    assert np.array_equal(lab, ol), np.nonzero(lab != ol)[0][:10]
+    # the device-pointer entry point the bench calls
+    import torch
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_lab = torch.empty(len(off) - 1, dtype=torch.int32, device=dev)
+    m.score_device(d_bytes.data_ptr(), int(len(data)), d_off.data_ptr(), len(off) - 1, d_lab.data_ptr(), 0,
+                   torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_lab.cpu().numpy(), ol)
+
+
+def test_config5_timed_path_buckets_and_bloom_lines():
+    """Config 5's exact product path: a count-mode table of more than 1.4M
+    keys of >= 3 bytes at L=200, grams 1-7, so the product library puts the
+    keys in 4-slot buckets AND the keyed bloom (>= 2^20 words, 4 MiB) in the
+    line layout (every key of >= 4 bytes of a window position in one 64-B
+    line).  Labels and fp64 scores against the C oracle, and the labels-only
+    count argmax the bench times."""
+    rng = np.random.default_rng(2055)
+    L, grams = 200, [1, 2, 3, 4, 5, 6, 7]
+    ls = synth.make_languages(L, seed=synth.SEED_BASE + 5)
+    d256, o256, _ = synth.generate(ls, 5000, 256, 256, seed=synth.SEED_BASE + 506)
+    dvar, ovar, _ = synth.generate(ls, 1500, 0, 400, seed=synth.SEED_BASE + 507)
+    docs = [d256[o256[i]:o256[i + 1]].tobytes() for i in range(5000)]
+    docs += [dvar[ovar[i]:ovar[i + 1]].tobytes() for i in range(1500)]
+    data, off = encoding.pack(docs)
+    keys = set()
+    for n in range(1, 8):
+        keys.update(_windows(data, off, n, rng, 150_000))
+    while len(keys) < 1_450_000:  # misses: random keys of 3..7 bytes
+        n = int(rng.integers(3, 8))
+        keys.update(bytes(r) for r in rng.integers(0, 256, size=(50_000, n), dtype=np.uint8))
+    keys = sorted(keys)
+    kb, ko = encoding.pack(keys)
+    S = (L + 63) // 64
+    masks = np.zeros((len(keys), S), dtype=np.uint64)
+    lang1 = rng.integers(0, L, size=len(keys))
+    masks[np.arange(len(keys)), lang1 // 64] = (np.uint64(1) << (lang1 % 64).astype(np.uint64))
+    multi = rng.random(len(keys)) < 0.2
+    extra = rng.integers(0, L, size=len(keys))
+    masks[multi, extra[multi] // 64] |= (np.uint64(1) << (extra[multi] % 64).astype(np.uint64))
+    vals = np.full(len(keys), math.log(2.0))
+    m = DeviceModel.from_masks(kb, ko, masks, vals, L, grams)
+    info = m.info()
+    assert info["mode"] == 2 and info["n_keys"] == len(keys), info
+    assert "buckets" in info["layout"] and "keyed_bloom_lines" in info["layout"], info
+    t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals, L)
+    ol, os_ = t.score(grams, data, off, want_scores=True, nthreads=8)
+    assert (ol != 0).sum() > 1000  # hits decide the labels, not the no-hit default
+    lab, sc = m.score(data, off, want_scores=True)
+    assert np.array_equal(lab, ol), np.nonzero(lab != ol)[0][:10]
+    assert np.array_equal(bits(sc), bits(os_))
+    lab2, _ = m.score(data, off)
+    assert np.array_equal(lab2, ol)
+
+
+def test_failed_call_leaves_pipeline_clean(monkeypatch):
+    """A host-buffer call that fails partway (an error injected after the
+    first chunk, diagnostics library) drains its copies before returning; the
+    next call on the same context and pipeline pool gets the oracle's labels
+    and scores, with nothing of the failed call written into its buffers."""
+    from languagedetection.runtime import DeviceModel as DM
+    ls = synth.make_languages(5, seed=61)
+    pdata, poff, _ = synth.generate(ls, 20000, 20, 120, seed=62)
+    data, off, _ = synth.tile(pdata, poff, np.zeros(20000, np.int32), 2_200_000)  # 3 chunks of 1M docs
+    rng = np.random.default_rng(63)
+    table = _random_table(rng, 5, 300, [1, 2, 3], np.frombuffer(b"abcdefghijklmnopqrstuvwxyz ", np.uint8), True)
+    m = DM(table, 5, [1, 2, 3], variant="diag")
+    monkeypatch.setenv("LDGPU_FAIL_CHUNK", "2")
+    with pytest.raises(_lib.LdgpuError, match="injected failure"):
+        m.score(data, off, want_scores=True)
+    monkeypatch.delenv("LDGPU_FAIL_CHUNK")
+    small = off[:300_001]
+    ol, os_ = oracle_c(table, 5, [1, 2, 3], data, small)
+    lab, sc = m.score(data, small, want_scores=True)
+    assert np.array_equal(lab, ol) and np.array_equal(bits(sc), bits(os_))
+    lab_full, _ = m.score(data, off)
+    assert np.array_equal(lab_full[:300_000], ol)
+
+
 def test_config5_shape_parity_large_profile_global_filter():
     """Config 5's shape at reduced size: 200 languages (four slices), grams
     1-7, a table too large for the LDS Bloom filter (global-filter variant)."""
