@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -1388,11 +1389,12 @@ struct ldgpu_counts {
     uint32_t ovf2_cap = 0;
     uint32_t ovf_cap = 1u << 20;  // windows per sub-launch; grown per call up to kOvfMax
     uint64_t size = 0;
-    // FIT v2 (radix-partitioned records, ldgpu_fit.hip): the record format
-    // ((sentinel << lb | lang) << cb | count) and the per-batch scratch
-    bool v2 = false;
+    // FIT v3 (ldgpu_fit.hip): K = words per record (ldgpu_internal.h); K = 1
+    // records are ((sentinel << lb | lang) << cb | count)
+    bool v3 = true;
+    int K = 1;
     uint32_t lb = 0, cb = 0;
-    int64_t batch_windows = 0;  // kBatchWindows (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
+    int64_t batch_windows = 0;  // kBatchWindows / K (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
     ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
     // grams of 8..15 bytes: a two-word-key table of their own (ldgpu_fit.hip)
     uint64_t wcap = 0, wsize = 0;
@@ -1613,141 +1615,6 @@ int ensure_ovf(ldgpu_counts* c, int64_t windows) {
     return LDGPU_OK;
 }
 
-// FIT v2 batches: at most kBatchWindows windows (~200 MB of corpus at grams
-// 1-5), so the record scratch (8 B per window for the emit records, 8 B per
-// record for the buckets, <= 12 B per record of reduce output) stays within
-// ~20 GB of HBM, and a batch's distinct (gram, language) pairs per bucket stay
-// within the reduce LDS table.
-constexpr int64_t kBatchWindows = 1ll << 30;
-
-int count_launch_v2(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
-                    const int32_t* d_lang, int64_t n_docs, const int64_t* h_off) {
-    ldgpu_ctx* x = c->ctx;
-    hipStream_t st = x->stream;
-    const int grid_a = std::max(kSplits, (c->ctx->cus / kSplits) * kSplits);
-    if (int rc = ensure_ovf(c, 1 << 20)) return rc;
-    std::vector<int64_t> meta(3 * (size_t)(grid_a + 1));
-    std::vector<uint32_t> cnt3((size_t)kQ * kQ * kSplits);
-    std::vector<uint64_t> p2off((size_t)kQ * kQ * kSplits), boff((size_t)kQ * kQ + 1);
-    auto win_of = [&](int64_t d) { return doc_windows(c, h_off[d + 1] - h_off[d]); };
-    int64_t d0 = 0;
-    while (d0 < n_docs) {
-        int64_t d1 = d0, W = 0;
-        while (d1 < n_docs) {
-            const int64_t w = win_of(d1);
-            if (d1 > d0 && W + w > c->batch_windows) break;
-            W += w;
-            ++d1;
-        }
-        // emit workgroups: document ranges balanced by windows; a workgroup's
-        // record region holds its windows (records <= windows), its block
-        // directory windows / 4096 + 2 blocks (every block but its last holds
-        // more than kBlkRecs - kRoundRecs records)
-        int64_t* wg_doc = meta.data();
-        int64_t* wg_rec = wg_doc + grid_a + 1;
-        int64_t* wg_dir = wg_rec + grid_a + 1;
-        int64_t d = d0, acc = 0, dirs = 0;
-        for (int k = 0; k < grid_a; ++k) {
-            const int64_t start_d = d, start_acc = acc, target = W * (k + 1) / grid_a;
-            while (d < d1 && acc < target) acc += win_of(d++);
-            wg_doc[k] = start_d - d0;
-            wg_rec[k] = start_acc;
-            wg_dir[k] = dirs;
-            dirs += (acc - start_acc) / (kBlkRecs - kRoundRecs) + 2;
-        }
-        wg_doc[grid_a] = d1 - d0;
-        wg_rec[grid_a] = W;
-        wg_dir[grid_a] = dirs;
-        HIP_TRY(x->f_wg.ensure(sizeof(int64_t) * meta.size()));
-        HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(W, 1)));
-        HIP_TRY(x->f_bstart.ensure(sizeof(int64_t) * (size_t)dirs));
-        HIP_TRY(x->f_bhdr.ensure(sizeof(uint32_t) * kHdr * (size_t)dirs));
-        HIP_TRY(x->f_nblk.ensure(sizeof(int32_t) * (size_t)grid_a));
-        HIP_TRY(x->f_cnt3.ensure(sizeof(uint32_t) * cnt3.size()));
-        HIP_TRY(hipMemcpyAsync(x->f_wg.p, meta.data(), sizeof(int64_t) * meta.size(), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemsetAsync(x->f_cnt3.p, 0, sizeof(uint32_t) * cnt3.size(), st));
-        PartParams pp{};
-        pp.bytes = d_bytes;
-        pp.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
-        pp.offsets = d_offsets + d0;
-        pp.doc_lang = d_lang + d0;
-        pp.L = c->L;
-        pp.nG = c->nGn;
-        for (int i = 0; i < c->nGn; ++i) pp.G[i] = c->Gn[i];
-        pp.lb = c->lb;
-        pp.cb = c->cb;
-        if (const char* ab = diag_env("LDGPU_FIT_EMIT_ABLATE")) pp.ablate = atoi(ab);
-        pp.grid_a = grid_a;
-        pp.wg_doc = (const int64_t*)x->f_wg.p;
-        pp.wg_rec = pp.wg_doc + grid_a + 1;
-        pp.wg_dir = pp.wg_rec + grid_a + 1;
-        pp.rec = (uint64_t*)x->f_rec.p;
-        pp.blk_start = (int64_t*)x->f_bstart.p;
-        pp.blk_hdr = (uint32_t*)x->f_bhdr.p;
-        pp.nblk = (int32_t*)x->f_nblk.p;
-        pp.cnt3 = (uint32_t*)x->f_cnt3.p;
-        pp.direct = count_params(c);
-        HIP_TRY(launch_emit(pp, st));
-        HIP_TRY(hipMemcpyAsync(cnt3.data(), x->f_cnt3.p, sizeof(uint32_t) * cnt3.size(), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        if (int rc = after_batch(c)) return rc;  // direct adds (a count too large for a record) that overflowed
-        // exact bucket offsets: (q1, q2) major, emit group minor
-        uint64_t off = 0;
-        for (int q = 0; q < kQ * kQ; ++q) {
-            boff[q] = off;
-            for (int s = 0; s < kSplits; ++s) {
-                p2off[(size_t)q * kSplits + s] = off;
-                off += cnt3[(size_t)q * kSplits + s];
-            }
-        }
-        boff[(size_t)kQ * kQ] = off;
-        const int64_t R = (int64_t)off;
-        HIP_TRY(x->f_p2.ensure(sizeof(uint64_t) * p2off.size()));
-        HIP_TRY(x->f_boff.ensure(sizeof(uint64_t) * boff.size()));
-        HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(R, 1)));
-        HIP_TRY(x->f_okl.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(R, 1)));
-        HIP_TRY(x->f_ocnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(R, 1)));
-        HIP_TRY(x->f_on.ensure(sizeof(uint32_t) * kQ * kQ + sizeof(uint64_t) * (kQ * kQ + 1)));
-        HIP_TRY(hipMemcpyAsync(x->f_p2.p, p2off.data(), sizeof(uint64_t) * p2off.size(), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(x->f_boff.p, boff.data(), sizeof(uint64_t) * boff.size(), hipMemcpyHostToDevice, st));
-        pp.p2off = (const uint64_t*)x->f_p2.p;
-        pp.rec2 = (uint64_t*)x->f_rec2.p;
-        pp.boff = (const uint64_t*)x->f_boff.p;
-        pp.out_kl = (uint64_t*)x->f_okl.p;
-        pp.out_cnt = (uint32_t*)x->f_ocnt.p;
-        pp.nout = (uint32_t*)x->f_on.p;
-        pp.epre = (const uint64_t*)((const uint8_t*)x->f_on.p + sizeof(uint32_t) * kQ * kQ);
-        std::vector<uint32_t> nout((size_t)kQ * kQ, 0u);
-        if (R > 0) {
-            HIP_TRY(launch_part2(pp, st));
-            HIP_TRY(launch_reduce(pp, st));
-            HIP_TRY(hipMemcpyAsync(nout.data(), pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
-        }
-        HIP_TRY(hipStreamSynchronize(st));
-        // the merge's entry order: buckets' outputs back to back
-        std::vector<uint64_t> epre((size_t)kQ * kQ + 1, 0);
-        for (int b = 0; b < kQ * kQ; ++b) {
-            if (nout[b] > boff[b + 1] - boff[b])
-                return fail(LDGPU_EDEVICE, "fit reduce: bucket %d wrote %u entries from %llu records", b, nout[b],
-                            (unsigned long long)(boff[b + 1] - boff[b]));
-            epre[b + 1] = epre[b] + nout[b];
-        }
-        const unsigned long long E = epre[(size_t)kQ * kQ];
-        HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
-        // room for every entry as a new key: load <= 1/2, so the merge's
-        // probes never reach the overflow list in practice (it still catches them)
-        if (2 * (c->size + E) > c->cap) {
-            if (int rc = grow(c, next_pow2(2 * (c->size + E)))) return rc;
-        }
-        if (int rc = ensure_ovf(c, (int64_t)E)) return rc;
-        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-        HIP_TRY(launch_merge(pp, count_params(c), (int64_t)E, st));
-        if (int rc = after_batch(c)) return rc;
-        d0 = d1;
-    }
-    return LDGPU_OK;
-}
-
 // ---- grams of 8..15 bytes (wide_count_kernel, ldgpu_fit.hip)
 WideCountParams wide_params(const ldgpu_counts* c) {
     WideCountParams p{};
@@ -1863,20 +1730,242 @@ int wide_count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, 
     return LDGPU_OK;
 }
 
-// Count documents [0, n_docs) of d_offsets / d_lang (h_off: the same offsets on
-// the host, used to plan sub-launches of at most ovf_cap windows each, so the
-// overflow list can never lose an entry): the one-word gram lengths, then the
-// wide ones.
+// FIT v3 batches: at most batch_windows windows (kBatchWindows / K: ~200 MB of
+// corpus at grams 1-5), so the record scratch (K words per window for the emit
+// records -- a record stands for at least one window --, K words per record for
+// the buckets, out_words per record of reduce output) stays within ~20 GB of
+// HBM.
+constexpr int64_t kBatchWindows = 1ll << 30;
+
+int out_words(int K) { return K == 1 ? 2 : K; }
+
+// windows of every gram length for a document of len bytes
+int64_t doc_windows_all(const ldgpu_counts* c, int64_t len) {
+    int64_t w = 0;
+    for (int i = 0; i < c->nG; ++i) w += n_windows(len, c->G[i]);
+    return w;
+}
+
+// Count documents [0, n_docs) on the device with FIT v3 (ldgpu_fit.hip): per
+// batch, the documents in language order (h_lang: their languages on the
+// host), emit -> part2 -> reduce -> merge.
+int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                    const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, const int32_t* h_lang) {
+    ldgpu_ctx* x = c->ctx;
+    hipStream_t st = x->stream;
+    const int K = c->K;
+    const int64_t thresh = emit_blk_recs(K) - emit_round_recs(K);
+    if (int rc = ensure_ovf(c, 1 << 20)) return rc;
+    std::vector<uint32_t> cnt3((size_t)kQ * kQ * kSplits);
+    std::vector<uint64_t> p2off((size_t)kQ * kQ * kSplits), boff((size_t)kQ * kQ + 1);
+    std::vector<int64_t> win((size_t)n_docs);
+    for (int64_t d = 0; d < n_docs; ++d) win[d] = doc_windows_all(c, h_off[d + 1] - h_off[d]);
+    const int L = c->L;
+    std::vector<int64_t> lcnt(L + 1), lwin(L);
+    std::vector<int32_t> perm;
+    std::vector<int64_t> wg_doc, wg_rec, wg_dir;
+    std::vector<int32_t> wg_lang;
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0, W = 0;
+        while (d1 < n_docs) {
+            if (d1 > d0 && W + win[d1] > c->batch_windows) break;
+            W += win[d1];
+            ++d1;
+        }
+        // the batch's documents of supported languages, in language order
+        // (a stable counting sort; reduceGrams drops the others)
+        std::fill(lcnt.begin(), lcnt.end(), 0);
+        std::fill(lwin.begin(), lwin.end(), 0);
+        for (int64_t d = d0; d < d1; ++d) {
+            const int32_t l = h_lang[d];
+            if (l < 0 || l >= L || win[d] == 0) continue;
+            lcnt[l + 1]++;
+            lwin[l] += win[d];
+        }
+        for (int l = 0; l < L; ++l) lcnt[l + 1] += lcnt[l];
+        const int64_t nd = lcnt[L];
+        perm.assign((size_t)std::max<int64_t>(nd, 1), 0);
+        {
+            std::vector<int64_t> at(lcnt.begin(), lcnt.end() - 1);
+            for (int64_t d = d0; d < d1; ++d) {
+                const int32_t l = h_lang[d];
+                if (l < 0 || l >= L || win[d] == 0) continue;
+                perm[at[l]++] = (int32_t)(d - d0);
+            }
+        }
+        // emit workgroups: each language's documents split into ranges
+        // balanced by windows, about 2 workgroups per CU in all; a
+        // workgroup's record region holds its windows, its block directory
+        // (windows + the table flush) / threshold + 2 blocks
+        const int64_t Wk = std::accumulate(lwin.begin(), lwin.end(), (int64_t)0);
+        const int64_t target = std::max<int64_t>(1, (Wk + 2 * x->cus - 1) / (2 * x->cus));
+        wg_doc.clear();
+        wg_rec.clear();
+        wg_dir.clear();
+        wg_lang.clear();
+        int64_t acc = 0, dirs = 0;
+        for (int l = 0; l < L; ++l) {
+            if (!lwin[l]) continue;
+            const int64_t parts = std::max<int64_t>(1, (lwin[l] + target - 1) / target);
+            int64_t i = lcnt[l], wacc = 0;
+            for (int64_t k = 0; k < parts; ++k) {
+                const int64_t start = i, start_acc = acc, goal = lwin[l] * (k + 1) / parts;
+                while (i < lcnt[l + 1] && (wacc < goal || k + 1 == parts)) {
+                    const int64_t w = win[d0 + perm[i]];
+                    wacc += w;
+                    acc += w;
+                    ++i;
+                }
+                if (i == start) continue;
+                wg_doc.push_back(start);
+                wg_rec.push_back(start_acc);
+                wg_dir.push_back(dirs);
+                wg_lang.push_back(l);
+                dirs += (acc - start_acc + 256 + kT23) / thresh + 2;
+            }
+        }
+        while (wg_doc.empty() || wg_doc.size() % kSplits) {  // empty workgroups: a multiple of kSplits
+            wg_doc.push_back(nd);
+            wg_rec.push_back(acc);
+            wg_dir.push_back(dirs);
+            wg_lang.push_back(0);
+        }
+        const int grid_a = (int)wg_doc.size();
+        wg_doc.push_back(nd);
+        wg_rec.push_back(acc);
+        wg_dir.push_back(dirs);
+        std::vector<int64_t> meta;
+        meta.reserve(3 * wg_doc.size());
+        meta.insert(meta.end(), wg_doc.begin(), wg_doc.end());
+        meta.insert(meta.end(), wg_rec.begin(), wg_rec.end());
+        meta.insert(meta.end(), wg_dir.begin(), wg_dir.end());
+        const size_t n_lang = wg_lang.size(), n_perm = perm.size();
+        HIP_TRY(x->f_wg.ensure(sizeof(int64_t) * meta.size() + sizeof(int32_t) * (n_lang + n_perm) + 16));
+        HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(acc, 1)));
+        HIP_TRY(x->f_bstart.ensure(sizeof(int64_t) * (size_t)dirs));
+        HIP_TRY(x->f_bhdr.ensure(sizeof(uint32_t) * kHdr * (size_t)dirs));
+        HIP_TRY(x->f_nblk.ensure(sizeof(int32_t) * (size_t)grid_a + sizeof(unsigned long long)));
+        HIP_TRY(x->f_cnt3.ensure(sizeof(uint32_t) * cnt3.size()));
+        uint8_t* wgp = (uint8_t*)x->f_wg.p;
+        int32_t* d_wg_lang = (int32_t*)(wgp + sizeof(int64_t) * meta.size());
+        int32_t* d_perm = d_wg_lang + n_lang;
+        HIP_TRY(hipMemcpyAsync(wgp, meta.data(), sizeof(int64_t) * meta.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_wg_lang, wg_lang.data(), sizeof(int32_t) * n_lang, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_perm, perm.data(), sizeof(int32_t) * n_perm, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(x->f_cnt3.p, 0, sizeof(uint32_t) * cnt3.size(), st));
+        PartParams pp{};
+        pp.bytes = d_bytes;
+        pp.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+        pp.offsets = d_offsets + d0;
+        pp.doc_lang = d_lang + d0;
+        pp.L = c->L;
+        pp.nG = c->nG;
+        for (int i = 0; i < c->nG; ++i) pp.G[i] = c->G[i];
+        pp.lb = c->lb;
+        pp.cb = c->cb;
+        if (const char* ab = diag_env("LDGPU_FIT_EMIT_ABLATE")) pp.ablate = atoi(ab);
+        pp.grid_a = grid_a;
+        pp.perm = d_perm;
+        pp.wg_lang = d_wg_lang;
+        pp.wg_doc = (const int64_t*)wgp;
+        pp.wg_rec = pp.wg_doc + grid_a + 1;
+        pp.wg_dir = pp.wg_rec + grid_a + 1;
+        pp.rec = (uint64_t*)x->f_rec.p;
+        pp.blk_start = (int64_t*)x->f_bstart.p;
+        pp.blk_hdr = (uint32_t*)x->f_bhdr.p;
+        pp.nblk = (int32_t*)x->f_nblk.p;
+        pp.cnt3 = (uint32_t*)x->f_cnt3.p;
+        pp.direct = count_params(c);
+        HIP_TRY(launch_emit(K, pp, st));
+        HIP_TRY(hipMemcpyAsync(cnt3.data(), x->f_cnt3.p, sizeof(uint32_t) * cnt3.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = after_batch(c)) return rc;  // direct adds (a count too large for a record) that overflowed
+        // exact bucket offsets: (q1, q2) major, emit group minor
+        uint64_t off = 0;
+        for (int q = 0; q < kQ * kQ; ++q) {
+            boff[q] = off;
+            for (int s = 0; s < kSplits; ++s) {
+                p2off[(size_t)q * kSplits + s] = off;
+                off += cnt3[(size_t)q * kSplits + s];
+            }
+        }
+        boff[(size_t)kQ * kQ] = off;
+        const int64_t R = (int64_t)off;
+        if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld windows", (long long)R, (long long)acc);
+        HIP_TRY(x->f_p2.ensure(sizeof(uint64_t) * p2off.size()));
+        HIP_TRY(x->f_boff.ensure(sizeof(uint64_t) * boff.size()));
+        HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(R, 1)));
+        HIP_TRY(x->f_okl.ensure(sizeof(uint64_t) * out_words(K) * (size_t)std::max<int64_t>(R, 1)));
+        HIP_TRY(x->f_on.ensure(sizeof(uint32_t) * kQ * kQ + sizeof(uint64_t) * (kQ * kQ + 1)));
+        HIP_TRY(hipMemcpyAsync(x->f_p2.p, p2off.data(), sizeof(uint64_t) * p2off.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(x->f_boff.p, boff.data(), sizeof(uint64_t) * boff.size(), hipMemcpyHostToDevice, st));
+        pp.p2off = (const uint64_t*)x->f_p2.p;
+        pp.rec2 = (uint64_t*)x->f_rec2.p;
+        pp.boff = (const uint64_t*)x->f_boff.p;
+        pp.out = (uint64_t*)x->f_okl.p;
+        pp.nout = (uint32_t*)x->f_on.p;
+        pp.epre = (const uint64_t*)((const uint8_t*)x->f_on.p + sizeof(uint32_t) * kQ * kQ);
+        std::vector<uint32_t> nout((size_t)kQ * kQ, 0u);
+        if (R > 0) {
+            HIP_TRY(launch_part2(K, pp, st));
+            HIP_TRY(launch_reduce(K, pp, st));
+            HIP_TRY(hipMemcpyAsync(nout.data(), pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        // the merge's entry order: buckets' outputs back to back
+        std::vector<uint64_t> epre((size_t)kQ * kQ + 1, 0);
+        for (int b = 0; b < kQ * kQ; ++b) {
+            if (nout[b] > boff[b + 1] - boff[b])
+                return fail(LDGPU_EDEVICE, "fit reduce: bucket %d wrote %u entries from %llu records", b, nout[b],
+                            (unsigned long long)(boff[b + 1] - boff[b]));
+            epre[b + 1] = epre[b] + nout[b];
+        }
+        const unsigned long long E = epre[(size_t)kQ * kQ];
+        HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
+        // room for every entry as a new key: load <= 1/2, so the merge's
+        // probes never reach the overflow list in practice (it still catches them)
+        if (2 * (c->size + E) > c->cap) {
+            if (int rc = grow(c, next_pow2(2 * (c->size + E)))) return rc;
+        }
+        if (K == 3 && c->nGw > 0) {
+            // wide entries: at most the batch's wide windows
+            int64_t ww = 0;
+            for (int64_t d = d0; d < d1; ++d) {
+                const int64_t len = h_off[d + 1] - h_off[d];
+                if (len < 8) continue;
+                for (int i = 0; i < c->nGw; ++i) ww += n_windows(len, c->Gw[i]);
+            }
+            if (int rc = wide_ensure(c, (uint64_t)std::min<int64_t>(ww, (int64_t)E))) return rc;
+        }
+        if (int rc = ensure_ovf(c, (int64_t)E)) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+        HIP_TRY(launch_merge(K, pp, count_params(c), wide_params(c), (int64_t)E, st));
+        if (K == 3 && c->nGw > 0) {
+            if (int rc = wide_after(c)) return rc;
+        }
+        if (int rc = after_batch(c)) return rc;
+        d0 = d1;
+    }
+    return LDGPU_OK;
+}
+
+// Count documents [0, n_docs) of d_offsets / d_lang (h_off / h_lang: the
+// same offsets and languages on the host, used to plan the batches): FIT v3
+// for every gram length; the diagnostics build's LDGPU_FIT_LEGACY runs the
+// round-1 atomic kernels instead (one-word lengths, then the wide ones).
 int count_launch_narrow(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                         const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st);
 
 int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
-                 const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
+                 const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, const int32_t* h_lang, hipStream_t st) {
+    if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
+    if (c->v3) return count_launch_v3(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, h_lang);
     if (c->nGn > 0) {
-        if (int rc = count_launch_narrow(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, st)) return rc;
+        if (int rc = count_launch_narrow(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, c->ctx->stream))
+            return rc;
     }
     if (c->nGw > 0) {
-        if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
         if (int rc = wide_count_launch(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off)) return rc;
     }
     return LDGPU_OK;
@@ -1884,10 +1973,6 @@ int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const
 
 int count_launch_narrow(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                         const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, hipStream_t st) {
-    if (c->v2) {
-        if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
-        return count_launch_v2(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off);
-    }
     int64_t total = 0;
     for (int64_t d = 0; d < n_docs; ++d) total += doc_windows(c, h_off[d + 1] - h_off[d]);
     if (int rc = ensure_ovf(c, total)) return rc;
@@ -1946,20 +2031,27 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
             c->Gw[c->nGw++] = gram_lengths[i];
     }
     c->cap = next_pow2(std::max<int64_t>(1 << 12, 2 * std::max<int64_t>(capacity_hint, 0)));
-    // FIT v2 when a (gram, language, count) record fits 64 bits with >= 8
-    // count bits: 8 max(G) + 1 sentinel-key bits + ceil(log2 L) language bits
+    // FIT v3 record form (ldgpu_internal.h): the compact one-word record when
+    // 8 max(G) + 1 sentinel-key bits + ceil(log2 L) language bits leave >= 8
+    // count bits, two words for any other table of grams <= 7 bytes, three
+    // with grams of 8..15 bytes
     {
         int maxg = 0;
-        for (int i = 0; i < c->nGn; ++i) maxg = std::max(maxg, c->Gn[i]);
+        for (int i = 0; i < c->nG; ++i) maxg = std::max(maxg, c->G[i]);
         c->lb = (uint32_t)std::max(1, log2u((uint64_t)n_langs));
-        const int cb = 64 - (8 * maxg + 1) - (int)c->lb;
+        const int cb = 64 - (8 * std::min(maxg, kMaxGram) + 1) - (int)c->lb;
         c->cb = (uint32_t)std::max(cb, 0);
-        c->v2 = cb >= 8 && !diag_env("LDGPU_FIT_LEGACY");
-        c->batch_windows = kBatchWindows;
+        c->K = maxg > kMaxGram ? 3 : (cb >= 8 ? 1 : 2);
+        if (const char* k = diag_env("LDGPU_FIT_K")) c->K = std::max(c->K, std::min(3, atoi(k)));  // tests: wider forms
+        c->v3 = !diag_env("LDGPU_FIT_LEGACY");
+        c->batch_windows = kBatchWindows / c->K;
         if (const char* bw = diag_env("LDGPU_FIT_BATCH_WINDOWS")) c->batch_windows = std::max(1ll, atoll(bw));
-        if (c->v2 && fit2_prepare() != hipSuccess) {  // dynamic-LDS limits of this device's kernels
-            (void)hipGetLastError();
-            c->v2 = false;
+        if (c->v3) {
+            const hipError_t pe = fit3_prepare(c->K);  // dynamic-LDS limits of this device's kernels
+            if (pe != hipSuccess) {
+                delete c;
+                return fail(LDGPU_EDEVICE, "fit kernels: %s", hipGetErrorString(pe));
+            }
         }
     }
     int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
@@ -1999,9 +2091,12 @@ extern "C" int ldgpu_count_device(ldgpu_counts* c, const uint8_t* d_bytes, int64
     hipStream_t st = (hipStream_t)stream;
     if (n_docs == 0) return ok();
     std::vector<int64_t> h_off(n_docs + 1);
+    std::vector<int32_t> h_lang(n_docs);
     HIP_TRY(hipMemcpyAsync(h_off.data(), d_offsets, sizeof(int64_t) * (n_docs + 1), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h_lang.data(), d_doc_lang, sizeof(int32_t) * n_docs, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (int rc = count_launch(c, d_bytes, n_bytes, d_offsets, d_doc_lang, n_docs, h_off.data(), st)) return rc;
+    if (int rc = count_launch(c, d_bytes, n_bytes, d_offsets, d_doc_lang, n_docs, h_off.data(), h_lang.data(), st))
+        return rc;
     return ok();
 }
 
@@ -2033,7 +2128,7 @@ extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t*
                                x->stream));
         HIP_TRY(hipMemcpyAsync(x->langs.p, doc_lang + d0, sizeof(int32_t) * nd, hipMemcpyHostToDevice, x->stream));
         if (int rc = count_launch(c, (const uint8_t*)x->bytes.p, nb, (const int64_t*)x->offsets.p,
-                                  (const int32_t*)x->langs.p, nd, off.data(), x->stream))
+                                  (const int32_t*)x->langs.p, nd, off.data(), doc_lang + d0, x->stream))
             return rc;
         d0 = d1;
     }

@@ -9,12 +9,12 @@
 // row of L u64 counters per slot (keys[cap], counts[cap][L]).  Integer atomics
 // are order-independent, so the counts are bit-exact whatever the schedule.
 //
-// Two counting paths share the table: FIT v2 (emit / part2 / reduce /
-// merge, below: radix-partitioned record aggregation, one table add per
-// distinct (gram, language) per batch -- the path every table whose
-// (gram, language, count) record fits 64 bits takes) and the single-pass
-// count_kernel here (tables whose record does not fit, e.g. 7-byte grams with
-// hundreds of languages; diagnostics builds force it: LDGPU_FIT_LEGACY).  count_kernel:
+// The counting path is FIT v3 (emit / part2 / reduce / merge, end of file:
+// language-grouped LDS aggregation and radix-partitioned records, one table
+// add per distinct (gram, language) per bucket and batch) for every gram
+// length and language count.  The single-pass count_kernel here and the
+// wide_count_kernel below are the round-1 atomic kernels, kept for A/B timing
+// in diagnostics builds only (LDGPU_FIT_LEGACY).  count_kernel:
 // one wave per document, lanes = 64 consecutive window positions of one gram
 // length; 1-gram windows aggregated in a per-wave 256-bin LDS histogram, 2-
 // and 3-byte keys in a per-wave LDS hash (kH2 slots, flushed after each gram
@@ -647,631 +647,6 @@ hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const u
 }  // namespace ldgpu
 
 // ---------------------------------------------------------------------------
-// FIT v2: radix-partitioned record aggregation -- the north star's "LDS-
-// privatised histogram, then a sort / segmented-reduce merge into HBM count
-// tables", built so that the global table sees ONE add per distinct
-// (gram, language) per batch instead of one device-scope atomic per window
-// (which bounded the single-pass count_kernel above: ~2.7e9 random atomics
-// per GiB).  Per batch of documents:
-//   emit    one wave per document: 1-byte windows into a per-wave LDS
-//           histogram, 2-/3-byte windows into a per-wave LDS hash (both
-//           flushed per document / gram length as counted records), longer
-//           windows straight to records.  Records gather in a workgroup LDS
-//           block; a full block is counting-sorted by q1 in LDS and written
-//           once, coalesced, into the workgroup's own region with a header
-//           of q1 starts.  The workgroup also histograms (q1, q2).
-//   part2   bucket q1 of one emit group: the group's q1 runs (load-balanced
-//           over a wave) are re-scattered by q2 to exact, host-scanned
-//           offsets -- 4096 contiguous buckets (q1, q2).
-//   reduce  one workgroup per bucket: an LDS hash (kAggSlots entries) sums
-//           the counts of equal (gram, language) records; distinct entries
-//           go out as (kl, count).
-//   merge   each entry is one find-or-insert + one u64 add in the table.
-// Integer sums are order-independent: counts stay bit-exact.
-namespace ldgpu {
-namespace {
-
-__device__ __forceinline__ bool emit_ablated(const PartParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
-
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ uint64_t make_rec(uint64_t bytes, int klen, uint32_t lang, uint64_t c, uint32_t lb,
-                                             uint32_t cb) {
-    const uint64_t sent = (1ull << (8 * klen)) | bytes;
-    return (((sent << lb) | (uint64_t)lang) << cb) | c;
-}
-
-// the packed gram key (ldgpu_common.h) of a record's kl = record >> cb
-__device__ __forceinline__ uint64_t kl_key(uint64_t kl, uint32_t lb) {
-    const uint64_t sent = kl >> lb;
-    const int klen = (63 - __builtin_clzll(sent)) >> 3;
-    return (sent ^ (1ull << (8 * klen))) | ((uint64_t)klen << 56);
-}
-
-__device__ __forceinline__ uint32_t q1_of(uint64_t r, uint32_t cb) { return (uint32_t)(mix64(r >> cb) >> (64 - kQBits)); }
-__device__ __forceinline__ uint32_t q2_of(uint64_t r, uint32_t cb) {
-    return (uint32_t)(mix64(r >> cb) >> (64 - 2 * kQBits)) & (kQ - 1);
-}
-
-// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations
-// (lgkmcnt), not for its outstanding global loads -- __syncthreads() would
-// drain those too, and emit keeps the next step's window loads in flight
-// across the round barriers.  Global stores before it need not be visible to
-// the other waves (each flushed block is read by the next kernel only).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// wave inclusive scan (64 lanes)
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
-
-// emit's per-wave LDS table of a document's 2-byte windows: 1024 packed
-// slots (16-bit key, 16-bit count), so a document's few hundred distinct
-// 2-grams probe short chains; documents of 64 Ki bytes or more skip it (a
-// count must stay below 0xffff)
-constexpr uint32_t kK2 = 1024;
-constexpr uint32_t kK2Empty = 0xffffffffu;
-constexpr int kK2Probe = 16;
-constexpr int64_t kK2MaxDoc = 0xffff;
-
-struct EmitLds {
-    uint64_t blk[kBlkRecs];
-    uint32_t hist2[kQ * kQ];
-    uint32_t h1[kEmitWaves][256];
-    uint32_t k2[kEmitWaves][kK2];      // per-document 2-gram counts: key << 16 | count, kK2Empty = free
-    uint32_t pcnt[kQ];
-    uint32_t pfill[kQ];
-    uint32_t pstart[kQ + 1];
-    uint32_t blk_n;
-    uint32_t active;
-    uint32_t next_doc;
-};
-
-enum { kNextDoc = 0, kWin = 1, kHFlush = 2, kH1Flush = 3, kDone = 4 };
-
-// one wave's position in its current document (wave-uniform)
-struct WaveState {
-    int64_t b, len, p0;
-    int32_t lang, gi, phase, cursor;
-    uint32_t used1;
-    bool pf;                     // pw holds the words of the next WIN step (issued a round early)
-    uint32_t pw[4][3];
-};
-
-// append the lanes' records (kSub per lane) to the workgroup block with one
-// reservation (the round bound keeps it from overflowing); every lane of the
-// wave must be active
-constexpr int kSubW = 4;  // window positions (or flushed slots) per lane per step
-
-__device__ __forceinline__ void emit_recs(EmitLds& S, const bool (&has)[kSubW], const uint64_t (&r)[kSubW],
-                                          int lane) {
-    uint64_t m[kSubW];
-    uint32_t tot = 0;
-#pragma unroll
-    for (int k = 0; k < kSubW; ++k) {
-        m[k] = __ballot(has[k]);
-        tot += (uint32_t)__popcll(m[k]);
-    }
-    if (!tot) return;
-    uint32_t base = 0;
-    if (lane == 0) base = __hip_atomic_fetch_add(&S.blk_n, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = __shfl(base, 0);
-#pragma unroll
-    for (int k = 0; k < kSubW; ++k) {
-        if (has[k]) S.blk[base + lane_rank(m[k])] = r[k];
-        base += (uint32_t)__popcll(m[k]);
-    }
-}
-
-__device__ __forceinline__ void next_gram(const PartParams& p, WaveState& w) {
-    w.gi += 1;
-    w.p0 = 0;
-    w.cursor = 0;
-    w.phase = w.gi < p.nG ? kWin : (w.used1 ? kH1Flush : kNextDoc);
-}
-
-// the dwords of the kSubW positions of a WIN step at (gi, p0)
-__device__ __forceinline__ void window_loads(const PartParams& p, const WaveState& w, int lane,
-                                             uint32_t (&pw)[4][3]) {
-    const int n = p.G[w.gi];
-    const int64_t nwin = n_windows(w.len, n);
-    const int klen = w.len < n ? (int)w.len : n;
-    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
-#pragma unroll
-    for (int k = 0; k < kSubW; ++k) {
-        const int64_t pos = w.p0 + 64 * k + lane;
-        const int64_t a = w.b + (pos < nwin ? pos : 0);
-        const int64_t i = a >> 2;
-        pw[k][0] = ld_dw(W, i, p.last_dword);
-        pw[k][1] = ld_dw(W, i + 1, p.last_dword);
-        pw[k][2] = klen > 4 ? ld_dw(W, i + 2, p.last_dword) : 0u;
-    }
-}
-
-// One step of a wave: <= 64 kSubW windows or flushed slots, <= 64 kSubW
-// records.  The positions' loads are all issued before any is used.
-__device__ __forceinline__ void emit_step(const PartParams& p, EmitLds& S, WaveState& w, int wave, int lane,
-                                          int64_t d0, int64_t d1) {
-    const uint64_t cmax = p.cb >= 32 ? 0xffffffffull : ((1ull << p.cb) - 1ull);
-    uint32_t* h1 = S.h1[wave];
-    uint32_t* k2 = S.k2[wave];
-    if (w.phase == kNextDoc) {
-        uint32_t k = 0;
-        if (lane == 0) k = __hip_atomic_fetch_add(&S.next_doc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int64_t d = d0 + (int64_t)__shfl(k, 0);
-        if (d >= d1) {
-            w.phase = kDone;
-            if (lane == 0) __hip_atomic_fetch_sub(&S.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return;
-        }
-        const int lang = p.doc_lang[d];
-        if (lang < 0 || lang >= p.L) return;  // reduceGrams keeps supported languages only
-        const int64_t b = p.offsets[d];
-        const int64_t len = p.offsets[d + 1] - b;
-        if (len <= 0 || p.nG == 0) return;
-        w.b = b;
-        w.len = len;
-        w.lang = lang;
-        w.gi = 0;
-        w.p0 = 0;
-        w.cursor = 0;
-        w.used1 = 0;
-        w.pf = false;
-        w.phase = kWin;
-        // fall through: the document's first windows in this step
-    }
-    bool has[kSubW];
-    uint64_t r[kSubW];
-#pragma unroll
-    for (int k = 0; k < kSubW; ++k) {
-        has[k] = false;
-        r[k] = 0;
-    }
-    if (w.phase == kWin) {
-        const int n = p.G[w.gi];
-        const int64_t nwin = n_windows(w.len, n);
-        const int klen = w.len < n ? (int)w.len : n;
-        const uint32_t lomask = klen >= 4 ? 0xffffffffu : ((1u << (8 * klen)) - 1u);
-        const uint32_t himask = klen <= 4 ? 0u : ((1u << (8 * (klen - 4))) - 1u);
-        uint32_t lo[kSubW], hi[kSubW];
-        bool valid[kSubW];
-        if (!w.pf) window_loads(p, w, lane, w.pw);
-        w.pf = false;
-#pragma unroll
-        for (int k = 0; k < kSubW; ++k) {
-            const int64_t pos = w.p0 + 64 * k + lane;
-            valid[k] = pos < nwin;
-            const uint32_t sh = (uint32_t)((w.b + (valid[k] ? pos : 0)) & 3);
-            lo[k] = __builtin_amdgcn_alignbyte(w.pw[k][1], w.pw[k][0], sh) & lomask;
-            hi[k] = __builtin_amdgcn_alignbyte(w.pw[k][2], w.pw[k][1], sh) & himask;
-        }
-        if (klen == 1) {
-#pragma unroll
-            for (int k = 0; k < kSubW; ++k)
-                if (valid[k]) __hip_atomic_fetch_add(&h1[lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            w.used1 = 1;
-        } else if (klen == 2 && w.len < kK2MaxDoc && !emit_ablated(p, 1)) {
-            // the kSubW positions probe together: one LDS round trip per
-            // probe step for all of them (most find their key at once)
-            uint32_t slot[kSubW];
-            bool pend[kSubW];
-#pragma unroll
-            for (int k = 0; k < kSubW; ++k) {
-                slot[k] = (uint32_t)(((uint64_t)(lo[k] * 0x9E3779B1u) * kK2) >> 32);
-                pend[k] = valid[k];
-            }
-            for (int t = 0; t < kK2Probe; ++t) {
-                uint32_t cur[kSubW];
-#pragma unroll
-                for (int k = 0; k < kSubW; ++k) cur[k] = pend[k] ? k2[slot[k]] : 0u;
-                bool any = false;
-#pragma unroll
-                for (int k = 0; k < kSubW; ++k) {
-                    if (!pend[k]) continue;
-                    if (cur[k] == kK2Empty &&
-                        atomicCAS(&k2[slot[k]], kK2Empty, (lo[k] << 16) | 1u) == kK2Empty) {
-                        pend[k] = false;  // inserted with count 1
-                        continue;
-                    }
-                    if (cur[k] == kK2Empty) cur[k] = k2[slot[k]];  // lost the race: see who won
-                    if ((cur[k] >> 16) == lo[k]) {
-                        __hip_atomic_fetch_add(&k2[slot[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        pend[k] = false;
-                    } else {
-                        slot[k] = (slot[k] + 1u) & (kK2 - 1u);
-                        any = true;
-                    }
-                }
-                if (!__ballot(any)) break;
-            }
-#pragma unroll
-            for (int k = 0; k < kSubW; ++k) {
-                if (pend[k]) {  // no slot: the window goes out as a record
-                    has[k] = true;
-                    r[k] = make_rec(lo[k], klen, (uint32_t)w.lang, 1, p.lb, p.cb);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kSubW; ++k) {
-                has[k] = valid[k];
-                r[k] = make_rec(((uint64_t)hi[k] << 32) | lo[k], klen, (uint32_t)w.lang, 1, p.lb, p.cb);
-            }
-        }
-        if (emit_ablated(p, 4)) {
-#pragma unroll
-            for (int k = 0; k < kSubW; ++k) has[k] = false;
-        }
-        emit_recs(S, has, r, lane);
-        w.p0 += 64 * kSubW;
-        if (w.p0 >= nwin) {
-            __builtin_amdgcn_wave_barrier();
-            if (klen == 2 && w.len < kK2MaxDoc && !emit_ablated(p, 1)) {
-                w.phase = kHFlush;
-                w.cursor = 0;
-            } else {
-                next_gram(p, w);
-            }
-        }
-        if (w.phase == kWin) {  // the next step's loads fly across the round barrier
-            window_loads(p, w, lane, w.pw);
-            w.pf = true;
-        }
-        return;
-    }
-    if (w.phase == kHFlush) {  // this gram length's 2-byte keys, 64 kSubW slots a step
-#pragma unroll
-        for (int k = 0; k < kSubW; ++k) {
-            const uint32_t slot = (uint32_t)w.cursor + 64u * k + lane;
-            const uint32_t v = k2[slot];
-            if (v == kK2Empty) continue;
-            k2[slot] = kK2Empty;
-            const uint32_t c = v & 0xffffu;
-            if (c <= cmax) {
-                has[k] = true;
-                r[k] = make_rec(v >> 16, 2, (uint32_t)w.lang, c, p.lb, p.cb);
-            } else {
-                add_count(p.direct, (2ull << 56) | (uint64_t)(v >> 16), w.lang, c);
-            }
-        }
-        emit_recs(S, has, r, lane);
-        w.cursor += 64 * kSubW;
-        if (w.cursor >= (int)kK2) {
-            __builtin_amdgcn_wave_barrier();
-            next_gram(p, w);
-            if (w.phase == kWin) {
-                window_loads(p, w, lane, w.pw);
-                w.pf = true;
-            }
-        }
-        return;
-    }
-    if (w.phase == kH1Flush) {  // the document's 1-byte keys (256 bins: one step)
-#pragma unroll
-        for (int k = 0; k < kSubW; ++k) {
-            const int bin = 64 * k + lane;
-            const uint32_t c = h1[bin];
-            if (!c) continue;
-            h1[bin] = 0u;
-            if (c <= cmax) {
-                has[k] = true;
-                r[k] = make_rec((uint64_t)bin, 1, (uint32_t)w.lang, c, p.lb, p.cb);
-            } else {
-                add_count(p.direct, (1ull << 56) | (uint64_t)bin, w.lang, c);
-            }
-        }
-        emit_recs(S, has, r, lane);
-        __builtin_amdgcn_wave_barrier();
-        w.used1 = 0;
-        w.phase = kNextDoc;
-    }
-}
-
-// Write the block: counting sort by q1 in LDS, scattered stores into the
-// block's own contiguous range (the lines fill in L2 and leave whole).
-__device__ __forceinline__ void flush_block(const PartParams& p, EmitLds& S, uint32_t n, int64_t rb, int64_t gid,
-                                            int tid) {
-    for (uint32_t i = tid; i < n; i += kEmitWaves * 64) {
-        const uint64_t h = mix64(S.blk[i] >> p.cb);
-        const uint32_t q1 = (uint32_t)(h >> (64 - kQBits));
-        const uint32_t q2 = (uint32_t)(h >> (64 - 2 * kQBits)) & (kQ - 1);
-        __hip_atomic_fetch_add(&S.pcnt[q1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&S.hist2[q1 * kQ + q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    lds_barrier();
-    if (tid < 64) {
-        const uint32_t v = S.pcnt[tid];
-        const uint32_t inc = wave_inclusive_scan(v, tid);
-        S.pstart[tid] = inc - v;
-        S.pfill[tid] = inc - v;
-        S.pcnt[tid] = 0u;
-        if (tid == 63) S.pstart[kQ] = inc;
-    }
-    lds_barrier();
-    for (uint32_t i = tid; i < n; i += kEmitWaves * 64) {
-        const uint64_t r = S.blk[i];
-        const uint32_t at =
-            __hip_atomic_fetch_add(&S.pfill[q1_of(r, p.cb)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (!emit_ablated(p, 2)) p.rec[rb + at] = r;
-    }
-    if (tid <= kQ) p.blk_hdr[(size_t)gid * kHdr + tid] = S.pstart[tid];
-    if (tid == 0) {
-        p.blk_start[gid] = rb;
-        S.blk_n = 0u;
-    }
-    lds_barrier();
-}
-
-__global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t emit_smem[];
-    EmitLds& S = *reinterpret_cast<EmitLds*>(emit_smem);
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int bid = blockIdx.x;
-    const int64_t d0 = p.wg_doc[bid], d1 = p.wg_doc[bid + 1];
-    const int64_t rbase = p.wg_rec[bid], dbase = p.wg_dir[bid];
-    for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64) S.hist2[i] = 0u;
-    for (int i = lane; i < 256; i += 64) S.h1[wave][i] = 0u;
-    for (int i = lane; i < (int)kK2; i += 64) S.k2[wave][i] = kK2Empty;
-    if (tid < kQ) S.pcnt[tid] = 0u;
-    if (tid == 0) {
-        S.blk_n = 0u;
-        S.active = kEmitWaves;
-        S.next_doc = 0u;
-    }
-    lds_barrier();
-    WaveState w{};
-    w.phase = kNextDoc;
-    int64_t written = 0;
-    int64_t nb = 0;
-    for (;;) {
-        // a round: every live wave takes one step (<= 64 kSubW records, so the
-        // block, flushed above kBlkRecs - kRoundRecs, never overflows)
-        if (w.phase != kDone) emit_step(p, S, w, wave, lane, d0, d1);
-        lds_barrier();
-        const uint32_t n = S.blk_n;
-        const uint32_t act = S.active;
-        lds_barrier();  // every thread has read n / act before the next round moves them
-        if (n > (uint32_t)(kBlkRecs - kRoundRecs) || (act == 0u && n > 0u)) {
-            flush_block(p, S, n, rbase + written, dbase + nb, tid);
-            written += n;
-            ++nb;
-        }
-        if (act == 0u) break;
-    }
-    if (tid == 0) p.nblk[bid] = (int32_t)nb;
-    const int grp = bid / (p.grid_a / kSplits);
-    for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64)
-        if (S.hist2[i]) atomicAdd(&p.cnt3[i * kSplits + grp], S.hist2[i]);
-}
-
-struct Part2Lds {
-    uint32_t cur[kQ];
-    int32_t gpre[257];
-};
-
-__device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) {
-    return (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
-                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32));
-}
-
-__global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams p) {
-    __shared__ Part2Lds S;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t q1 = blockIdx.x / kSplits;
-    const int s = blockIdx.x % kSplits;
-    const int per = p.grid_a / kSplits;
-    const int w0 = s * per;
-    if (tid == 0) {
-        int32_t acc = 0;
-        for (int k = 0; k < per; ++k) {
-            S.gpre[k] = acc;
-            acc += p.nblk[w0 + k];
-        }
-        S.gpre[per] = acc;
-    }
-    if (tid < kQ) S.cur[tid] = 0u;
-    __syncthreads();
-    const int64_t tb = S.gpre[per];
-    for (int64_t u0 = (int64_t)wave * 64; u0 < tb; u0 += kEmitWaves * 64) {
-        const int64_t u = u0 + lane;
-        int64_t start = 0;
-        uint32_t len = 0;
-        if (u < tb) {
-            int lo = 0, hi = per;  // emit workgroup of unit u: largest k with gpre[k] <= u
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (S.gpre[mid] <= u) lo = mid;
-                else hi = mid;
-            }
-            const int64_t gid = p.wg_dir[w0 + lo] + (u - S.gpre[lo]);
-            const uint32_t a = p.blk_hdr[(size_t)gid * kHdr + q1];
-            const uint32_t e = p.blk_hdr[(size_t)gid * kHdr + q1 + 1];
-            start = p.blk_start[gid] + a;
-            len = e - a;
-        }
-        // the chunk's 64 runs, kR at a time: the wave loads the runs' records
-        // cooperatively (runs average kBlkRecs / kQ records), kR loads in flight
-        constexpr int kR = 8;
-        for (int i = 0; i < 64; i += kR) {
-            int64_t st[kR];
-            uint32_t ln[kR];
-            uint32_t lm = 0;
-#pragma unroll
-            for (int k = 0; k < kR; ++k) {
-                st[k] = rdlane_i64(start, i + k);
-                ln[k] = (uint32_t)__builtin_amdgcn_readlane((int)len, i + k);
-                lm = ln[k] > lm ? ln[k] : lm;
-            }
-            for (uint32_t j = lane; j < ((lm + 63u) & ~63u); j += 64) {
-                uint64_t r[kR];
-#pragma unroll
-                for (int k = 0; k < kR; ++k) r[k] = j < ln[k] ? p.rec[st[k] + j] : 0ull;
-#pragma unroll
-                for (int k = 0; k < kR; ++k) {
-                    if (j < ln[k]) {
-                        const uint32_t q2 = q2_of(r[k], p.cb);
-                        const uint32_t at =
-                            __hip_atomic_fetch_add(&S.cur[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        p.rec2[p.p2off[(q1 * kQ + q2) * kSplits + s] + at] = r[k];
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// distinct (kl, count) out: bucket b writes its entries from boff[b] on (it
-// has at most as many as records), through a workgroup-local counter -- one
-// global counter for every bucket's appends would serialise ~0.5M atomics
-// per batch on one address
-__device__ __forceinline__ void out_append(const PartParams& p, uint32_t* n_out, int64_t base, bool has, uint64_t kl,
-                                           uint32_t c, int lane) {
-    const uint64_t m = __ballot(has);
-    if (!m) return;
-    uint32_t at = 0;
-    if (lane == 0) at = __hip_atomic_fetch_add(n_out, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    at = __shfl(at, 0);
-    if (has) {
-        const int64_t o = base + at + lane_rank(m);
-        p.out_kl[o] = kl;
-        p.out_cnt[o] = c;
-    }
-}
-
-__global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t red_smem[];
-    uint64_t* keys = reinterpret_cast<uint64_t*>(red_smem);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(keys + kAggSlots);
-    uint32_t* n_out = cnt + kAggSlots;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    for (int i = tid; i < kAggSlots; i += kEmitWaves * 64) {
-        keys[i] = 0ull;
-        cnt[i] = 0u;
-    }
-    if (tid == 0) *n_out = 0u;
-    __syncthreads();
-    const int64_t beg = (int64_t)p.boff[blockIdx.x], end = (int64_t)p.boff[blockIdx.x + 1];
-    const uint64_t cmask = p.cb >= 64 ? ~0ull : ((1ull << p.cb) - 1ull);
-    constexpr int kU = 8;  // records per lane in flight; their probes advance together
-    for (int64_t i00 = beg + (int64_t)wave * 64 * kU; i00 < end; i00 += kEmitWaves * 64 * kU) {
-        uint64_t kl[kU];
-        uint32_t c[kU], slot[kU];
-        bool pend[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int64_t i = i00 + 64 * u + lane;
-            const uint64_t r = i < end ? p.rec2[i] : 0ull;
-            pend[u] = i < end;
-            kl[u] = r >> p.cb;  // never 0 for a record: the sentinel bit
-            c[u] = (uint32_t)(r & cmask);
-            slot[u] = (uint32_t)(((uint64_t)(uint32_t)mix64(kl[u]) * kAggSlots) >> 32);
-        }
-        for (int t = 0; t < 32; ++t) {
-            uint64_t cur[kU];
-#pragma unroll
-            for (int u = 0; u < kU; ++u) cur[u] = pend[u] ? keys[slot[u]] : 0ull;  // read first: most records find their key
-            bool any = false;
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                if (!pend[u]) continue;
-                if (cur[u] == 0ull) {
-                    const unsigned long long old =
-                        atomicCAS(reinterpret_cast<unsigned long long*>(&keys[slot[u]]), 0ull, (unsigned long long)kl[u]);
-                    cur[u] = old == 0ull ? kl[u] : old;
-                }
-                if (cur[u] == kl[u]) {
-                    __hip_atomic_fetch_add(&cnt[slot[u]], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    pend[u] = false;
-                } else {
-                    slot[u] = (slot[u] + 1u) & (kAggSlots - 1u);
-                    any = true;
-                }
-            }
-            if (!__ballot(any)) break;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u)  // no LDS room: the record goes out as it is
-            out_append(p, n_out, beg, pend[u], kl[u], c[u], lane);
-    }
-    __syncthreads();
-    for (int i0 = wave * 64; i0 < kAggSlots; i0 += kEmitWaves * 64) {
-        const int i = i0 + lane;
-        const uint64_t k = keys[i];
-        out_append(p, n_out, beg, k != 0ull, k, cnt[i], lane);
-    }
-    __syncthreads();
-    if (tid == 0) p.nout[blockIdx.x] = *n_out;
-}
-
-// entry i of the batch (buckets' outputs in bucket order, prefix epre) ->
-// bucket b = the last with epre[b] <= i, stored at boff[b] + (i - epre[b])
-__global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const CountParams c, int64_t n) {
-    __shared__ uint64_t pre[kQ * kQ + 1];
-    for (int i = threadIdx.x; i <= kQ * kQ; i += blockDim.x) pre[i] = p.epre[i];
-    __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int lo = 0;
-#pragma unroll
-    for (int step = 2048; step >= 1; step >>= 1)
-        if (lo + step <= kQ * kQ && pre[lo + step] <= (uint64_t)i) lo += step;
-    const int64_t at = (int64_t)p.boff[lo] + (i - (int64_t)pre[lo]);
-    const uint64_t kl = p.out_kl[at];
-    add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out_cnt[at]);
-}
-
-}  // namespace
-
-size_t emit_lds_bytes() { return sizeof(EmitLds); }
-size_t reduce_lds_bytes() { return (size_t)kAggSlots * (sizeof(uint64_t) + sizeof(uint32_t)) + 16; }
-
-hipError_t fit2_prepare() {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&emit_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)emit_lds_bytes());
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&reduce_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes());
-    return e;
-}
-
-hipError_t launch_emit(const PartParams& p, hipStream_t stream) {
-    hipLaunchKernelGGL(emit_kernel, dim3(p.grid_a), dim3(kEmitWaves * 64), emit_lds_bytes(), stream, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_part2(const PartParams& p, hipStream_t stream) {
-    hipLaunchKernelGGL(part2_kernel, dim3(kQ * kSplits), dim3(kEmitWaves * 64), 0, stream, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_reduce(const PartParams& p, hipStream_t stream) {
-    hipLaunchKernelGGL(reduce_kernel, dim3(kQ * kQ), dim3(kEmitWaves * 64), reduce_lds_bytes(), stream, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_merge(const PartParams& p, const CountParams& c, int64_t n, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, stream, p, c, n);
-    return hipGetLastError();
-}
-
-}  // namespace ldgpu
-
-// ---------------------------------------------------------------------------
 // FIT of gram lengths 8..15 (computeGrams + reduceGrams, LanguageDetector.
 // scala:25-66, for windows too long for a one-word key).  Such windows count
 // into a table of two-word keys of their own -- lo = bytes 0..7, hi = bytes
@@ -1290,29 +665,40 @@ constexpr uint64_t kWidePending = 1ull << 63;  // never set in hi (klen <= 15 in
 
 __device__ __forceinline__ uint64_t wide_slot(uint64_t lo, uint64_t hi) { return mix64(lo ^ mix64(hi)); }
 
-// find-or-insert of (lo, hi); -1 only if every slot is taken
+// find-or-insert of (lo, hi); -1 if every slot is taken (or, never expected,
+// a slot stays "being written" for 2^22 looks).  No lane ever waits inside a
+// branch: a lane that wins a slot publishes lo and hi in the same pass of the
+// loop body, in straight-line code that every lane passes before the loop's
+// exits, and a lane that meets another insert in flight looks at the same
+// slot again on its next pass -- so the wave makes progress whatever order
+// the compiler gives the divergent paths (a winner and a waiter may share a
+// wave: a wait nested in the loser's branch could run before the winner's
+// stores and never end).
 __device__ __forceinline__ int64_t wide_find_or_insert(const WideCountParams& p, uint64_t lo, uint64_t hi,
                                                        bool& new_key) {
     uint64_t s = wide_slot(lo, hi) >> p.shift;
-    for (uint64_t probe = 0; probe <= p.mask; ++probe) {
+    uint64_t probes = 0;
+    for (uint32_t pass = 0; pass < (1u << 22); ++pass) {
         uint64_t h = __hip_atomic_load(&p.khi[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        bool won = false;
         if (h == kEmpty) {
             const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&p.khi[s]), 0ull,
                                                      (unsigned long long)(hi | kWidePending));
-            if (old == 0ull) {
-                __hip_atomic_store(&p.klo[s], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&p.khi[s], hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                new_key = true;
-                return (int64_t)s;
-            }
-            h = old;
+            won = old == 0ull;
+            h = won ? (hi | kWidePending) : old;
         }
-        // another lane's insert in flight: its lo is stored before hi is
-        // published (a lane of this wave wrote it above, before this loop)
-        while (h & kWidePending) h = __hip_atomic_load(&p.khi[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (h == hi && __hip_atomic_load(&p.klo[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo)
+        if (won) {  // publish: lo first, then hi without the pending bit
+            __hip_atomic_store(&p.klo[s], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&p.khi[s], hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            h = hi;
+        }
+        if (h & kWidePending) continue;  // another insert in flight: look at this slot again
+        if (h == hi && (won || __hip_atomic_load(&p.klo[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo)) {
+            new_key = won;
             return (int64_t)s;
+        }
         s = (s + 1) & p.mask;
+        if (++probes > p.mask) return -1;
     }
     return -1;
 }
@@ -1447,6 +833,807 @@ hipError_t launch_wide_compact(const WideCountParams& p, uint64_t cap, uint64_t*
     if (cap == 0) return hipSuccess;
     hipLaunchKernelGGL(wide_compact_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, stream, p, cap, out_lo,
                        out_hi, out_counts, out_n);
+    return hipGetLastError();
+}
+
+}  // namespace ldgpu
+
+// ---------------------------------------------------------------------------
+// FIT v3: language-grouped LDS aggregation + radix-partitioned record
+// aggregation -- the north star's "LDS-privatised histogram, then a sort /
+// segmented-reduce merge into HBM count tables" for every gram length (1..15)
+// and language count (<= 4096).  The global table sees one add per distinct
+// (gram, language) per bucket and batch instead of one device-scope atomic
+// per window.  Per batch of documents:
+//   emit    the host orders the batch's documents by language and gives each
+//           workgroup documents of ONE language, so the workgroup's LDS tables
+//           aggregate across its documents: 1-byte windows in a 256-bin
+//           histogram, 2- and 3-byte windows in an 8192-slot hash (a window
+//           that finds no slot within the probe limit becomes a record);
+//           longer windows become records.  Records gather in a workgroup LDS
+//           block; a full block is counting-sorted by q1 in LDS and written
+//           once, coalesced, with a header of q1 starts.  At the end the tables
+//           go out as counted records.  The workgroup also histograms (q1, q2).
+//   part2   each q1 run is re-scattered by q2 to exact, host-scanned offsets --
+//           4096 contiguous buckets.
+//   reduce  one workgroup per bucket sums equal (gram, language) records in an
+//           LDS hash and writes (key, count) entries (a record the hash cannot
+//           place goes out as it is: the merge adds it all the same).
+//   merge   each entry is one find-or-insert + one u64 add in the table.
+// Integer sums are order-independent and nothing is dropped: counts are
+// bit-exact whatever the schedule and whatever the LDS tables absorbed.
+namespace ldgpu {
+namespace {
+
+__device__ __forceinline__ bool emit_ablated(const PartParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+constexpr uint64_t kCntMask = (1ull << kCntBits) - 1ull;
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+
+// ---- record forms (ldgpu_internal.h).  lo = the window's first min(klen, 8)
+// bytes, hi = bytes 8.. (klen > 8), both masked to the window.
+template <int K>
+struct Rec {
+    uint64_t w[K];
+};
+
+template <int K>
+__device__ __forceinline__ Rec<K> make_rec(uint64_t lo, uint64_t hi, int klen, uint32_t lang, uint64_t c,
+                                           const PartParams& p) {
+    Rec<K> r;
+    if constexpr (K == 1) {
+        const uint64_t sent = (1ull << (8 * klen)) | lo;
+        r.w[0] = (((sent << p.lb) | (uint64_t)lang) << p.cb) | c;
+    } else if constexpr (K == 2) {
+        r.w[0] = lo | ((uint64_t)klen << 56);
+        r.w[1] = ((uint64_t)lang << kCntBits) | c;
+    } else {
+        if (klen <= kMaxGram) {
+            r.w[0] = lo | ((uint64_t)klen << 56);
+            r.w[1] = 0ull;
+        } else {
+            r.w[0] = lo;
+            r.w[1] = hi | ((uint64_t)klen << 56);
+        }
+        r.w[2] = ((uint64_t)lang << kCntBits) | c;
+    }
+    return r;
+}
+
+template <int K>
+__device__ __forceinline__ uint64_t rec_count(const Rec<K>& r, uint32_t cb) {
+    if constexpr (K == 1) return r.w[0] & (cb >= 64 ? ~0ull : ((1ull << cb) - 1ull));
+    else return r.w[K - 1] & kCntMask;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t rec_lang(const Rec<K>& r, uint32_t lb, uint32_t cb) {
+    if constexpr (K == 1) return (uint32_t)((r.w[0] >> cb) & ((1ull << lb) - 1ull));
+    else return (uint32_t)(r.w[K - 1] >> kCntBits);
+}
+
+// route hash of the record's (gram, language) pair
+template <int K>
+__device__ __forceinline__ uint64_t rec_hash(const Rec<K>& r, uint32_t cb) {
+    if constexpr (K == 1) return mix64(r.w[0] >> cb);
+    else if constexpr (K == 2) return mix64(r.w[0] + (r.w[1] >> kCntBits) * kGolden);
+    else return mix64(r.w[0] ^ mix64(r.w[1] + (r.w[2] >> kCntBits) * kGolden));
+}
+
+template <int K>
+__device__ __forceinline__ bool rec_same_key(const Rec<K>& a, const Rec<K>& b, uint32_t cb) {
+    if constexpr (K == 1) return (a.w[0] >> cb) == (b.w[0] >> cb);
+    else if constexpr (K == 2) return a.w[0] == b.w[0] && (a.w[1] >> kCntBits) == (b.w[1] >> kCntBits);
+    else return a.w[0] == b.w[0] && a.w[1] == b.w[1] && (a.w[2] >> kCntBits) == (b.w[2] >> kCntBits);
+}
+
+template <int K>
+__device__ __forceinline__ Rec<K> load_rec(const uint64_t* base, int64_t i) {
+    Rec<K> r;
+#pragma unroll
+    for (int k = 0; k < K; ++k) r.w[k] = base[i * K + k];
+    return r;
+}
+
+template <int K>
+__device__ __forceinline__ void store_rec(uint64_t* base, int64_t i, const Rec<K>& r) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) base[i * K + k] = r.w[k];
+}
+
+// the packed key (ldgpu_common.h) of a K = 1 record's kl = record >> cb
+__device__ __forceinline__ uint64_t kl_key(uint64_t kl, uint32_t lb) {
+    const uint64_t sent = kl >> lb;
+    const int klen = (63 - __builtin_clzll(sent)) >> 3;
+    return (sent ^ (1ull << (8 * klen))) | ((uint64_t)klen << 56);
+}
+
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations
+// (lgkmcnt), not for its outstanding global loads -- __syncthreads() would
+// drain those too, and emit keeps the next step's window loads in flight
+// across the round barriers.  Global stores before it need not be visible to
+// the other waves (each flushed block is read by the next kernel only).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// wave inclusive scan (64 lanes)
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+constexpr int kT23Probe = 16;
+
+template <int K>
+struct EmitLds {
+    uint64_t blk[kBlkWords];
+    uint8_t bq1[emit_blk_recs(K)];  // q1 of each block record (computed once per record)
+    uint32_t hist2[kQ * kQ];
+    uint32_t h1[256];
+    uint32_t tkey[kT23];   // 2-/3-byte grams: bytes | klen << 24 (0: empty)
+    uint32_t tcnt[kT23];
+    uint32_t pcnt[kQ];
+    uint32_t pfill[kQ];
+    uint32_t pstart[kQ + 1];
+    uint32_t blk_n;
+    uint32_t active;
+    uint32_t next_doc;
+};
+
+enum { kNextDoc = 0, kWin = 1, kDone = 2 };
+
+// one wave's position in its current document (wave-uniform)
+template <int K>
+struct WaveState {
+    static constexpr int kW = K == 3 ? 5 : 3;  // dwords per window position
+    int64_t b, len, p0;
+    int32_t gi, phase;
+    bool pf;                       // pw holds the words of the next WIN step (issued a round early)
+    uint32_t pw[emit_sub(K)][kW];
+};
+
+// append the lanes' records (sub per lane) to the workgroup block with one
+// reservation (the round bound keeps it from overflowing); every lane of the
+// wave must be active
+template <int K, int SUB>
+__device__ __forceinline__ void emit_recs(EmitLds<K>& S, const bool (&has)[SUB], const Rec<K> (&r)[SUB],
+                                          const PartParams& p, int lane) {
+    uint64_t m[SUB];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < SUB; ++k) {
+        m[k] = __ballot(has[k]);
+        tot += (uint32_t)__popcll(m[k]);
+    }
+    if (!tot) return;
+    uint32_t base = 0;
+    if (lane == 0) base = __hip_atomic_fetch_add(&S.blk_n, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __shfl(base, 0);
+#pragma unroll
+    for (int k = 0; k < SUB; ++k) {
+        if (has[k]) {
+            const uint32_t at = base + lane_rank(m[k]);
+            store_rec<K>(S.blk, at, r[k]);
+            const uint64_t h = rec_hash<K>(r[k], p.cb);
+            const uint32_t q1 = (uint32_t)(h >> (64 - kQBits));
+            const uint32_t q2 = (uint32_t)(h >> (64 - 2 * kQBits)) & (kQ - 1);
+            S.bq1[at] = (uint8_t)q1;
+            __hip_atomic_fetch_add(&S.pcnt[q1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&S.hist2[q1 * kQ + q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        base += (uint32_t)__popcll(m[k]);
+    }
+}
+
+__device__ __forceinline__ uint32_t ld_dw3(const uint32_t* w, int64_t i, int64_t last) {
+    return w[i < last ? i : last];
+}
+
+// the dwords of the positions of a WIN step at (gi, p0): 3 per position for
+// windows of <= 7 bytes, 5 for wide ones
+template <int K>
+__device__ __forceinline__ void window_loads(const PartParams& p, const WaveState<K>& w, int lane,
+                                             uint32_t (&pw)[emit_sub(K)][WaveState<K>::kW]) {
+    constexpr int SUB = emit_sub(K);
+    const int n = p.G[w.gi];
+    const int64_t nwin = n_windows(w.len, n);
+    const int klen = w.len < n ? (int)w.len : n;
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+#pragma unroll
+    for (int k = 0; k < SUB; ++k) {
+        const int64_t pos = w.p0 + 64 * k + lane;
+        const int64_t a = w.b + (pos < nwin ? pos : 0);
+        const int64_t i = a >> 2;
+        pw[k][0] = ld_dw3(W, i, p.last_dword);
+        pw[k][1] = ld_dw3(W, i + 1, p.last_dword);
+        pw[k][2] = klen > 4 ? ld_dw3(W, i + 2, p.last_dword) : 0u;
+        if constexpr (K == 3) {
+            pw[k][3] = klen > 8 ? ld_dw3(W, i + 3, p.last_dword) : 0u;
+            pw[k][4] = klen > 12 ? ld_dw3(W, i + 4, p.last_dword) : 0u;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t byte_mask(int n) { return n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull); }
+
+// One step of a wave: <= 64 sub windows, <= 64 sub records.  The positions'
+// loads are all issued before any is used.
+template <int K>
+__device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, WaveState<K>& w, int lane, int64_t d0,
+                                          int64_t d1, uint32_t lang) {
+    constexpr int SUB = emit_sub(K);
+    if (w.phase == kNextDoc) {
+        uint32_t k = 0;
+        if (lane == 0) k = __hip_atomic_fetch_add(&S.next_doc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int64_t i = d0 + (int64_t)__shfl(k, 0);
+        if (i >= d1) {
+            w.phase = kDone;
+            if (lane == 0) __hip_atomic_fetch_sub(&S.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+        const int64_t d = p.perm[i];
+        const int64_t b = p.offsets[d];
+        const int64_t len = p.offsets[d + 1] - b;
+        if (len <= 0 || p.nG == 0) return;
+        w.b = b;
+        w.len = len;
+        w.gi = 0;
+        w.p0 = 0;
+        w.pf = false;
+        w.phase = kWin;
+        // fall through: the document's first windows in this step
+    }
+    bool has[SUB];
+    Rec<K> r[SUB];
+#pragma unroll
+    for (int k = 0; k < SUB; ++k) has[k] = false;
+    const int n = p.G[w.gi];
+    const int64_t nwin = n_windows(w.len, n);
+    const int klen = w.len < n ? (int)w.len : n;
+    if (!w.pf) window_loads<K>(p, w, lane, w.pw);
+    w.pf = false;
+    uint64_t lo[SUB], hi[SUB];
+    bool valid[SUB];
+#pragma unroll
+    for (int k = 0; k < SUB; ++k) {
+        const int64_t pos = w.p0 + 64 * k + lane;
+        valid[k] = pos < nwin;
+        const uint32_t sh = (uint32_t)((w.b + (valid[k] ? pos : 0)) & 3);
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(w.pw[k][1], w.pw[k][0], sh);
+        const uint32_t a1 = __builtin_amdgcn_alignbyte(w.pw[k][2], w.pw[k][1], sh);
+        lo[k] = (((uint64_t)a1 << 32) | a0) & byte_mask(klen);
+        hi[k] = 0;
+        if constexpr (K == 3) {
+            if (klen > 8) {
+                const uint32_t a2 = __builtin_amdgcn_alignbyte(w.pw[k][3], w.pw[k][2], sh);
+                const uint32_t a3 = __builtin_amdgcn_alignbyte(w.pw[k][4], w.pw[k][3], sh);
+                hi[k] = (((uint64_t)a3 << 32) | a2) & byte_mask(klen - 8);
+            }
+        }
+    }
+    if (klen == 1) {
+#pragma unroll
+        for (int k = 0; k < SUB; ++k)
+            if (valid[k])
+                __hip_atomic_fetch_add(&S.h1[(uint32_t)lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (klen <= 3 && !emit_ablated(p, 1)) {
+        // the sub positions probe together: one LDS round trip per probe step
+        // for all of them (most find their key at once)
+        uint32_t key[SUB], slot[SUB];
+        bool pend[SUB];
+#pragma unroll
+        for (int k = 0; k < SUB; ++k) {
+            key[k] = (uint32_t)lo[k] | ((uint32_t)klen << 24);
+            slot[k] = (key[k] * 0x9E3779B1u) >> (32 - 13);  // kT23 = 2^13
+            pend[k] = valid[k];
+        }
+        for (int t = 0; t < kT23Probe; ++t) {
+            uint32_t cur[SUB];
+#pragma unroll
+            for (int k = 0; k < SUB; ++k) cur[k] = pend[k] ? S.tkey[slot[k]] : 0u;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < SUB; ++k) {
+                if (!pend[k]) continue;
+                if (cur[k] == 0u) {
+                    const uint32_t old = atomicCAS(&S.tkey[slot[k]], 0u, key[k]);
+                    cur[k] = old == 0u ? key[k] : old;
+                }
+                if (cur[k] == key[k]) {
+                    __hip_atomic_fetch_add(&S.tcnt[slot[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pend[k] = false;
+                } else {
+                    slot[k] = (slot[k] + 1u) & (kT23 - 1u);
+                    any = true;
+                }
+            }
+            if (!__ballot(any)) break;
+        }
+#pragma unroll
+        for (int k = 0; k < SUB; ++k) {
+            if (pend[k]) {  // no slot: the window goes out as a record
+                has[k] = true;
+                r[k] = make_rec<K>(lo[k], 0, klen, lang, 1, p);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SUB; ++k) {
+            has[k] = valid[k];
+            r[k] = make_rec<K>(lo[k], hi[k], klen, lang, 1, p);
+        }
+    }
+    if (emit_ablated(p, 4)) {
+#pragma unroll
+        for (int k = 0; k < SUB; ++k) has[k] = false;
+    }
+    emit_recs<K, SUB>(S, has, r, p, lane);
+    w.p0 += 64 * SUB;
+    if (w.p0 >= nwin) {
+        w.gi += 1;
+        w.p0 = 0;
+        if (w.gi >= p.nG) w.phase = kNextDoc;
+    }
+    if (w.phase == kWin) {  // the next step's loads fly across the round barrier
+        window_loads<K>(p, w, lane, w.pw);
+        w.pf = true;
+    }
+}
+
+// Write the block: counting sort by q1 in LDS, scattered stores into the
+// block's own contiguous range (the lines fill in L2 and leave whole).
+template <int K>
+__device__ __forceinline__ void flush_block(const PartParams& p, EmitLds<K>& S, uint32_t n, int64_t rb, int64_t gid,
+                                            int tid) {
+    if (tid < 64) {
+        const uint32_t v = S.pcnt[tid];
+        const uint32_t inc = wave_inclusive_scan(v, tid);
+        S.pstart[tid] = inc - v;
+        S.pfill[tid] = inc - v;
+        S.pcnt[tid] = 0u;
+        if (tid == 63) S.pstart[kQ] = inc;
+    }
+    lds_barrier();
+    for (uint32_t i = tid; i < n; i += kEmitWaves * 64) {
+        const Rec<K> r = load_rec<K>(S.blk, i);
+        const uint32_t at = __hip_atomic_fetch_add(&S.pfill[S.bq1[i]], 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!emit_ablated(p, 2)) store_rec<K>(p.rec, rb + at, r);
+    }
+    if (tid <= kQ) p.blk_hdr[(size_t)gid * kHdr + tid] = S.pstart[tid];
+    if (tid == 0) {
+        p.blk_start[gid] = rb;
+        S.blk_n = 0u;
+    }
+    lds_barrier();
+}
+
+template <int K>
+__global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t emit_smem[];
+    EmitLds<K>& S = *reinterpret_cast<EmitLds<K>*>(emit_smem);
+    constexpr uint32_t kThresh = (uint32_t)(emit_blk_recs(K) - emit_round_recs(K));
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int bid = blockIdx.x;
+    const int64_t d0 = p.wg_doc[bid], d1 = p.wg_doc[bid + 1];
+    const int64_t rbase = p.wg_rec[bid], dbase = p.wg_dir[bid];
+    const uint32_t lang = (uint32_t)p.wg_lang[bid];
+    for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64) S.hist2[i] = 0u;
+    for (int i = tid; i < 256; i += kEmitWaves * 64) S.h1[i] = 0u;
+    for (int i = tid; i < kT23; i += kEmitWaves * 64) S.tkey[i] = S.tcnt[i] = 0u;
+    if (tid < kQ) S.pcnt[tid] = 0u;
+    if (tid == 0) {
+        S.blk_n = 0u;
+        S.active = kEmitWaves;
+        S.next_doc = 0u;
+    }
+    lds_barrier();
+    WaveState<K> w{};
+    w.phase = d0 < d1 ? kNextDoc : kDone;
+    if (w.phase == kDone && lane == 0)
+        __hip_atomic_fetch_sub(&S.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int64_t written = 0;
+    int64_t nb = 0;
+    lds_barrier();
+    for (;;) {
+        // a round: every live wave takes one step (<= emit_round_recs records,
+        // so the block, flushed above kThresh, never overflows)
+        if (w.phase != kDone) emit_step<K>(p, S, w, lane, d0, d1, lang);
+        lds_barrier();
+        const uint32_t n = S.blk_n;
+        const uint32_t act = S.active;
+        lds_barrier();  // every thread has read n / act before the next round moves them
+        if (n > kThresh) {
+            flush_block<K>(p, S, n, rbase + written, dbase + nb, tid);
+            written += n;
+            ++nb;
+        }
+        if (act == 0u) break;
+    }
+    // the workgroup tables go out as counted records, one slot per thread per
+    // pass (<= 1024 records: a pass fits a round's bound); K = 1 counts beyond
+    // the record's count field go straight to the global table
+    const uint64_t cmax = K == 1 ? (p.cb >= 64 ? ~0ull : ((1ull << p.cb) - 1ull)) : kCntMask;
+    for (int base = 0; base < 256 + kT23; base += kEmitWaves * 64) {
+        const int s = base + tid;
+        uint32_t c = 0, key = 0;
+        if (s < 256) {
+            c = S.h1[s];
+            key = (uint32_t)s | (1u << 24);
+        } else if (s < 256 + kT23) {
+            c = S.tcnt[s - 256];
+            key = S.tkey[s - 256];
+        }
+        bool has[1] = {false};
+        Rec<K> r[1];
+        if (c) {
+            const int klen = (int)(key >> 24);
+            const uint64_t bytes = key & 0xffffffu;
+            if ((uint64_t)c <= cmax) {
+                has[0] = true;
+                r[0] = make_rec<K>(bytes, 0, klen, lang, c, p);
+            } else {
+                add_count(p.direct, bytes | ((uint64_t)klen << 56), (int)lang, (unsigned long long)c);
+            }
+        }
+        if (emit_ablated(p, 4)) has[0] = false;
+        emit_recs<K, 1>(S, has, r, p, lane);
+        lds_barrier();
+        const uint32_t n = S.blk_n;
+        lds_barrier();
+        const bool last = base + kEmitWaves * 64 >= 256 + kT23;
+        if (n > kThresh || (last && n > 0)) {
+            flush_block<K>(p, S, n, rbase + written, dbase + nb, tid);
+            written += n;
+            ++nb;
+        }
+    }
+    if (tid == 0) p.nblk[bid] = (int32_t)nb;
+    const int grp = bid / (p.grid_a / kSplits);
+    for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64)
+        if (S.hist2[i]) atomicAdd(&p.cnt3[i * kSplits + grp], S.hist2[i]);
+}
+
+struct Part2Lds {
+    uint32_t cur[kQ];
+    int32_t gpre[257];
+};
+
+__device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) {
+    return (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32));
+}
+
+// q1 bucket of one emit group -> its q2 sub-buckets (per-group units of
+// part2: blocks of the group's workgroups, load-balanced over the waves)
+template <int K>
+__global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams p) {
+    __shared__ Part2Lds S;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t q1 = blockIdx.x / kSplits;
+    const int s = blockIdx.x % kSplits;
+    const int per = p.grid_a / kSplits;
+    const int w0 = s * per;
+    if (tid == 0) {
+        int32_t acc = 0;
+        for (int k = 0; k < per; ++k) {
+            S.gpre[k] = acc;
+            acc += p.nblk[w0 + k];
+        }
+        S.gpre[per] = acc;
+    }
+    if (tid < kQ) S.cur[tid] = 0u;
+    __syncthreads();
+    const int64_t tb = S.gpre[per];
+    for (int64_t u0 = (int64_t)wave * 64; u0 < tb; u0 += kEmitWaves * 64) {
+        const int64_t u = u0 + lane;
+        int64_t start = 0;
+        uint32_t len = 0;
+        if (u < tb) {
+            int lo = 0, hi = per;  // emit workgroup of unit u: largest k with gpre[k] <= u
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (S.gpre[mid] <= u) lo = mid;
+                else hi = mid;
+            }
+            const int64_t gid = p.wg_dir[w0 + lo] + (u - S.gpre[lo]);
+            const uint32_t a = p.blk_hdr[(size_t)gid * kHdr + q1];
+            const uint32_t e = p.blk_hdr[(size_t)gid * kHdr + q1 + 1];
+            start = p.blk_start[gid] + a;
+            len = e - a;
+        }
+        // the chunk's 64 runs, kR at a time: the wave loads the runs' records
+        // cooperatively (runs average emit_blk_recs / kQ records), kR loads in flight
+        constexpr int kR = K == 1 ? 8 : 4;
+        for (int i = 0; i < 64; i += kR) {
+            int64_t st[kR];
+            uint32_t ln[kR];
+            uint32_t lm = 0;
+#pragma unroll
+            for (int k = 0; k < kR; ++k) {
+                st[k] = rdlane_i64(start, i + k);
+                ln[k] = (uint32_t)__builtin_amdgcn_readlane((int)len, i + k);
+                lm = ln[k] > lm ? ln[k] : lm;
+            }
+            for (uint32_t j = lane; j < ((lm + 63u) & ~63u); j += 64) {
+                Rec<K> r[kR];
+#pragma unroll
+                for (int k = 0; k < kR; ++k) {
+                    if (j < ln[k]) r[k] = load_rec<K>(p.rec, st[k] + j);
+                }
+#pragma unroll
+                for (int k = 0; k < kR; ++k) {
+                    if (j < ln[k]) {
+                        const uint32_t q2 = (uint32_t)(rec_hash<K>(r[k], p.cb) >> (64 - 2 * kQBits)) & (kQ - 1);
+                        const uint32_t at =
+                            __hip_atomic_fetch_add(&S.cur[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        store_rec<K>(p.rec2, (int64_t)p.p2off[(q1 * kQ + q2) * kSplits + s] + at, r[k]);
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// reduce: LDS hash slots per bucket (K u64 key words + a u32 count each, within
+// one workgroup's LDS)
+template <int K>
+constexpr int agg_slots() {
+    return K == 1 ? 8192 : (K == 2 ? 6144 : 4096);
+}
+
+// entries out: bucket b writes from boff[b] on (it has at most as many as
+// records), through a workgroup-local counter -- one global counter for every
+// bucket's appends would serialise ~0.5M atomics per batch on one address.
+// An entry is out_words(K) words: K = 1 (kl, count) -- a bucket's sum may
+// exceed a record's count bits --, K >= 2 the record form with the sum in its
+// count field.
+template <int K>
+__device__ __forceinline__ void out_append(const PartParams& p, uint32_t* n_out, int64_t base, bool has,
+                                           const Rec<K>& r, uint64_t c, int lane) {
+    const uint64_t m = __ballot(has);
+    if (!m) return;
+    uint32_t at = 0;
+    if (lane == 0) at = __hip_atomic_fetch_add(n_out, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    at = __shfl(at, 0);
+    if (!has) return;
+    const int64_t o = base + at + lane_rank(m);
+    if constexpr (K == 1) {
+        p.out[2 * o] = r.w[0] >> p.cb;
+        p.out[2 * o + 1] = c;
+    } else {
+        Rec<K> e = r;
+        e.w[K - 1] = (e.w[K - 1] & ~kCntMask) | c;
+        store_rec<K>(p.out, o, e);
+    }
+}
+
+// LDS claim protocol for keys of several words (K >= 2): a slot is claimed
+// by a CAS of its tag word from 0 to kBusy, the claimer stores the key words
+// and then the tag (a nonzero hash of the key); a reader compares the key words
+// only after it has seen the tag.  A reader that meets kBusy, or a tag that
+// matches while the key differs, probes on: at worst one key gets two slots
+// (two entries out, summed by the merge).
+constexpr uint32_t kBusy = 1u;
+
+template <int K>
+__global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartParams p) {
+    constexpr int N = agg_slots<K>();
+    extern __shared__ __attribute__((aligned(16))) uint8_t red_smem[];
+    // K = 1: keys[N] (kl, 0 = empty) + cnt[N]; K >= 2: kw[N][K - 1] key words,
+    // lang[N], tag[N], cnt[N]
+    uint64_t* kw = reinterpret_cast<uint64_t*>(red_smem);
+    uint32_t* lg = reinterpret_cast<uint32_t*>(kw + (size_t)N * (K == 1 ? 1 : K - 1));
+    uint32_t* tag = lg + (K == 1 ? 0 : N);
+    uint32_t* cnt = tag + (K == 1 ? 0 : N);
+    uint32_t* n_out = cnt + N;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    for (int i = tid; i < N; i += kEmitWaves * 64) {
+        cnt[i] = 0u;
+        if (K == 1) kw[i] = 0ull;
+        else tag[i] = 0u;
+    }
+    if (tid == 0) *n_out = 0u;
+    __syncthreads();
+    const int64_t beg = (int64_t)p.boff[blockIdx.x], end = (int64_t)p.boff[blockIdx.x + 1];
+    constexpr int kU = K == 1 ? 8 : 4;  // records per lane in flight; their probes advance together
+    for (int64_t i00 = beg + (int64_t)wave * 64 * kU; i00 < end; i00 += kEmitWaves * 64 * kU) {
+        Rec<K> r[kU];
+        uint32_t c[kU], slot[kU], tg[kU];
+        bool pend[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i00 + 64 * u + lane;
+            pend[u] = i < end;
+            if (pend[u]) r[u] = load_rec<K>(p.rec2, i);
+            else r[u] = Rec<K>{};
+            c[u] = (uint32_t)rec_count<K>(r[u], p.cb);
+            const uint64_t h = rec_hash<K>(r[u], p.cb);
+            slot[u] = (uint32_t)(((uint64_t)(uint32_t)h * (uint64_t)N) >> 32);
+            tg[u] = (uint32_t)(h >> 32) | 2u;  // never 0 (empty) or kBusy
+        }
+        for (int t = 0; t < 32; ++t) {
+            bool any = false;
+            if constexpr (K == 1) {
+                uint64_t cur[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) cur[u] = pend[u] ? kw[slot[u]] : 0ull;  // read first: most find their key
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    if (!pend[u]) continue;
+                    const uint64_t kl = r[u].w[0] >> p.cb;  // never 0 for a record: the sentinel bit
+                    if (cur[u] == 0ull) {
+                        const unsigned long long old =
+                            atomicCAS(reinterpret_cast<unsigned long long*>(&kw[slot[u]]), 0ull, (unsigned long long)kl);
+                        cur[u] = old == 0ull ? kl : old;
+                    }
+                    if (cur[u] == kl) {
+                        __hip_atomic_fetch_add(&cnt[slot[u]], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        pend[u] = false;
+                    } else {
+                        slot[u] = slot[u] + 1u == (uint32_t)N ? 0u : slot[u] + 1u;
+                        any = true;
+                    }
+                }
+            } else {
+                uint32_t cur[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) cur[u] = pend[u] ? tag[slot[u]] : 0u;
+                bool won[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    won[u] = false;
+                    if (pend[u] && cur[u] == 0u) {
+                        const uint32_t old = atomicCAS(&tag[slot[u]], 0u, kBusy);
+                        won[u] = old == 0u;
+                        cur[u] = won[u] ? kBusy : old;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    if (!won[u]) continue;  // a claimed slot: key words, then the tag
+#pragma unroll
+                    for (int k = 0; k < K - 1; ++k) kw[(size_t)slot[u] * (K - 1) + k] = r[u].w[k];
+                    lg[slot[u]] = (uint32_t)(r[u].w[K - 1] >> kCntBits);
+                    __hip_atomic_fetch_add(&cnt[slot[u]], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&tag[slot[u]], tg[u], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pend[u] = false;
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    if (!pend[u]) continue;
+                    bool same = cur[u] == tg[u];
+                    if (same) {
+#pragma unroll
+                        for (int k = 0; k < K - 1; ++k) same &= kw[(size_t)slot[u] * (K - 1) + k] == r[u].w[k];
+                        same &= lg[slot[u]] == (uint32_t)(r[u].w[K - 1] >> kCntBits);
+                    }
+                    if (same) {
+                        __hip_atomic_fetch_add(&cnt[slot[u]], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        pend[u] = false;
+                    } else {
+                        slot[u] = slot[u] + 1u == (uint32_t)N ? 0u : slot[u] + 1u;
+                        any = true;
+                    }
+                }
+            }
+            if (!__ballot(any)) break;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)  // no LDS room: the record goes out as it is
+            out_append<K>(p, n_out, beg, pend[u], r[u], c[u], lane);
+    }
+    __syncthreads();
+    for (int i0 = wave * 64; i0 < N; i0 += kEmitWaves * 64) {
+        const int i = i0 + lane;
+        Rec<K> r{};
+        bool has;
+        if constexpr (K == 1) {
+            has = kw[i] != 0ull;
+            r.w[0] = kw[i] << p.cb;  // the record form of the entry's kl (out_append shifts it back)
+        } else {
+            has = tag[i] > kBusy;
+#pragma unroll
+            for (int k = 0; k < K - 1; ++k) r.w[k] = kw[(size_t)i * (K - 1) + k];
+            r.w[K - 1] = (uint64_t)lg[i] << kCntBits;
+        }
+        out_append<K>(p, n_out, beg, has, r, cnt[i], lane);
+    }
+    __syncthreads();
+    if (tid == 0) p.nout[blockIdx.x] = *n_out;
+}
+
+// entry i of the batch (buckets' outputs in bucket order, prefix epre) ->
+// bucket b = the last with epre[b] <= i, stored at boff[b] + (i - epre[b])
+template <int K>
+__global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const CountParams c, const WideCountParams w,
+                                                     int64_t n) {
+    __shared__ uint64_t pre[kQ * kQ + 1];
+    for (int i = threadIdx.x; i <= kQ * kQ; i += blockDim.x) pre[i] = p.epre[i];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int lo = 0;
+#pragma unroll
+    for (int step = 2048; step >= 1; step >>= 1)
+        if (lo + step <= kQ * kQ && pre[lo + step] <= (uint64_t)i) lo += step;
+    const int64_t at = (int64_t)p.boff[lo] + (i - (int64_t)pre[lo]);
+    if constexpr (K == 1) {
+        const uint64_t kl = p.out[2 * at];
+        add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out[2 * at + 1]);
+    } else {
+        const Rec<K> r = load_rec<K>(p.out, at);
+        const int lang = (int)(r.w[K - 1] >> kCntBits);
+        const unsigned long long cn = r.w[K - 1] & kCntMask;
+        if (K == 3 && r.w[1] != 0ull) wide_add(w, r.w[0], r.w[1], lang, cn);
+        else add_count(c, r.w[0], lang, cn);
+    }
+}
+
+}  // namespace
+
+size_t emit_lds_bytes(int K) {
+    return K == 1 ? sizeof(EmitLds<1>) : (K == 2 ? sizeof(EmitLds<2>) : sizeof(EmitLds<3>));
+}
+
+size_t reduce_lds_bytes(int K) {
+    const size_t N = K == 1 ? agg_slots<1>() : (K == 2 ? agg_slots<2>() : agg_slots<3>());
+    return K == 1 ? N * (8 + 4) + 16 : N * (8 * (size_t)(K - 1) + 12) + 16;
+}
+
+hipError_t fit3_prepare(int K) {
+    const void* e = K == 1 ? (const void*)&emit_kernel<1> : (K == 2 ? (const void*)&emit_kernel<2> : (const void*)&emit_kernel<3>);
+    const void* r =
+        K == 1 ? (const void*)&reduce_kernel<1> : (K == 2 ? (const void*)&reduce_kernel<2> : (const void*)&reduce_kernel<3>);
+    hipError_t x = hipFuncSetAttribute(e, hipFuncAttributeMaxDynamicSharedMemorySize, (int)emit_lds_bytes(K));
+    if (x == hipSuccess) x = hipFuncSetAttribute(r, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes(K));
+    return x;
+}
+
+hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream) {
+    const dim3 g(p.grid_a), b(kEmitWaves * 64);
+    if (K == 1) hipLaunchKernelGGL(emit_kernel<1>, g, b, emit_lds_bytes(1), stream, p);
+    else if (K == 2) hipLaunchKernelGGL(emit_kernel<2>, g, b, emit_lds_bytes(2), stream, p);
+    else hipLaunchKernelGGL(emit_kernel<3>, g, b, emit_lds_bytes(3), stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_part2(int K, const PartParams& p, hipStream_t stream) {
+    const dim3 g(kQ * kSplits), b(kEmitWaves * 64);
+    if (K == 1) hipLaunchKernelGGL(part2_kernel<1>, g, b, 0, stream, p);
+    else if (K == 2) hipLaunchKernelGGL(part2_kernel<2>, g, b, 0, stream, p);
+    else hipLaunchKernelGGL(part2_kernel<3>, g, b, 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream) {
+    const dim3 g(kQ * kQ), b(kEmitWaves * 64);
+    if (K == 1) hipLaunchKernelGGL(reduce_kernel<1>, g, b, reduce_lds_bytes(1), stream, p);
+    else if (K == 2) hipLaunchKernelGGL(reduce_kernel<2>, g, b, reduce_lds_bytes(2), stream, p);
+    else hipLaunchKernelGGL(reduce_kernel<3>, g, b, reduce_lds_bytes(3), stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t n,
+                        hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const dim3 g((unsigned)((n + 1023) / 1024)), b(1024);
+    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, n);
+    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, n);
+    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, n);
     return hipGetLastError();
 }
 

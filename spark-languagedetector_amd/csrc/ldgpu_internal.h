@@ -165,20 +165,33 @@ hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const u
                              const int32_t* lang_of /*nullable: row is one count cnt_of[i] at lang_of[i]*/,
                              const unsigned long long* cnt_of, int64_t n, hipStream_t stream);
 
-// ---- FIT v2: radix-partitioned record aggregation (ldgpu_fit.hip) ----
-// A window (or a per-document LDS-aggregated group of equal windows) becomes
-// one 64-bit record  ((sentinel << lb | lang) << cb) | count  with sentinel =
-// 1 << 8 klen | key bytes (klen <= 7).  kl = record >> cb identifies the
-// (gram, language) pair; h = mix64(kl) routes it: q1 = h >> 58, q2 = bits
-// 52..57 (4096 buckets), slot = low 32 bits (LDS hash in a bucket).
+// ---- FIT v3: language-grouped LDS aggregation + radix-partitioned record
+// aggregation (ldgpu_count.hip) -- every gram length, every language count.
+// A window that no workgroup table absorbs (or a table entry at the end of a
+// workgroup's documents) becomes one record of K u64 words:
+//   K = 1 (compact; 8 max(G) + 1 + lb + cb <= 64 with cb >= 8):
+//        ((sentinel << lb | lang) << cb) | count, sentinel = 1 << 8 klen | bytes
+//   K = 2 (grams of <= 7 bytes, any L): {packed key (ldgpu_common.h),
+//        lang << 52 | count}
+//   K = 3 (some gram length of 8..15 bytes): {lo, hi, lang << 52 | count};
+//        a key of <= 7 bytes is lo = its packed key, hi = 0, a wide key is
+//        lo = bytes 0..7, hi = bytes 8.. | klen << 56
+// h = route hash of the (gram, language) pair: q1 = h >> 58, q2 = bits
+// 52..57 (4096 buckets), LDS slot = low 32 bits (reduce).
 constexpr int kQBits = 6;
 constexpr int kQ = 1 << kQBits;                 // buckets per level
-constexpr int kBlkRecs = 6144;                  // records per emit block (LDS); flushed above 2048
-constexpr int kRoundRecs = 4096;                // records one emit round can add (16 waves x 64 lanes x 4)
+constexpr int kBlkWords = 6144;                 // u64 words of records per emit block (LDS, 48 KiB)
 constexpr int kHdr = 68;                        // u32 per block header (kQ + 1 used)
 constexpr int kEmitWaves = 16;
-constexpr int kAggSlots = 8192;                 // LDS hash entries per bucket (reduce)
 constexpr int kSplits = 4;                      // emit workgroup groups (part2 inputs)
+constexpr int kT23 = 8192;                      // emit: workgroup LDS table of 2- and 3-byte grams
+constexpr uint64_t kCntBits = 52;               // K >= 2: count bits of the last record word
+// emit rounds: a wave step adds at most 64 x sub records (sub = 4 positions per
+// lane for K = 1, 1 otherwise); a block is flushed once it could not take
+// another round
+constexpr int emit_sub(int K) { return K == 1 ? 4 : 1; }
+constexpr int emit_blk_recs(int K) { return kBlkWords / K; }
+constexpr int emit_round_recs(int K) { return kEmitWaves * 64 * emit_sub(K); }
 
 struct PartParams {
     // corpus of the batch
@@ -189,43 +202,50 @@ struct PartParams {
     int32_t L;
     int32_t nG;
     int32_t G[kMaxGramLengths];
-    uint32_t lb, cb;            // language / count bit widths of a record
+    uint32_t lb, cb;            // K = 1: language / count bit widths of a record
     int32_t ablate;             // diagnostics build only (LDGPU_FIT_EMIT_ABLATE; compiled out otherwise):
-                                // bit 0 2-byte windows skip the LDS table (records instead), bit 1 the
-                                // block flush skips its global stores, bit 2 no records at all
-    // emit (phase A): workgroup w owns documents [wg_doc[w], wg_doc[w+1]),
-    // records [wg_rec[w], ...) (capacity: its windows) and block ids
-    // [wg_dir[w], ...); blocks are sorted by q1 with a kHdr header
+                                // bit 0 2-/3-byte windows skip the workgroup table (records instead),
+                                // bit 1 the block flush skips its global stores, bit 2 no records at all
+    // emit (phase A): the batch's documents in language order (perm, a
+    // permutation of 0 .. n-1); workgroup w owns perm[wg_doc[w] .. wg_doc[w+1]),
+    // all of language wg_lang[w], records [wg_rec[w], ...) (capacity: its
+    // windows) and block ids [wg_dir[w], ...); blocks are sorted by q1 with a
+    // kHdr header
     int32_t grid_a;             // emit workgroups (a multiple of kSplits)
+    const int32_t* perm;
+    const int32_t* wg_lang;
     const int64_t* wg_doc;
     const int64_t* wg_rec;
     const int64_t* wg_dir;
-    uint64_t* rec;
+    uint64_t* rec;              // K words per record
     int64_t* blk_start;         // [blocks] record offset of the block
     uint32_t* blk_hdr;          // [blocks][kHdr] exclusive q1 starts (+ total)
     int32_t* nblk;              // [grid_a] blocks written
     uint32_t* cnt3;             // [kQ][kQ][kSplits] records per (q1, q2, emit group)
-    CountParams direct;         // global table: counts too large for a record
+    CountParams direct;         // global table: K = 1 counts too large for a record
     // part2: q1 bucket of emit group s -> q2 sub-buckets at exact offsets
     const uint64_t* p2off;      // [kQ][kQ][kSplits]
-    uint64_t* rec2;
-    // reduce: bucket (q1, q2) = rec2[boff[b] .. boff[b+1]) -> distinct (kl,
-    // count) entries at out[boff[b] ..] (at most one per record), nout[b] of them
+    uint64_t* rec2;             // K words per record
+    // reduce: bucket (q1, q2) = rec2[boff[b] .. boff[b+1]) -> (key, count)
+    // entries at out[boff[b] ..] (at most one per record; equal keys summed
+    // as far as the LDS hash holds them), nout[b] of them
     const uint64_t* boff;       // [kQ * kQ + 1]
-    uint64_t* out_kl;
-    uint32_t* out_cnt;          // a batch counts < 2^32 windows
+    uint64_t* out;              // K words per entry (the record form, the count field a batch sum)
     uint32_t* nout;             // [kQ * kQ]
     const uint64_t* epre;       // merge: exclusive prefix of nout [kQ * kQ + 1]
 };
 
-size_t emit_lds_bytes();
-size_t reduce_lds_bytes();
-hipError_t fit2_prepare();
-hipError_t launch_emit(const PartParams& p, hipStream_t stream);
-hipError_t launch_part2(const PartParams& p, hipStream_t stream);
-hipError_t launch_reduce(const PartParams& p, hipStream_t stream);
-// add the reduce output (kl, count) entries 0..n into the global table
-hipError_t launch_merge(const PartParams& p, const CountParams& c, int64_t n, hipStream_t stream);
+size_t emit_lds_bytes(int K);
+size_t reduce_lds_bytes(int K);
+hipError_t fit3_prepare(int K);
+hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream);
+hipError_t launch_part2(int K, const PartParams& p, hipStream_t stream);
+hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
+struct WideCountParams;
+// add the reduce output entries 0..n into the global tables (K = 3: keys of
+// 8..15 bytes into the wide table)
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t n,
+                        hipStream_t stream);
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
 hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
                          hipStream_t stream);

@@ -264,26 +264,35 @@ def test_config3_shape_counts_and_table():
 
 
 @pytest.mark.parametrize("variant,env", [
-    ("product", {}),                                         # FIT v2: one batch
-    ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v2: many small batches
-    ("diag", {"LDGPU_FIT_LEGACY": "1"}),                     # single-pass count_kernel
+    ("product", {}),                                         # FIT v3, the table's own record form: one batch
+    ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v3: many small batches
+    ("diag", {"LDGPU_FIT_K": "2"}),                          # two-word records (any L, grams <= 7 bytes)
+    ("diag", {"LDGPU_FIT_K": "3", "LDGPU_FIT_BATCH_WINDOWS": "50000"}),  # three-word records, several batches
+    ("diag", {"LDGPU_FIT_EMIT_ABLATE": "1"}),                # no workgroup 2-/3-gram table: every window a record
+    ("diag", {"LDGPU_FIT_LEGACY": "1"}),                     # round-1 single-pass atomic kernels (A/B only)
 ])
-@pytest.mark.parametrize("L,grams", [(20, [1, 2, 3, 4, 5]), (100, [1, 2, 6]), (256, [3, 1, 3]), (2, [5, 4])])
+@pytest.mark.parametrize("L,grams", [(20, [1, 2, 3, 4, 5]), (100, [1, 2, 6]), (256, [3, 1, 3]), (2, [5, 4]),
+                                     (200, [1, 2, 3, 4, 5, 6, 7]), (20, [7]), (5, [2, 9, 15]), (30, [8, 1])])
 def test_count_paths_match_oracle(L, grams, variant, env, monkeypatch):
-    """Both counting paths, bit-exact against the C restatement: the radix-
-    partitioned record path (FIT v2: records of (gram, language, count),
-    bucketed twice, LDS-aggregated) in one and in many batches, and the
-    single-pass kernel.  (100, [1, 2, 6]) leaves a record 8 count bits, so
-    hot 1-/2-grams of the long repetitive documents exceed a record's count
-    and take the direct global add; unsupported labels (-1) are skipped."""
+    """Every counting path, bit-exact against the C restatement over two
+    calls: FIT v3 (documents grouped by language, workgroup LDS tables for
+    1-3-byte grams, records of (gram, language, count) bucketed twice and
+    LDS-aggregated) in the table's own record form -- one word when it fits
+    (L=20, grams 1-5), two for grams of <= 7 bytes with many languages (L=200,
+    grams 1-7; L=4096), three with grams of 8..15 bytes -- in one and in many
+    batches, the wider forms forced on small tables, and the legacy kernels.
+    (100, [1, 2, 6]) leaves a one-word record 8 count bits, so hot 1-/2-grams
+    of the long repetitive documents exceed a record's count and take the
+    direct global add; unsupported labels (-1) are skipped; documents shorter
+    than n count their whole text (partial windows)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(L + len(grams))
     ls = synth.make_languages(L, seed=L + 7)
     data, off, lang = synth.generate(ls, 900, 0, 900, seed=L + 8)
     docs = [bytes(data[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
-    docs += [b"a" * 3000, b"ab" * 1500, b"abc" * 700, b"", b"x", b"xy"]
-    dl = np.concatenate([lang, rng.integers(0, L, size=6).astype(np.int32)])
+    docs += [b"a" * 3000, b"ab" * 1500, b"abc" * 700, b"", b"x", b"xy", b"abcdefghijklmnopq" * 20]
+    dl = np.concatenate([lang, rng.integers(0, L, size=7).astype(np.int32)])
     dl[::29] = -1
     d, o = encoding.pack(docs)
     counts = DeviceCounts(L, grams, variant=variant)
@@ -296,6 +305,48 @@ def test_count_paths_match_oracle(L, grams, variant, env, monkeypatch):
     expect = np.array([ocnt[i] + extra.get(k, 0) for i, k in enumerate(okeys)])
     assert keys == okeys
     assert np.array_equal(cnt, expect)
+
+
+@pytest.mark.parametrize("variant", ["product", "diag"])
+def test_count_4096_languages(variant, monkeypatch):
+    """The largest language count: two-word records (12 language bits leave
+    a one-word record no count bits at grams up to 6), a few short documents
+    per language id spread over all 4096 (dense export rows stay small)."""
+    if variant == "diag":
+        monkeypatch.setenv("LDGPU_FIT_BATCH_WINDOWS", "3000")
+    L, grams = 4096, [2, 6, 1]
+    rng = np.random.default_rng(4096)
+    alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in rng.integers(0, 60, size=40)]
+    dl = rng.integers(0, L, size=len(docs)).astype(np.int32)
+    dl[-1] = L - 1
+    d, o = encoding.pack(docs)
+    counts = DeviceCounts(L, grams, variant=variant)
+    counts.count(d, o, dl)
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(d, o, dl, L, grams)
+    assert keys == okeys
+    assert np.array_equal(cnt, ocnt)
+
+
+def test_count_single_language_long_corpus():
+    """One language, long documents: the workgroup tables of a language group
+    fill (2-/3-grams beyond 8192 slots go out as records) and hot grams count
+    far past a record's count field; counts bit-exact."""
+    rng = np.random.default_rng(12)
+    ls = synth.make_languages(3, seed=12)
+    lang = np.zeros(400, np.int32)
+    data, off, lang = synth.generate(ls, 400, 3000, 9000, seed=13, doc_lang=lang)
+    rnd = [bytes(rng.integers(0, 256, size=20000, dtype=np.uint8)) for _ in range(20)]  # many distinct 3-grams
+    docs = [bytes(data[off[i]:off[i + 1]]) for i in range(len(off) - 1)] + rnd
+    d, o = encoding.pack(docs)
+    dl = np.zeros(len(docs), np.int32)
+    counts = DeviceCounts(3, [1, 2, 3, 4, 5])
+    counts.count(d, o, dl)
+    keys, cnt = counts.export()
+    okeys, ocnt = OC.count(d, o, dl, 3, [1, 2, 3, 4, 5])
+    assert keys == okeys
+    assert np.array_equal(cnt, ocnt)
 
 
 def _wide_corpus(grams, L, seed):
