@@ -1409,6 +1409,15 @@ struct ldgpu_counts {
     std::vector<std::pair<uint64_t, uint64_t>> wide_sorted;
     // cached fit table (ldgpu_fit_table_size -> _export)
     bool tbl_valid = false;
+    // sparse host copy of the table for ranged exports (ldgpu_counts_export_sparse),
+    // valid until the counts change: keys (one-word or wide stand-ins, see
+    // counts_pull) in (length, bytes) order, their nonzero (language, count) pairs
+    bool sp_valid = false;
+    std::vector<uint64_t> sp_keys;
+    std::vector<int64_t> sp_koff;   // key byte offsets [n + 1]
+    std::vector<int64_t> sp_poff;   // pair offsets [n + 1]
+    std::vector<int32_t> sp_lang;
+    std::vector<int64_t> sp_cnt;
     std::vector<uint8_t> tbl_bytes;
     std::vector<int64_t> tbl_off;
     std::vector<uint64_t> tbl_masks;  // [rows][S] presence masks of the chosen grams
@@ -1510,6 +1519,8 @@ int after_batch(ldgpu_counts* c) {
             if (int rc = grow(c, next_pow2(4 * size + 16))) return rc;
         }
         c->tbl_valid = false;
+        c->sp_valid = false;
+    c->sp_valid = false;
         return LDGPU_OK;
     }
     // Entries whose key found no slot are on the overflow list: grow, then
@@ -1569,6 +1580,7 @@ int after_batch(ldgpu_counts* c) {
         target = 2 * c->cap;
     }
     c->tbl_valid = false;
+    c->sp_valid = false;
     return LDGPU_OK;
 }
 
@@ -1680,6 +1692,7 @@ int wide_after(ldgpu_counts* c) {
     if (full) return fail(LDGPU_EDEVICE, "wide count table: an insert found no slot");
     c->wsize = size;
     c->tbl_valid = false;
+    c->sp_valid = false;
     return LDGPU_OK;
 }
 
@@ -2336,6 +2349,165 @@ extern "C" int ldgpu_counts_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t*
     return ok();
 }
 
+namespace {
+// the sparse host copy (ldgpu_counts::sp_*), pulled once per table state
+int sparse_pull(ldgpu_counts* c) {
+    if (c->sp_valid) return LDGPU_OK;
+    std::vector<uint64_t> k;
+    std::vector<unsigned long long> cc;
+    if (int rc = counts_pull(c, k, cc)) return rc;
+    const int L = c->L;
+    const size_t n = k.size();
+    c->sp_keys = std::move(k);
+    c->sp_koff.assign(n + 1, 0);
+    c->sp_poff.assign(n + 1, 0);
+    c->sp_lang.clear();
+    c->sp_cnt.clear();
+    for (size_t i = 0; i < n; ++i) {
+        c->sp_koff[i + 1] = c->sp_koff[i] + gram_bytes(c, c->sp_keys[i], nullptr);
+        for (int l = 0; l < L; ++l) {
+            const unsigned long long v = cc[i * (size_t)L + l];
+            if (!v) continue;
+            c->sp_lang.push_back(l);
+            c->sp_cnt.push_back((int64_t)v);
+        }
+        c->sp_poff[i + 1] = (int64_t)c->sp_lang.size();
+    }
+    c->sp_valid = true;
+    return LDGPU_OK;
+}
+
+int check_range(const ldgpu_counts* c, int64_t first, int64_t n) {
+    const int64_t total = (int64_t)c->sp_keys.size();
+    if (first < 0 || n < 0 || first > total || n > total - first)
+        return fail(LDGPU_EINVAL, "gram range [%lld, %lld) outside [0, %lld)", (long long)first,
+                    (long long)(first + n), (long long)total);
+    return LDGPU_OK;
+}
+}  // namespace
+
+extern "C" int ldgpu_counts_sparse_size(ldgpu_counts* c, int64_t first, int64_t n, int64_t* key_bytes,
+                                        int64_t* n_pairs) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    if (int rc = sparse_pull(c)) return rc;
+    if (int rc = check_range(c, first, n)) return rc;
+    if (key_bytes) *key_bytes = c->sp_koff[first + n] - c->sp_koff[first];
+    if (n_pairs) *n_pairs = c->sp_poff[first + n] - c->sp_poff[first];
+    return ok();
+}
+
+extern "C" int ldgpu_counts_export_sparse(ldgpu_counts* c, int64_t first, int64_t n, uint8_t* key_bytes,
+                                          int64_t* key_offsets, int64_t* pair_offsets, int32_t* pair_langs,
+                                          int64_t* pair_counts) {
+    if (!c || !key_offsets || !pair_offsets) return fail(LDGPU_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    if (int rc = sparse_pull(c)) return rc;
+    if (int rc = check_range(c, first, n)) return rc;
+    const int64_t k0 = c->sp_koff[first], p0 = c->sp_poff[first];
+    const int64_t nk = c->sp_koff[first + n] - k0, np = c->sp_poff[first + n] - p0;
+    if ((nk && !key_bytes) || (np && (!pair_langs || !pair_counts))) return fail(LDGPU_EINVAL, "NULL argument");
+    for (int64_t i = 0; i < n; ++i) gram_bytes(c, c->sp_keys[first + i], key_bytes + c->sp_koff[first + i] - k0);
+    for (int64_t i = 0; i <= n; ++i) {
+        key_offsets[i] = c->sp_koff[first + i] - k0;
+        pair_offsets[i] = c->sp_poff[first + i] - p0;
+    }
+    if (np) {
+        memcpy(pair_langs, c->sp_lang.data() + p0, sizeof(int32_t) * (size_t)np);
+        memcpy(pair_counts, c->sp_cnt.data() + p0, sizeof(int64_t) * (size_t)np);
+    }
+    return ok();
+}
+
+extern "C" int ldgpu_counts_add_sparse(ldgpu_counts* c, int64_t n, const uint8_t* key_bytes,
+                                       const int64_t* key_offsets, const int64_t* pair_offsets,
+                                       const int32_t* pair_langs, const int64_t* pair_counts) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (c->comm) return fail(LDGPU_EINVAL, "the count table is merged (ldgpu_counts_merge): it takes no more counts");
+    if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
+    if (n == 0) return ok();
+    if (!key_bytes || !key_offsets || !pair_offsets) return fail(LDGPU_EINVAL, "NULL argument");
+    const int64_t np = pair_offsets[n] - pair_offsets[0];
+    if (np < 0 || (np && (!pair_langs || !pair_counts))) return fail(LDGPU_EINVAL, "bad pair offsets / NULL pairs");
+    // one-word keys as (key, language, count) triples; wide keys as dense rows
+    std::vector<uint64_t> tk, wlo, whi;
+    std::vector<int32_t> tl;
+    std::vector<unsigned long long> tc, wrows;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = key_offsets[i + 1] - key_offsets[i];
+        if (len < 1 || len > LDGPU_MAX_FIT_GRAM)
+            return fail(LDGPU_EINVAL, "key %lld has length %lld outside [1, %d]", (long long)i, (long long)len,
+                        LDGPU_MAX_FIT_GRAM);
+        if (pair_offsets[i + 1] < pair_offsets[i]) return fail(LDGPU_EINVAL, "pair offsets decrease at %lld", (long long)i);
+        const uint8_t* kb = key_bytes + key_offsets[i];
+        for (int64_t j = pair_offsets[i]; j < pair_offsets[i + 1]; ++j) {
+            const int64_t q = j - pair_offsets[0];
+            if (pair_langs[q] < 0 || pair_langs[q] >= c->L)
+                return fail(LDGPU_EINVAL, "pair %lld: language %d outside [0, %d)", (long long)q, pair_langs[q], c->L);
+            if (pair_counts[q] < 0) return fail(LDGPU_EINVAL, "pair %lld: negative count", (long long)q);
+        }
+        if (len <= kMaxGram) {
+            const uint64_t key = pack_key_host(kb, (int)len);
+            for (int64_t j = pair_offsets[i]; j < pair_offsets[i + 1]; ++j) {
+                const int64_t q = j - pair_offsets[0];
+                if (!pair_counts[q]) continue;
+                tk.push_back(key);
+                tl.push_back(pair_langs[q]);
+                tc.push_back((unsigned long long)pair_counts[q]);
+            }
+        } else {
+            wlo.push_back((pack_key_host(kb, 8) & ((1ull << 56) - 1)) | ((uint64_t)kb[7] << 56));
+            whi.push_back((pack_key_host(kb + 8, (int)len - 8) & ((1ull << 56) - 1)) | ((uint64_t)len << 56));
+            wrows.resize(wrows.size() + c->L, 0ull);
+            for (int64_t j = pair_offsets[i]; j < pair_offsets[i + 1]; ++j) {
+                const int64_t q = j - pair_offsets[0];
+                wrows[wrows.size() - c->L + pair_langs[q]] += (unsigned long long)pair_counts[q];
+            }
+        }
+    }
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
+    HIP_TRY(hipSetDevice(c->ctx->device));
+    hipStream_t st = c->ctx->stream;
+    if (!wlo.empty()) {
+        const int64_t nw = (int64_t)wlo.size();
+        if (int rc = wide_ensure(c, (uint64_t)nw)) return rc;
+        DevBufs wb;
+        uint64_t *d_lo, *d_hi;
+        unsigned long long* d_r;
+        HIP_TRY(wb.alloc(&d_lo, nw));
+        HIP_TRY(wb.alloc(&d_hi, nw));
+        HIP_TRY(wb.alloc(&d_r, (size_t)nw * c->L));
+        HIP_TRY(hipMemcpyAsync(d_lo, wlo.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_hi, whi.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_r, wrows.data(), wrows.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_wide_add(wide_params(c), d_lo, d_hi, d_r, nw, st));
+        if (int rc = wide_after(c)) return rc;
+    }
+    const int64_t nt = (int64_t)tk.size();
+    if (!nt) return ok();
+    if (2 * (c->size + (uint64_t)nt) > c->cap) {
+        if (int rc = grow(c, next_pow2(4 * (c->size + nt) + 16))) return rc;
+    }
+    if (int rc = ensure_ovf(c, nt)) return rc;
+    DevBufs tb;
+    uint64_t* d_k;
+    int32_t* d_l;
+    unsigned long long* d_c;
+    HIP_TRY(tb.alloc(&d_k, nt));
+    HIP_TRY(tb.alloc(&d_l, nt));
+    HIP_TRY(tb.alloc(&d_c, nt));
+    HIP_TRY(hipMemcpyAsync(d_k, tk.data(), nt * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_l, tl.data(), nt * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_c, tc.data(), nt * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+    HIP_TRY(launch_counts_add(count_params(c), d_k, nullptr, d_l, d_c, nt, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = after_batch(c)) return rc;
+    return ok();
+}
+
 extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_bytes, const int64_t* key_offsets,
                                 const int64_t* counts_in) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
@@ -2755,76 +2927,105 @@ int merge_wide(ldgpu_counts* c, ldgpu_comm* m) {
 }
 }  // namespace
 
+namespace {
+// Every rank's status before a collective phase: a failure that one rank
+// alone meets (an allocation, a count check) ends the merge on EVERY rank
+// instead of leaving the others waiting in the next exchange.  Returns the
+// local code (with its message) or LDGPU_EDEVICE naming the failed rank.
+int comm_agree(ldgpu_comm* m, int rc) {
+    if (m->world == 1) return rc;
+    const std::string mine = g_err;
+    int32_t v = rc;
+    std::vector<int32_t> all(m->world);
+    if (int r = comm_allgather_host(m, &v, sizeof v, all.data())) return r;
+    if (rc) {
+        g_err = mine;
+        return rc;
+    }
+    for (int r = 0; r < m->world; ++r)
+        if (all[r]) return fail(LDGPU_EDEVICE, "merge: rank %d failed (status %d)", r, all[r]);
+    return LDGPU_OK;
+}
+}  // namespace
+
 // Owner exchange: every rank partitions its table by owner, one
-// all-to-all moves each rank's keys and count rows to their owners, and each
-// rank rebuilds its table from what it received: the global counts of the
-// grams it owns (integer sums: bit-exact in any order).
+// all-to-all moves each rank's nonzero (gram, language) counts -- 16-B pairs
+// (key, lang << 52 | count), not dense rows of L counters -- to their owners,
+// and each rank rebuilds its table from what it received: the global counts
+// of the grams it owns (integer sums: bit-exact in any order).  Every rank's
+// status is agreed before each exchange (comm_agree).
 extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     if (!c || !m) return fail(LDGPU_EINVAL, "NULL argument");
     if (c->comm) return fail(LDGPU_EINVAL, "the count table is already merged");
     if (m->ctx != c->ctx) return fail(LDGPU_EINVAL, "communicator and count table belong to different contexts");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    const int W = m->world, L = c->L;
+    const int W = m->world;
     hipStream_t st = c->ctx->stream;
-    const int64_t n = (int64_t)c->size;
     DevBufs db;
-    unsigned long long *d_nof, *d_cur, *d_rows, *d_rrows;
-    uint64_t *d_keys, *d_rkeys;
-    HIP_TRY(db.alloc(&d_nof, W));
-    HIP_TRY(db.alloc(&d_cur, W));
-    HIP_TRY(db.alloc(&d_keys, n));
-    HIP_TRY(db.alloc(&d_rows, (size_t)n * L));
-    HIP_TRY(hipMemsetAsync(d_nof, 0, sizeof(unsigned long long) * W, st));
-    HIP_TRY(launch_owner_count(count_params(c), c->cap, (uint32_t)W, d_nof, st));
+    unsigned long long *d_nof = nullptr, *d_cur = nullptr;
+    uint64_t *d_pairs = nullptr, *d_rpairs = nullptr;
     std::vector<unsigned long long> nof(W), cur(W);
-    HIP_TRY(hipMemcpyAsync(nof.data(), d_nof, sizeof(unsigned long long) * W, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
     std::vector<int64_t> send_n(W);
-    unsigned long long acc = 0;
-    for (int r = 0; r < W; ++r) {
-        cur[r] = acc;
-        acc += nof[r];
-        send_n[r] = (int64_t)nof[r];
-    }
-    if ((int64_t)acc != n) return fail(LDGPU_EDEVICE, "merge: %llu grams partitioned, %lld held", acc, (long long)n);
-    HIP_TRY(hipMemcpyAsync(d_cur, cur.data(), sizeof(unsigned long long) * W, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_owner_scatter(count_params(c), c->cap, (uint32_t)W, d_cur, d_keys, d_rows, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    // phase 1: this rank's pairs, partitioned by owner
+    auto partition = [&]() -> int {
+        HIP_TRY(db.alloc(&d_nof, W));
+        HIP_TRY(db.alloc(&d_cur, W));
+        HIP_TRY(hipMemsetAsync(d_nof, 0, sizeof(unsigned long long) * W, st));
+        HIP_TRY(launch_owner_pair_count(count_params(c), c->cap, (uint32_t)W, d_nof, st));
+        HIP_TRY(hipMemcpyAsync(nof.data(), d_nof, sizeof(unsigned long long) * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        unsigned long long acc = 0;
+        for (int r = 0; r < W; ++r) {
+            cur[r] = acc;
+            acc += nof[r];
+            send_n[r] = (int64_t)nof[r];
+        }
+        HIP_TRY(db.alloc(&d_pairs, 2 * (size_t)acc));
+        HIP_TRY(hipMemcpyAsync(d_cur, cur.data(), sizeof(unsigned long long) * W, hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_owner_pair_scatter(count_params(c), c->cap, (uint32_t)W, d_cur, d_pairs, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return LDGPU_OK;
+    };
+    if (int rc = comm_agree(m, partition())) return rc;
     std::vector<int64_t> all((size_t)W * W);
     if (int rc = comm_allgather_host(m, send_n.data(), sizeof(int64_t) * W, all.data())) return rc;
     std::vector<int64_t> recv_n(W);
     int64_t R = 0;
     for (int r = 0; r < W; ++r) R += recv_n[r] = all[(size_t)r * W + m->rank];
-    HIP_TRY(db.alloc(&d_rkeys, R));
-    HIP_TRY(db.alloc(&d_rrows, (size_t)R * L));
+    // phase 2: receive buffers and the fresh owned-shard table, then the exchange
+    auto prepare = [&]() -> int {
+        HIP_TRY(db.alloc(&d_rpairs, 2 * (size_t)R));
+        return LDGPU_OK;
+    };
+    if (int rc = comm_agree(m, prepare())) return rc;
     std::vector<int64_t> sb(W), rb(W);
     for (int r = 0; r < W; ++r) {
-        sb[r] = send_n[r] * 8;
-        rb[r] = recv_n[r] * 8;
+        sb[r] = send_n[r] * 16;
+        rb[r] = recv_n[r] * 16;
     }
-    if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_keys, sb, (uint8_t*)d_rkeys, rb)) return rc;
-    for (int r = 0; r < W; ++r) {
-        sb[r] *= L;
-        rb[r] *= L;
-    }
-    if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_rows, sb, (uint8_t*)d_rrows, rb)) return rc;
-    // the owned shard, rebuilt: the same key arrives from several ranks
-    cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
-    cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
-    c->d_keys = nullptr;
-    c->d_counts = nullptr;
-    c->cap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
-    if (int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts)) return rc;
-    HIP_TRY(hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-    c->size = 0;
-    HIP_TRY(launch_counts_add(count_params(c), d_rkeys, d_rrows, nullptr, nullptr, R, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (int rc = after_batch(c)) return rc;
-    if (int rc = merge_wide(c, m)) return rc;
+    if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_pairs, sb, (uint8_t*)d_rpairs, rb)) return rc;
+    // the owned shard, rebuilt: one key may arrive from several ranks
+    auto rebuild = [&]() -> int {
+        cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
+        c->d_keys = nullptr;
+        c->d_counts = nullptr;
+        c->cap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
+        if (int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts)) return rc;
+        if (int rc = ensure_ovf(c, R)) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), st));
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+        c->size = 0;
+        HIP_TRY(launch_pairs_add(count_params(c), d_rpairs, R, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return after_batch(c);
+    };
+    if (int rc = comm_agree(m, rebuild())) return rc;
+    if (int rc = comm_agree(m, merge_wide(c, m))) return rc;
     c->comm = m;
     c->tbl_valid = false;
+    c->sp_valid = false;
     return ok();
 }
 

@@ -519,6 +519,45 @@ __global__ void owner_scatter_kernel(const CountParams p, uint64_t cap, uint32_t
     for (int l = 0; l < p.L; ++l) out_rows[o * p.L + l] = p.counts[i * p.L + l];
 }
 
+// sparse exchange (ldgpu_counts_merge): a slot's nonzero (language, count)
+// pairs, 16 B each -- (key, lang << 52 | count) -- instead of its dense row of
+// L counters (1.3 pairs per gram against L = 20..200 counters on the fit
+// corpora)
+__global__ void owner_pair_count_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* n_of) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || p.keys[i] == kEmpty) return;
+    unsigned long long k = 0;
+    for (int l = 0; l < p.L; ++l) k += p.counts[i * p.L + l] != 0ull;
+    if (k) atomicAdd(&n_of[owner_of(p.keys[i], world)], k);
+}
+
+__global__ void owner_pair_scatter_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                          uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || p.keys[i] == kEmpty) return;
+    const uint64_t key = p.keys[i];
+    const unsigned long long* row = p.counts + i * p.L;
+    unsigned long long k = 0;
+    for (int l = 0; l < p.L; ++l) k += row[l] != 0ull;
+    if (!k) return;
+    unsigned long long o = atomicAdd(&cursor[owner_of(key, world)], k);
+    for (int l = 0; l < p.L; ++l) {
+        if (!row[l]) continue;
+        out[2 * o] = key;
+        out[2 * o + 1] = ((uint64_t)l << kPairCntBits) | row[l];
+        ++o;
+    }
+}
+
+// add received (key, lang << 52 | count) pairs into the table (probe-limit
+// overflows go to the overflow list, re-inserted by the host)
+__global__ void pairs_add_kernel(const CountParams p, const uint64_t* pairs, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t v = pairs[2 * i + 1];
+    add_count(p, pairs[2 * i], (int)(v >> kPairCntBits), (unsigned long long)(v & ((1ull << kPairCntBits) - 1ull)));
+}
+
 // distributed top-K: a candidate is chosen when its (length, bytes) sort key
 // is at most its language's global threshold
 __global__ void mark_threshold_kernel(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key,
@@ -544,6 +583,26 @@ hipError_t launch_owner_scatter(const CountParams& p, uint64_t cap, uint32_t wor
                                 uint64_t* out_keys, unsigned long long* out_rows, hipStream_t stream) {
     hipLaunchKernelGGL(owner_scatter_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap, world,
                        cursor, out_keys, out_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_owner_pair_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
+                                   hipStream_t stream) {
+    hipLaunchKernelGGL(owner_pair_count_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap, world,
+                       n_of);
+    return hipGetLastError();
+}
+
+hipError_t launch_owner_pair_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                     uint64_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL(owner_pair_scatter_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap,
+                       world, cursor, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairs_add(const CountParams& p, const uint64_t* pairs, int64_t n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pairs_add_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, p, pairs, n);
     return hipGetLastError();
 }
 

@@ -311,6 +311,15 @@ hipError_t launch_owner_count(const CountParams& p, uint64_t cap, uint32_t world
                               hipStream_t stream);
 hipError_t launch_owner_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
                                 uint64_t* out_keys, unsigned long long* out_rows, hipStream_t stream);
+// sparse owner exchange: n_of[r] += nonzero (gram, language) pairs owned by
+// rank r; scatter them as (key, lang << kPairCntBits | count) to out at
+// cursor[owner]++; add such pairs into a table
+constexpr uint32_t kPairCntBits = 52;
+hipError_t launch_owner_pair_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
+                                   hipStream_t stream);
+hipError_t launch_owner_pair_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                     uint64_t* out, hipStream_t stream);
+hipError_t launch_pairs_add(const CountParams& p, const uint64_t* pairs, int64_t n, hipStream_t stream);
 hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream);
 // gather the chosen grams: out_keys[m], out_masks[m][S], out_k[m]
 hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,

@@ -67,6 +67,9 @@ SIGNATURES = [
     ("ldgpu_counts_stats", ctypes.c_int, [_p, _pi64, _pi64, _pi64]),
     ("ldgpu_counts_export", ctypes.c_int, [_p, _p, _p, _p]),
     ("ldgpu_counts_add", ctypes.c_int, [_p, _i64, _p, _p, _p]),
+    ("ldgpu_counts_sparse_size", ctypes.c_int, [_p, _i64, _i64, _pi64, _pi64]),
+    ("ldgpu_counts_export_sparse", ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _p, _p]),
+    ("ldgpu_counts_add_sparse", ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _p]),
     ("ldgpu_counts_export_device", ctypes.c_int, [_p, _i64, _p, _p, _pi64, _p]),
     ("ldgpu_counts_add_device", ctypes.c_int, [_p, _i64, _p, _p, _p]),
     ("ldgpu_comm_unique_id", ctypes.c_int, [_p]),

@@ -225,6 +225,34 @@ class DeviceCounts(_Owner):
         b = kb.tobytes()
         return [b[ko[i]:ko[i + 1]] for i in range(n.value)], cnt
 
+    def export_sparse(self, first: int = 0, n: Optional[int] = None):
+        """Grams [first, first + n) in (length, bytes) order with their nonzero
+        (language, count) pairs: (key_bytes uint8, key_offsets int64 [n+1],
+        pair_offsets int64 [n+1], pair_langs int32, pair_counts int64)."""
+        if n is None:
+            n = self.size() - first
+        nb = ctypes.c_int64()
+        npairs = ctypes.c_int64()
+        self._check(self.lib.ldgpu_counts_sparse_size(self.h, first, n, ctypes.byref(nb), ctypes.byref(npairs)))
+        kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        ko = np.zeros(n + 1, dtype=np.int64)
+        po = np.zeros(n + 1, dtype=np.int64)
+        pl = np.zeros(max(npairs.value, 1), dtype=np.int32)
+        pc = np.zeros(max(npairs.value, 1), dtype=np.int64)
+        self._check(self.lib.ldgpu_counts_export_sparse(self.h, first, n, _ptr(kb), _ptr(ko), _ptr(po), _ptr(pl),
+                                                       _ptr(pc)))
+        return kb[:nb.value], ko, po, pl[:npairs.value], pc[:npairs.value]
+
+    def add_sparse(self, key_bytes: np.ndarray, key_offsets: np.ndarray, pair_offsets: np.ndarray,
+                   pair_langs: np.ndarray, pair_counts: np.ndarray) -> None:
+        kb = np.ascontiguousarray(key_bytes, dtype=np.uint8)
+        ko = np.ascontiguousarray(key_offsets, dtype=np.int64)
+        po = np.ascontiguousarray(pair_offsets, dtype=np.int64)
+        pl = np.ascontiguousarray(pair_langs, dtype=np.int32)
+        pc = np.ascontiguousarray(pair_counts, dtype=np.int64)
+        self._check(self.lib.ldgpu_counts_add_sparse(self.h, len(ko) - 1, _ptr(kb if len(kb) else np.zeros(1, np.uint8)),
+                                                    _ptr(ko), _ptr(po), _ptr(pl), _ptr(pc)))
+
     def add(self, keys: Sequence[bytes], counts: np.ndarray) -> None:
         counts = np.ascontiguousarray(counts, dtype=np.int64).reshape(len(keys), self.L)
         kb, ko = pack(list(keys))

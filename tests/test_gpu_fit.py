@@ -419,3 +419,35 @@ def test_wide_gram_counts_add_and_limits():
         a.export_device()
     with pytest.raises(NotImplementedError):
         DeviceCounts(L, [16])
+
+
+@pytest.mark.parametrize("grams", [[1, 2, 3], [2, 9]])
+def test_sparse_export_ranges_and_add(grams):
+    """ldgpu_counts_export_sparse / _add_sparse (the Scala shuffle payload):
+    ranges of the (length, bytes) order carry each gram's nonzero (language,
+    count) pairs; concatenated they equal the dense export, and adding them
+    (twice, in ranges) into a fresh table doubles every count."""
+    L = 7
+    data, off, lang = _wide_corpus(grams, L, 99)
+    a = DeviceCounts(L, grams)
+    a.count(data, off, lang)
+    keys, cnt = a.export()
+    n = len(keys)
+    b = DeviceCounts(L, grams)
+    cuts = [0, 1, n // 3, n // 2, n]
+    for first, last in zip(cuts[:-1], cuts[1:]):
+        kb, ko, po, pl, pc = a.export_sparse(first, last - first)
+        got = [kb[ko[i]:ko[i + 1]].tobytes() for i in range(last - first)]
+        assert got == keys[first:last]
+        for i in range(last - first):
+            row = np.zeros(L, dtype=np.int64)
+            row[pl[po[i]:po[i + 1]]] = pc[po[i]:po[i + 1]]
+            assert np.array_equal(row, cnt[first + i])
+            assert np.all(np.diff(pl[po[i]:po[i + 1]]) > 0)   # language order, no zero pairs
+            assert np.all(pc[po[i]:po[i + 1]] > 0)
+        b.add_sparse(kb, ko, po, pl, pc)
+        b.add_sparse(kb, ko, po, pl, pc)
+    k2, c2 = b.export()
+    assert k2 == keys and np.array_equal(c2, 2 * cnt)
+    with pytest.raises(ValueError, match="outside"):
+        a.export_sparse(n, 1)
