@@ -64,7 +64,10 @@ def parse():
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--mode", choices=["score", "fit"], default="score",
                     help="score = the headline metric (config 2); fit = config 3's count + table build")
-    ap.add_argument("--fit-bytes", type=int, default=1 << 30, help="fit mode: corpus bytes per GPU")
+    ap.add_argument("--fit-bytes", type=int, default=6_250_000_000,
+                    help="fit mode: corpus bytes per GPU (default: config 3's 50 GB over 8 GPUs)")
+    ap.add_argument("--check-merge", action="store_true",
+                    help="fit mode, N > 1: check the merged table against the oracle over every rank's corpus")
     args = ap.parse_args()
     # SURVEY §8d shapes; explicit flags override
     preset = {1: dict(docs=10_000, doc_min=128, doc_max=384, langs=3, grams="1,2,3", profile_size=1000,
@@ -184,6 +187,7 @@ def cpu_baseline_fit(args, grams, data, off, lang):
     rate = int(off[probe]) / max(run(probe)[0], 1e-9)
     target = rate * args.cpu_seconds
     n = int(min(len(off) - 1, max(probe, np.searchsorted(off, target))))
+    n = int(min(n, np.searchsorted(off, len(data), side="right") - 1))  # within the host copy of the corpus
     dt, exported = run(n, keep=True)
     return {"value": round(int(off[n]) / dt, 1), "unit": "bytes/s", "cores": 1, "kind": "port",
             "sample": f"first {n} documents ({int(off[n])} corpus bytes) of the GPU's corpus, "
@@ -273,24 +277,47 @@ def traffic_from_profiles(workload_key):
     return same_shape
 
 
+def fit_corpus(args, ls, rank, dev):
+    """This rank's config-3 shard: fit_bytes of 1-7 KB synthetic documents
+    drawn on the GPU (synth.generate_device, seed per rank), untiled."""
+    from languagedetection import synth as S
+    n_docs = max(1, int(args.fit_bytes // 4096))  # U[1024, 7168]: 4096 B per document on average
+    return S.generate_device(ls, n_docs, 1024, 7168, seed=S.SEED_BASE + 3 + 1000 * rank, device=dev)
+
+
+def topk_table_from_counts(kb, ko, cnt, K):
+    """filterTopGrams (LanguageDetector.scala:100-132) over oracle counts (keys
+    in (length, bytes) order): v_l = log(1 + [l] / k), per language the K
+    largest v_l, ties by the key order -> {gram: row}."""
+    pres = cnt > 0
+    k = pres.sum(axis=1)
+    w = np.zeros(len(k))
+    w[k > 0] = np.log(1.0 + 1.0 / k[k > 0])
+    chosen = np.zeros(len(k), dtype=bool)
+    idx = np.arange(len(k))
+    for l in range(cnt.shape[1]):
+        v = np.where(pres[:, l], w, 0.0)
+        chosen[np.lexsort((idx, -v))[:K]] = True
+    b = kb.tobytes()
+    return {b[ko[i]:ko[i + 1]]: [float(w[i]) if pres[i, l] else 0.0 for l in range(cnt.shape[1])]
+            for i in np.nonzero(chosen)[0]}
+
+
 def fit_main(args, world, rank, local, dev, backend):
     """Config 3 (FIT): count every window of a synthetic multilingual corpus
-    (docs of 1-7 KB) resident in HBM, merge across ranks (all_gather keys +
-    all_reduce counts), build the K-profile table.  A step = one full fit."""
+    (docs of 1-7 KB, drawn on the GPU, resident in HBM), merge across ranks
+    (owner exchange of sparse (gram, language, count) pairs), build the
+    K-profile table.  A step = one full fit."""
     from languagedetection.distributed import Communicator, merge_counts_device
     grams = [int(x) for x in args.grams.split(",")]
     comm = Communicator(device=local) if world > 1 else None
     ls = synth.make_languages(args.langs)
-    pool_docs = max(1, min(16384, args.fit_bytes // 4096))
-    pdata, poff, plang = synth.generate(ls, pool_docs, 1024, 7168, seed=synth.SEED_BASE + 3 + 1000 * rank)
-    n_docs = max(1, int(args.fit_bytes // max(1, poff[-1] // pool_docs)))
-    data, off, lang = synth.tile(pdata, poff, plang, n_docs)
-    n_bytes = int(off[-1])
-    d_bytes = torch.empty(((n_bytes + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
-    d_bytes[:n_bytes].copy_(torch.from_numpy(data))
-    d_off = torch.from_numpy(off).to(dev)
-    d_lang = torch.from_numpy(lang).to(dev)
+    d_bytes, d_off, d_lang = fit_corpus(args, ls, rank, dev)
+    n_docs = len(d_off) - 1
+    n_bytes = int(d_off[-1].item())
+    off = d_off.cpu().numpy()
     stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
 
     def step():
         t = {}
@@ -313,7 +340,7 @@ def fit_main(args, world, rank, local, dev, backend):
         c.close()
         t["close_s"] = time.perf_counter() - t2
         t["total_s"] = time.perf_counter() - t0
-        return t, distinct, len(table)
+        return t, distinct, table
 
     for _ in range(args.warmup):
         step()
@@ -345,17 +372,18 @@ def fit_main(args, world, rank, local, dev, backend):
         "value": round(n_bytes * world * args.steps / elapsed, 1), "unit": "bytes/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64 (integer counts)",
-        "data": "synthetic (Markov-chain text per language, docs 1-7 KB, pool tiled)",
-        "config": {"workload": f"config3-shaped: fit {n_bytes} corpus bytes per GPU, {args.langs} languages, "
+        "data": "synthetic (Markov-chain text per language, docs 1-7 KB, drawn on the GPU, untiled)",
+        "config": {"workload": f"config3: fit {n_bytes} corpus bytes per GPU, {args.langs} languages, "
                                f"grams {args.grams}, profile size {args.profile_size}",
                    "docs_per_gpu": n_docs, "corpus_bytes_per_gpu": n_bytes, "windows_per_gpu": windows,
                    "distinct_grams": parts[-1][1], "distinct_gram_language_pairs": st["pairs"],
-                   "table_rows": parts[-1][2],
+                   "table_rows": len(parts[-1][2]),
                    "parallelism": f"dp{world} (corpus sharded; owner-exchange merge + distributed top-K)"},
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
                      for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
         "count_s_per_step": [round(float(p[0].get("count_s", 0.0)), 4) for p in parts],
         "count_windows_per_s": round(windows / count_s, 1),
+        "count_ms_per_gib": round(count_s * 1e3 * (1 << 30) / n_bytes, 2),
         "windows_counted_exactly_once": windows_ok,
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
@@ -364,8 +392,32 @@ def fit_main(args, world, rank, local, dev, backend):
                      "kernel": "count (emit + part2 + reduce + merge)", "count_ms": round(count_s * 1e3, 3),
                      "algorithmic_bytes_per_count": int(algo)},
     }
+    if world > 1 and args.check_merge:
+        # every rank's corpus regenerated on this GPU (same seeds), counted by
+        # the oracle; the merged table (the same on every rank) must equal the
+        # top-K rule over those global counts
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import ldoracle_c as OC
+        datas, offs, langs = [], [], []
+        base = 0
+        for r in range(world):
+            b_, o_, l_ = fit_corpus(args, ls, r, dev)
+            o_ = o_.cpu().numpy()
+            datas.append(b_[:int(o_[-1])].cpu().numpy())
+            offs.append(o_[1:] + base if r else o_ + base)
+            base += int(o_[-1])
+            langs.append(l_.cpu().numpy())
+        okeys, ocnt = OC.count(np.concatenate(datas), np.concatenate(offs), np.concatenate(langs), args.langs, grams)
+        kb = np.frombuffer(b"".join(okeys), dtype=np.uint8)
+        ko = np.zeros(len(okeys) + 1, dtype=np.int64)
+        np.cumsum([len(k) for k in okeys], out=ko[1:])
+        expect = topk_table_from_counts(kb, ko, ocnt, args.profile_size)
+        line["merged_table_matches_oracle"] = bool(parts[-1][2] == expect)
+        line["merge_check"] = {"ranks": world, "global_grams": len(okeys), "table_rows": len(expect)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"], n_s, (okb, oko, ocnt) = cpu_baseline_fit(args, grams, data, off, lang)
+        data_h = d_bytes[:min(n_bytes, 256 << 20)].cpu().numpy()
+        lang_h = d_lang.cpu().numpy()
+        line["cpu_baseline"], n_s, (okb, oko, ocnt) = cpu_baseline_fit(args, grams, data_h, off, lang_h)
         # the GPU count of the same sample documents against the oracle's
         c = DeviceCounts(args.langs, grams, device=local)
         c.count_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), d_lang.data_ptr(), n_s, stream.cuda_stream)

@@ -115,3 +115,44 @@ def tile(data: np.ndarray, offsets: np.ndarray, doc_lang: np.ndarray, n_docs: in
 def texts(data: np.ndarray, offsets: np.ndarray) -> List[str]:
     b = data.tobytes()
     return [b[offsets[i]:offsets[i + 1]].decode("ascii") for i in range(len(offsets) - 1)]
+
+
+def generate_device(ls: LanguageSet, n_docs: int, len_lo: int, len_hi: int, seed: int, device,
+                    chunk_docs: int = 1 << 18):
+    """The same Markov-chain text as generate(), drawn on a GPU with torch (a
+    bench-scale corpus -- config 3's 6.25 GB shard per GPU -- in seconds, not
+    tiled from a small pool).  Deterministic for a seed (torch's GPU Philox
+    generator), not the same draws as generate().  Returns device tensors
+    (bytes uint8 padded to whole dwords + 16, offsets int64 [n + 1], lang int32)."""
+    import torch
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    L = ls.n_langs
+    lang = torch.randint(0, L, (n_docs,), generator=g, device=dev, dtype=torch.int64)
+    lens = torch.randint(len_lo, len_hi + 1, (n_docs,), generator=g, device=dev, dtype=torch.int64)
+    off = torch.zeros(n_docs + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=off[1:])
+    total = int(off[-1].item())
+    out = torch.zeros(((total + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
+    alpha = torch.from_numpy(ls.alpha).to(dev).reshape(-1)              # [L * S]
+    nxt = torch.from_numpy(ls.nxt).to(dev).reshape(-1)                  # [L * S * 4096]
+    size = torch.from_numpy(ls.size.astype(np.int64)).to(dev)
+    S = ls.alpha.shape[1]
+    for c0 in range(0, n_docs, chunk_docs):
+        c1 = min(n_docs, c0 + chunk_docs)
+        cl = lang[c0:c1]
+        maxlen = int(lens[c0:c1].max().item()) if c1 > c0 else 0
+        state = torch.randint(0, 1 << 16, (c1 - c0,), generator=g, device=dev, dtype=torch.int64) % size[cl]
+        grid = torch.empty((c1 - c0, maxlen), dtype=torch.uint8, device=dev)
+        abase = cl * S
+        nbase = cl * (S << _QBITS)
+        for t in range(maxlen):
+            grid[:, t] = alpha[abase + state]
+            u = torch.randint(0, 1 << _QBITS, (c1 - c0,), generator=g, device=dev, dtype=torch.int64)
+            state = nxt[nbase + (state << _QBITS) + u].to(torch.int64)
+        mask = torch.arange(maxlen, device=dev)[None, :] < lens[c0:c1, None]
+        b0, b1 = int(off[c0].item()), int(off[c1].item())
+        out[b0:b1] = grid[mask]
+        del grid, mask
+    return out, off, lang.to(torch.int32)

@@ -451,3 +451,25 @@ def test_sparse_export_ranges_and_add(grams):
     assert k2 == keys and np.array_equal(c2, 2 * cnt)
     with pytest.raises(ValueError, match="outside"):
         a.export_sparse(n, 1)
+
+
+def test_bench_fit_two_ranks_merged_table_matches_oracle():
+    """bench.py --mode fit --gpus 2 over the host transport (gloo; two ranks
+    on this box's GPU): each rank counts its own GPU-drawn shard, the owner
+    exchange sends sparse (gram, language, count) pairs, the distributed top-K
+    builds the table; the merged table equals the top-K rule over the
+    oracle's counts of both shards together."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LDGPU_BENCH_BACKEND="gloo")
+    out = os.path.join(root, "gpurun_out", "test_fit_world2.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--mode", "fit", "--gpus", "2", "--fit-bytes", "3000000",
+           "--steps", "1", "--warmup", "0", "--profile-size", "200", "--check-merge", "--json-out", out]
+    r = subprocess.run(cmd, env=env, cwd=root, timeout=240, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(open(out).read())
+    assert line["n_gpus"] == 2
+    assert line["merged_table_matches_oracle"] is True, line.get("merge_check")
+    assert line["windows_counted_exactly_once"] is True
