@@ -4,22 +4,65 @@
  * symbol names) and the C ABI of libldgpu.so (include/ldgpu.h).
  *
  * Every buffer is a direct java.nio.ByteBuffer in native byte order; the shim
- * passes its address straight through (no copies).  Handles are the C
- * pointers as jlong.  Status codes are returned unchanged; the Scala side
- * turns them into the reference's exceptions (LdgpuNative.check).
+ * passes its address straight through (no copies) after checking that the
+ * buffer's capacity covers every byte the call reads or writes (the C ABI
+ * trusts its pointers: a short buffer would be read or written past its end).
+ * A short or missing buffer fails the call with LDGPU_EINVAL and a message of
+ * the shim's own (lastError).  Handles are the C pointers as jlong.  Status
+ * codes are returned unchanged; the Scala side turns them into the
+ * reference's exceptions (LdgpuNative.check).
  *
  * Build (on a box with a JDK; not in this image):
  *   make -C jni JAVA_HOME=/usr/lib/jvm/java-8-openjdk-amd64
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include "../include/ldgpu.h"
 
 #define FN(name) Java_org_apache_spark_ml_feature_languagedetection_LdgpuNative_00024_##name
 
+/* the shim's own failure message (a buffer check), else the library's */
+static __thread char jerr[256];
+
+static void jclear(void) { jerr[0] = 0; }
+
 static void* addr(JNIEnv* env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
+
+/* LDGPU_OK when `buf` is a direct buffer of at least `bytes` bytes (or the
+ * call touches none of it), else LDGPU_EINVAL with a message */
+static int need(JNIEnv* env, jobject buf, int64_t bytes, const char* what) {
+    if (bytes <= 0) return LDGPU_OK;
+    if (!buf) {
+        snprintf(jerr, sizeof jerr, "%s is null but %lld bytes are needed", what, (long long)bytes);
+        return LDGPU_EINVAL;
+    }
+    const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (cap < 0 || !addr(env, buf)) {
+        snprintf(jerr, sizeof jerr, "%s is not a direct buffer", what);
+        return LDGPU_EINVAL;
+    }
+    if ((int64_t)cap < bytes) {
+        snprintf(jerr, sizeof jerr, "%s holds %lld bytes, the call needs %lld", what, (long long)cap,
+                 (long long)bytes);
+        return LDGPU_EINVAL;
+    }
+    return LDGPU_OK;
+}
+
+/* offsets[n] of a checked int64 offsets buffer (its last entry), or -1 */
+static int64_t last_offset(JNIEnv* env, jobject offsets, int64_t n) {
+    const int64_t* o = (const int64_t*)addr(env, offsets);
+    return o ? o[n] : -1;
+}
+
+#define CHECK(expr)                      \
+    do {                                 \
+        const int rc_ = (expr);          \
+        if (rc_ != LDGPU_OK) return rc_; \
+    } while (0)
 
 static int put_handle(JNIEnv* env, jlongArray out, void* h, int rc) {
     if (rc == LDGPU_OK) {
@@ -41,11 +84,12 @@ static void ints_release(JNIEnv* env, jintArray a, int32_t* p) {
 
 JNIEXPORT jstring JNICALL FN(lastError)(JNIEnv* env, jobject self) {
     (void)self;
-    return (*env)->NewStringUTF(env, ldgpu_last_error());
+    return (*env)->NewStringUTF(env, jerr[0] ? jerr : ldgpu_last_error());
 }
 
 JNIEXPORT jint JNICALL FN(ctxCreate)(JNIEnv* env, jobject self, jint device, jlongArray out) {
     (void)self;
+    jclear();
     ldgpu_ctx* c = NULL;
     const int rc = ldgpu_ctx_create(device, &c);
     return put_handle(env, out, c, rc);
@@ -54,13 +98,15 @@ JNIEXPORT jint JNICALL FN(ctxCreate)(JNIEnv* env, jobject self, jint device, jlo
 /* pinned host memory wrapped as a direct ByteBuffer (NULL on failure) */
 JNIEXPORT jobject JNICALL FN(hostAlloc)(JNIEnv* env, jobject self, jlong ctx, jlong bytes) {
     (void)self;
+    jclear();
     void* p = NULL;
-    if (ldgpu_host_alloc((ldgpu_ctx*)(intptr_t)ctx, bytes, &p) != LDGPU_OK || !p) return NULL;
+    if (bytes < 0 || ldgpu_host_alloc((ldgpu_ctx*)(intptr_t)ctx, bytes, &p) != LDGPU_OK || !p) return NULL;
     return (*env)->NewDirectByteBuffer(env, p, bytes > 0 ? bytes : 1);
 }
 
 JNIEXPORT jint JNICALL FN(hostFree)(JNIEnv* env, jobject self, jlong ctx, jobject buf) {
     (void)self;
+    jclear();
     return ldgpu_host_free((ldgpu_ctx*)(intptr_t)ctx, addr(env, buf));
 }
 
@@ -68,6 +114,13 @@ JNIEXPORT jint JNICALL FN(modelCreate)(JNIEnv* env, jobject self, jlong ctx, jlo
                                        jobject key_offsets, jobject rows, jobject row_ok, jint n_langs,
                                        jintArray gram_lengths, jlongArray out) {
     (void)self;
+    jclear();
+    if (n_rows < 0 || n_langs < 1) return ldgpu_model_create((ldgpu_ctx*)(intptr_t)ctx, n_rows, NULL, NULL, NULL,
+                                                             NULL, n_langs, NULL, 0, NULL);  /* its own EINVAL */
+    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
+    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n_rows), "keyBytes"));
+    CHECK(need(env, rows, 8 * n_rows * (int64_t)n_langs, "rows"));
+    if (row_ok) CHECK(need(env, row_ok, n_rows, "rowOk"));
     jsize ng = 0;
     int32_t* g = ints(env, gram_lengths, &ng);
     ldgpu_model* m = NULL;
@@ -78,16 +131,46 @@ JNIEXPORT jint JNICALL FN(modelCreate)(JNIEnv* env, jobject self, jlong ctx, jlo
     return put_handle(env, out, m, rc);
 }
 
+JNIEXPORT jint JNICALL FN(modelCreateMasks)(JNIEnv* env, jobject self, jlong ctx, jlong n_rows, jobject key_bytes,
+                                            jobject key_offsets, jobject masks, jobject vals, jint n_langs,
+                                            jintArray gram_lengths, jlongArray out) {
+    (void)self;
+    jclear();
+    if (n_rows < 0 || n_langs < 1)
+        return ldgpu_model_create_masks((ldgpu_ctx*)(intptr_t)ctx, n_rows, NULL, NULL, NULL, NULL, n_langs, NULL, 0,
+                                        NULL);  /* its own EINVAL */
+    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
+    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n_rows), "keyBytes"));
+    CHECK(need(env, masks, 8 * n_rows * (int64_t)((n_langs + 63) / 64), "masks"));
+    CHECK(need(env, vals, 8 * n_rows, "vals"));
+    jsize ng = 0;
+    int32_t* g = ints(env, gram_lengths, &ng);
+    ldgpu_model* m = NULL;
+    const int rc = ldgpu_model_create_masks((ldgpu_ctx*)(intptr_t)ctx, n_rows, (const uint8_t*)addr(env, key_bytes),
+                                            (const int64_t*)addr(env, key_offsets),
+                                            (const uint64_t*)addr(env, masks), (const double*)addr(env, vals),
+                                            n_langs, g, ng, &m);
+    ints_release(env, gram_lengths, g);
+    return put_handle(env, out, m, rc);
+}
+
 JNIEXPORT jint JNICALL FN(modelDestroy)(JNIEnv* env, jobject self, jlong model) {
     (void)env;
     (void)self;
+    jclear();
     return ldgpu_model_destroy((ldgpu_model*)(intptr_t)model);
 }
 
 /* ldgpu_score: thread-safe; concurrent task threads run on their own streams */
 JNIEXPORT jint JNICALL FN(score)(JNIEnv* env, jobject self, jlong model, jobject bytes, jobject offsets,
-                                 jlong n_docs, jobject labels, jobject scores) {
+                                 jlong n_docs, jobject labels, jobject scores, jint n_langs) {
     (void)self;
+    jclear();
+    if (n_docs < 0) return ldgpu_score((ldgpu_model*)(intptr_t)model, NULL, NULL, n_docs, NULL, NULL);
+    CHECK(need(env, offsets, 8 * (n_docs + 1), "offsets"));
+    CHECK(need(env, bytes, last_offset(env, offsets, n_docs), "bytes"));
+    CHECK(need(env, labels, 4 * n_docs, "labels"));
+    if (scores) CHECK(need(env, scores, 8 * n_docs * (int64_t)n_langs, "scores"));
     return ldgpu_score((ldgpu_model*)(intptr_t)model, (const uint8_t*)addr(env, bytes),
                        (const int64_t*)addr(env, offsets), n_docs, (int32_t*)addr(env, labels),
                        (double*)addr(env, scores));
@@ -96,6 +179,7 @@ JNIEXPORT jint JNICALL FN(score)(JNIEnv* env, jobject self, jlong model, jobject
 JNIEXPORT jint JNICALL FN(countsCreate)(JNIEnv* env, jobject self, jlong ctx, jint n_langs, jintArray gram_lengths,
                                         jlong capacity_hint, jlongArray out) {
     (void)self;
+    jclear();
     jsize ng = 0;
     int32_t* g = ints(env, gram_lengths, &ng);
     ldgpu_counts* c = NULL;
@@ -107,18 +191,25 @@ JNIEXPORT jint JNICALL FN(countsCreate)(JNIEnv* env, jobject self, jlong ctx, ji
 JNIEXPORT jint JNICALL FN(countsDestroy)(JNIEnv* env, jobject self, jlong counts) {
     (void)env;
     (void)self;
+    jclear();
     return ldgpu_counts_destroy((ldgpu_counts*)(intptr_t)counts);
 }
 
 JNIEXPORT jint JNICALL FN(count)(JNIEnv* env, jobject self, jlong counts, jobject bytes, jobject offsets,
                                  jobject doc_lang, jlong n_docs) {
     (void)self;
+    jclear();
+    if (n_docs < 0) return ldgpu_count((ldgpu_counts*)(intptr_t)counts, NULL, NULL, NULL, n_docs);
+    CHECK(need(env, offsets, 8 * (n_docs + 1), "offsets"));
+    CHECK(need(env, bytes, last_offset(env, offsets, n_docs), "bytes"));
+    CHECK(need(env, doc_lang, 4 * n_docs, "docLang"));
     return ldgpu_count((ldgpu_counts*)(intptr_t)counts, (const uint8_t*)addr(env, bytes),
                        (const int64_t*)addr(env, offsets), (const int32_t*)addr(env, doc_lang), n_docs);
 }
 
 JNIEXPORT jint JNICALL FN(countsSize)(JNIEnv* env, jobject self, jlong counts, jlongArray out) {
     (void)self;
+    jclear();
     int64_t v[2] = {0, 0};
     const int rc = ldgpu_counts_size((ldgpu_counts*)(intptr_t)counts, &v[0], &v[1]);
     if (rc == LDGPU_OK) {
@@ -129,21 +220,83 @@ JNIEXPORT jint JNICALL FN(countsSize)(JNIEnv* env, jobject self, jlong counts, j
 }
 
 JNIEXPORT jint JNICALL FN(countsExport)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
-                                        jobject key_offsets, jobject counts_out) {
+                                        jobject key_offsets, jobject counts_out, jint n_langs) {
     (void)self;
+    jclear();
+    int64_t n = 0, nb = 0;
+    CHECK(ldgpu_counts_size((ldgpu_counts*)(intptr_t)counts, &n, &nb));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
+    CHECK(need(env, counts_out, 8 * n * (int64_t)n_langs, "counts"));
     return ldgpu_counts_export((ldgpu_counts*)(intptr_t)counts, (uint8_t*)addr(env, key_bytes),
                                (int64_t*)addr(env, key_offsets), (int64_t*)addr(env, counts_out));
 }
 
-JNIEXPORT jint JNICALL FN(countsAdd)(JNIEnv* env, jobject self, jlong counts, jlong n, jobject key_bytes,
-                                     jobject key_offsets, jobject rows) {
+/* out(0) = key bytes, out(1) = (language, count) pairs of grams [first, first + n) */
+JNIEXPORT jint JNICALL FN(countsSparseSize)(JNIEnv* env, jobject self, jlong counts, jlong first, jlong n,
+                                            jlongArray out) {
     (void)self;
+    jclear();
+    int64_t v[2] = {0, 0};
+    const int rc = ldgpu_counts_sparse_size((ldgpu_counts*)(intptr_t)counts, first, n, &v[0], &v[1]);
+    if (rc == LDGPU_OK) {
+        jlong j[2] = {(jlong)v[0], (jlong)v[1]};
+        (*env)->SetLongArrayRegion(env, out, 0, 2, j);
+    }
+    return rc;
+}
+
+JNIEXPORT jint JNICALL FN(countsExportSparse)(JNIEnv* env, jobject self, jlong counts, jlong first, jlong n,
+                                              jobject key_bytes, jobject key_offsets, jobject pair_offsets,
+                                              jobject pair_langs, jobject pair_counts) {
+    (void)self;
+    jclear();
+    int64_t nb = 0, np = 0;
+    CHECK(ldgpu_counts_sparse_size((ldgpu_counts*)(intptr_t)counts, first, n, &nb, &np));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
+    CHECK(need(env, pair_offsets, 8 * (n + 1), "pairOffsets"));
+    CHECK(need(env, pair_langs, 4 * np, "pairLangs"));
+    CHECK(need(env, pair_counts, 8 * np, "pairCounts"));
+    return ldgpu_counts_export_sparse((ldgpu_counts*)(intptr_t)counts, first, n, (uint8_t*)addr(env, key_bytes),
+                                      (int64_t*)addr(env, key_offsets), (int64_t*)addr(env, pair_offsets),
+                                      (int32_t*)addr(env, pair_langs), (int64_t*)addr(env, pair_counts));
+}
+
+JNIEXPORT jint JNICALL FN(countsAddSparse)(JNIEnv* env, jobject self, jlong counts, jlong n, jobject key_bytes,
+                                           jobject key_offsets, jobject pair_offsets, jobject pair_langs,
+                                           jobject pair_counts) {
+    (void)self;
+    jclear();
+    if (n <= 0)
+        return ldgpu_counts_add_sparse((ldgpu_counts*)(intptr_t)counts, n, NULL, NULL, NULL, NULL, NULL);
+    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
+    CHECK(need(env, pair_offsets, 8 * (n + 1), "pairOffsets"));
+    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n), "keyBytes"));
+    const int64_t* po = (const int64_t*)addr(env, pair_offsets);
+    const int64_t np = po[n] - po[0];
+    CHECK(need(env, pair_langs, 4 * np, "pairLangs"));
+    CHECK(need(env, pair_counts, 8 * np, "pairCounts"));
+    return ldgpu_counts_add_sparse((ldgpu_counts*)(intptr_t)counts, n, (const uint8_t*)addr(env, key_bytes),
+                                   (const int64_t*)addr(env, key_offsets), po, (const int32_t*)addr(env, pair_langs),
+                                   (const int64_t*)addr(env, pair_counts));
+}
+
+JNIEXPORT jint JNICALL FN(countsAdd)(JNIEnv* env, jobject self, jlong counts, jlong n, jobject key_bytes,
+                                     jobject key_offsets, jobject rows, jint n_langs) {
+    (void)self;
+    jclear();
+    if (n <= 0) return ldgpu_counts_add((ldgpu_counts*)(intptr_t)counts, n, NULL, NULL, NULL);
+    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
+    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n), "keyBytes"));
+    CHECK(need(env, rows, 8 * n * (int64_t)n_langs, "rows"));
     return ldgpu_counts_add((ldgpu_counts*)(intptr_t)counts, n, (const uint8_t*)addr(env, key_bytes),
                             (const int64_t*)addr(env, key_offsets), (const int64_t*)addr(env, rows));
 }
 
 JNIEXPORT jint JNICALL FN(fitTableSize)(JNIEnv* env, jobject self, jlong counts, jint profile_size, jlongArray out) {
     (void)self;
+    jclear();
     int64_t v[2] = {0, 0};
     const int rc = ldgpu_fit_table_size((ldgpu_counts*)(intptr_t)counts, profile_size, &v[0], &v[1]);
     if (rc == LDGPU_OK) {
@@ -153,16 +306,38 @@ JNIEXPORT jint JNICALL FN(fitTableSize)(JNIEnv* env, jobject self, jlong counts,
     return rc;
 }
 
+/* n_rows / key_bytes_n: what fitTableSize returned for the cached table */
 JNIEXPORT jint JNICALL FN(fitTableExport)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
-                                          jobject key_offsets, jobject rows) {
+                                          jobject key_offsets, jobject rows, jlong n_rows, jlong key_bytes_n,
+                                          jint n_langs) {
     (void)self;
+    jclear();
+    CHECK(need(env, key_bytes, key_bytes_n, "keyBytes"));
+    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
+    CHECK(need(env, rows, 8 * n_rows * (int64_t)n_langs, "rows"));
     return ldgpu_fit_table_export((ldgpu_counts*)(intptr_t)counts, (uint8_t*)addr(env, key_bytes),
                                   (int64_t*)addr(env, key_offsets), (double*)addr(env, rows));
+}
+
+/* the same table in mask form: masks [n_rows][ceil(n_langs / 64)], vals [n_rows] */
+JNIEXPORT jint JNICALL FN(fitTableExportMasks)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
+                                               jobject key_offsets, jobject masks, jobject vals, jlong n_rows,
+                                               jlong key_bytes_n, jint n_langs) {
+    (void)self;
+    jclear();
+    CHECK(need(env, key_bytes, key_bytes_n, "keyBytes"));
+    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
+    CHECK(need(env, masks, 8 * n_rows * (int64_t)((n_langs + 63) / 64), "masks"));
+    CHECK(need(env, vals, 8 * n_rows, "vals"));
+    return ldgpu_fit_table_export_masks((ldgpu_counts*)(intptr_t)counts, (uint8_t*)addr(env, key_bytes),
+                                        (int64_t*)addr(env, key_offsets), (uint64_t*)addr(env, masks),
+                                        (double*)addr(env, vals));
 }
 
 /* ---- multi-GPU merge: one task per GPU (Spark barrier execution) */
 JNIEXPORT jbyteArray JNICALL FN(commUniqueId)(JNIEnv* env, jobject self) {
     (void)self;
+    jclear();
     uint8_t id[LDGPU_COMM_ID_BYTES];
     if (ldgpu_comm_unique_id(id) != LDGPU_OK) return NULL;
     jbyteArray a = (*env)->NewByteArray(env, LDGPU_COMM_ID_BYTES);
@@ -173,8 +348,12 @@ JNIEXPORT jbyteArray JNICALL FN(commUniqueId)(JNIEnv* env, jobject self) {
 JNIEXPORT jint JNICALL FN(commCreateRccl)(JNIEnv* env, jobject self, jlong ctx, jbyteArray id, jint rank,
                                           jint world, jlongArray out) {
     (void)self;
+    jclear();
     uint8_t buf[LDGPU_COMM_ID_BYTES];
-    if (!id || (*env)->GetArrayLength(env, id) != LDGPU_COMM_ID_BYTES) return LDGPU_EINVAL;
+    if (!id || (*env)->GetArrayLength(env, id) != LDGPU_COMM_ID_BYTES) {
+        snprintf(jerr, sizeof jerr, "communicator id must hold %d bytes", LDGPU_COMM_ID_BYTES);
+        return LDGPU_EINVAL;
+    }
     (*env)->GetByteArrayRegion(env, id, 0, LDGPU_COMM_ID_BYTES, (jbyte*)buf);
     ldgpu_comm* m = NULL;
     const int rc = ldgpu_comm_create_rccl((ldgpu_ctx*)(intptr_t)ctx, buf, rank, world, &m);
@@ -184,11 +363,13 @@ JNIEXPORT jint JNICALL FN(commCreateRccl)(JNIEnv* env, jobject self, jlong ctx, 
 JNIEXPORT jint JNICALL FN(commDestroy)(JNIEnv* env, jobject self, jlong comm) {
     (void)env;
     (void)self;
+    jclear();
     return ldgpu_comm_destroy((ldgpu_comm*)(intptr_t)comm);
 }
 
 JNIEXPORT jint JNICALL FN(countsMerge)(JNIEnv* env, jobject self, jlong counts, jlong comm) {
     (void)env;
     (void)self;
+    jclear();
     return ldgpu_counts_merge((ldgpu_counts*)(intptr_t)counts, (ldgpu_comm*)(intptr_t)comm);
 }

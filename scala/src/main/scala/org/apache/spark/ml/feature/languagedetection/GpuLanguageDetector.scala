@@ -66,25 +66,51 @@ class LanguageDetector(val uid: String,
   }
 }
 
+/** One gram's nonzero (language, count) pairs, languages ascending: the sparse
+  * row of the count table that crosses the shuffle (~1.3 pairs per gram on
+  * the fit corpora against nLangs dense Longs). */
+final case class SparseCounts(langs: Array[Int], counts: Array[Long]) {
+  /** the sum of two rows (a merge of the two sorted language lists) */
+  def +(o: SparseCounts): SparseCounts = {
+    val l = new Array[Int](langs.length + o.langs.length)
+    val c = new Array[Long](l.length)
+    var (i, j, k) = (0, 0, 0)
+    while (i < langs.length || j < o.langs.length) {
+      if (j == o.langs.length || (i < langs.length && langs(i) < o.langs(j))) {
+        l(k) = langs(i); c(k) = counts(i); i += 1
+      } else if (i == langs.length || o.langs(j) < langs(i)) {
+        l(k) = o.langs(j); c(k) = o.counts(j); j += 1
+      } else {
+        l(k) = langs(i); c(k) = counts(i) + o.counts(j); i += 1; j += 1
+      }
+      k += 1
+    }
+    SparseCounts(java.util.Arrays.copyOf(l, k), java.util.Arrays.copyOf(c, k))
+  }
+}
+
 object LanguageDetector extends Logging {
 
   /** documents / bytes per ldgpu_count call */
   var batchDocs: Int = 1 << 20
   var batchBytes: Int = 64 << 20
+  /** grams per ranged sparse export / import (each range's buffers stay < 2 GiB) */
+  var rangeGrams: Long = 1L << 20
 
   /**
     * computeGramProbabilities (LanguageDetector.scala:145-165) on the GPUs:
     *  1. every partition counts its rows on its executor's GPU (ldgpu_count:
     *     computeGrams + reduceGrams for the partition) and emits one row per
-    *     distinct gram: (key, counts[L]);
-    *  2. one shuffle sums those rows per gram (integer sums: the reference's
-    *     counts, bit-exact) -- instead of the reference's L + 1 shuffles of
-    *     every window record;
+    *     distinct gram: (key, its nonzero (language, count) pairs);
+    *  2. one shuffle sums those sparse rows per gram (integer sums: the
+    *     reference's counts, bit-exact) -- instead of the reference's L + 1
+    *     shuffles of every window record;
     *  3. every partition of the global rows -- each gram in exactly one, with
     *     its global counts, hence its global presence class -- builds its own
     *     top-K table on its GPU (ldgpu_fit_table_size): per language the K best
     *     by (value, then (length, bytes)), which holds every gram of the global
-    *     top-K that lives in the partition;
+    *     top-K that lives in the partition; it leaves in mask form (key, mask
+    *     words, value);
     *  4. the driver keeps, per language, the K best candidates (same order).
     * Ties follow the build's deterministic (length, unsigned bytes) rule where
     * the reference's follow Spark's shuffle order (DESIGN.md, stated
@@ -101,24 +127,17 @@ object LanguageDetector extends Logging {
     val nLangs = supportedLanguages.length
     val index = supportedLanguages.zipWithIndex.toMap
     val grams = gramLengths.toArray
-    val (docs, bytes) = (batchDocs, batchBytes)
-    val counted = data.rdd.mapPartitions(it => countPartition(it, index, nLangs, grams, docs, bytes))
-    val global = counted.reduceByKey { (a, b) =>
-      val s = new Array[Long](a.length)
-      var l = 0
-      while (l < a.length) {
-        s(l) = a(l) + b(l)
-        l += 1
-      }
-      s
-    }
-    val candidates = global.mapPartitions(it => partitionTopK(it, nLangs, grams, languageProfileSize))
+    val (docs, bytes, range) = (batchDocs, batchBytes, rangeGrams)
+    val counted = data.rdd.mapPartitions(it => countPartition(it, index, nLangs, grams, docs, bytes, range))
+    val global = counted.reduceByKey(_ + _)
+    val candidates = global.mapPartitions(it => partitionTopK(it, nLangs, grams, languageProfileSize, range))
     val table = selectTopK(candidates.collect(), nLangs, languageProfileSize)
     spark.createDataset(table.toSeq)
   }
 
   private def countPartition(it: Iterator[(String, String)], index: Map[String, Int], nLangs: Int,
-                             grams: Array[Int], docs: Int, bytes: Int): Iterator[(String, Array[Long])] = {
+                             grams: Array[Int], docs: Int, bytes: Int,
+                             range: Long): Iterator[(String, SparseCounts)] = {
     if (!it.hasNext) return Iterator.empty
     val ctx = LdgpuNative.context()
     val out = new Array[Long](1)
@@ -134,7 +153,7 @@ object LanguageDetector extends Logging {
         }
         LdgpuNative.check(LdgpuNative.count(counts, batch.bytes, batch.offsets, batch.langs, batch.n.toLong))
       }
-      exportCounts(counts, nLangs).iterator
+      exportCounts(counts, range).iterator
     } finally {
       batch.close()
       LdgpuNative.countsDestroy(counts)
@@ -142,35 +161,56 @@ object LanguageDetector extends Logging {
   }
 
   /** (key bytes as an ISO-8859-1 string: one char per byte, a hashable
-    * shuffle key; counts[L]) of every distinct gram of a count table */
-  private def exportCounts(counts: Long, nLangs: Int): Array[(String, Array[Long])] = {
+    * shuffle key; its sparse counts) of every distinct gram of a count table,
+    * exported in ranges of at most `range` grams (halved while a range's
+    * buffers would pass 1 GiB) */
+  private def exportCounts(counts: Long, range: Long): Array[(String, SparseCounts)] = {
     val size = new Array[Long](2)
     LdgpuNative.check(LdgpuNative.countsSize(counts, size))
-    val (n, nb) = (size(0).toInt, size(1))
-    val kb = LdgpuNative.direct(nb)
-    val ko = LdgpuNative.direct(8L * (n + 1))
-    val cs = LdgpuNative.direct(8L * n * nLangs)
-    LdgpuNative.check(LdgpuNative.countsExport(counts, kb, ko, cs))
-    Array.tabulate(n) { i =>
-      val (a, b) = (ko.getLong(8 * i).toInt, ko.getLong(8 * (i + 1)).toInt)
-      val key = new Array[Byte](b - a)
-      var j = 0
-      while (j < key.length) {
-        key(j) = kb.get(a + j)
-        j += 1
+    val total = size(0)
+    val out = new java.util.ArrayList[(String, SparseCounts)](math.min(total, Int.MaxValue - 8).toInt)
+    var first = 0L
+    while (first < total) {
+      var n = math.min(range, total - first)
+      val sz = new Array[Long](2)
+      LdgpuNative.check(LdgpuNative.countsSparseSize(counts, first, n, sz))
+      while (n > 1 && (sz(0) > (1L << 30) || 8L * sz(1) > (1L << 30) || 8L * (n + 1) > (1L << 30))) {
+        n = n / 2
+        LdgpuNative.check(LdgpuNative.countsSparseSize(counts, first, n, sz))
       }
-      val row = new Array[Long](nLangs)
-      var l = 0
-      while (l < nLangs) {
-        row(l) = cs.getLong(8 * (i * nLangs + l))
-        l += 1
+      val kb = LdgpuNative.direct(sz(0))
+      val ko = LdgpuNative.direct(8L * (n + 1))
+      val po = LdgpuNative.direct(8L * (n + 1))
+      val pl = LdgpuNative.direct(4L * sz(1))
+      val pc = LdgpuNative.direct(8L * sz(1))
+      LdgpuNative.check(LdgpuNative.countsExportSparse(counts, first, n, kb, ko, po, pl, pc))
+      var i = 0
+      while (i < n) {
+        val (a, b) = (ko.getLong(8 * i).toInt, ko.getLong(8 * (i + 1)).toInt)
+        val key = new Array[Byte](b - a)
+        kb.position(a)
+        kb.get(key)
+        val (p0, p1) = (po.getLong(8 * i).toInt, po.getLong(8 * (i + 1)).toInt)
+        val langs = new Array[Int](p1 - p0)
+        val cnts = new Array[Long](p1 - p0)
+        var j = 0
+        while (j < langs.length) {
+          langs(j) = pl.getInt(4 * (p0 + j))
+          cnts(j) = pc.getLong(8 * (p0 + j))
+          j += 1
+        }
+        out.add((new String(key, ISO_8859_1), SparseCounts(langs, cnts)))
+        i += 1
       }
-      (new String(key, ISO_8859_1), row)
+      first += n
     }
+    out.toArray(new Array[(String, SparseCounts)](out.size))
   }
 
-  private def partitionTopK(it: Iterator[(String, Array[Long])], nLangs: Int, grams: Array[Int],
-                            profileSize: Int): Iterator[(Array[Byte], Array[Double])] = {
+  /** the partition's global rows into a device table (ranged sparse imports),
+    * its top-K table out in mask form: (key, mask words, value) */
+  private def partitionTopK(it: Iterator[(String, SparseCounts)], nLangs: Int, grams: Array[Int],
+                            profileSize: Int, range: Long): Iterator[(Array[Byte], Array[Long], Double)] = {
     val rows = it.toArray
     if (rows.isEmpty) return Iterator.empty
     val ctx = LdgpuNative.context()
@@ -178,38 +218,68 @@ object LanguageDetector extends Logging {
     LdgpuNative.check(LdgpuNative.countsCreate(ctx, nLangs, grams, rows.length.toLong, out))
     val counts = out(0)
     try {
-      val keys = rows.map(_._1.getBytes(ISO_8859_1))
-      val ko = LdgpuNative.direct(8L * (keys.length + 1))
-      var off = 0L
-      ko.putLong(0, 0L)
-      keys.indices.foreach { i =>
-        off += keys(i).length
-        ko.putLong(8 * (i + 1), off)
-      }
-      val kb = LdgpuNative.direct(off)
-      keys.foreach(k => kb.put(k))
-      kb.flip()
-      val cs = LdgpuNative.direct(8L * rows.length * nLangs)
-      rows.iterator.zipWithIndex.foreach { case ((_, row), i) =>
-        var l = 0
-        while (l < nLangs) {
-          cs.putLong(8 * (i * nLangs + l), row(l))
-          l += 1
+      var first = 0
+      while (first < rows.length) {
+        // the next range: at most `range` rows, its buffers within 1 GiB each
+        var n = 0
+        var keyBytes = 0L
+        var pairs = 0L
+        def fits(r: Int): Boolean = n == 0 ||
+          (n < range && keyBytes + rows(r)._1.length <= (1L << 30) && 8L * (pairs + rows(r)._2.langs.length) <= (1L << 30))
+        while (first + n < rows.length && fits(first + n)) {
+          keyBytes += rows(first + n)._1.length
+          pairs += rows(first + n)._2.langs.length
+          n += 1
         }
+        var i = 0
+        val kb = LdgpuNative.direct(keyBytes)
+        val ko = LdgpuNative.direct(8L * (n + 1))
+        val po = LdgpuNative.direct(8L * (n + 1))
+        val pl = LdgpuNative.direct(4L * pairs)
+        val pc = LdgpuNative.direct(8L * pairs)
+        var (ko_, po_) = (0L, 0L)
+        ko.putLong(0, 0L)
+        po.putLong(0, 0L)
+        i = 0
+        while (i < n) {
+          val (key, sc) = rows(first + i)
+          kb.put(key.getBytes(ISO_8859_1))
+          ko_ += key.length
+          ko.putLong(8 * (i + 1), ko_)
+          var j = 0
+          while (j < sc.langs.length) {
+            pl.putInt(4 * (po_ + j).toInt, sc.langs(j))
+            pc.putLong(8 * (po_ + j).toInt, sc.counts(j))
+            j += 1
+          }
+          po_ += sc.langs.length
+          po.putLong(8 * (i + 1), po_)
+          i += 1
+        }
+        kb.flip()
+        LdgpuNative.check(LdgpuNative.countsAddSparse(counts, n.toLong, kb, ko, po, pl, pc))
+        first += n
       }
-      LdgpuNative.check(LdgpuNative.countsAdd(counts, rows.length.toLong, kb, ko, cs))
       val size = new Array[Long](2)
       LdgpuNative.check(LdgpuNative.fitTableSize(counts, profileSize, size))
-      val (n, nb) = (size(0).toInt, size(1))
+      val (n, nb) = (size(0), size(1))
+      val s = (nLangs + 63) / 64
       val tkb = LdgpuNative.direct(nb)
       val tko = LdgpuNative.direct(8L * (n + 1))
-      val trw = LdgpuNative.direct(8L * n * nLangs)
-      LdgpuNative.check(LdgpuNative.fitTableExport(counts, tkb, tko, trw))
-      Array.tabulate(n) { i =>
+      val tmk = LdgpuNative.direct(8L * n * s)
+      val tvl = LdgpuNative.direct(8L * n)
+      LdgpuNative.check(LdgpuNative.fitTableExportMasks(counts, tkb, tko, tmk, tvl, n, nb, nLangs))
+      Iterator.tabulate(n.toInt) { i =>
         val (a, b) = (tko.getLong(8 * i).toInt, tko.getLong(8 * (i + 1)).toInt)
-        val key = Array.tabulate(b - a)(j => tkb.get(a + j))
-        (key, Array.tabulate(nLangs)(l => trw.getDouble(8 * (i * nLangs + l))))
-      }.iterator
+        val key = new Array[Byte](b - a)
+        var j = 0
+        while (j < key.length) {
+          key(j) = tkb.get(a + j)
+          j += 1
+        }
+        val mask = Array.tabulate(s)(w => tmk.getLong(8 * (i * s + w)))
+        (key, mask, tvl.getDouble(8 * i))
+      }.toArray.iterator
     } finally {
       LdgpuNative.countsDestroy(counts)
     }
@@ -229,20 +299,23 @@ object LanguageDetector extends Logging {
     }
   }
 
-  /** filterTopGrams' final step over the partitions' candidates: per
-    * language the K largest values (ties by key order), union of the picks */
-  private def selectTopK(candidates: Array[(Array[Byte], Array[Double])], nLangs: Int,
+  /** filterTopGrams' final step over the partitions' candidates (mask form):
+    * per language the K largest values (ties by key order), the union of the
+    * picks with their dense rows (the reference's table type) */
+  private def selectTopK(candidates: Array[(Array[Byte], Array[Long], Double)], nLangs: Int,
                          profileSize: Int): Map[Seq[Byte], Array[Double]] = {
     val byKey = candidates.sortWith((a, b) => keyOrder.lt(a._1, b._1))
+    def v(i: Int, l: Int): Double = if (((byKey(i)._2(l / 64) >>> (l % 64)) & 1L) != 0L) byKey(i)._3 else 0.0
     val chosen = new java.util.BitSet(byKey.length)
     var l = 0
     while (l < nLangs) {
       val lang = l
-      val order = byKey.indices.sortBy(i => -byKey(i)._2(lang))  // stable: key order among equal values
+      val order = byKey.indices.sortBy(i => -v(i, lang))  // stable: key order among equal values
       order.take(math.max(profileSize, 0)).foreach(i => chosen.set(i))
       l += 1
     }
-    byKey.indices.filter(i => chosen.get(i)).map(i => (byKey(i)._1.toSeq: Seq[Byte]) -> byKey(i)._2).toMap
+    byKey.indices.filter(i => chosen.get(i))
+      .map(i => (byKey(i)._1.toSeq: Seq[Byte]) -> Array.tabulate(nLangs)(x => v(i, x))).toMap
   }
 
   def save[T](saveFile: String, ds: Dataset[T]): Unit = {

@@ -6,8 +6,12 @@ import org.apache.spark.ml.Model
 import org.apache.spark.ml.param.ParamMap
 import org.apache.spark.ml.param.shared.{HasInputCol, HasOutputCol}
 import org.apache.spark.ml.util._
+import org.apache.spark.TaskContext
+import org.apache.spark.sql.catalyst.InternalRow
+import org.apache.spark.sql.catalyst.expressions.{GenericInternalRow, JoinedRow, UnsafeProjection}
 import org.apache.spark.sql.types.{StringType, StructType}
-import org.apache.spark.sql.{DataFrame, Dataset, Row, SaveMode}
+import org.apache.spark.sql.{DataFrame, Dataset, LdgpuSqlBridge, SaveMode}
+import org.apache.spark.unsafe.types.UTF8String
 import org.json4s.JsonDSL._
 import org.json4s.{DefaultFormats, JArray, JString}
 
@@ -50,60 +54,76 @@ class LanguageDetectorModel(override val uid: String,
     copyValues(m, extra).setParent(parent)
   }
 
+  /**
+    * transform (LanguageDetectorModel.scala:219-240) on the executor's GPU:
+    * the table is broadcast once in packed form (mask form for fit-produced
+    * tables), each partition's rows are read as catalyst rows -- the text as
+    * Spark's own UTF-8 bytes, copied as they are when ASCII (then UTF-8 IS the
+    * reference's low-byte encoding, :161), decoded and low-byte encoded
+    * otherwise -- packed into pinned buffers and scored in batches
+    * (ldgpu_score), and the label is appended to every row.  The device table
+    * and the pinned buffers are released when the task completes, also when
+    * the iterator is not drained (limit, show, a failed task).
+    */
   override def transform(dataset: Dataset[_]): DataFrame = {
     val schema = transformSchema(dataset.schema)
     val spark = dataset.sparkSession
     val table = spark.sparkContext.broadcast(PackedTable.of(gramProbabilities, supportedLanguages.length))
     val grams = gramLenghts.toArray
-    val langs = supportedLanguages.toArray
-    val col = $(inputCol)
+    val nLangs = supportedLanguages.length
+    val labels = supportedLanguages.map(l => UTF8String.fromString(l)).toArray
+    val idx = dataset.schema.fieldIndex($(inputCol))
     val nDocs = batchDocs
     val nBytes = batchBytes
-    val rows = dataset.toDF().rdd.mapPartitions { it =>
+    val df = dataset.toDF()
+    val rows = LdgpuSqlBridge.internalRows(df).mapPartitions { it =>
       if (!it.hasNext) Iterator.empty
       else {
-        val model = LdgpuNative.model(table.id, table.value, grams)
+        val model = LdgpuNative.acquireModel(table.id, table.value, grams)
         val batch = new DocBatch(LdgpuNative.context(), nDocs, nBytes)
-        val pending = new java.util.ArrayList[Row](math.min(nDocs, 1 << 16))
-        new Iterator[Row] {
-          private var out: Iterator[Row] = Iterator.empty
-          private var idx = -1
-          private var open = true
+        val task = TaskContext.get()
+        if (task != null) task.addTaskCompletionListener { _: TaskContext =>
+          batch.close()
+          LdgpuNative.releaseModel(table.id)
+        }
+        val pending = new java.util.ArrayList[InternalRow](math.min(nDocs, 1 << 16))
+        val project = UnsafeProjection.create(schema)
+        new Iterator[InternalRow] {
+          private var out: Iterator[InternalRow] = Iterator.empty
           // the next batch of rows: packed, scored in one ldgpu_score call
           private def fill(): Unit = {
             batch.clear()
             pending.clear()
             while (it.hasNext && !batch.full) {
               val row = it.next()
-              if (idx < 0) idx = row.fieldIndex(col)
-              batch.addScore(row.getString(idx))
-              pending.add(row)
+              val text = row.getUTF8String(idx)
+              if (text == null) throw new NullPointerException(s"null text in column ${schema(idx).name}")
+              batch.addScoreUtf8(text.getBaseObject, text.getBaseOffset, text.numBytes, text.toString)
+              pending.add(row.copy())  // the child iterator may reuse its row object
             }
-            LdgpuNative.check(LdgpuNative.score(model, batch.bytes, batch.offsets, batch.n.toLong, batch.labels, null))
-            val scored = new Array[Row](batch.n)
+            LdgpuNative.check(
+              LdgpuNative.score(model, batch.bytes, batch.offsets, batch.n.toLong, batch.labels, null, nLangs))
+            val scored = new Array[InternalRow](batch.n)
             var i = 0
             while (i < batch.n) {
-              scored(i) = Row.fromSeq(pending.get(i).toSeq :+ langs(batch.label(i)))
+              val label = new GenericInternalRow(Array[Any](labels(batch.label(i))))
+              scored(i) = project(new JoinedRow(pending.get(i), label)).copy()
               i += 1
             }
             out = scored.iterator
           }
           override def hasNext: Boolean = {
             if (!out.hasNext && it.hasNext) fill()
-            if (!out.hasNext && open) {
-              batch.close()
-              open = false
-            }
             out.hasNext
           }
-          override def next(): Row = {
+          override def next(): InternalRow = {
             if (!hasNext) throw new NoSuchElementException
             out.next()
           }
         }
       }
     }
-    spark.createDataFrame(rows, schema)
+    LdgpuSqlBridge.fromInternalRows(spark, rows, schema)
   }
 
   override def write: MLWriter = new LanguageDetectorModel.LanguageDetectorModelWriter(this)
@@ -130,7 +150,7 @@ object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
       offsets.putLong(0, 0L)
       offsets.putLong(8, text.length.toLong)
       val label = LdgpuNative.direct(4)
-      LdgpuNative.check(LdgpuNative.score(model, bytes, offsets, 1L, label, null))
+      LdgpuNative.check(LdgpuNative.score(model, bytes, offsets, 1L, label, null, supportedLanguages.length))
       supportedLanguages(label.getInt(0))
     } finally {
       LdgpuNative.modelDestroy(model)

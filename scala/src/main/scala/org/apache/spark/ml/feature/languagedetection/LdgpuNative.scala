@@ -34,20 +34,36 @@ object LdgpuNative {
   @native def hostFree(ctx: Long, buf: ByteBuffer): Int
   @native def modelCreate(ctx: Long, nRows: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, rows: ByteBuffer,
                           rowOk: ByteBuffer, nLangs: Int, gramLengths: Array[Int], out: Array[Long]): Int
+  /** mask form: row i = vals(i) at the languages set in masks [nRows][ceil(nLangs / 64)] */
+  @native def modelCreateMasks(ctx: Long, nRows: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer,
+                               masks: ByteBuffer, vals: ByteBuffer, nLangs: Int, gramLengths: Array[Int],
+                               out: Array[Long]): Int
   @native def modelDestroy(model: Long): Int
+  /** nLangs: the model's languages (the shim checks a non-null scores buffer's capacity with it) */
   @native def score(model: Long, bytes: ByteBuffer, offsets: ByteBuffer, nDocs: Long, labels: ByteBuffer,
-                    scores: ByteBuffer): Int
+                    scores: ByteBuffer, nLangs: Int): Int
   @native def countsCreate(ctx: Long, nLangs: Int, gramLengths: Array[Int], capacityHint: Long,
                            out: Array[Long]): Int
   @native def countsDestroy(counts: Long): Int
   @native def count(counts: Long, bytes: ByteBuffer, offsets: ByteBuffer, docLang: ByteBuffer, nDocs: Long): Int
   /** out(0) = distinct grams, out(1) = their total key bytes */
   @native def countsSize(counts: Long, out: Array[Long]): Int
-  @native def countsExport(counts: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, counts_ : ByteBuffer): Int
-  @native def countsAdd(counts: Long, n: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, rows: ByteBuffer): Int
+  @native def countsExport(counts: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, counts_ : ByteBuffer,
+                           nLangs: Int): Int
+  @native def countsAdd(counts: Long, n: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, rows: ByteBuffer,
+                        nLangs: Int): Int
+  /** grams [first, first + n) of the (length, bytes) order: out(0) = key bytes, out(1) = (language, count) pairs */
+  @native def countsSparseSize(counts: Long, first: Long, n: Long, out: Array[Long]): Int
+  @native def countsExportSparse(counts: Long, first: Long, n: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer,
+                                 pairOffsets: ByteBuffer, pairLangs: ByteBuffer, pairCounts: ByteBuffer): Int
+  @native def countsAddSparse(counts: Long, n: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer,
+                              pairOffsets: ByteBuffer, pairLangs: ByteBuffer, pairCounts: ByteBuffer): Int
   /** out(0) = table rows, out(1) = their total key bytes */
   @native def fitTableSize(counts: Long, profileSize: Int, out: Array[Long]): Int
-  @native def fitTableExport(counts: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, rows: ByteBuffer): Int
+  @native def fitTableExport(counts: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, rows: ByteBuffer,
+                             nRows: Long, keyBytesN: Long, nLangs: Int): Int
+  @native def fitTableExportMasks(counts: Long, keyBytes: ByteBuffer, keyOffsets: ByteBuffer, masks: ByteBuffer,
+                                  vals: ByteBuffer, nRows: Long, keyBytesN: Long, nLangs: Int): Int
   // multi-GPU merge (Spark with barrier execution: one task per GPU)
   @native def commUniqueId(): Array[Byte]
   @native def commCreateRccl(ctx: Long, id: Array[Byte], rank: Int, world: Int, out: Array[Long]): Int
@@ -65,8 +81,16 @@ object LdgpuNative {
     case _ => throw new RuntimeException(s"libldgpu: ${lastError()}")
   }
 
-  def direct(bytes: Long): ByteBuffer =
+  /** A JVM direct buffer holds at most Int.MaxValue bytes: larger requests
+    * fail here (callers export / import in ranges that stay below it) instead
+    * of wrapping to a small or negative size. */
+  val MaxDirect: Long = Int.MaxValue.toLong
+
+  def direct(bytes: Long): ByteBuffer = {
+    if (bytes < 0L || bytes > MaxDirect)
+      throw new IllegalArgumentException(s"a direct buffer of $bytes bytes is outside [0, $MaxDirect]")
     ByteBuffer.allocateDirect(math.max(bytes, 1L).toInt).order(ByteOrder.nativeOrder())
+  }
 
   /** The executor's GPU: executors are pinned one per GPU (HIP_VISIBLE_DEVICES),
     * so device 0 unless LDGPU_DEVICE says otherwise. */
@@ -89,25 +113,65 @@ object LdgpuNative {
     }
   }
 
-  // device tables of this executor, keyed by the broadcast that carries them
-  private val models = new ConcurrentHashMap[java.lang.Long, java.lang.Long]()
+  // Device tables of this executor, keyed by the broadcast that carries them,
+  // least recently used first.  A transform creates a new broadcast, so the
+  // cache is bounded: at most maxModels tables (and maxModelBytes of their
+  // uploaded host form) stay on the GPU, the least recently used is freed
+  // first -- never one a running task still scores with (refs > 0).
+  var maxModels: Int = 4
+  var maxModelBytes: Long = 8L << 30
 
-  def model(broadcastId: Long, table: PackedTable, gramLengths: Array[Int]): Long = {
+  private final class Entry(val handle: Long, val bytes: Long) {
+    var refs: Int = 0
+  }
+
+  private val models = new java.util.LinkedHashMap[java.lang.Long, Entry](16, 0.75f, true)
+
+  /** The device table of a broadcast, uploaded on first use; pair every call
+    * with releaseModel(broadcastId) once the task is done scoring. */
+  def acquireModel(broadcastId: Long, table: PackedTable, gramLengths: Array[Int]): Long = models.synchronized {
     val have = models.get(broadcastId)
-    if (have != null) have.longValue
-    else models.synchronized {
-      val again = models.get(broadcastId)
-      if (again != null) again.longValue
-      else {
-        val h = table.upload(context(), gramLengths)
-        models.put(broadcastId, h)
-        h
-      }
+    val e = if (have != null) have else {
+      val fresh = new Entry(table.upload(context(), gramLengths), table.hostBytes)
+      models.put(broadcastId, fresh)
+      evict(broadcastId)
+      fresh
+    }
+    e.refs += 1
+    e.handle
+  }
+
+  def releaseModel(broadcastId: Long): Unit = models.synchronized {
+    val e = models.get(broadcastId)
+    if (e != null) {
+      e.refs -= 1
+      evict(-1L)
     }
   }
 
-  def releaseModel(broadcastId: Long): Unit = {
-    val h = models.remove(broadcastId)
-    if (h != null) modelDestroy(h.longValue)
+  /** Drop a broadcast's table at once (when the broadcast is destroyed). */
+  def forgetModel(broadcastId: Long): Unit = models.synchronized {
+    val e = models.get(broadcastId)
+    if (e != null && e.refs <= 0) {
+      models.remove(broadcastId)
+      modelDestroy(e.handle)
+    }
+  }
+
+  // least recently used first, skipping tables in use and `keep`
+  private def evict(keep: Long): Unit = {
+    var bytes = 0L
+    val it0 = models.values().iterator()
+    while (it0.hasNext) bytes += it0.next().bytes
+    val it = models.entrySet().iterator()
+    while (it.hasNext && (models.size > maxModels || bytes > maxModelBytes)) {
+      val kv = it.next()
+      val e = kv.getValue
+      if (e.refs <= 0 && kv.getKey.longValue != keep) {
+        it.remove()
+        bytes -= e.bytes
+        modelDestroy(e.handle)
+      }
+    }
   }
 }
