@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--no-alt-paths", action="store_true",
                     help="skip timing the same table on the ordered mask-replay path (diagnostics library)")
     ap.add_argument("--empty-table", action="store_true", help="calibration: table with no keys")
+    ap.add_argument("--path", choices=["product", "replay"], default="product",
+                    help="replay: time the ordered mask-replay path on the same table (diagnostics library, "
+                         "LDGPU_NO_COUNT_MODE) instead of the product path -- for profiling, never the headline")
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--mode", choices=["score", "fit"], default="score",
                     help="score = the headline metric (config 2); fit = config 3's count + table build")
@@ -488,7 +491,12 @@ def main():
         model = DeviceModel(table, args.langs, grams, device=local)
     else:
         packed, table, grams, fit_info = build_table(args, ls, local)
-        model = DeviceModel.from_masks(*packed, args.langs, grams, device=local)
+        if args.path == "replay":
+            os.environ["LDGPU_NO_COUNT_MODE"] = "1"
+            model = DeviceModel.from_masks(*packed, args.langs, grams, device=local, variant="diag")
+            del os.environ["LDGPU_NO_COUNT_MODE"]
+        else:
+            model = DeviceModel.from_masks(*packed, args.langs, grams, device=local)
 
     # this rank's documents: a generated pool tiled to --docs, resident in HBM
     pool = min(args.pool, args.docs)
@@ -573,7 +581,9 @@ def main():
 
     total_docs = n_docs * world * args.steps
     doc_desc = f"{args.doc_min} B" if args.doc_min == args.doc_max else f"U[{args.doc_min},{args.doc_max}] B"
-    if args.config != 2:
+    if args.path == "replay":
+        line_note = "profiling run: the ordered mask-replay path (diagnostics library), not the product path"
+    elif args.config != 2:
         line_note = {1: "config 1: the reference's CPU-sized case (SURVEY §8d), timed beside its CPU restatement",
                      4: "config 4 is quoted on 1B docs over 8 GPUs (1.25e8 per GPU); --docs sets this run's count",
                      5: "config 5: table of up to L*K rows far beyond LDS: bloom in L2/MALL, slots in HBM"}[args.config]

@@ -1936,28 +1936,36 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         }
         const unsigned long long E = epre[(size_t)kQ * kQ];
         HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
-        // room for every entry as a new key: load <= 1/2, so the merge's
-        // probes never reach the overflow list in practice (it still catches them)
-        if (2 * (c->size + E) > c->cap) {
-            if (int rc = grow(c, next_pow2(2 * (c->size + E)))) return rc;
+        // The merge in chunks, each small enough that even if every entry of
+        // it were a new key the tables would stay at most half full (so probes
+        // stay short and never reach the overflow list in practice -- it still
+        // catches them): the table grows with the keys actually inserted, not
+        // with the batch's entries (most of which find their key, and whose
+        // dense rows of L counters are 8 L bytes per slot).
+        if (int rc = ensure_ovf(c, std::min<int64_t>((int64_t)E, (int64_t)c->cap))) return rc;
+        const bool wide = K == 3 && c->nGw > 0;
+        if (wide) {
+            if (int rc = wide_ensure(c, 1)) return rc;
         }
-        if (K == 3 && c->nGw > 0) {
-            // wide entries: at most the batch's wide windows
-            int64_t ww = 0;
-            for (int64_t d = d0; d < d1; ++d) {
-                const int64_t len = h_off[d + 1] - h_off[d];
-                if (len < 8) continue;
-                for (int i = 0; i < c->nGw; ++i) ww += n_windows(len, c->Gw[i]);
+        for (int64_t e0 = 0; e0 < (int64_t)E;) {
+            if (8 * c->size > 3 * c->cap) {  // load above 3/8: double first
+                if (int rc = grow(c, 2 * c->cap)) return rc;
             }
-            if (int rc = wide_ensure(c, (uint64_t)std::min<int64_t>(ww, (int64_t)E))) return rc;
+            if (wide && 8 * c->wsize > 3 * c->wcap) {
+                if (int rc = wide_ensure(c, c->wcap / 2)) return rc;
+            }
+            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(c->cap / 2 - c->size));
+            if (wide) n = std::min<int64_t>(n, (int64_t)(c->wcap / 2 - c->wsize));
+            n = std::max<int64_t>(n, 1);
+            if (int rc = ensure_ovf(c, n)) return rc;
+            HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+            HIP_TRY(launch_merge(K, pp, count_params(c), wide_params(c), e0, n, st));
+            if (wide) {
+                if (int rc = wide_after(c)) return rc;
+            }
+            if (int rc = after_batch(c)) return rc;
+            e0 += n;
         }
-        if (int rc = ensure_ovf(c, (int64_t)E)) return rc;
-        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-        HIP_TRY(launch_merge(K, pp, count_params(c), wide_params(c), (int64_t)E, st));
-        if (K == 3 && c->nGw > 0) {
-            if (int rc = wide_after(c)) return rc;
-        }
-        if (int rc = after_batch(c)) return rc;
         d0 = d1;
     }
     return LDGPU_OK;

@@ -1619,12 +1619,12 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
 // bucket b = the last with epre[b] <= i, stored at boff[b] + (i - epre[b])
 template <int K>
 __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const CountParams c, const WideCountParams w,
-                                                     int64_t n) {
+                                                     int64_t e0, int64_t n) {
     __shared__ uint64_t pre[kQ * kQ + 1];
     for (int i = threadIdx.x; i <= kQ * kQ; i += blockDim.x) pre[i] = p.epre[i];
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const int64_t i = e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e0 + n) return;
     int lo = 0;
 #pragma unroll
     for (int step = 2048; step >= 1; step >>= 1)
@@ -1686,13 +1686,13 @@ hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t n,
-                        hipStream_t stream) {
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
+                        int64_t n, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     const dim3 g((unsigned)((n + 1023) / 1024)), b(1024);
-    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, n);
-    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, n);
-    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, n);
+    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, e0, n);
+    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, e0, n);
+    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, e0, n);
     return hipGetLastError();
 }
 

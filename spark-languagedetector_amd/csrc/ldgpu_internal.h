@@ -242,10 +242,10 @@ hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream);
 hipError_t launch_part2(int K, const PartParams& p, hipStream_t stream);
 hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
 struct WideCountParams;
-// add the reduce output entries 0..n into the global tables (K = 3: keys of
-// 8..15 bytes into the wide table)
-hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t n,
-                        hipStream_t stream);
+// add the reduce output entries e0 .. e0 + n into the global tables (K = 3:
+// keys of 8..15 bytes into the wide table)
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
+                        int64_t n, hipStream_t stream);
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
 hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
                          hipStream_t stream);

@@ -14,7 +14,9 @@ from typing import List, Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.environ.get("LDGPU_LIB", os.path.join(PKG_ROOT, "lib", "libldgpu.so"))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libldgpu.so")
+# LDGPU_LIB: another build of the library for A/B timing (tools only)
+_LIB_OVERRIDE = os.environ.get("LDGPU_LIB")
 # diagnostics build (make -C spark-languagedetector_amd diag): the only one that
 # reads the LDGPU_* path / ablation switches from the environment; tests load
 # it explicitly (variant="diag") to cover the alternative kernel paths
@@ -83,7 +85,7 @@ SIGNATURES = [
 ]
 
 _libs = {}
-_lock = threading.Lock()
+_lock = threading.RLock()
 
 
 COMM_ID_BYTES = 128
@@ -110,6 +112,10 @@ def load(path: Optional[str] = None, variant: str = "product"):
     with _lock:
         if path is None and variant in _libs:
             return _libs[variant]
+        if path is None and variant == "product" and _LIB_OVERRIDE:
+            lib = load(_LIB_OVERRIDE)
+            _libs[variant] = lib
+            return lib
         p = path or (DIAG_LIB_PATH if variant == "diag" else LIB_PATH)
         if not os.path.exists(p):
             raise ImportError(
@@ -121,6 +127,8 @@ def load(path: Optional[str] = None, variant: str = "product"):
             pass
         lib = ctypes.CDLL(p)
         for name, res, args in SIGNATURES:
+            if path is not None and not hasattr(lib, name):
+                continue  # an explicitly named older build (A/B timing): only its own entry points
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
