@@ -1515,12 +1515,11 @@ int after_batch(ldgpu_counts* c) {
         return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost)", novf);
     c->size = size;
     if (novf == 0) {
-        if (2 * size > c->cap) {
-            if (int rc = grow(c, next_pow2(4 * size + 16))) return rc;
+        if (2 * size > c->cap) {  // over half full: the next power of two above twice the keys
+            if (int rc = grow(c, next_pow2(2 * size + 16))) return rc;
         }
         c->tbl_valid = false;
         c->sp_valid = false;
-    c->sp_valid = false;
         return LDGPU_OK;
     }
     // Entries whose key found no slot are on the overflow list: grow, then
@@ -1937,25 +1936,25 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         const unsigned long long E = epre[(size_t)kQ * kQ];
         HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
         // The merge in chunks, each small enough that even if every entry of
-        // it were a new key the tables would stay at most half full (so probes
-        // stay short and never reach the overflow list in practice -- it still
-        // catches them): the table grows with the keys actually inserted, not
-        // with the batch's entries (most of which find their key, and whose
-        // dense rows of L counters are 8 L bytes per slot).
-        if (int rc = ensure_ovf(c, std::min<int64_t>((int64_t)E, (int64_t)c->cap))) return rc;
+        // it were a new key the tables would stay at most 3/4 full (probes
+        // stay short and practically never reach the overflow list -- which
+        // still catches them), doubling a table once it is over half full:
+        // the table grows with the keys actually inserted, not with the
+        // batch's entries (most of which find their key; a slot holds a dense
+        // row of L counters, 1.6 KB at L = 200).
         const bool wide = K == 3 && c->nGw > 0;
         if (wide) {
             if (int rc = wide_ensure(c, 1)) return rc;
         }
         for (int64_t e0 = 0; e0 < (int64_t)E;) {
-            if (8 * c->size > 3 * c->cap) {  // load above 3/8: double first
+            while (2 * c->size > c->cap) {
                 if (int rc = grow(c, 2 * c->cap)) return rc;
             }
-            if (wide && 8 * c->wsize > 3 * c->wcap) {
-                if (int rc = wide_ensure(c, c->wcap / 2)) return rc;
+            if (wide && 2 * c->wsize > c->wcap) {
+                if (int rc = wide_ensure(c, 0)) return rc;
             }
-            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(c->cap / 2 - c->size));
-            if (wide) n = std::min<int64_t>(n, (int64_t)(c->wcap / 2 - c->wsize));
+            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(3 * (c->cap / 4) - c->size));
+            if (wide) n = std::min<int64_t>(n, (int64_t)(3 * (c->wcap / 4) - c->wsize));
             n = std::max<int64_t>(n, 1);
             if (int rc = ensure_ovf(c, n)) return rc;
             HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
