@@ -1504,6 +1504,18 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
     return LDGPU_OK;
 }
 
+// Load a count table may reach before it doubles: 1/2, or 0.8 once the
+// doubled table would pass kBigTableBytes -- a slot holds a dense row of L
+// counters (1.6 KB at L = 200), so config 5's fit of 45M grams would need 2^27
+// slots (216 GB) at load 1/2, more than the device holds next to the old table
+// during the rehash.  Linear probes at load 0.8 stay far below kMaxProbe.
+constexpr uint64_t kBigTableBytes = 96ull << 30;
+
+double max_load(const ldgpu_counts* c) {
+    const uint64_t slot = 8ull + 8ull * (uint64_t)c->L;
+    return 2 * c->cap * slot > kBigTableBytes ? 0.8 : 0.5;
+}
+
 // after a batch: read size / overflow, grow, re-insert overflow entries
 int after_batch(ldgpu_counts* c) {
     unsigned long long size = 0;
@@ -1515,8 +1527,8 @@ int after_batch(ldgpu_counts* c) {
         return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost)", novf);
     c->size = size;
     if (novf == 0) {
-        if (2 * size > c->cap) {  // over half full: the next power of two above twice the keys
-            if (int rc = grow(c, next_pow2(2 * size + 16))) return rc;
+        while ((double)c->size > max_load(c) * (double)c->cap) {  // past the load limit: double
+            if (int rc = grow(c, 2 * c->cap)) return rc;
         }
         c->tbl_valid = false;
         c->sp_valid = false;
@@ -1555,6 +1567,8 @@ int after_batch(ldgpu_counts* c) {
     uint32_t dst_cap = c->ovf2_cap, src_cap = c->ovf_cap;
     uint64_t target = std::min<uint64_t>(next_pow2(4 * (size + (uint64_t)novf) + 16), 8 * c->cap);
     target = std::max<uint64_t>(target, 2 * c->cap);
+    // a big table with room left takes the first re-insert in place
+    if (max_load(c) > 0.5 && (double)(size + novf) < 0.85 * (double)c->cap) target = c->cap;
     for (unsigned int n = novf; n > 0;) {
         if (int rc = grow(c, target)) return rc;
         CountParams p = count_params(c);
@@ -1947,13 +1961,14 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             if (int rc = wide_ensure(c, 1)) return rc;
         }
         for (int64_t e0 = 0; e0 < (int64_t)E;) {
-            while (2 * c->size > c->cap) {
+            while ((double)c->size > max_load(c) * (double)c->cap) {
                 if (int rc = grow(c, 2 * c->cap)) return rc;
             }
             if (wide && 2 * c->wsize > c->wcap) {
                 if (int rc = wide_ensure(c, 0)) return rc;
             }
-            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(3 * (c->cap / 4) - c->size));
+            const double ceil_load = std::min(0.9, max_load(c) + 0.25);
+            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(ceil_load * (double)c->cap) - (int64_t)c->size);
             if (wide) n = std::min<int64_t>(n, (int64_t)(3 * (c->wcap / 4) - c->wsize));
             n = std::max<int64_t>(n, 1);
             if (int rc = ensure_ovf(c, n)) return rc;
