@@ -1437,6 +1437,7 @@ CountParams count_params(const ldgpu_counts* c) {
     p.ovf_cnt = c->d_ovf_cnt;
     p.ovf_n = c->d_ovf_n;
     p.ovf_cap = c->ovf_cap;
+    p.max_probe = kMaxProbe;
     p.L = c->L;
     p.nG = c->nGn;
     for (int i = 0; i < c->nGn; ++i) p.G[i] = c->Gn[i];
@@ -1508,7 +1509,8 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
 // doubled table would pass kBigTableBytes -- a slot holds a dense row of L
 // counters (1.6 KB at L = 200), so config 5's fit of 45M grams would need 2^27
 // slots (216 GB) at load 1/2, more than the device holds next to the old table
-// during the rehash.  Linear probes at load 0.8 stay far below kMaxProbe.
+// during the rehash.  (A rare insert that meets a linear-probe cluster longer
+// than kMaxProbe goes to the overflow list and is re-inserted by the host.)
 constexpr uint64_t kBigTableBytes = 96ull << 30;
 
 double max_load(const ldgpu_counts* c) {
@@ -1565,13 +1567,21 @@ int after_batch(ldgpu_counts* c) {
     unsigned int* dst_n = c->d_ovf2_n;
     unsigned int* src_n = c->d_ovf_n;
     uint32_t dst_cap = c->ovf2_cap, src_cap = c->ovf_cap;
-    uint64_t target = std::min<uint64_t>(next_pow2(4 * (size + (uint64_t)novf) + 16), 8 * c->cap);
-    target = std::max<uint64_t>(target, 2 * c->cap);
-    // a big table with room left takes the first re-insert in place
-    if (max_load(c) > 0.5 && (double)(size + novf) < 0.85 * (double)c->cap) target = c->cap;
+    // While the table, with every overflow entry a new key, stays within 0.9
+    // load, the entries are re-inserted in place with a long probe limit
+    // (kReinsertProbe: an overflow is a long linear-probe cluster, not a full
+    // table); otherwise the table grows to the load limit first.  The list may
+    // count windows, duplicates included (legacy count kernel), so a grow is
+    // sized within 8x the table.
+    uint64_t target = c->cap;
+    if ((double)(size + novf) > 0.9 * (double)c->cap) {
+        target = next_pow2((uint64_t)((double)(size + novf) / max_load(c)) + 16);
+        target = std::max<uint64_t>(std::min<uint64_t>(target, 8 * c->cap), 2 * c->cap);
+    }
     for (unsigned int n = novf; n > 0;) {
         if (int rc = grow(c, target)) return rc;
         CountParams p = count_params(c);
+        p.max_probe = kReinsertProbe;
         p.ovf_keys = dst_k;
         p.ovf_lang = dst_l;
         p.ovf_cnt = dst_c;
@@ -1950,9 +1960,9 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         const unsigned long long E = epre[(size_t)kQ * kQ];
         HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
         // The merge in chunks, each small enough that even if every entry of
-        // it were a new key the tables would stay at most 3/4 full (probes
-        // stay short and practically never reach the overflow list -- which
-        // still catches them), doubling a table once it is over half full:
+        // it were a new key a table would stay within 0.1 of its load limit
+        // (probes stay short and rarely reach the overflow list -- which
+        // catches them), doubling a table once it is past the limit:
         // the table grows with the keys actually inserted, not with the
         // batch's entries (most of which find their key; a slot holds a dense
         // row of L counters, 1.6 KB at L = 200).
@@ -1967,7 +1977,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             if (wide && 2 * c->wsize > c->wcap) {
                 if (int rc = wide_ensure(c, 0)) return rc;
             }
-            const double ceil_load = std::min(0.9, max_load(c) + 0.25);
+            const double ceil_load = max_load(c) + 0.1;
             int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(ceil_load * (double)c->cap) - (int64_t)c->size);
             if (wide) n = std::min<int64_t>(n, (int64_t)(3 * (c->wcap / 4) - c->wsize));
             n = std::max<int64_t>(n, 1);

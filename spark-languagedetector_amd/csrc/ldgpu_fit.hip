@@ -74,7 +74,7 @@ __device__ __forceinline__ unsigned long long block_compact(bool occ, unsigned l
 // find-or-insert; returns the slot or -1 when the probe limit is reached
 __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key, bool& new_key) {
     uint64_t s = mix64(key) >> p.shift;
-    for (int probe = 0; probe < kMaxProbe; ++probe) {
+    for (uint32_t probe = 0; probe < p.max_probe; ++probe) {
         uint64_t k = __hip_atomic_load(&p.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == key) return (int64_t)s;
         if (k == kEmpty) {

@@ -151,13 +151,15 @@ struct CountParams {
     unsigned long long* ovf_cnt;
     unsigned int* ovf_n;
     uint32_t ovf_cap;
+    uint32_t max_probe;         // probe limit of an insert (kMaxProbe; re-inserts of overflow entries: more)
     int32_t L;
     int32_t nG;
     int32_t G[kMaxGramLengths];
 };
 
 constexpr int kCountWaves = 16;
-constexpr int kMaxProbe = 128;
+constexpr uint32_t kMaxProbe = 128;
+constexpr uint32_t kReinsertProbe = 1u << 16;
 
 hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream);
 // insert keys[i] with counts rows[i][L] (add) into the table; n entries
