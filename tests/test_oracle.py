@@ -182,3 +182,18 @@ def test_c_oracle_mask_form_equals_dense_rows():
     l1, s1 = OC.Table(dense, L).score([1, 2, 3], dd, doff, want_scores=True)
     l2, s2 = OC.Table.from_masks(kb, off, masks, vals, L).score([1, 2, 3], dd, doff, want_scores=True)
     assert np.array_equal(l1, l2) and np.array_equal(s1.view(np.uint64), s2.view(np.uint64))
+
+
+def test_c_restatement_under_address_and_ub_sanitizers():
+    """SURVEY §5 (race detection / sanitizers): the C restatement built with
+    -fsanitize=address,undefined (make -C oracle asan) runs every entry point
+    on random corpora with the rules' edge cases; any out-of-bounds access,
+    leak or undefined behaviour aborts it."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "asan"], check=True, timeout=240)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(root, "oracle", "build", "asan_check")], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "clean" in r.stdout
