@@ -1395,6 +1395,7 @@ struct ldgpu_counts {
     int K = 1;
     uint32_t lb = 0, cb = 0;
     int64_t batch_windows = 0;  // kBatchWindows / K (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
+    double new_per_entry = 1.0; // new keys per merged entry in the last batch (projected growth)
     ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
     // grams of 8..15 bytes: a two-word-key table of their own (ldgpu_fit.hip)
     uint64_t wcap = 0, wsize = 0;
@@ -1970,6 +1971,24 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         if (wide) {
             if (int rc = wide_ensure(c, 1)) return rc;
         }
+        // Projected growth: the batch adds about E x (the last batch's new
+        // keys per entry) keys.  A table short of that grows once, here --
+        // doubling through the chunks would rehash what it holds each time
+        // (an empty table's first grow is only an allocation).  If the
+        // projection cannot be allocated, the chunks grow as they need.
+        {
+            const double est = (double)c->size + c->new_per_entry * (double)E;
+            if (est > max_load(c) * (double)c->cap) {
+                const uint64_t slot = 8ull + 8ull * (uint64_t)c->L;
+                uint64_t target = next_pow2((uint64_t)(est / 0.5) + 1);
+                if (target * slot > kBigTableBytes) target = next_pow2((uint64_t)(est / 0.8) + 1);
+                if (target > c->cap && grow(c, target) != LDGPU_OK) {
+                    (void)hipGetLastError();  // (a failed allocation's sticky error)
+                    (void)ok();
+                }
+            }
+        }
+        const uint64_t size0 = c->size;
         for (int64_t e0 = 0; e0 < (int64_t)E;) {
             while ((double)c->size > max_load(c) * (double)c->cap) {
                 if (int rc = grow(c, 2 * c->cap)) return rc;
@@ -1990,6 +2009,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             if (int rc = after_batch(c)) return rc;
             e0 += n;
         }
+        if (E) c->new_per_entry = std::max(0.02, (double)(c->size - size0) / (double)E);
         d0 = d1;
     }
     return LDGPU_OK;

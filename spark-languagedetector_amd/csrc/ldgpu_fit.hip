@@ -1028,7 +1028,9 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
     return v;
 }
 
-constexpr int kT23Probe = 16;
+constexpr int kT23Rounds = 4;                           // LDS bucket reads a 2-/3-byte window may take
+constexpr int kT23BucketBits = 11;                      // kT23 / 4 buckets of 4 slots
+static_assert(kT23 == 4 << kT23BucketBits, "t23 buckets");
 
 template <int K>
 struct EmitLds {
@@ -1036,7 +1038,7 @@ struct EmitLds {
     uint8_t bq1[emit_blk_recs(K)];  // q1 of each block record (computed once per record)
     uint32_t hist2[kQ * kQ];
     uint32_t h1[256];
-    uint32_t tkey[kT23];   // 2-/3-byte grams: bytes | klen << 24 (0: empty)
+    alignas(16) uint32_t tkey[kT23];   // 2-/3-byte grams: bytes | klen << 24 (0: empty), buckets of 4
     uint32_t tcnt[kT23];
     uint32_t pcnt[kQ];
     uint32_t pfill[kQ];
@@ -1183,33 +1185,50 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, Wa
             if (valid[k])
                 __hip_atomic_fetch_add(&S.h1[(uint32_t)lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if (klen <= 3 && !emit_ablated(p, 1)) {
-        // the sub positions probe together: one LDS round trip per probe step
-        // for all of them (most find their key at once)
-        uint32_t key[SUB], slot[SUB];
-        bool pend[SUB];
+        // buckets of 4 slots: one ds_read_b128 reads a bucket's keys (filled
+        // in slot order, never emptied).  A window looks in its home bucket
+        // and the next one, within kT23Rounds reads -- the wave waits for its
+        // slowest lane, so no lane may walk a long chain; a window that finds
+        // no slot goes out as a record (~2 % at 13k distinct 3-grams a language)
+        uint32_t key[SUB], bk[SUB];
+        bool pend[SUB], second[SUB];
 #pragma unroll
         for (int k = 0; k < SUB; ++k) {
             key[k] = (uint32_t)lo[k] | ((uint32_t)klen << 24);
-            slot[k] = (key[k] * 0x9E3779B1u) >> (32 - 13);  // kT23 = 2^13
+            bk[k] = (key[k] * 0x9E3779B1u) >> (32 - kT23BucketBits);
             pend[k] = valid[k];
+            second[k] = false;
         }
-        for (int t = 0; t < kT23Probe; ++t) {
-            uint32_t cur[SUB];
+        const uint4* T4 = reinterpret_cast<const uint4*>(S.tkey);
+        for (int t = 0; t < kT23Rounds; ++t) {
+            uint4 cur[SUB];
 #pragma unroll
-            for (int k = 0; k < SUB; ++k) cur[k] = pend[k] ? S.tkey[slot[k]] : 0u;
+            for (int k = 0; k < SUB; ++k) cur[k] = pend[k] ? T4[bk[k]] : make_uint4(0u, 0u, 0u, 0u);
             bool any = false;
 #pragma unroll
             for (int k = 0; k < SUB; ++k) {
                 if (!pend[k]) continue;
-                if (cur[k] == 0u) {
-                    const uint32_t old = atomicCAS(&S.tkey[slot[k]], 0u, key[k]);
-                    cur[k] = old == 0u ? key[k] : old;
+                const uint4 c = cur[k];
+                int hit = c.x == key[k] ? 0 : (c.y == key[k] ? 1 : (c.z == key[k] ? 2 : (c.w == key[k] ? 3 : -1)));
+                if (hit < 0) {
+                    const int emp = c.x == 0u ? 0 : (c.y == 0u ? 1 : (c.z == 0u ? 2 : (c.w == 0u ? 3 : -1)));
+                    if (emp >= 0) {
+                        const uint32_t old = atomicCAS(&S.tkey[4u * bk[k] + (uint32_t)emp], 0u, key[k]);
+                        if (old == 0u || old == key[k]) hit = emp;  // else: lost the slot, read the bucket again
+                    } else if (!second[k]) {
+                        bk[k] = (bk[k] + 1u) & ((1u << kT23BucketBits) - 1u);
+                        second[k] = true;
+                    } else {
+                        pend[k] = false;  // both buckets full: a record
+                        has[k] = true;
+                        continue;
+                    }
                 }
-                if (cur[k] == key[k]) {
-                    __hip_atomic_fetch_add(&S.tcnt[slot[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (hit >= 0) {
+                    __hip_atomic_fetch_add(&S.tcnt[4u * bk[k] + (uint32_t)hit], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                     pend[k] = false;
                 } else {
-                    slot[k] = (slot[k] + 1u) & (kT23 - 1u);
                     any = true;
                 }
             }
@@ -1217,7 +1236,7 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, Wa
         }
 #pragma unroll
         for (int k = 0; k < SUB; ++k) {
-            if (pend[k]) {  // no slot: the window goes out as a record
+            if (pend[k] || has[k]) {  // no slot: the window goes out as a record
                 has[k] = true;
                 r[k] = make_rec<K>(lo[k], 0, klen, lang, 1, p);
             }
@@ -1486,6 +1505,8 @@ __device__ __forceinline__ void out_append(const PartParams& p, uint32_t* n_out,
 // (two entries out, summed by the merge).
 constexpr uint32_t kBusy = 1u;
 
+constexpr int kRedRounds = 8;  // reduce: LDS probe rounds per record
+
 template <int K>
 __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartParams p) {
     constexpr int N = agg_slots<K>();
@@ -1524,26 +1545,39 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
             slot[u] = (uint32_t)(((uint64_t)(uint32_t)h * (uint64_t)N) >> 32);
             tg[u] = (uint32_t)(h >> 32) | 2u;  // never 0 (empty) or kBusy
         }
-        for (int t = 0; t < 32; ++t) {
+        // a bounded number of probe rounds: the wave waits for its slowest
+        // lane, and a record still unplaced goes out as it is
+        for (int t = 0; t < kRedRounds; ++t) {
             bool any = false;
             if constexpr (K == 1) {
-                uint64_t cur[kU];
+                // slot pairs: one ds_read_b128 reads both keys of a pair
+                // (filled in slot order, never emptied)
+                const uint4* KW2 = reinterpret_cast<const uint4*>(kw);
+                uint4 cur[kU];
 #pragma unroll
-                for (int u = 0; u < kU; ++u) cur[u] = pend[u] ? kw[slot[u]] : 0ull;  // read first: most find their key
+                for (int u = 0; u < kU; ++u) cur[u] = pend[u] ? KW2[slot[u] >> 1] : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     if (!pend[u]) continue;
                     const uint64_t kl = r[u].w[0] >> p.cb;  // never 0 for a record: the sentinel bit
-                    if (cur[u] == 0ull) {
-                        const unsigned long long old =
-                            atomicCAS(reinterpret_cast<unsigned long long*>(&kw[slot[u]]), 0ull, (unsigned long long)kl);
-                        cur[u] = old == 0ull ? kl : old;
+                    const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                    const uint64_t k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                    const uint32_t pr = slot[u] & ~1u;
+                    int hit = k0 == kl ? 0 : (k1 == kl ? 1 : -1);
+                    if (hit < 0) {
+                        const int emp = k0 == 0ull ? 0 : (k1 == 0ull ? 1 : -1);
+                        if (emp >= 0) {
+                            const unsigned long long old = atomicCAS(
+                                reinterpret_cast<unsigned long long*>(&kw[pr + (uint32_t)emp]), 0ull, (unsigned long long)kl);
+                            if (old == 0ull || old == kl) hit = emp;  // else: lost the slot, read the pair again
+                        } else {
+                            slot[u] = pr + 2u == (uint32_t)N ? 0u : pr + 2u;
+                        }
                     }
-                    if (cur[u] == kl) {
-                        __hip_atomic_fetch_add(&cnt[slot[u]], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (hit >= 0) {
+                        __hip_atomic_fetch_add(&cnt[pr + (uint32_t)hit], c[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         pend[u] = false;
                     } else {
-                        slot[u] = slot[u] + 1u == (uint32_t)N ? 0u : slot[u] + 1u;
                         any = true;
                     }
                 }
