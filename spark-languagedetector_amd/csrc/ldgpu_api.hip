@@ -17,7 +17,7 @@
 #include <rccl/rccl.h>
 
 #include "../../include/ldgpu.h"
-#include "ldgpu_internal.h"
+#include "ldgpu_fit.h"
 
 using namespace ldgpu;
 
@@ -1394,7 +1394,9 @@ struct ldgpu_counts {
     bool v3 = true;
     int K = 1;
     uint32_t lb = 0, cb = 0;
-    int64_t batch_windows = 0;  // kBatchWindows / K (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
+    int64_t batch_recs = 0;     // kBatchRecords / K (diagnostics: LDGPU_FIT_BATCH_WINDOWS)
+    ldgpu_counts* pend = nullptr; // FIT v4: T1, the table of maximal windows of a count call
+    int64_t pend_hint = 0;      // T1's keys in the last call (sizes the next one)
     double new_per_entry = 1.0; // new keys per merged entry in the last batch (projected growth)
     ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
     // grams of 8..15 bytes: a two-word-key table of their own (ldgpu_fit.hip)
@@ -1447,6 +1449,7 @@ CountParams count_params(const ldgpu_counts* c) {
 
 void counts_free(ldgpu_counts* c) {
     if (!c) return;
+    if (c->pend) counts_free(c->pend);
     for (void* p : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts, (void*)c->d_wsize, (void*)c->d_wfull})
         if (p) (void)hipFree(p);
     if (c->ctx) {
@@ -1767,36 +1770,151 @@ int wide_count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, 
     return LDGPU_OK;
 }
 
-// FIT v3 batches: at most batch_windows windows (kBatchWindows / K: ~200 MB of
-// corpus at grams 1-5), so the record scratch (K words per window for the emit
-// records -- a record stands for at least one window --, K words per record for
-// the buckets, out_words per record of reduce output) stays within ~20 GB of
-// HBM.
-constexpr int64_t kBatchWindows = 1ll << 30;
+// FIT v4 batches: at most batch_recs records (kBatchRecords / K: one per
+// byte position, ~256 MB of corpus), so the record scratch (K words per
+// record for the emit blocks and the buckets, out_words per record of reduce
+// output) stays within ~8 GB of HBM.
+constexpr int64_t kBatchRecords = 1ll << 28;
 
 int out_words(int K) { return K == 1 ? 2 : K; }
 
-// windows of every gram length for a document of len bytes
-int64_t doc_windows_all(const ldgpu_counts* c, int64_t len) {
-    int64_t w = 0;
-    for (int i = 0; i < c->nG; ++i) w += n_windows(len, c->G[i]);
-    return w;
+int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, int64_t capacity_hint,
+               ldgpu_counts** out);
+
+// distinct gram lengths, ascending, with their multiplicity in gramLengths
+DeriveParams derive_params(const ldgpu_counts* c) {
+    DeriveParams d{};
+    for (int n = 1; n <= kMaxWideGram; ++n) {
+        uint32_t m = 0;
+        for (int i = 0; i < c->nG; ++i) m += c->G[i] == n;
+        if (!m) continue;
+        d.len[d.n] = n;
+        d.mult[d.n] = m;
+        ++d.n;
+    }
+    return d;
 }
 
-// Count documents [0, n_docs) on the device with FIT v3 (ldgpu_fit.hip): per
+// T1 (c->pend) -> T (c): every T1 count adds to the prefixes of its window
+// (derive_kernel).  In chunks of T1 slots small enough that the overflow
+// list holds every add of the chunk and T, even if every add were a new key,
+// stays within 0.1 of its load limit (T grows with the keys actually
+// inserted); T is first grown once to the projection (T1's windows are
+// mostly new keys of T).
+int derive_pending(ldgpu_counts* c) {
+    ldgpu_counts* t = c->pend;
+    if (!t || (t->size == 0 && t->wsize == 0)) return LDGPU_OK;
+    hipStream_t st = c->ctx->stream;
+    const DeriveParams d = derive_params(c);
+    int nw = 0;
+    for (int j = 0; j < d.n; ++j) nw += d.len[j] > kMaxGram;
+    const uint64_t L = (uint64_t)c->L;
+    {
+        const double est = (double)c->size + 1.1 * (double)(t->size + t->wsize);
+        if (est > max_load(c) * (double)c->cap) {
+            const uint64_t slot = 8ull + 8ull * L;
+            uint64_t target = next_pow2((uint64_t)(est / 0.5) + 1);
+            if (target * slot > kBigTableBytes) target = next_pow2((uint64_t)(est / 0.8) + 1);
+            if (target > c->cap && grow(c, target) != LDGPU_OK) {
+                (void)hipGetLastError();
+                (void)ok();
+            }
+        }
+    }
+    const uint64_t per_slot = L * (uint64_t)d.n;  // adds of one T1 slot at most
+    for (int pass = 0; pass < 2; ++pass) {
+        const bool wide = pass == 1;
+        const uint64_t tcap = wide ? t->wcap : t->cap;
+        const uint64_t tsize = wide ? t->wsize : t->size;
+        if (!tcap || !tsize) continue;
+        const double tload = std::max(1e-6, (double)tsize / (double)tcap);
+        for (uint64_t s0 = 0; s0 < tcap;) {
+            while ((double)c->size > max_load(c) * (double)c->cap) {
+                if (int rc = grow(c, 2 * c->cap)) return rc;
+            }
+            const double room = std::max(1.0, (max_load(c) + 0.1) * (double)c->cap - (double)c->size);
+            uint64_t slots = (uint64_t)(room / (tload * (double)d.n));
+            slots = std::min<uint64_t>(slots, kOvfMax / per_slot);
+            slots = std::max<uint64_t>(slots, 1);
+            slots = std::min<uint64_t>(slots, tcap - s0);
+            if (int rc = ensure_ovf(c, (int64_t)std::min<uint64_t>(slots * per_slot, kOvfMax))) return rc;
+            if (wide && nw) {
+                const uint64_t occ = std::min<uint64_t>(tsize, (uint64_t)(2.0 * tload * (double)slots) + 64);
+                if (int rc = wide_ensure(c, occ * (uint64_t)nw)) return rc;
+            }
+            HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+            if (wide) HIP_TRY(launch_wide_derive(wide_params(t), s0, s0 + slots, count_params(c), wide_params(c), d, st));
+            else HIP_TRY(launch_derive(count_params(t), s0, s0 + slots, count_params(c), wide_params(c), d, st));
+            if (wide && nw) {
+                if (int rc = wide_after(c)) return rc;
+            }
+            if (int rc = after_batch(c)) return rc;
+            s0 += slots;
+        }
+    }
+    return LDGPU_OK;
+}
+
+// Partial windows of the call's documents shorter than some gram length
+// (partial_kernel): one add each, straight into T.
+int count_partial(ldgpu_counts* c, const uint8_t* d_bytes, const int64_t* d_offsets, const int32_t* d_lang,
+                  int64_t n_docs, const int64_t* h_off, const int32_t* h_lang) {
+    int maxg = 0;
+    for (int i = 0; i < c->nG; ++i) maxg = std::max(maxg, c->G[i]);
+    std::vector<int64_t> docs;
+    bool any_wide = false;
+    for (int64_t d = 0; d < n_docs; ++d) {
+        const int64_t len = h_off[d + 1] - h_off[d];
+        if (len <= 0 || len >= maxg || h_lang[d] < 0 || h_lang[d] >= c->L) continue;
+        docs.push_back(d);
+        any_wide |= len > kMaxGram;
+    }
+    if (docs.empty()) return LDGPU_OK;
+    ldgpu_ctx* x = c->ctx;
+    hipStream_t st = x->stream;
+    const int64_t n = (int64_t)docs.size();
+    if (int rc = ensure_ovf(c, n)) return rc;
+    if ((double)(c->size + (uint64_t)n) > max_load(c) * (double)c->cap) {
+        if (int rc = grow(c, next_pow2((uint64_t)((double)(c->size + (uint64_t)n) / max_load(c)) + 16))) return rc;
+    }
+    if (any_wide) {
+        if (int rc = wide_ensure(c, (uint64_t)n)) return rc;
+    }
+    HIP_TRY(x->f_ocnt.ensure(sizeof(int64_t) * (size_t)n));
+    HIP_TRY(hipMemcpyAsync(x->f_ocnt.p, docs.data(), sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+    HIP_TRY(launch_partial(d_bytes, d_offsets, d_lang, (const int64_t*)x->f_ocnt.p, n, count_params(c), wide_params(c),
+                           derive_params(c), st));
+    if (any_wide) {
+        if (int rc = wide_after(c)) return rc;
+    }
+    return after_batch(c);
+}
+
+// Count documents [0, n_docs) on the device with FIT v4 (ldgpu_fit.hip): per
 // batch, the documents in language order (h_lang: their languages on the
-// host), emit -> part2 -> reduce -> merge.
+// host), emit -> part2 -> reduce -> merge into T1 (c->pend, the per-call table
+// of maximal windows); then T1 derives every gram length's counts into T.
 int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                     const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, const int32_t* h_lang) {
     ldgpu_ctx* x = c->ctx;
     hipStream_t st = x->stream;
     const int K = c->K;
     const int64_t thresh = emit_blk_recs(K) - emit_round_recs(K);
-    if (int rc = ensure_ovf(c, 1 << 20)) return rc;
+    int maxg = 0;
+    for (int i = 0; i < c->nG; ++i) maxg = std::max(maxg, c->G[i]);
+    if (c->pend) {  // left by a call that failed part-way: its counts are not carried over
+        counts_free(c->pend);
+        c->pend = nullptr;
+    }
+    if (int rc = count_partial(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
+    if (!c->pend) {
+        if (int rc = counts_new(x, c->L, c->G, c->nG, std::max<int64_t>(1 << 16, c->pend_hint), &c->pend)) return rc;
+    }
+    ldgpu_counts* t1 = c->pend;
+    if (int rc = ensure_ovf(t1, 1 << 20)) return rc;
     std::vector<uint32_t> cnt3((size_t)kQ * kQ * kSplits);
     std::vector<uint64_t> p2off((size_t)kQ * kQ * kSplits), boff((size_t)kQ * kQ + 1);
-    std::vector<int64_t> win((size_t)n_docs);
-    for (int64_t d = 0; d < n_docs; ++d) win[d] = doc_windows_all(c, h_off[d + 1] - h_off[d]);
     const int L = c->L;
     std::vector<int64_t> lcnt(L + 1), lwin(L);
     std::vector<int32_t> perm;
@@ -1804,10 +1922,12 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     std::vector<int32_t> wg_lang;
     int64_t d0 = 0;
     while (d0 < n_docs) {
+        // records of a document: one per byte position
         int64_t d1 = d0, W = 0;
         while (d1 < n_docs) {
-            if (d1 > d0 && W + win[d1] > c->batch_windows) break;
-            W += win[d1];
+            const int64_t len = h_off[d1 + 1] - h_off[d1];
+            if (d1 > d0 && W + len > c->batch_recs) break;
+            W += len;
             ++d1;
         }
         // the batch's documents of supported languages, in language order
@@ -1816,9 +1936,10 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         std::fill(lwin.begin(), lwin.end(), 0);
         for (int64_t d = d0; d < d1; ++d) {
             const int32_t l = h_lang[d];
-            if (l < 0 || l >= L || win[d] == 0) continue;
+            const int64_t len = h_off[d + 1] - h_off[d];
+            if (l < 0 || l >= L || len <= 0) continue;
             lcnt[l + 1]++;
-            lwin[l] += win[d];
+            lwin[l] += len;
         }
         for (int l = 0; l < L; ++l) lcnt[l + 1] += lcnt[l];
         const int64_t nd = lcnt[L];
@@ -1827,14 +1948,14 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             std::vector<int64_t> at(lcnt.begin(), lcnt.end() - 1);
             for (int64_t d = d0; d < d1; ++d) {
                 const int32_t l = h_lang[d];
-                if (l < 0 || l >= L || win[d] == 0) continue;
+                if (l < 0 || l >= L || h_off[d + 1] <= h_off[d]) continue;
                 perm[at[l]++] = (int32_t)(d - d0);
             }
         }
         // emit workgroups: each language's documents split into ranges
-        // balanced by windows, about 2 workgroups per CU in all; a
-        // workgroup's record region holds its windows, its block directory
-        // (windows + the table flush) / threshold + 2 blocks
+        // balanced by records, about 2 workgroups per CU in all; a
+        // workgroup's record region holds its records, its block directory
+        // records / threshold + 2 blocks
         const int64_t Wk = std::accumulate(lwin.begin(), lwin.end(), (int64_t)0);
         const int64_t target = std::max<int64_t>(1, (Wk + 2 * x->cus - 1) / (2 * x->cus));
         wg_doc.clear();
@@ -1849,7 +1970,8 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             for (int64_t k = 0; k < parts; ++k) {
                 const int64_t start = i, start_acc = acc, goal = lwin[l] * (k + 1) / parts;
                 while (i < lcnt[l + 1] && (wacc < goal || k + 1 == parts)) {
-                    const int64_t w = win[d0 + perm[i]];
+                    const int64_t dd = d0 + perm[i];
+                    const int64_t w = h_off[dd + 1] - h_off[dd];
                     wacc += w;
                     acc += w;
                     ++i;
@@ -1859,7 +1981,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
                 wg_rec.push_back(start_acc);
                 wg_dir.push_back(dirs);
                 wg_lang.push_back(l);
-                dirs += (acc - start_acc + 256 + kT23) / thresh + 2;
+                dirs += (acc - start_acc) / thresh + 2;
             }
         }
         while (wg_doc.empty() || wg_doc.size() % kSplits) {  // empty workgroups: a multiple of kSplits
@@ -1899,6 +2021,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         pp.L = c->L;
         pp.nG = c->nG;
         for (int i = 0; i < c->nG; ++i) pp.G[i] = c->G[i];
+        pp.maxg = maxg;
         pp.lb = c->lb;
         pp.cb = c->cb;
         if (const char* ab = diag_env("LDGPU_FIT_EMIT_ABLATE")) pp.ablate = atoi(ab);
@@ -1913,11 +2036,9 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         pp.blk_hdr = (uint32_t*)x->f_bhdr.p;
         pp.nblk = (int32_t*)x->f_nblk.p;
         pp.cnt3 = (uint32_t*)x->f_cnt3.p;
-        pp.direct = count_params(c);
         HIP_TRY(launch_emit(K, pp, st));
         HIP_TRY(hipMemcpyAsync(cnt3.data(), x->f_cnt3.p, sizeof(uint32_t) * cnt3.size(), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        if (int rc = after_batch(c)) return rc;  // direct adds (a count too large for a record) that overflowed
         // exact bucket offsets: (q1, q2) major, emit group minor
         uint64_t off = 0;
         for (int q = 0; q < kQ * kQ; ++q) {
@@ -1929,7 +2050,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         }
         boff[(size_t)kQ * kQ] = off;
         const int64_t R = (int64_t)off;
-        if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld windows", (long long)R, (long long)acc);
+        if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld positions", (long long)R, (long long)acc);
         HIP_TRY(x->f_p2.ensure(sizeof(uint64_t) * p2off.size()));
         HIP_TRY(x->f_boff.ensure(sizeof(uint64_t) * boff.size()));
         HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(R, 1)));
@@ -1960,16 +2081,16 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         }
         const unsigned long long E = epre[(size_t)kQ * kQ];
         HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
-        // The merge in chunks, each small enough that even if every entry of
-        // it were a new key a table would stay within 0.1 of its load limit
-        // (probes stay short and rarely reach the overflow list -- which
-        // catches them), doubling a table once it is past the limit:
-        // the table grows with the keys actually inserted, not with the
-        // batch's entries (most of which find their key; a slot holds a dense
-        // row of L counters, 1.6 KB at L = 200).
-        const bool wide = K == 3 && c->nGw > 0;
+        // The merge into T1 in chunks, each small enough that even if every
+        // entry of it were a new key a table would stay within 0.1 of its load
+        // limit (probes stay short and rarely reach the overflow list -- which
+        // catches them), doubling a table once it is past the limit: the table
+        // grows with the keys actually inserted, not with the batch's entries
+        // (most of which find their key; a slot holds a dense row of L
+        // counters, 1.6 KB at L = 200).
+        const bool wide = K == 3 && maxg > kMaxGram;
         if (wide) {
-            if (int rc = wide_ensure(c, 1)) return rc;
+            if (int rc = wide_ensure(t1, 1)) return rc;
         }
         // Projected growth: the batch adds about E x (the last batch's new
         // keys per entry) keys.  A table short of that grows once, here --
@@ -1977,41 +2098,50 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         // (an empty table's first grow is only an allocation).  If the
         // projection cannot be allocated, the chunks grow as they need.
         {
-            const double est = (double)c->size + c->new_per_entry * (double)E;
-            if (est > max_load(c) * (double)c->cap) {
-                const uint64_t slot = 8ull + 8ull * (uint64_t)c->L;
+            const double est = (double)t1->size + t1->new_per_entry * (double)E;
+            if (est > max_load(t1) * (double)t1->cap) {
+                const uint64_t slot = 8ull + 8ull * (uint64_t)t1->L;
                 uint64_t target = next_pow2((uint64_t)(est / 0.5) + 1);
                 if (target * slot > kBigTableBytes) target = next_pow2((uint64_t)(est / 0.8) + 1);
-                if (target > c->cap && grow(c, target) != LDGPU_OK) {
+                if (target > t1->cap && grow(t1, target) != LDGPU_OK) {
                     (void)hipGetLastError();  // (a failed allocation's sticky error)
                     (void)ok();
                 }
             }
         }
-        const uint64_t size0 = c->size;
+        const uint64_t size0 = t1->size + t1->wsize;
         for (int64_t e0 = 0; e0 < (int64_t)E;) {
-            while ((double)c->size > max_load(c) * (double)c->cap) {
-                if (int rc = grow(c, 2 * c->cap)) return rc;
+            while ((double)t1->size > max_load(t1) * (double)t1->cap) {
+                if (int rc = grow(t1, 2 * t1->cap)) return rc;
             }
-            if (wide && 2 * c->wsize > c->wcap) {
-                if (int rc = wide_ensure(c, 0)) return rc;
+            if (wide && 2 * t1->wsize > t1->wcap) {
+                if (int rc = wide_ensure(t1, 0)) return rc;
             }
-            const double ceil_load = max_load(c) + 0.1;
-            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(ceil_load * (double)c->cap) - (int64_t)c->size);
-            if (wide) n = std::min<int64_t>(n, (int64_t)(3 * (c->wcap / 4) - c->wsize));
+            const double ceil_load = max_load(t1) + 0.1;
+            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(ceil_load * (double)t1->cap) - (int64_t)t1->size);
+            if (wide) n = std::min<int64_t>(n, (int64_t)(3 * (t1->wcap / 4) - t1->wsize));
             n = std::max<int64_t>(n, 1);
-            if (int rc = ensure_ovf(c, n)) return rc;
-            HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-            HIP_TRY(launch_merge(K, pp, count_params(c), wide_params(c), e0, n, st));
+            if (int rc = ensure_ovf(t1, n)) return rc;
+            HIP_TRY(hipMemsetAsync(t1->d_ovf_n, 0, sizeof(unsigned int), st));
+            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), e0, n, st));
             if (wide) {
-                if (int rc = wide_after(c)) return rc;
+                if (int rc = wide_after(t1)) return rc;
             }
-            if (int rc = after_batch(c)) return rc;
+            if (int rc = after_batch(t1)) return rc;
             e0 += n;
         }
-        if (E) c->new_per_entry = std::max(0.02, (double)(c->size - size0) / (double)E);
+        if (E) t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - size0) / (double)E);
         d0 = d1;
     }
+    // every gram length from the call's maximal windows; T1 back to the
+    // context's block cache (the next call starts an empty one, sized by this)
+    const int rc = derive_pending(c);
+    c->pend_hint = (int64_t)(c->pend->size + c->pend->wsize);
+    counts_free(c->pend);
+    c->pend = nullptr;
+    if (rc) return rc;
+    c->tbl_valid = false;
+    c->sp_valid = false;
     return LDGPU_OK;
 }
 
@@ -2084,6 +2214,14 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
                     LDGPU_MAX_LANGS);
     if (int rc = check_grams(gram_lengths, n_grams, kMaxWideGram)) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = counts_new(ctx, n_langs, gram_lengths, n_grams, capacity_hint, out)) return rc;
+    return ok();
+}
+
+namespace {
+// a count table (validated arguments; the caller has set the device)
+int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, int64_t capacity_hint,
+               ldgpu_counts** out) {
     auto* c = new ldgpu_counts();
     c->ctx = ctx;
     c->L = n_langs;
@@ -2109,8 +2247,8 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
         c->K = maxg > kMaxGram ? 3 : (cb >= 8 ? 1 : 2);
         if (const char* k = diag_env("LDGPU_FIT_K")) c->K = std::max(c->K, std::min(3, atoi(k)));  // tests: wider forms
         c->v3 = !diag_env("LDGPU_FIT_LEGACY");
-        c->batch_windows = kBatchWindows / c->K;
-        if (const char* bw = diag_env("LDGPU_FIT_BATCH_WINDOWS")) c->batch_windows = std::max(1ll, atoll(bw));
+        c->batch_recs = kBatchRecords / c->K;
+        if (const char* bw = diag_env("LDGPU_FIT_BATCH_WINDOWS")) c->batch_recs = std::max(1ll, atoll(bw));
         if (c->v3) {
             const hipError_t pe = fit3_prepare(c->K);  // dynamic-LDS limits of this device's kernels
             if (pe != hipSuccess) {
@@ -2135,8 +2273,9 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
         return rc ? rc : fail(LDGPU_ENOMEM, "count table: %s", hipGetErrorString(e));
     }
     *out = c;
-    return ok();
+    return LDGPU_OK;
 }
+}  // namespace
 
 extern "C" int ldgpu_counts_destroy(ldgpu_counts* c) {
     counts_free(c);

@@ -1,0 +1,223 @@
+// ldgpu_fit.h -- FIT kernel parameter blocks and launchers shared between
+// ldgpu_fit.hip and the host runtime (ldgpu_api.hip).  (Kept apart from
+// ldgpu_internal.h so the SCORE objects do not depend on it.)
+#pragma once
+
+#include "ldgpu_internal.h"
+
+namespace ldgpu {
+
+// -------------------------------------------------------------------- FIT
+struct CountParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    int64_t last_dword;
+    const int64_t* offsets;
+    const int32_t* doc_lang;
+    int64_t n_docs;
+    uint64_t* keys;             // [cap] gram keys (0 = empty)
+    unsigned long long* counts; // [cap][L]
+    uint32_t shift;             // slot = mix64(key) >> shift
+    uint64_t mask;              // cap - 1
+    unsigned long long* size;   // distinct keys inserted
+    uint64_t* ovf_keys;         // overflow (probe limit reached): key, lang, count
+    int32_t* ovf_lang;
+    unsigned long long* ovf_cnt;
+    unsigned int* ovf_n;
+    uint32_t ovf_cap;
+    uint32_t max_probe;         // probe limit of an insert (kMaxProbe; re-inserts of overflow entries: more)
+    int32_t L;
+    int32_t nG;
+    int32_t G[kMaxGramLengths];
+};
+
+constexpr int kCountWaves = 16;
+constexpr uint32_t kMaxProbe = 128;
+constexpr uint32_t kReinsertProbe = 1u << 16;
+
+hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream);
+// insert keys[i] with counts rows[i][L] (add) into the table; n entries
+hipError_t launch_counts_add(const CountParams& p, const uint64_t* keys, const unsigned long long* rows,
+                             const int32_t* lang_of /*nullable: row is one count cnt_of[i] at lang_of[i]*/,
+                             const unsigned long long* cnt_of, int64_t n, hipStream_t stream);
+
+// ---- FIT v4: maximal-window records, radix-partitioned record aggregation
+// and prefix derivation (ldgpu_fit.hip) -- every gram length, every language
+// count.  Every byte position of a document makes ONE record: its maximal
+// window, min(N, len - pos) bytes (N = max(G)); the records of a batch are
+// summed per (window, language) into a table T1, and T1 derives every gram
+// length's counts (the n-gram at a position is the n-byte prefix of its
+// maximal window).  A record is K u64 words:
+//   K = 1 (compact; 8 max(G) + 1 + lb + cb <= 64 with cb >= 8):
+//        ((sentinel << lb | lang) << cb) | count, sentinel = 1 << 8 klen | bytes
+//   K = 2 (grams of <= 7 bytes, any L): {packed key (ldgpu_common.h),
+//        lang << 52 | count}
+//   K = 3 (some gram length of 8..15 bytes): {lo, hi, lang << 52 | count};
+//        a key of <= 7 bytes is lo = its packed key, hi = 0, a wide key is
+//        lo = bytes 0..7, hi = bytes 8.. | klen << 56
+// h = route hash of the (window, language) pair: q1 = h >> 58, q2 = bits
+// 52..57 (4096 buckets), LDS slot = low 32 bits (reduce).
+constexpr int kQBits = 6;
+constexpr int kQ = 1 << kQBits;                 // buckets per level
+constexpr int kBlkWords = 6144;                 // u64 words of records per emit block (LDS, 48 KiB)
+constexpr int kHdr = 68;                        // u32 per block header (kQ + 1 used)
+constexpr int kEmitWaves = 16;
+constexpr int kSplits = 4;                      // emit workgroup groups (part2 inputs)
+constexpr uint64_t kCntBits = 52;               // K >= 2: count bits of the last record word
+// emit rounds: a wave step adds at most 64 x sub records (sub = 4 positions per
+// lane for K = 1, 1 otherwise); a block is flushed once it could not take
+// another round
+constexpr int emit_sub(int K) { return K == 1 ? 4 : 1; }
+constexpr int emit_blk_recs(int K) { return kBlkWords / K; }
+constexpr int emit_round_recs(int K) { return kEmitWaves * 64 * emit_sub(K); }
+
+struct PartParams {
+    // corpus of the batch
+    const uint8_t* bytes;
+    int64_t last_dword;
+    const int64_t* offsets;
+    const int32_t* doc_lang;
+    int32_t L;
+    int32_t nG;
+    int32_t G[kMaxGramLengths];
+    uint32_t lb, cb;            // K = 1: language / count bit widths of a record
+    int32_t maxg;               // N = max(G): the maximal window length
+    int32_t ablate;             // diagnostics build only (LDGPU_FIT_EMIT_ABLATE; compiled out otherwise):
+                                // bit 1 the block flush skips its global stores, bit 2 no records at all
+    // emit (phase A): the batch's documents in language order (perm, a
+    // permutation of 0 .. n-1); workgroup w owns perm[wg_doc[w] .. wg_doc[w+1]),
+    // all of language wg_lang[w], records [wg_rec[w], ...) (capacity: its
+    // windows) and block ids [wg_dir[w], ...); blocks are sorted by q1 with a
+    // kHdr header
+    int32_t grid_a;             // emit workgroups (a multiple of kSplits)
+    const int32_t* perm;
+    const int32_t* wg_lang;
+    const int64_t* wg_doc;
+    const int64_t* wg_rec;
+    const int64_t* wg_dir;
+    uint64_t* rec;              // K words per record
+    int64_t* blk_start;         // [blocks] record offset of the block
+    uint32_t* blk_hdr;          // [blocks][kHdr] exclusive q1 starts (+ total)
+    int32_t* nblk;              // [grid_a] blocks written
+    uint32_t* cnt3;             // [kQ][kQ][kSplits] records per (q1, q2, emit group)
+    // part2: q1 bucket of emit group s -> q2 sub-buckets at exact offsets
+    const uint64_t* p2off;      // [kQ][kQ][kSplits]
+    uint64_t* rec2;             // K words per record
+    // reduce: bucket (q1, q2) = rec2[boff[b] .. boff[b+1]) -> (key, count)
+    // entries at out[boff[b] ..] (at most one per record; equal keys summed
+    // as far as the LDS hash holds them), nout[b] of them
+    const uint64_t* boff;       // [kQ * kQ + 1]
+    uint64_t* out;              // K words per entry (the record form, the count field a batch sum)
+    uint32_t* nout;             // [kQ * kQ]
+    const uint64_t* epre;       // merge: exclusive prefix of nout [kQ * kQ + 1]
+};
+
+size_t emit_lds_bytes(int K);
+size_t reduce_lds_bytes(int K);
+hipError_t fit3_prepare(int K);
+hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream);
+hipError_t launch_part2(int K, const PartParams& p, hipStream_t stream);
+hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
+struct WideCountParams;
+// add the reduce output entries e0 .. e0 + n into the tables of T1 (K = 3:
+// windows of 8..15 bytes into the wide table)
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
+                        int64_t n, hipStream_t stream);
+// rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
+hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
+                         hipStream_t stream);
+// out[0] += distinct (gram, language) pairs, out[1] += sum of all counts
+hipError_t launch_stats(const CountParams& p, uint64_t cap, unsigned long long* out, hipStream_t stream);
+// compact occupied slots: out_keys[i], out_counts[i][L]; *out_n = number written
+hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys,
+                          unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
+
+// ---- FIT of gram lengths 8..15 (ldgpu_fit.hip): a table of two-word keys
+// (lo = bytes 0..7, hi = bytes 8.. | klen << 56; hi = 0: empty slot) with a
+// u64 counter row per slot
+struct WideCountParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    int64_t last_dword;
+    const int64_t* offsets;
+    const int32_t* doc_lang;
+    int64_t n_docs;
+    uint64_t* klo;              // [cap]
+    uint64_t* khi;              // [cap]
+    unsigned long long* counts; // [cap][L]
+    uint32_t shift;             // slot = wide_slot(lo, hi) >> shift
+    uint64_t mask;              // cap - 1
+    unsigned long long* size;   // distinct keys inserted
+    unsigned int* full;         // set when an insert found no slot (the host keeps load <= 1/2)
+    int32_t L;
+    int32_t nG;                 // the wide gram lengths, in gramLengths order
+    int32_t G[kMaxGramLengths];
+    CountParams narrow;         // partial windows of documents shorter than 8 bytes: one-word keys
+};
+
+hipError_t launch_wide_count(const WideCountParams& p, int grid, hipStream_t stream);
+hipError_t launch_wide_rehash(const WideCountParams& from, const WideCountParams& to, uint64_t from_cap,
+                              hipStream_t stream);
+hipError_t launch_wide_add(const WideCountParams& p, const uint64_t* lo, const uint64_t* hi,
+                           const unsigned long long* rows, int64_t n, hipStream_t stream);
+hipError_t launch_wide_compact(const WideCountParams& p, uint64_t cap, uint64_t* out_lo, uint64_t* out_hi,
+                               unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
+
+// ---- FIT v4 derive: the distinct gram lengths (ascending) and their
+// multiplicity in gramLengths
+struct DeriveParams {
+    int32_t n;
+    int32_t len[kMaxGramLengths];
+    uint32_t mult[kMaxGramLengths];
+};
+// every (window w, language, c) of T1's slots [s0, s1) adds mult c to
+// (prefix of each distinct length <= |w|, language) in T (to / tow)
+hipError_t launch_derive(const CountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
+                         const WideCountParams& tow, const DeriveParams& d, hipStream_t stream);
+hipError_t launch_wide_derive(const WideCountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
+                              const WideCountParams& tow, const DeriveParams& d, hipStream_t stream);
+// partial windows of docs[0 .. n) (documents shorter than some gram length)
+hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, const int64_t* docs,
+                          int64_t n_docs, const CountParams& to, const WideCountParams& tow, const DeriveParams& d,
+                          hipStream_t stream);
+
+// ---- device probability / top-K (computeProbabilities + filterTopGrams)
+// presence: compact occupied slots into keys[n], masks[n][S] (count > 0 per
+// language) and k[n] (= popcount), and histogram hist[l][k] over (gram, l).
+hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
+                           int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream);
+// select: chosen[j] = 1 when k_j < kstar[l] for some l in the gram's mask;
+// grams with k_j == kstar[l] (need[l] > 0) are appended as threshold
+// candidates (lang, sort key, index).
+hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
+                         const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
+                         uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream);
+// chosen[idx[i]] = 1
+// sorted_keys (nullable): instead of marking, write the candidates' sort keys
+// in (language, key) order (the distributed top-K takes each segment's prefix)
+hipError_t launch_topk_candidates(int64_t cn, int L, const int32_t* cand_lang, const uint64_t* cand_key,
+                                  const uint32_t* cand_idx, const int64_t* seg_start, const int32_t* need,
+                                  uint8_t* chosen, uint64_t* sorted_keys, hipStream_t stream);
+// chosen[cand_idx[i]] = 1 when cand_key[i] <= thr[cand_lang[i]]
+hipError_t launch_mark_threshold(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key,
+                                 const uint32_t* cand_idx, const uint64_t* thr, uint8_t* chosen, hipStream_t stream);
+// multi-GPU merge: n_of[r] += occupied slots owned by rank r; scatter them
+// (keys, count rows) to out at cursor[owner]++
+hipError_t launch_owner_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
+                              hipStream_t stream);
+hipError_t launch_owner_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                uint64_t* out_keys, unsigned long long* out_rows, hipStream_t stream);
+// sparse owner exchange: n_of[r] += nonzero (gram, language) pairs owned by
+// rank r; scatter them as (key, lang << kPairCntBits | count) to out at
+// cursor[owner]++; add such pairs into a table
+constexpr uint32_t kPairCntBits = 52;
+hipError_t launch_owner_pair_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
+                                   hipStream_t stream);
+hipError_t launch_owner_pair_scatter(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* cursor,
+                                     uint64_t* out, hipStream_t stream);
+hipError_t launch_pairs_add(const CountParams& p, const uint64_t* pairs, int64_t n, hipStream_t stream);
+hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream);
+// gather the chosen grams: out_keys[m], out_masks[m][S], out_k[m]
+hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,
+                                const int32_t* ks, uint64_t* out_keys, uint64_t* out_masks, int32_t* out_k,
+                                unsigned long long* out_n, hipStream_t stream);
+
+}  // namespace ldgpu

@@ -28,7 +28,7 @@
 
 #include <hipcub/hipcub.hpp>
 
-#include "ldgpu_internal.h"
+#include "ldgpu_fit.h"
 
 namespace ldgpu {
 
@@ -1028,18 +1028,11 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
     return v;
 }
 
-constexpr int kT23Rounds = 4;                           // LDS bucket reads a 2-/3-byte window may take
-constexpr int kT23BucketBits = 11;                      // kT23 / 4 buckets of 4 slots
-static_assert(kT23 == 4 << kT23BucketBits, "t23 buckets");
-
 template <int K>
 struct EmitLds {
     uint64_t blk[kBlkWords];
     uint8_t bq1[emit_blk_recs(K)];  // q1 of each block record (computed once per record)
     uint32_t hist2[kQ * kQ];
-    uint32_t h1[256];
-    alignas(16) uint32_t tkey[kT23];   // 2-/3-byte grams: bytes | klen << 24 (0: empty), buckets of 4
-    uint32_t tcnt[kT23];
     uint32_t pcnt[kQ];
     uint32_t pfill[kQ];
     uint32_t pstart[kQ + 1];
@@ -1055,7 +1048,7 @@ template <int K>
 struct WaveState {
     static constexpr int kW = K == 3 ? 5 : 3;  // dwords per window position
     int64_t b, len, p0;
-    int32_t gi, phase;
+    int32_t phase;
     bool pf;                       // pw holds the words of the next WIN step (issued a round early)
     uint32_t pw[emit_sub(K)][kW];
 };
@@ -1097,35 +1090,33 @@ __device__ __forceinline__ uint32_t ld_dw3(const uint32_t* w, int64_t i, int64_t
     return w[i < last ? i : last];
 }
 
-// the dwords of the positions of a WIN step at (gi, p0): 3 per position for
-// windows of <= 7 bytes, 5 for wide ones
+// the dwords of the positions of a WIN step at p0: 3 per position for
+// windows of <= 7 bytes, 5 for wide ones (as many as max(G) needs)
 template <int K>
 __device__ __forceinline__ void window_loads(const PartParams& p, const WaveState<K>& w, int lane,
                                              uint32_t (&pw)[emit_sub(K)][WaveState<K>::kW]) {
     constexpr int SUB = emit_sub(K);
-    const int n = p.G[w.gi];
-    const int64_t nwin = n_windows(w.len, n);
-    const int klen = w.len < n ? (int)w.len : n;
     const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
 #pragma unroll
     for (int k = 0; k < SUB; ++k) {
         const int64_t pos = w.p0 + 64 * k + lane;
-        const int64_t a = w.b + (pos < nwin ? pos : 0);
+        const int64_t a = w.b + (pos < w.len ? pos : 0);
         const int64_t i = a >> 2;
         pw[k][0] = ld_dw3(W, i, p.last_dword);
         pw[k][1] = ld_dw3(W, i + 1, p.last_dword);
-        pw[k][2] = klen > 4 ? ld_dw3(W, i + 2, p.last_dword) : 0u;
+        pw[k][2] = p.maxg > 4 ? ld_dw3(W, i + 2, p.last_dword) : 0u;
         if constexpr (K == 3) {
-            pw[k][3] = klen > 8 ? ld_dw3(W, i + 3, p.last_dword) : 0u;
-            pw[k][4] = klen > 12 ? ld_dw3(W, i + 4, p.last_dword) : 0u;
+            pw[k][3] = p.maxg > 8 ? ld_dw3(W, i + 3, p.last_dword) : 0u;
+            pw[k][4] = p.maxg > 12 ? ld_dw3(W, i + 4, p.last_dword) : 0u;
         }
     }
 }
 
 __device__ __forceinline__ uint64_t byte_mask(int n) { return n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull); }
 
-// One step of a wave: <= 64 sub windows, <= 64 sub records.  The positions'
-// loads are all issued before any is used.
+// One step of a wave: <= 64 sub positions of its document, one record each
+// -- the maximal window at the position, min(N, len - pos) bytes (N =
+// max(G)).  The positions' loads are all issued before any is used.
 template <int K>
 __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, WaveState<K>& w, int lane, int64_t d0,
                                           int64_t d1, uint32_t lang) {
@@ -1142,111 +1133,37 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, Wa
         const int64_t d = p.perm[i];
         const int64_t b = p.offsets[d];
         const int64_t len = p.offsets[d + 1] - b;
-        if (len <= 0 || p.nG == 0) return;
+        if (len <= 0) return;
         w.b = b;
         w.len = len;
-        w.gi = 0;
         w.p0 = 0;
         w.pf = false;
         w.phase = kWin;
-        // fall through: the document's first windows in this step
+        // fall through: the document's first positions in this step
     }
+    if (!w.pf) window_loads<K>(p, w, lane, w.pw);
+    w.pf = false;
     bool has[SUB];
     Rec<K> r[SUB];
 #pragma unroll
-    for (int k = 0; k < SUB; ++k) has[k] = false;
-    const int n = p.G[w.gi];
-    const int64_t nwin = n_windows(w.len, n);
-    const int klen = w.len < n ? (int)w.len : n;
-    if (!w.pf) window_loads<K>(p, w, lane, w.pw);
-    w.pf = false;
-    uint64_t lo[SUB], hi[SUB];
-    bool valid[SUB];
-#pragma unroll
     for (int k = 0; k < SUB; ++k) {
         const int64_t pos = w.p0 + 64 * k + lane;
-        valid[k] = pos < nwin;
-        const uint32_t sh = (uint32_t)((w.b + (valid[k] ? pos : 0)) & 3);
+        has[k] = pos < w.len;
+        const int64_t rem = w.len - pos;
+        const int klen = rem >= p.maxg ? p.maxg : (rem > 0 ? (int)rem : 1);
+        const uint32_t sh = (uint32_t)((w.b + (has[k] ? pos : 0)) & 3);
         const uint32_t a0 = __builtin_amdgcn_alignbyte(w.pw[k][1], w.pw[k][0], sh);
         const uint32_t a1 = __builtin_amdgcn_alignbyte(w.pw[k][2], w.pw[k][1], sh);
-        lo[k] = (((uint64_t)a1 << 32) | a0) & byte_mask(klen);
-        hi[k] = 0;
+        const uint64_t lo = (((uint64_t)a1 << 32) | a0) & byte_mask(klen);
+        uint64_t hi = 0;
         if constexpr (K == 3) {
             if (klen > 8) {
                 const uint32_t a2 = __builtin_amdgcn_alignbyte(w.pw[k][3], w.pw[k][2], sh);
                 const uint32_t a3 = __builtin_amdgcn_alignbyte(w.pw[k][4], w.pw[k][3], sh);
-                hi[k] = (((uint64_t)a3 << 32) | a2) & byte_mask(klen - 8);
+                hi = (((uint64_t)a3 << 32) | a2) & byte_mask(klen - 8);
             }
         }
-    }
-    if (klen == 1) {
-#pragma unroll
-        for (int k = 0; k < SUB; ++k)
-            if (valid[k])
-                __hip_atomic_fetch_add(&S.h1[(uint32_t)lo[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else if (klen <= 3 && !emit_ablated(p, 1)) {
-        // buckets of 4 slots: one ds_read_b128 reads a bucket's keys (filled
-        // in slot order, never emptied).  A window looks in its home bucket
-        // and the next one, within kT23Rounds reads -- the wave waits for its
-        // slowest lane, so no lane may walk a long chain; a window that finds
-        // no slot goes out as a record (~2 % at 13k distinct 3-grams a language)
-        uint32_t key[SUB], bk[SUB];
-        bool pend[SUB], second[SUB];
-#pragma unroll
-        for (int k = 0; k < SUB; ++k) {
-            key[k] = (uint32_t)lo[k] | ((uint32_t)klen << 24);
-            bk[k] = (key[k] * 0x9E3779B1u) >> (32 - kT23BucketBits);
-            pend[k] = valid[k];
-            second[k] = false;
-        }
-        const uint4* T4 = reinterpret_cast<const uint4*>(S.tkey);
-        for (int t = 0; t < kT23Rounds; ++t) {
-            uint4 cur[SUB];
-#pragma unroll
-            for (int k = 0; k < SUB; ++k) cur[k] = pend[k] ? T4[bk[k]] : make_uint4(0u, 0u, 0u, 0u);
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < SUB; ++k) {
-                if (!pend[k]) continue;
-                const uint4 c = cur[k];
-                int hit = c.x == key[k] ? 0 : (c.y == key[k] ? 1 : (c.z == key[k] ? 2 : (c.w == key[k] ? 3 : -1)));
-                if (hit < 0) {
-                    const int emp = c.x == 0u ? 0 : (c.y == 0u ? 1 : (c.z == 0u ? 2 : (c.w == 0u ? 3 : -1)));
-                    if (emp >= 0) {
-                        const uint32_t old = atomicCAS(&S.tkey[4u * bk[k] + (uint32_t)emp], 0u, key[k]);
-                        if (old == 0u || old == key[k]) hit = emp;  // else: lost the slot, read the bucket again
-                    } else if (!second[k]) {
-                        bk[k] = (bk[k] + 1u) & ((1u << kT23BucketBits) - 1u);
-                        second[k] = true;
-                    } else {
-                        pend[k] = false;  // both buckets full: a record
-                        has[k] = true;
-                        continue;
-                    }
-                }
-                if (hit >= 0) {
-                    __hip_atomic_fetch_add(&S.tcnt[4u * bk[k] + (uint32_t)hit], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    pend[k] = false;
-                } else {
-                    any = true;
-                }
-            }
-            if (!__ballot(any)) break;
-        }
-#pragma unroll
-        for (int k = 0; k < SUB; ++k) {
-            if (pend[k] || has[k]) {  // no slot: the window goes out as a record
-                has[k] = true;
-                r[k] = make_rec<K>(lo[k], 0, klen, lang, 1, p);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < SUB; ++k) {
-            has[k] = valid[k];
-            r[k] = make_rec<K>(lo[k], hi[k], klen, lang, 1, p);
-        }
+        r[k] = make_rec<K>(lo, hi, klen, lang, 1, p);
     }
     if (emit_ablated(p, 4)) {
 #pragma unroll
@@ -1254,12 +1171,9 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, Wa
     }
     emit_recs<K, SUB>(S, has, r, p, lane);
     w.p0 += 64 * SUB;
-    if (w.p0 >= nwin) {
-        w.gi += 1;
-        w.p0 = 0;
-        if (w.gi >= p.nG) w.phase = kNextDoc;
-    }
-    if (w.phase == kWin) {  // the next step's loads fly across the round barrier
+    if (w.p0 >= w.len) {
+        w.phase = kNextDoc;
+    } else {  // the next step's loads fly across the round barrier
         window_loads<K>(p, w, lane, w.pw);
         w.pf = true;
     }
@@ -1305,8 +1219,6 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartPara
     const int64_t rbase = p.wg_rec[bid], dbase = p.wg_dir[bid];
     const uint32_t lang = (uint32_t)p.wg_lang[bid];
     for (int i = tid; i < kQ * kQ; i += kEmitWaves * 64) S.hist2[i] = 0u;
-    for (int i = tid; i < 256; i += kEmitWaves * 64) S.h1[i] = 0u;
-    for (int i = tid; i < kT23; i += kEmitWaves * 64) S.tkey[i] = S.tcnt[i] = 0u;
     if (tid < kQ) S.pcnt[tid] = 0u;
     if (tid == 0) {
         S.blk_n = 0u;
@@ -1329,50 +1241,12 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartPara
         const uint32_t n = S.blk_n;
         const uint32_t act = S.active;
         lds_barrier();  // every thread has read n / act before the next round moves them
-        if (n > kThresh) {
+        if (n > kThresh || (act == 0u && n > 0u)) {
             flush_block<K>(p, S, n, rbase + written, dbase + nb, tid);
             written += n;
             ++nb;
         }
         if (act == 0u) break;
-    }
-    // the workgroup tables go out as counted records, one slot per thread per
-    // pass (<= 1024 records: a pass fits a round's bound); K = 1 counts beyond
-    // the record's count field go straight to the global table
-    const uint64_t cmax = K == 1 ? (p.cb >= 64 ? ~0ull : ((1ull << p.cb) - 1ull)) : kCntMask;
-    for (int base = 0; base < 256 + kT23; base += kEmitWaves * 64) {
-        const int s = base + tid;
-        uint32_t c = 0, key = 0;
-        if (s < 256) {
-            c = S.h1[s];
-            key = (uint32_t)s | (1u << 24);
-        } else if (s < 256 + kT23) {
-            c = S.tcnt[s - 256];
-            key = S.tkey[s - 256];
-        }
-        bool has[1] = {false};
-        Rec<K> r[1];
-        if (c) {
-            const int klen = (int)(key >> 24);
-            const uint64_t bytes = key & 0xffffffu;
-            if ((uint64_t)c <= cmax) {
-                has[0] = true;
-                r[0] = make_rec<K>(bytes, 0, klen, lang, c, p);
-            } else {
-                add_count(p.direct, bytes | ((uint64_t)klen << 56), (int)lang, (unsigned long long)c);
-            }
-        }
-        if (emit_ablated(p, 4)) has[0] = false;
-        emit_recs<K, 1>(S, has, r, p, lane);
-        lds_barrier();
-        const uint32_t n = S.blk_n;
-        lds_barrier();
-        const bool last = base + kEmitWaves * 64 >= 256 + kT23;
-        if (n > kThresh || (last && n > 0)) {
-            flush_block<K>(p, S, n, rbase + written, dbase + nb, tid);
-            written += n;
-            ++nb;
-        }
     }
     if (tid == 0) p.nblk[bid] = (int32_t)nb;
     const int grp = bid / (p.grid_a / kSplits);
@@ -1676,6 +1550,90 @@ __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const C
     }
 }
 
+// Derive (FIT v4): T1 holds, per (maximal window w of t bytes, language),
+// the number of positions whose maximal window is w.  The n-gram at a
+// position is the n-byte prefix of its maximal window whenever t >= n, so
+// every T1 count c adds mult(n) c to (prefix_n(w), language) in T for each
+// distinct gram length n <= t -- exactly the windows of length n the
+// positions start (LanguageDetector.scala:32-43; duplicates in gramLengths
+// count mult(n) times).  One thread per (slot, language) counter: a wave reads
+// consecutive counters of consecutive slots.
+__device__ __forceinline__ void derive_add(const CountParams& to, const WideCountParams& tow, const DeriveParams& d,
+                                           uint64_t lo, uint64_t hi, int t, int lang, unsigned long long c) {
+    for (int j = 0; j < d.n; ++j) {
+        const int n = d.len[j];
+        if (n > t) break;
+        const unsigned long long cm = c * (unsigned long long)d.mult[j];
+        if (n <= kMaxGram) {
+            add_count(to, (lo & byte_mask(n)) | ((uint64_t)n << 56), lang, cm);
+        } else {
+            const uint64_t h = (n == 8 ? 0ull : (hi & byte_mask(n - 8))) | ((uint64_t)n << 56);
+            wide_add(tow, lo, h, lang, cm);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void derive_kernel(const CountParams from, uint64_t s0, uint64_t s1,
+                                                     const CountParams to, const WideCountParams tow,
+                                                     const DeriveParams d) {
+    const uint64_t L = (uint64_t)from.L;
+    const uint64_t end = s1 * L;
+    for (uint64_t i = s0 * L + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t s = i / L;
+        const uint64_t key = from.keys[s];
+        if (key == kEmpty) continue;
+        const unsigned long long c = from.counts[i];
+        if (!c) continue;
+        derive_add(to, tow, d, key & 0x00ffffffffffffffull, 0ull, key_len(key), (int)(i - s * L), c);
+    }
+}
+
+__global__ __launch_bounds__(256) void wide_derive_kernel(const WideCountParams from, uint64_t s0, uint64_t s1,
+                                                          const CountParams to, const WideCountParams tow,
+                                                          const DeriveParams d) {
+    const uint64_t L = (uint64_t)from.L;
+    const uint64_t end = s1 * L;
+    for (uint64_t i = s0 * L + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t s = i / L;
+        const uint64_t hi = from.khi[s];
+        if (hi == kEmpty) continue;
+        const unsigned long long c = from.counts[i];
+        if (!c) continue;
+        derive_add(to, tow, d, from.klo[s], hi & 0x00ffffffffffffffull, (int)(hi >> 56), (int)(i - s * L), c);
+    }
+}
+
+// Partial windows (Scala sliding: 0 < len < n gives the whole text once):
+// a document shorter than some gram length adds, for every such n in
+// gramLengths (duplicates included), one count of its whole text -- a key of
+// len bytes, straight into T.  Its windows of lengths n <= len are its
+// maximal windows' prefixes (emit / derive).
+__global__ __launch_bounds__(256) void partial_kernel(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang,
+                                                      const int64_t* docs, int64_t n_docs, const CountParams to,
+                                                      const WideCountParams tow, const DeriveParams d) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_docs) return;
+    const int64_t doc = docs[i];
+    const int lang = doc_lang[doc];
+    if (lang < 0 || lang >= to.L) return;
+    const int64_t b = offsets[doc];
+    const int len = (int)(offsets[doc + 1] - b);
+    unsigned long long c = 0;
+    for (int j = 0; j < d.n; ++j)
+        if (d.len[j] > len) c += d.mult[j];
+    if (len <= 0 || len > kMaxWideGram || !c) return;
+    uint64_t lo = 0, hi = 0;
+    for (int k = 0; k < len; ++k) {
+        const uint64_t v = bytes[b + k];
+        if (k < 8) lo |= v << (8 * k);
+        else hi |= v << (8 * (k - 8));
+    }
+    if (len <= kMaxGram) add_count(to, lo | ((uint64_t)len << 56), lang, c);
+    else wide_add(tow, lo, hi | ((uint64_t)len << 56), lang, c);
+}
+
 }  // namespace
 
 size_t emit_lds_bytes(int K) {
@@ -1727,6 +1685,33 @@ hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const 
     if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, e0, n);
     else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, e0, n);
     else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, e0, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_derive(const CountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
+                         const WideCountParams& tow, const DeriveParams& d, hipStream_t stream) {
+    if (s1 <= s0) return hipSuccess;
+    const uint64_t n = (s1 - s0) * (uint64_t)from.L;
+    const unsigned g = (unsigned)std::min<uint64_t>(16384, (n + 255) / 256);
+    hipLaunchKernelGGL(derive_kernel, dim3(g), dim3(256), 0, stream, from, s0, s1, to, tow, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_derive(const WideCountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
+                              const WideCountParams& tow, const DeriveParams& d, hipStream_t stream) {
+    if (s1 <= s0) return hipSuccess;
+    const uint64_t n = (s1 - s0) * (uint64_t)from.L;
+    const unsigned g = (unsigned)std::min<uint64_t>(16384, (n + 255) / 256);
+    hipLaunchKernelGGL(wide_derive_kernel, dim3(g), dim3(256), 0, stream, from, s0, s1, to, tow, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, const int64_t* docs,
+                          int64_t n_docs, const CountParams& to, const WideCountParams& tow, const DeriveParams& d,
+                          hipStream_t stream) {
+    if (n_docs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(partial_kernel, dim3((unsigned)((n_docs + 255) / 256)), dim3(256), 0, stream, bytes, offsets,
+                       doc_lang, docs, n_docs, to, tow, d);
     return hipGetLastError();
 }
 

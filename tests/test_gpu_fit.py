@@ -264,27 +264,27 @@ def test_config3_shape_counts_and_table():
 
 
 @pytest.mark.parametrize("variant,env", [
-    ("product", {}),                                         # FIT v3, the table's own record form: one batch
-    ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v3: many small batches
+    ("product", {}),                                         # FIT v4, the table's own record form: one batch
+    ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v4: many small batches
     ("diag", {"LDGPU_FIT_K": "2"}),                          # two-word records (any L, grams <= 7 bytes)
     ("diag", {"LDGPU_FIT_K": "3", "LDGPU_FIT_BATCH_WINDOWS": "50000"}),  # three-word records, several batches
-    ("diag", {"LDGPU_FIT_EMIT_ABLATE": "1"}),                # no workgroup 2-/3-gram table: every window a record
+    ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "700"}),            # batches of one document (most are longer)
     ("diag", {"LDGPU_FIT_LEGACY": "1"}),                     # round-1 single-pass atomic kernels (A/B only)
 ])
 @pytest.mark.parametrize("L,grams", [(20, [1, 2, 3, 4, 5]), (100, [1, 2, 6]), (256, [3, 1, 3]), (2, [5, 4]),
                                      (200, [1, 2, 3, 4, 5, 6, 7]), (20, [7]), (5, [2, 9, 15]), (30, [8, 1])])
 def test_count_paths_match_oracle(L, grams, variant, env, monkeypatch):
     """Every counting path, bit-exact against the C restatement over two
-    calls: FIT v3 (documents grouped by language, workgroup LDS tables for
-    1-3-byte grams, records of (gram, language, count) bucketed twice and
-    LDS-aggregated) in the table's own record form -- one word when it fits
-    (L=20, grams 1-5), two for grams of <= 7 bytes with many languages (L=200,
-    grams 1-7; L=4096), three with grams of 8..15 bytes -- in one and in many
-    batches, the wider forms forced on small tables, and the legacy kernels.
-    (100, [1, 2, 6]) leaves a one-word record 8 count bits, so hot 1-/2-grams
-    of the long repetitive documents exceed a record's count and take the
-    direct global add; unsupported labels (-1) are skipped; documents shorter
-    than n count their whole text (partial windows)."""
+    calls: FIT v4 (documents grouped by language, one record per byte
+    position -- its maximal window of min(max(G), rest) bytes --, records
+    bucketed twice and LDS-aggregated into the call's table of maximal
+    windows, which derives every gram length as prefixes) in the table's own
+    record form -- one word when it fits (L=20, grams 1-5), two for grams of
+    <= 7 bytes with many languages (L=200, grams 1-7; L=4096), three with
+    grams of 8..15 bytes -- in one and in many batches, the wider forms forced
+    on small tables, and the legacy kernels.  Duplicate lengths count twice
+    (256, [3, 1, 3]); unsupported labels (-1) are skipped; documents shorter
+    than n count their whole text (partial windows, also of 8..14 bytes)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(L + len(grams))
@@ -330,9 +330,9 @@ def test_count_4096_languages(variant, monkeypatch):
 
 
 def test_count_single_language_long_corpus():
-    """One language, long documents: the workgroup tables of a language group
-    fill (2-/3-grams beyond 8192 slots go out as records) and hot grams count
-    far past a record's count field; counts bit-exact."""
+    """One language, long documents: the reduce buckets' LDS hashes fill
+    (random bytes: many distinct windows, some go out unaggregated) and hot
+    grams count far past a record's count field; counts bit-exact."""
     rng = np.random.default_rng(12)
     ls = synth.make_languages(3, seed=12)
     lang = np.zeros(400, np.int32)
