@@ -1523,7 +1523,10 @@ double max_load(const ldgpu_counts* c) {
 }
 
 // after a batch: read size / overflow, grow, re-insert overflow entries
-int after_batch(ldgpu_counts* c) {
+// (may_grow = false: a table being scanned -- the derive's T1 -- keeps its
+// slots: entries are re-inserted in place; the caller keeps it within 0.9
+// load)
+int after_batch(ldgpu_counts* c, bool may_grow = true) {
     unsigned long long size = 0;
     unsigned int novf = 0;
     HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
@@ -1533,7 +1536,7 @@ int after_batch(ldgpu_counts* c) {
         return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost)", novf);
     c->size = size;
     if (novf == 0) {
-        while ((double)c->size > max_load(c) * (double)c->cap) {  // past the load limit: double
+        while (may_grow && (double)c->size > max_load(c) * (double)c->cap) {  // past the load limit: double
             if (int rc = grow(c, 2 * c->cap)) return rc;
         }
         c->tbl_valid = false;
@@ -1578,7 +1581,7 @@ int after_batch(ldgpu_counts* c) {
     // count windows, duplicates included (legacy count kernel), so a grow is
     // sized within 8x the table.
     uint64_t target = c->cap;
-    if ((double)(size + novf) > 0.9 * (double)c->cap) {
+    if (may_grow && (double)(size + novf) > 0.9 * (double)c->cap) {
         target = next_pow2((uint64_t)((double)(size + novf) / max_load(c)) + 16);
         target = std::max<uint64_t>(std::min<uint64_t>(target, 8 * c->cap), 2 * c->cap);
     }
@@ -1604,6 +1607,7 @@ int after_batch(ldgpu_counts* c) {
         std::swap(src_c, dst_c);
         std::swap(src_n, dst_n);
         std::swap(src_cap, dst_cap);
+        if (!may_grow && n > 0) return fail(LDGPU_EDEVICE, "count table: %u entries found no slot", n);
         target = 2 * c->cap;
     }
     c->tbl_valid = false;
@@ -1771,10 +1775,11 @@ int wide_count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, 
 }
 
 // FIT v4 batches: at most batch_recs records (kBatchRecords / K: one per
-// byte position, ~256 MB of corpus), so the record scratch (K words per
+// byte position, ~512 MB of corpus), so the record scratch (K words per
 // record for the emit blocks and the buckets, out_words per record of reduce
-// output) stays within ~8 GB of HBM.
-constexpr int64_t kBatchRecords = 1ll << 28;
+// output) stays within ~16 GB of HBM.  Larger batches merge a frequent
+// (window, language) pair into T1 fewer times.
+constexpr int64_t kBatchRecords = 1ll << 29;
 
 int out_words(int K) { return K == 1 ? 2 : K; }
 
@@ -1795,22 +1800,42 @@ DeriveParams derive_params(const ldgpu_counts* c) {
     return d;
 }
 
-// T1 (c->pend) -> T (c): every T1 count adds to the prefixes of its window
-// (derive_kernel).  In chunks of T1 slots small enough that the overflow
-// list holds every add of the chunk and T, even if every add were a new key,
-// stays within 0.1 of its load limit (T grows with the keys actually
-// inserted); T is first grown once to the projection (T1's windows are
-// mostly new keys of T).
+// T1 (c->pend) -> T (c), level by level (derive_level_kernel): level t
+// reads T1's entries of t bytes, adds them to T (t in gramLengths) and to
+// their (t-1)-byte prefixes in T1.  A level's passes go in chunks of T1 slots
+// small enough that the overflow lists hold every add of the chunk and T,
+// even if every add were a new key, stays within 0.1 of its load limit (T
+// grows with the keys actually inserted).  T1 may not move during a level:
+// it is grown before the level to hold the level's new prefixes (at most its
+// entries) within 0.9 load, and its overflow entries go back in place.
 int derive_pending(ldgpu_counts* c) {
     ldgpu_counts* t = c->pend;
     if (!t || (t->size == 0 && t->wsize == 0)) return LDGPU_OK;
     hipStream_t st = c->ctx->stream;
-    const DeriveParams d = derive_params(c);
-    int nw = 0;
-    for (int j = 0; j < d.n; ++j) nw += d.len[j] > kMaxGram;
+    uint32_t mult[kMaxWideGram + 1] = {};
+    int maxg = 0;
+    for (int i = 0; i < c->nG; ++i) {
+        mult[c->G[i]]++;
+        maxg = std::max(maxg, c->G[i]);
+    }
     const uint64_t L = (uint64_t)c->L;
+    const bool pairs = c->K == 1;           // T1 of (window, language) pairs
+    const uint64_t per_slot = pairs ? 1 : L;  // adds of one T1 slot (to T; to T1)
+    // T1's occupied slots per key length
+    unsigned long long cnt[16] = {};
     {
-        const double est = (double)c->size + 1.1 * (double)(t->size + t->wsize);
+        void* d_h = nullptr;
+        HIP_TRY(cache_alloc(c->ctx, &d_h, sizeof cnt));
+        HIP_TRY(hipMemsetAsync(d_h, 0, sizeof cnt, st));
+        HIP_TRY(launch_len_hist(count_params(t), wide_params(t), pairs, c->lb, (unsigned long long*)d_h, st));
+        HIP_TRY(hipMemcpyAsync(cnt, d_h, sizeof cnt, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        cache_free(c->ctx, d_h, sizeof cnt);
+    }
+    // T's projected growth: the N-byte windows (most of T1) are new keys
+    // (a pair table holds ~2 languages per window on multilingual corpora)
+    {
+        const double est = (double)c->size + (pairs ? 0.55 : 1.1) * (double)(t->size + t->wsize);
         if (est > max_load(c) * (double)c->cap) {
             const uint64_t slot = 8ull + 8ull * L;
             uint64_t target = next_pow2((uint64_t)(est / 0.5) + 1);
@@ -1821,34 +1846,57 @@ int derive_pending(ldgpu_counts* c) {
             }
         }
     }
-    const uint64_t per_slot = L * (uint64_t)d.n;  // adds of one T1 slot at most
-    for (int pass = 0; pass < 2; ++pass) {
-        const bool wide = pass == 1;
+    for (int lev = maxg; lev >= 1; --lev) {
+        const uint32_t mt = mult[lev];
+        const int n = lev - 1;
+        if (!cnt[lev] || (!mt && n < 1)) continue;
+        const bool wide = lev > kMaxGram;
+        // T1 room for this level's prefixes (one per entry at most)
+        if (n >= 1) {
+            if (n <= kMaxGram) {
+                const double need = (double)(t->size + cnt[lev]);
+                if (need > 0.9 * (double)t->cap) {
+                    if (int rc = grow(t, next_pow2((uint64_t)(need / max_load(t)) + 16))) return rc;
+                }
+            } else if (int rc = wide_ensure(t, cnt[lev])) {
+                return rc;
+            }
+            cnt[n] += cnt[lev];
+        }
         const uint64_t tcap = wide ? t->wcap : t->cap;
-        const uint64_t tsize = wide ? t->wsize : t->size;
-        if (!tcap || !tsize) continue;
-        const double tload = std::max(1e-6, (double)tsize / (double)tcap);
+        const double tload = std::max(1e-6, (double)cnt[lev] / (double)tcap);
         for (uint64_t s0 = 0; s0 < tcap;) {
             while ((double)c->size > max_load(c) * (double)c->cap) {
                 if (int rc = grow(c, 2 * c->cap)) return rc;
             }
-            const double room = std::max(1.0, (max_load(c) + 0.1) * (double)c->cap - (double)c->size);
-            uint64_t slots = (uint64_t)(room / (tload * (double)d.n));
-            slots = std::min<uint64_t>(slots, kOvfMax / per_slot);
-            slots = std::max<uint64_t>(slots, 1);
-            slots = std::min<uint64_t>(slots, tcap - s0);
-            if (int rc = ensure_ovf(c, (int64_t)std::min<uint64_t>(slots * per_slot, kOvfMax))) return rc;
-            if (wide && nw) {
-                const uint64_t occ = std::min<uint64_t>(tsize, (uint64_t)(2.0 * tload * (double)slots) + 64);
-                if (int rc = wide_ensure(c, occ * (uint64_t)nw)) return rc;
+            uint64_t slots = kOvfMax / per_slot;
+            if (mt) {
+                const double room = std::max(1.0, (max_load(c) + 0.1) * (double)c->cap - (double)c->size);
+                slots = std::min<uint64_t>(slots, (uint64_t)(room / tload));
+                if (wide) {
+                    const uint64_t occ = std::min<uint64_t>(cnt[lev], (uint64_t)(2.0 * tload * (double)slots) + 64);
+                    if (int rc = wide_ensure(c, occ)) return rc;
+                }
             }
+            slots = std::min<uint64_t>(std::max<uint64_t>(slots, 1), tcap - s0);
+            const int64_t adds = (int64_t)std::min<uint64_t>(slots * per_slot, kOvfMax);
+            if (int rc = ensure_ovf(c, adds)) return rc;
+            if (int rc = ensure_ovf(t, adds)) return rc;
             HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-            if (wide) HIP_TRY(launch_wide_derive(wide_params(t), s0, s0 + slots, count_params(c), wide_params(c), d, st));
-            else HIP_TRY(launch_derive(count_params(t), s0, s0 + slots, count_params(c), wide_params(c), d, st));
-            if (wide && nw) {
+            HIP_TRY(hipMemsetAsync(t->d_ovf_n, 0, sizeof(unsigned int), st));
+            if (pairs)
+                HIP_TRY(launch_derive_pairs_level(count_params(t), c->lb, s0, s0 + slots, lev, mt, count_params(c), st));
+            else
+                HIP_TRY(launch_derive_level(count_params(t), wide_params(t), wide, s0, s0 + slots, lev, mt,
+                                            count_params(c), wide_params(c), st));
+            if (wide && mt) {
                 if (int rc = wide_after(c)) return rc;
             }
+            if (n > kMaxGram) {
+                if (int rc = wide_after(t)) return rc;
+            }
             if (int rc = after_batch(c)) return rc;
+            if (int rc = after_batch(t, false)) return rc;
             s0 += slots;
         }
     }
@@ -1909,7 +1957,10 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     }
     if (int rc = count_partial(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
     if (!c->pend) {
-        if (int rc = counts_new(x, c->L, c->G, c->nG, std::max<int64_t>(1 << 16, c->pend_hint), &c->pend)) return rc;
+        // one-word records: T1 keyed by (window, language) pairs, one counter
+        // each (a dense row of L counters per window otherwise)
+        if (int rc = counts_new(x, K == 1 ? 1 : c->L, c->G, c->nG, std::max<int64_t>(1 << 16, c->pend_hint), &c->pend))
+            return rc;
     }
     ldgpu_counts* t1 = c->pend;
     if (int rc = ensure_ovf(t1, 1 << 20)) return rc;
@@ -2123,7 +2174,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             n = std::max<int64_t>(n, 1);
             if (int rc = ensure_ovf(t1, n)) return rc;
             HIP_TRY(hipMemsetAsync(t1->d_ovf_n, 0, sizeof(unsigned int), st));
-            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), e0, n, st));
+            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), e0, n, K == 1, st));
             if (wide) {
                 if (int rc = wide_after(t1)) return rc;
             }

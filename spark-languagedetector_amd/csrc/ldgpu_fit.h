@@ -25,6 +25,7 @@ struct CountParams {
     unsigned int* ovf_n;
     uint32_t ovf_cap;
     uint32_t max_probe;         // probe limit of an insert (kMaxProbe; re-inserts of overflow entries: more)
+
     int32_t L;
     int32_t nG;
     int32_t G[kMaxGramLengths];
@@ -120,8 +121,9 @@ hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
 struct WideCountParams;
 // add the reduce output entries e0 .. e0 + n into the tables of T1 (K = 3:
 // windows of 8..15 bytes into the wide table)
+// (pairs, K = 1: T1 keyed by the entries' kl, one counter)
 hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
-                        int64_t n, hipStream_t stream);
+                        int64_t n, bool pairs, hipStream_t stream);
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
 hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
                          hipStream_t stream);
@@ -168,12 +170,18 @@ struct DeriveParams {
     int32_t len[kMaxGramLengths];
     uint32_t mult[kMaxGramLengths];
 };
-// every (window w, language, c) of T1's slots [s0, s1) adds mult c to
-// (prefix of each distinct length <= |w|, language) in T (to / tow)
-hipError_t launch_derive(const CountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
-                         const WideCountParams& tow, const DeriveParams& d, hipStream_t stream);
-hipError_t launch_wide_derive(const WideCountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
-                              const WideCountParams& tow, const DeriveParams& d, hipStream_t stream);
+// level lev of the derive: T1's entries of lev bytes in slots [s0, s1) of its
+// one-word (wide = false) or wide table add mult c to T and c to their
+// (lev - 1)-byte prefix (flagged) in T1
+hipError_t launch_derive_level(const CountParams& t1, const WideCountParams& t1w, bool wide, uint64_t s0, uint64_t s1,
+                               int lev, uint32_t mt, const CountParams& to, const WideCountParams& tow,
+                               hipStream_t stream);
+// the same for a pair table T1 (K = 1: keys kl, one counter; lb language bits)
+hipError_t launch_derive_pairs_level(const CountParams& t1, uint32_t lb, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
+                                     const CountParams& to, hipStream_t stream);
+// out[t] += occupied T1 slots of t-byte keys (16 counters)
+hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, bool pairs, uint32_t lb,
+                           unsigned long long* out, hipStream_t stream);
 // partial windows of docs[0 .. n) (documents shorter than some gram length)
 hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, const int64_t* docs,
                           int64_t n_docs, const CountParams& to, const WideCountParams& tow, const DeriveParams& d,

@@ -71,6 +71,17 @@ __device__ __forceinline__ unsigned long long block_compact(bool occ, unsigned l
     return o;
 }
 
+// FIT v4 derive: flag of the prefix aggregates a level adds to T1 (never a
+// key bit: klen <= 15 in bits 56..59; pair keys use <= 57 bits)
+constexpr uint64_t kDerived = 1ull << 62;
+
+// the packed key (ldgpu_common.h) of a K = 1 record's kl = record >> cb
+__device__ __forceinline__ uint64_t kl_key(uint64_t kl, uint32_t lb) {
+    const uint64_t sent = kl >> lb;
+    const int klen = (63 - __builtin_clzll(sent)) >> 3;
+    return (sent ^ (1ull << (8 * klen))) | ((uint64_t)klen << 56);
+}
+
 // find-or-insert; returns the slot or -1 when the probe limit is reached
 __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key, bool& new_key) {
     uint64_t s = mix64(key) >> p.shift;
@@ -975,7 +986,9 @@ __device__ __forceinline__ uint32_t rec_lang(const Rec<K>& r, uint32_t lb, uint3
     else return (uint32_t)(r.w[K - 1] >> kCntBits);
 }
 
-// route hash of the record's (gram, language) pair
+// route hash of the record's (gram, language) pair; K = 1: the T1 pair
+// table's slot hash of the entry (mix64(kl)), so a bucket of records maps to
+// one contiguous slice of T1 (the merge's inserts stay local)
 template <int K>
 __device__ __forceinline__ uint64_t rec_hash(const Rec<K>& r, uint32_t cb) {
     if constexpr (K == 1) return mix64(r.w[0] >> cb);
@@ -1004,12 +1017,6 @@ __device__ __forceinline__ void store_rec(uint64_t* base, int64_t i, const Rec<K
     for (int k = 0; k < K; ++k) base[i * K + k] = r.w[k];
 }
 
-// the packed key (ldgpu_common.h) of a K = 1 record's kl = record >> cb
-__device__ __forceinline__ uint64_t kl_key(uint64_t kl, uint32_t lb) {
-    const uint64_t sent = kl >> lb;
-    const int klen = (63 - __builtin_clzll(sent)) >> 3;
-    return (sent ^ (1ull << (8 * klen))) | ((uint64_t)klen << 56);
-}
 
 // Workgroup barrier for LDS traffic only: waits for this wave's LDS operations
 // (lgkmcnt), not for its outstanding global loads -- __syncthreads() would
@@ -1342,7 +1349,7 @@ __global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams
 // one workgroup's LDS)
 template <int K>
 constexpr int agg_slots() {
-    return K == 1 ? 8192 : (K == 2 ? 6144 : 4096);
+    return K == 1 ? 12288 : (K == 2 ? 6144 : 4096);
 }
 
 // entries out: bucket b writes from boff[b] on (it has at most as many as
@@ -1525,9 +1532,11 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
 
 // entry i of the batch (buckets' outputs in bucket order, prefix epre) ->
 // bucket b = the last with epre[b] <= i, stored at boff[b] + (i - epre[b])
+// pairs (K = 1): T1 is a table of (window, language) pairs -- key = the
+// entry's kl (sentinel key << lb | lang), one counter (L = 1)
 template <int K>
 __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const CountParams c, const WideCountParams w,
-                                                     int64_t e0, int64_t n) {
+                                                     int64_t e0, int64_t n, int pairs) {
     __shared__ uint64_t pre[kQ * kQ + 1];
     for (int i = threadIdx.x; i <= kQ * kQ; i += blockDim.x) pre[i] = p.epre[i];
     __syncthreads();
@@ -1540,7 +1549,8 @@ __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const C
     const int64_t at = (int64_t)p.boff[lo] + (i - (int64_t)pre[lo]);
     if constexpr (K == 1) {
         const uint64_t kl = p.out[2 * at];
-        add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out[2 * at + 1]);
+        if (pairs) add_count(c, kl, 0, p.out[2 * at + 1]);
+        else add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out[2 * at + 1]);
     } else {
         const Rec<K> r = load_rec<K>(p.out, at);
         const int lang = (int)(r.w[K - 1] >> kCntBits);
@@ -1550,59 +1560,101 @@ __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const C
     }
 }
 
-// Derive (FIT v4): T1 holds, per (maximal window w of t bytes, language),
-// the number of positions whose maximal window is w.  The n-gram at a
-// position is the n-byte prefix of its maximal window whenever t >= n, so
-// every T1 count c adds mult(n) c to (prefix_n(w), language) in T for each
-// distinct gram length n <= t -- exactly the windows of length n the
-// positions start (LanguageDetector.scala:32-43; duplicates in gramLengths
-// count mult(n) times).  One thread per (slot, language) counter: a wave reads
-// consecutive counters of consecutive slots.
-__device__ __forceinline__ void derive_add(const CountParams& to, const WideCountParams& tow, const DeriveParams& d,
-                                           uint64_t lo, uint64_t hi, int t, int lang, unsigned long long c) {
-    for (int j = 0; j < d.n; ++j) {
-        const int n = d.len[j];
-        if (n > t) break;
-        const unsigned long long cm = c * (unsigned long long)d.mult[j];
-        if (n <= kMaxGram) {
-            add_count(to, (lo & byte_mask(n)) | ((uint64_t)n << 56), lang, cm);
+// Derive (FIT v4), level by level.  T1 holds, per (maximal window w of t
+// bytes, language), the number of positions whose maximal window is w.  With
+// S_n(g) = the positions whose maximal window has g as prefix and >= n bytes
+// -- the count of the n-gram g (LanguageDetector.scala:32-43) --
+//   S_N = the windows of N bytes,   S_n(g) = sum_x S_{n+1}(g x) + A_n(g)
+// (A_n: the maximal windows of exactly n bytes, the tails of documents).
+// Level t: every T1 entry of t bytes -- a maximal window or an aggregate of
+// level t made by level t + 1 (key flag kDerived) -- adds mult(t) c to its
+// key in T when t is in gramLengths (duplicates count mult(t) times) and c to
+// its (t-1)-byte prefix, flagged, in T1.  The entries a level inserts are one
+// byte shorter than the ones it reads, so one pass per level sees each
+// entry once; the host keeps T1 from growing during a level.  Compared with
+// adding every maximal window to all its prefixes, a level adds only its own
+// distinct keys to the next (the hot 1- and 2-byte prefixes receive a few
+// thousand adds instead of one per window of the table).
+
+__global__ __launch_bounds__(256) void derive_level_kernel(const CountParams t1, const WideCountParams t1w, int wide,
+                                                           uint64_t s0, uint64_t s1, int lev, uint32_t mt,
+                                                           const CountParams to, const WideCountParams tow) {
+    const int L = t1.L;
+    for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo, hi = 0;
+        const unsigned long long* row;
+        if (!wide) {
+            const uint64_t key = t1.keys[s];
+            if (key == kEmpty || (int)((key >> 56) & 15) != lev) continue;
+            lo = key & 0x00ffffffffffffffull;
+            row = t1.counts + s * (uint64_t)L;
         } else {
-            const uint64_t h = (n == 8 ? 0ull : (hi & byte_mask(n - 8))) | ((uint64_t)n << 56);
-            wide_add(tow, lo, h, lang, cm);
+            const uint64_t h = t1w.khi[s];
+            if (h == kEmpty || (int)((h >> 56) & 15) != lev) continue;
+            lo = t1w.klo[s];
+            hi = h & 0x00ffffffffffffffull;
+            row = t1w.counts + s * (uint64_t)L;
+        }
+        const int n = lev - 1;
+        for (int l = 0; l < L; ++l) {
+            const unsigned long long c = row[l];
+            if (!c) continue;
+            if (mt) {
+                if (lev <= kMaxGram) add_count(to, lo | ((uint64_t)lev << 56), l, c * mt);
+                else wide_add(tow, lo, hi | ((uint64_t)lev << 56), l, c * mt);
+            }
+            if (n >= 1) {
+                if (n <= kMaxGram) add_count(t1, (lo & byte_mask(n)) | ((uint64_t)n << 56) | kDerived, l, c);
+                else wide_add(t1w, lo, (hi & byte_mask(n - 8)) | ((uint64_t)n << 56) | kDerived, l, c);
+            }
         }
     }
 }
 
-__global__ __launch_bounds__(256) void derive_kernel(const CountParams from, uint64_t s0, uint64_t s1,
-                                                     const CountParams to, const WideCountParams tow,
-                                                     const DeriveParams d) {
-    const uint64_t L = (uint64_t)from.L;
-    const uint64_t end = s1 * L;
-    for (uint64_t i = s0 * L + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t s = i / L;
-        const uint64_t key = from.keys[s];
+// the same level for a pair table T1 (K = 1 records: key = kl | kDerived,
+// one counter): one thread per (window, language) entry
+__device__ __forceinline__ int kl_len(uint64_t kl, uint32_t lb) {
+    return (63 - __builtin_clzll(kl >> lb)) >> 3;
+}
+
+__global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountParams t1, uint32_t lb, uint64_t s0,
+                                                                 uint64_t s1, int lev, uint32_t mt,
+                                                                 const CountParams to) {
+    const uint64_t lmask = (1ull << lb) - 1ull;
+    for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = t1.keys[s];
         if (key == kEmpty) continue;
-        const unsigned long long c = from.counts[i];
-        if (!c) continue;
-        derive_add(to, tow, d, key & 0x00ffffffffffffffull, 0ull, key_len(key), (int)(i - s * L), c);
+        const uint64_t kl = key & ~kDerived;
+        const int klen = kl_len(kl, lb);
+        if (klen != lev) continue;
+        const unsigned long long c = t1.counts[s];
+        const int lang = (int)(kl & lmask);
+        const uint64_t bytes = (kl >> lb) ^ (1ull << (8 * klen));
+        if (mt) add_count(to, bytes | ((uint64_t)klen << 56), lang, c * mt);
+        const int n = lev - 1;
+        if (n >= 1) {
+            const uint64_t sent = (1ull << (8 * n)) | (bytes & byte_mask(n));
+            add_count(t1, ((sent << lb) | (uint64_t)lang) | kDerived, 0, c);
+        }
     }
 }
 
-__global__ __launch_bounds__(256) void wide_derive_kernel(const WideCountParams from, uint64_t s0, uint64_t s1,
-                                                          const CountParams to, const WideCountParams tow,
-                                                          const DeriveParams d) {
-    const uint64_t L = (uint64_t)from.L;
-    const uint64_t end = s1 * L;
-    for (uint64_t i = s0 * L + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t s = i / L;
-        const uint64_t hi = from.khi[s];
-        if (hi == kEmpty) continue;
-        const unsigned long long c = from.counts[i];
-        if (!c) continue;
-        derive_add(to, tow, d, from.klo[s], hi & 0x00ffffffffffffffull, (int)(hi >> 56), (int)(i - s * L), c);
+// occupied T1 slots per key length (one-word and wide tables)
+__global__ __launch_bounds__(256) void len_hist_kernel(const CountParams t1, const WideCountParams t1w, int pairs,
+                                                       uint32_t lb, unsigned long long* out) {
+    __shared__ unsigned int h[16];
+    if (threadIdx.x < 16) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint64_t cap = t1.mask + 1, wcap = t1w.klo ? t1w.mask + 1 : 0;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap + wcap;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = s < cap ? t1.keys[s] : t1w.khi[s - cap];
+        if (k != kEmpty) atomicAdd(&h[pairs ? kl_len(k & ~kDerived, lb) : (int)((k >> 56) & 15)], 1u);
     }
+    __syncthreads();
+    if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&out[threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
 // Partial windows (Scala sliding: 0 < len < n gives the whole text once):
@@ -1679,30 +1731,39 @@ hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream) {
 }
 
 hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
-                        int64_t n, hipStream_t stream) {
+                        int64_t n, bool pairs, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     const dim3 g((unsigned)((n + 1023) / 1024)), b(1024);
-    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, e0, n);
-    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, e0, n);
-    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, e0, n);
+    const int pr = pairs && K == 1;
+    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, e0, n, pr);
+    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, e0, n, 0);
+    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, e0, n, 0);
     return hipGetLastError();
 }
 
-hipError_t launch_derive(const CountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
-                         const WideCountParams& tow, const DeriveParams& d, hipStream_t stream) {
+hipError_t launch_derive_level(const CountParams& t1, const WideCountParams& t1w, bool wide, uint64_t s0, uint64_t s1,
+                               int lev, uint32_t mt, const CountParams& to, const WideCountParams& tow,
+                               hipStream_t stream) {
     if (s1 <= s0) return hipSuccess;
-    const uint64_t n = (s1 - s0) * (uint64_t)from.L;
-    const unsigned g = (unsigned)std::min<uint64_t>(16384, (n + 255) / 256);
-    hipLaunchKernelGGL(derive_kernel, dim3(g), dim3(256), 0, stream, from, s0, s1, to, tow, d);
+    const unsigned g = (unsigned)std::min<uint64_t>(16384, (s1 - s0 + 255) / 256);
+    hipLaunchKernelGGL(derive_level_kernel, dim3(g), dim3(256), 0, stream, t1, t1w, (int)wide, s0, s1, lev, mt, to,
+                       tow);
     return hipGetLastError();
 }
 
-hipError_t launch_wide_derive(const WideCountParams& from, uint64_t s0, uint64_t s1, const CountParams& to,
-                              const WideCountParams& tow, const DeriveParams& d, hipStream_t stream) {
+hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, bool pairs, uint32_t lb,
+                           unsigned long long* out, hipStream_t stream) {
+    const uint64_t n = t1.mask + 1 + (t1w.klo ? t1w.mask + 1 : 0);
+    const unsigned g = (unsigned)std::min<uint64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(len_hist_kernel, dim3(g), dim3(256), 0, stream, t1, t1w, (int)pairs, lb, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_derive_pairs_level(const CountParams& t1, uint32_t lb, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
+                                     const CountParams& to, hipStream_t stream) {
     if (s1 <= s0) return hipSuccess;
-    const uint64_t n = (s1 - s0) * (uint64_t)from.L;
-    const unsigned g = (unsigned)std::min<uint64_t>(16384, (n + 255) / 256);
-    hipLaunchKernelGGL(wide_derive_kernel, dim3(g), dim3(256), 0, stream, from, s0, s1, to, tow, d);
+    const unsigned g = (unsigned)std::min<uint64_t>(16384, (s1 - s0 + 255) / 256);
+    hipLaunchKernelGGL(derive_pairs_level_kernel, dim3(g), dim3(256), 0, stream, t1, lb, s0, s1, lev, mt, to);
     return hipGetLastError();
 }
 
