@@ -2004,11 +2004,12 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             }
         }
         // emit workgroups: each language's documents split into ranges
-        // balanced by records, about 2 workgroups per CU in all; a
+        // balanced by records, about 4 workgroups per CU in all (2 resident:
+        // the tail of the launch stays short); a
         // workgroup's record region holds its records, its block directory
         // records / threshold + 2 blocks
         const int64_t Wk = std::accumulate(lwin.begin(), lwin.end(), (int64_t)0);
-        const int64_t target = std::max<int64_t>(1, (Wk + 2 * x->cus - 1) / (2 * x->cus));
+        const int64_t target = std::max<int64_t>(1, (Wk + 4 * x->cus - 1) / (4 * x->cus));
         wg_doc.clear();
         wg_rec.clear();
         wg_dir.clear();

@@ -62,7 +62,7 @@ constexpr int kQ = 1 << kQBits;                 // buckets per level
 constexpr int kBlkWords = 6144;                 // u64 words of records per emit block (LDS, 48 KiB)
 constexpr int kHdr = 68;                        // u32 per block header (kQ + 1 used)
 constexpr int kEmitWaves = 16;
-constexpr int kSplits = 4;                      // emit workgroup groups (part2 inputs)
+constexpr int kSplits = 8;                      // emit workgroup groups (part2 inputs)
 constexpr uint64_t kCntBits = 52;               // K >= 2: count bits of the last record word
 // emit rounds: a wave step adds at most 64 x sub records (sub = 4 positions per
 // lane for K = 1, 1 otherwise); a block is flushed once it could not take

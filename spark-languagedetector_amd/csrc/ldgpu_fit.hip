@@ -1215,7 +1215,7 @@ __device__ __forceinline__ void flush_block(const PartParams& p, EmitLds<K>& S, 
 }
 
 template <int K>
-__global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartParams p) {
+__global__ __launch_bounds__(kEmitWaves * 64, 2) void emit_kernel(const PartParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t emit_smem[];
     EmitLds<K>& S = *reinterpret_cast<EmitLds<K>*>(emit_smem);
     constexpr uint32_t kThresh = (uint32_t)(emit_blk_recs(K) - emit_round_recs(K));
@@ -1261,9 +1261,34 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void emit_kernel(const PartPara
         if (S.hist2[i]) atomicAdd(&p.cnt3[i * kSplits + grp], S.hist2[i]);
 }
 
+// part2: the q1 runs of one emit group's blocks -> q2 sub-buckets at exact
+// offsets.  Per round the workgroup gathers up to p2_cap records of
+// consecutive runs into LDS (a run longer than the room continues in the next
+// round), counting-sorts them by q2 there and writes each q2 segment
+// contiguously at the workgroup's running cursor of that sub-bucket -- stores
+// of consecutive addresses, where scattering each record to its sub-bucket
+// straight from the run would touch 64 lines per store instruction.  (Order
+// within a sub-bucket is free: reduce sums.)
+template <int K>
+constexpr int p2_cap() {
+    return K == 1 ? 4096 : (K == 2 ? 2048 : 1024);
+}
+
+template <int K>
 struct Part2Lds {
-    uint32_t cur[kQ];
-    int32_t gpre[257];
+    uint64_t in[p2_cap<K>() * K];
+    uint64_t out[p2_cap<K>() * K];
+    uint8_t q2in[p2_cap<K>()];
+    uint8_t q2out[p2_cap<K>()];
+    int64_t rstart[64];    // the round's runs: first record (global index)
+    uint32_t roff[65];     // their offsets in the round (exclusive prefix), roff[64] = total
+    uint32_t hist[kQ];
+    uint32_t fill[kQ];
+    uint32_t lstart[kQ];
+    uint64_t cur[kQ];      // records written per q2 sub-bucket so far
+    int64_t base[kQ];      // global index of the round's first record of q2, minus its LDS start
+    int32_t gpre[257];     // blocks of the group's emit workgroups (exclusive prefix)
+    int64_t unit, uoff;    // next run and the records of it already taken
 };
 
 __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) {
@@ -1271,14 +1296,13 @@ __device__ __forceinline__ int64_t rdlane_i64(int64_t v, int l) {
                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32));
 }
 
-// q1 bucket of one emit group -> its q2 sub-buckets (per-group units of
-// part2: blocks of the group's workgroups, load-balanced over the waves)
 template <int K>
 __global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams p) {
-    __shared__ Part2Lds S;
+    constexpr int CAP = p2_cap<K>();
+    constexpr int NT = kEmitWaves * 64;
+    __shared__ Part2Lds<K> S;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t q1 = blockIdx.x / kSplits;
     const int s = blockIdx.x % kSplits;
     const int per = p.grid_a / kSplits;
@@ -1290,58 +1314,101 @@ __global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams
             acc += p.nblk[w0 + k];
         }
         S.gpre[per] = acc;
+        S.unit = 0;
+        S.uoff = 0;
     }
-    if (tid < kQ) S.cur[tid] = 0u;
+    if (tid < kQ) {
+        S.cur[tid] = 0;
+        S.hist[tid] = 0u;
+    }
     __syncthreads();
     const int64_t tb = S.gpre[per];
-    for (int64_t u0 = (int64_t)wave * 64; u0 < tb; u0 += kEmitWaves * 64) {
-        const int64_t u = u0 + lane;
-        int64_t start = 0;
-        uint32_t len = 0;
-        if (u < tb) {
-            int lo = 0, hi = per;  // emit workgroup of unit u: largest k with gpre[k] <= u
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (S.gpre[mid] <= u) lo = mid;
-                else hi = mid;
-            }
-            const int64_t gid = p.wg_dir[w0 + lo] + (u - S.gpre[lo]);
-            const uint32_t a = p.blk_hdr[(size_t)gid * kHdr + q1];
-            const uint32_t e = p.blk_hdr[(size_t)gid * kHdr + q1 + 1];
-            start = p.blk_start[gid] + a;
-            len = e - a;
-        }
-        // the chunk's 64 runs, kR at a time: the wave loads the runs' records
-        // cooperatively (runs average emit_blk_recs / kQ records), kR loads in flight
-        constexpr int kR = K == 1 ? 8 : 4;
-        for (int i = 0; i < 64; i += kR) {
-            int64_t st[kR];
-            uint32_t ln[kR];
-            uint32_t lm = 0;
-#pragma unroll
-            for (int k = 0; k < kR; ++k) {
-                st[k] = rdlane_i64(start, i + k);
-                ln[k] = (uint32_t)__builtin_amdgcn_readlane((int)len, i + k);
-                lm = ln[k] > lm ? ln[k] : lm;
-            }
-            for (uint32_t j = lane; j < ((lm + 63u) & ~63u); j += 64) {
-                Rec<K> r[kR];
-#pragma unroll
-                for (int k = 0; k < kR; ++k) {
-                    if (j < ln[k]) r[k] = load_rec<K>(p.rec, st[k] + j);
+    for (;;) {
+        if (tid < 64) {  // wave 0 plans the round: runs unit .. unit + 63
+            const int64_t u0 = S.unit, o0 = S.uoff;
+            const int64_t u = u0 + lane;
+            int64_t st = 0;
+            uint32_t ln = 0;
+            if (u < tb) {
+                int lo = 0, hi = per;  // emit workgroup of unit u: largest k with gpre[k] <= u
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (S.gpre[mid] <= u) lo = mid;
+                    else hi = mid;
                 }
-#pragma unroll
-                for (int k = 0; k < kR; ++k) {
-                    if (j < ln[k]) {
-                        const uint32_t q2 = (uint32_t)(rec_hash<K>(r[k], p.cb) >> (64 - 2 * kQBits)) & (kQ - 1);
-                        const uint32_t at =
-                            __hip_atomic_fetch_add(&S.cur[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        store_rec<K>(p.rec2, (int64_t)p.p2off[(q1 * kQ + q2) * kSplits + s] + at, r[k]);
-                    }
+                const int64_t gid = p.wg_dir[w0 + lo] + (u - S.gpre[lo]);
+                const uint32_t a = p.blk_hdr[(size_t)gid * kHdr + q1];
+                const uint32_t e = p.blk_hdr[(size_t)gid * kHdr + q1 + 1];
+                st = p.blk_start[gid] + a;
+                ln = e - a;
+                if (lane == 0) {
+                    st += o0;
+                    ln -= (uint32_t)o0;
                 }
             }
+            const uint32_t inc = wave_inclusive_scan(ln, lane);
+            const uint32_t exc = inc - ln;
+            const uint64_t over = __ballot(inc > (uint32_t)CAP);
+            S.rstart[lane] = st;
+            S.roff[lane] = exc < (uint32_t)CAP ? exc : (uint32_t)CAP;
+            if (lane == 63) {
+                const int64_t nu = u0 + 64 < tb ? u0 + 64 : tb;
+                if (!over) {
+                    S.roff[64] = inc;
+                    S.unit = nu;
+                    S.uoff = 0;
+                }
+            }
+            if (over) {
+                const int l = __builtin_ctzll(over);  // the run the room ends in
+                const uint32_t ex_l = (uint32_t)__shfl((int)exc, l);
+                if (lane == 0) {
+                    S.roff[64] = CAP;
+                    S.unit = u0 + l;
+                    S.uoff = (l == 0 ? o0 : 0) + (int64_t)(CAP - ex_l);
+                }
+            }
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        const uint32_t T = S.roff[64];
+        const bool done = S.unit >= tb;
+        if (T == 0u) {  // 64 empty runs (or none left)
+            __syncthreads();  // every thread has read T / unit before wave 0 plans again
+            if (done) break;
+            continue;
+        }
+        // gather: record i of the round from its run
+        for (uint32_t i = tid; i < T; i += NT) {
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (S.roff[lo + step] <= i) lo += step;
+            const Rec<K> r = load_rec<K>(p.rec, S.rstart[lo] + (int64_t)(i - S.roff[lo]));
+            const uint32_t q2 = (uint32_t)(rec_hash<K>(r, p.cb) >> (64 - 2 * kQBits)) & (kQ - 1);
+            store_rec<K>(S.in, i, r);
+            S.q2in[i] = (uint8_t)q2;
+            __hip_atomic_fetch_add(&S.hist[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const uint32_t v = S.hist[tid];
+            const uint32_t inc = wave_inclusive_scan(v, tid);
+            S.lstart[tid] = inc - v;
+            S.fill[tid] = inc - v;
+            S.base[tid] = (int64_t)p.p2off[((size_t)q1 * kQ + tid) * kSplits + s] + (int64_t)S.cur[tid] - (int64_t)(inc - v);
+            S.cur[tid] += v;
+            S.hist[tid] = 0u;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < T; i += NT) {
+            const uint32_t q2 = S.q2in[i];
+            const uint32_t at = __hip_atomic_fetch_add(&S.fill[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            store_rec<K>(S.out, at, load_rec<K>(S.in, i));
+            S.q2out[at] = (uint8_t)q2;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < T; i += NT) store_rec<K>(p.rec2, S.base[S.q2out[i]] + (int64_t)i, load_rec<K>(S.out, i));
+        __syncthreads();  // the next round's plan overwrites roff / rstart; its gather, in
     }
 }
 
