@@ -1807,7 +1807,8 @@ DeriveParams derive_params(const ldgpu_counts* c) {
 // even if every add were a new key, stays within 0.1 of its load limit (T
 // grows with the keys actually inserted).  T1 may not move during a level:
 // it is grown before the level to hold the level's new prefixes (at most its
-// entries) within 0.9 load, and its overflow entries go back in place.
+// entries) within 0.1 of its load limit, and its overflow entries go back in
+// place.
 int derive_pending(ldgpu_counts* c) {
     ldgpu_counts* t = c->pend;
     if (!t || (t->size == 0 && t->wsize == 0)) return LDGPU_OK;
@@ -1819,6 +1820,8 @@ int derive_pending(ldgpu_counts* c) {
         maxg = std::max(maxg, c->G[i]);
     }
     const uint64_t L = (uint64_t)c->L;
+    const char* dab = diag_env("LDGPU_FIT_DERIVE_ABLATE");  // timing only (counts wrong)
+    const int derive_ablate = dab ? atoi(dab) : 0;
     const bool pairs = c->K == 1;           // T1 of (window, language) pairs
     const uint64_t per_slot = pairs ? 1 : L;  // adds of one T1 slot (to T; to T1)
     // T1's occupied slots per key length
@@ -1851,11 +1854,12 @@ int derive_pending(ldgpu_counts* c) {
         const int n = lev - 1;
         if (!cnt[lev] || (!mt && n < 1)) continue;
         const bool wide = lev > kMaxGram;
-        // T1 room for this level's prefixes (one per entry at most)
+        // T1 room for this level's prefixes (one per entry at most), within
+        // 0.1 of its load limit (linear probes stay short)
         if (n >= 1) {
             if (n <= kMaxGram) {
                 const double need = (double)(t->size + cnt[lev]);
-                if (need > 0.9 * (double)t->cap) {
+                if (need > (max_load(t) + 0.1) * (double)t->cap) {
                     if (int rc = grow(t, next_pow2((uint64_t)(need / max_load(t)) + 16))) return rc;
                 }
             } else if (int rc = wide_ensure(t, cnt[lev])) {
@@ -1885,7 +1889,8 @@ int derive_pending(ldgpu_counts* c) {
             HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
             HIP_TRY(hipMemsetAsync(t->d_ovf_n, 0, sizeof(unsigned int), st));
             if (pairs)
-                HIP_TRY(launch_derive_pairs_level(count_params(t), c->lb, s0, s0 + slots, lev, mt, count_params(c), st));
+                HIP_TRY(launch_derive_pairs_level(count_params(t), c->lb, s0, s0 + slots, lev, mt, count_params(c),
+                                                  derive_ablate, st));
             else
                 HIP_TRY(launch_derive_level(count_params(t), wide_params(t), wide, s0, s0 + slots, lev, mt,
                                             count_params(c), wide_params(c), st));
@@ -2115,7 +2120,6 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         pp.boff = (const uint64_t*)x->f_boff.p;
         pp.out = (uint64_t*)x->f_okl.p;
         pp.nout = (uint32_t*)x->f_on.p;
-        pp.epre = (const uint64_t*)((const uint8_t*)x->f_on.p + sizeof(uint32_t) * kQ * kQ);
         std::vector<uint32_t> nout((size_t)kQ * kQ, 0u);
         if (R > 0) {
             HIP_TRY(launch_part2(K, pp, st));
@@ -2123,16 +2127,13 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             HIP_TRY(hipMemcpyAsync(nout.data(), pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
         }
         HIP_TRY(hipStreamSynchronize(st));
-        // the merge's entry order: buckets' outputs back to back
-        std::vector<uint64_t> epre((size_t)kQ * kQ + 1, 0);
+        unsigned long long E = 0;
         for (int b = 0; b < kQ * kQ; ++b) {
             if (nout[b] > boff[b + 1] - boff[b])
                 return fail(LDGPU_EDEVICE, "fit reduce: bucket %d wrote %u entries from %llu records", b, nout[b],
                             (unsigned long long)(boff[b + 1] - boff[b]));
-            epre[b + 1] = epre[b] + nout[b];
+            E += nout[b];
         }
-        const unsigned long long E = epre[(size_t)kQ * kQ];
-        HIP_TRY(hipMemcpyAsync((void*)pp.epre, epre.data(), sizeof(uint64_t) * epre.size(), hipMemcpyHostToDevice, st));
         // The merge into T1 in chunks, each small enough that even if every
         // entry of it were a new key a table would stay within 0.1 of its load
         // limit (probes stay short and rarely reach the overflow list -- which
@@ -2162,7 +2163,8 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             }
         }
         const uint64_t size0 = t1->size + t1->wsize;
-        for (int64_t e0 = 0; e0 < (int64_t)E;) {
+        // (no entries: nout on the device is the last batch's, reduce did not run)
+        for (int b0 = E ? 0 : kQ * kQ; b0 < kQ * kQ;) {
             while ((double)t1->size > max_load(t1) * (double)t1->cap) {
                 if (int rc = grow(t1, 2 * t1->cap)) return rc;
             }
@@ -2170,17 +2172,20 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
                 if (int rc = wide_ensure(t1, 0)) return rc;
             }
             const double ceil_load = max_load(t1) + 0.1;
-            int64_t n = std::min<int64_t>((int64_t)E - e0, (int64_t)(ceil_load * (double)t1->cap) - (int64_t)t1->size);
-            if (wide) n = std::min<int64_t>(n, (int64_t)(3 * (t1->wcap / 4) - t1->wsize));
-            n = std::max<int64_t>(n, 1);
-            if (int rc = ensure_ovf(t1, n)) return rc;
+            int64_t room = (int64_t)(ceil_load * (double)t1->cap) - (int64_t)t1->size;
+            if (wide) room = std::min<int64_t>(room, (int64_t)(3 * (t1->wcap / 4) - t1->wsize));
+            // buckets b0 .. b1 (at least one) whose entries fit the room
+            int b1 = b0;
+            int64_t n = 0;
+            while (b1 < kQ * kQ && (b1 == b0 || n + (int64_t)nout[b1] <= room)) n += nout[b1++];
+            if (int rc = ensure_ovf(t1, std::max<int64_t>(n, 1))) return rc;
             HIP_TRY(hipMemsetAsync(t1->d_ovf_n, 0, sizeof(unsigned int), st));
-            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), e0, n, K == 1, st));
+            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), b0, b1, K == 1, st));
             if (wide) {
                 if (int rc = wide_after(t1)) return rc;
             }
             if (int rc = after_batch(t1)) return rc;
-            e0 += n;
+            b0 = b1;
         }
         if (E) t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - size0) / (double)E);
         d0 = d1;

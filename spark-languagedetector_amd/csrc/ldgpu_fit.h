@@ -109,7 +109,6 @@ struct PartParams {
     const uint64_t* boff;       // [kQ * kQ + 1]
     uint64_t* out;              // K words per entry (the record form, the count field a batch sum)
     uint32_t* nout;             // [kQ * kQ]
-    const uint64_t* epre;       // merge: exclusive prefix of nout [kQ * kQ + 1]
 };
 
 size_t emit_lds_bytes(int K);
@@ -119,11 +118,11 @@ hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream);
 hipError_t launch_part2(int K, const PartParams& p, hipStream_t stream);
 hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
 struct WideCountParams;
-// add the reduce output entries e0 .. e0 + n into the tables of T1 (K = 3:
-// windows of 8..15 bytes into the wide table)
-// (pairs, K = 1: T1 keyed by the entries' kl, one counter)
-hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
-                        int64_t n, bool pairs, hipStream_t stream);
+// add the reduce output entries of buckets b0 .. b1 into the tables of T1
+// (K = 3: windows of 8..15 bytes into the wide table)
+// (buckets b0 .. b1; pairs, K = 1: T1 keyed by the entries' kl, one counter)
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int b0, int b1,
+                        bool pairs, hipStream_t stream);
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
 hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
                          hipStream_t stream);
@@ -177,8 +176,9 @@ hipError_t launch_derive_level(const CountParams& t1, const WideCountParams& t1w
                                int lev, uint32_t mt, const CountParams& to, const WideCountParams& tow,
                                hipStream_t stream);
 // the same for a pair table T1 (K = 1: keys kl, one counter; lb language bits)
+// (ablate: diagnostics build only, bit 0 no adds to T, bit 1 no prefix adds)
 hipError_t launch_derive_pairs_level(const CountParams& t1, uint32_t lb, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
-                                     const CountParams& to, hipStream_t stream);
+                                     const CountParams& to, int ablate, hipStream_t stream);
 // out[t] += occupied T1 slots of t-byte keys (16 counters)
 hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, bool pairs, uint32_t lb,
                            unsigned long long* out, hipStream_t stream);

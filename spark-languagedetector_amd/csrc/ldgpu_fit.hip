@@ -116,6 +116,35 @@ __device__ __forceinline__ void count_new_keys(const CountParams& p, bool new_ke
 #define LDGPU_FIT_ABLATE 0
 #endif
 
+// The table's distinct-key counter, for kernels whose threads make many
+// inserts: each thread counts its new keys and the wave adds them with ONE
+// atomic when the thread is done (every lane of the wave must call it) --
+// one atomic per insert ballot on the single counter serialises at its L2
+// channel (~1M atomics in a 60M-key derive level).
+__device__ __forceinline__ void flush_new_keys(unsigned long long* size, unsigned int n) {
+    unsigned int v = n;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(size, (unsigned long long)v);
+}
+
+// add_count without the counter update: returns whether the key is new
+__device__ __forceinline__ bool add_count_q(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
+    bool new_key = false;
+    const int64_t s = find_or_insert(p, key, new_key);
+    if (s >= 0) {
+        atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
+    } else {
+        const unsigned int at = atomicAdd(p.ovf_n, 1u);
+        if (at < p.ovf_cap) {
+            p.ovf_keys[at] = key;
+            p.ovf_lang[at] = lang;
+            p.ovf_cnt[at] = c;
+        }
+    }
+    return new_key;
+}
+
 __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
     if (LDGPU_FIT_ABLATE & 2) return;
     bool new_key = false;
@@ -783,6 +812,18 @@ __device__ __forceinline__ void wide_add(const WideCountParams& p, uint64_t lo, 
         atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
     else
         atomicOr(p.full, 1u);
+}
+
+// wide_add without the counter update (flush_new_keys): returns whether the key is new
+__device__ __forceinline__ bool wide_add_q(const WideCountParams& p, uint64_t lo, uint64_t hi, int lang,
+                                           unsigned long long c) {
+    bool new_key = false;
+    const int64_t s = wide_find_or_insert(p, lo, hi, new_key);
+    if (s >= 0)
+        atomicAdd(&p.counts[(size_t)s * p.L + lang], c);
+    else
+        atomicOr(p.full, 1u);
+    return new_key;
 }
 
 __global__ __launch_bounds__(kCountWaves * 64) void wide_count_kernel(const WideCountParams p) {
@@ -1597,36 +1638,40 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
     if (tid == 0) p.nout[blockIdx.x] = *n_out;
 }
 
-// entry i of the batch (buckets' outputs in bucket order, prefix epre) ->
-// bucket b = the last with epre[b] <= i, stored at boff[b] + (i - epre[b])
+// merge: one workgroup per reduce bucket b (b0 + block) adds the bucket's
+// nout[b] entries (at boff[b]) into T1 -- a bucket's keys share the top bits
+// of their route hash, which (K = 1 pairs) are the top bits of their T1 slot:
+// the workgroup's inserts stay within one slice of the table.
 // pairs (K = 1): T1 is a table of (window, language) pairs -- key = the
 // entry's kl (sentinel key << lb | lang), one counter (L = 1)
 template <int K>
 __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const CountParams c, const WideCountParams w,
-                                                     int64_t e0, int64_t n, int pairs) {
-    __shared__ uint64_t pre[kQ * kQ + 1];
-    for (int i = threadIdx.x; i <= kQ * kQ; i += blockDim.x) pre[i] = p.epre[i];
-    __syncthreads();
-    const int64_t i = e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= e0 + n) return;
-    int lo = 0;
-#pragma unroll
-    for (int step = 2048; step >= 1; step >>= 1)
-        if (lo + step <= kQ * kQ && pre[lo + step] <= (uint64_t)i) lo += step;
-    const int64_t at = (int64_t)p.boff[lo] + (i - (int64_t)pre[lo]);
-    if constexpr (K == 1) {
-        const uint64_t kl = p.out[2 * at];
-        if (pairs) add_count(c, kl, 0, p.out[2 * at + 1]);
-        else add_count(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out[2 * at + 1]);
-    } else {
-        const Rec<K> r = load_rec<K>(p.out, at);
-        const int lang = (int)(r.w[K - 1] >> kCntBits);
-        const unsigned long long cn = r.w[K - 1] & kCntMask;
-        if (K == 3 && r.w[1] != 0ull) wide_add(w, r.w[0], r.w[1], lang, cn);
-        else add_count(c, r.w[0], lang, cn);
+                                                     int b0, int pairs) {
+    const int b = b0 + blockIdx.x;
+    const int64_t n = p.nout[b];
+    const int64_t base = (int64_t)p.boff[b];
+    unsigned int nn = 0, nw = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const int64_t at = base + i;
+        if constexpr (K == 1) {
+            const uint64_t kl = p.out[2 * at];
+            if (pairs) nn += add_count_q(c, kl, 0, p.out[2 * at + 1]);
+            else nn += add_count_q(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out[2 * at + 1]);
+        } else {
+            const Rec<K> r = load_rec<K>(p.out, at);
+            const int lang = (int)(r.w[K - 1] >> kCntBits);
+            const unsigned long long cn = r.w[K - 1] & kCntMask;
+            if (K == 3 && r.w[1] != 0ull) nw += wide_add_q(w, r.w[0], r.w[1], lang, cn);
+            else nn += add_count_q(c, r.w[0], lang, cn);
+        }
     }
+    flush_new_keys(c.size, nn);
+    if (K == 3) flush_new_keys(w.size, nw);
 }
 
+}  // namespace
+
+namespace {
 // Derive (FIT v4), level by level.  T1 holds, per (maximal window w of t
 // bytes, language), the number of positions whose maximal window is w.  With
 // S_n(g) = the positions whose maximal window has g as prefix and >= n bytes
@@ -1647,6 +1692,7 @@ __global__ __launch_bounds__(256) void derive_level_kernel(const CountParams t1,
                                                            uint64_t s0, uint64_t s1, int lev, uint32_t mt,
                                                            const CountParams to, const WideCountParams tow) {
     const int L = t1.L;
+    unsigned int n_to = 0, n_tow = 0, n_t1 = 0, n_t1w = 0;
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
          s += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t lo, hi = 0;
@@ -1668,15 +1714,19 @@ __global__ __launch_bounds__(256) void derive_level_kernel(const CountParams t1,
             const unsigned long long c = row[l];
             if (!c) continue;
             if (mt) {
-                if (lev <= kMaxGram) add_count(to, lo | ((uint64_t)lev << 56), l, c * mt);
-                else wide_add(tow, lo, hi | ((uint64_t)lev << 56), l, c * mt);
+                if (lev <= kMaxGram) n_to += add_count_q(to, lo | ((uint64_t)lev << 56), l, c * mt);
+                else n_tow += wide_add_q(tow, lo, hi | ((uint64_t)lev << 56), l, c * mt);
             }
             if (n >= 1) {
-                if (n <= kMaxGram) add_count(t1, (lo & byte_mask(n)) | ((uint64_t)n << 56) | kDerived, l, c);
-                else wide_add(t1w, lo, (hi & byte_mask(n - 8)) | ((uint64_t)n << 56) | kDerived, l, c);
+                if (n <= kMaxGram) n_t1 += add_count_q(t1, (lo & byte_mask(n)) | ((uint64_t)n << 56) | kDerived, l, c);
+                else n_t1w += wide_add_q(t1w, lo, (hi & byte_mask(n - 8)) | ((uint64_t)n << 56) | kDerived, l, c);
             }
         }
     }
+    flush_new_keys(to.size, n_to);
+    flush_new_keys(t1.size, n_t1);
+    if (tow.size) flush_new_keys(tow.size, n_tow);
+    if (t1w.size) flush_new_keys(t1w.size, n_t1w);
 }
 
 // the same level for a pair table T1 (K = 1 records: key = kl | kDerived,
@@ -1687,8 +1737,9 @@ __device__ __forceinline__ int kl_len(uint64_t kl, uint32_t lb) {
 
 __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountParams t1, uint32_t lb, uint64_t s0,
                                                                  uint64_t s1, int lev, uint32_t mt,
-                                                                 const CountParams to) {
+                                                                 const CountParams to, int ablate) {
     const uint64_t lmask = (1ull << lb) - 1ull;
+    unsigned int n_to = 0, n_t1 = 0;
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t key = t1.keys[s];
@@ -1699,13 +1750,15 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
         const unsigned long long c = t1.counts[s];
         const int lang = (int)(kl & lmask);
         const uint64_t bytes = (kl >> lb) ^ (1ull << (8 * klen));
-        if (mt) add_count(to, bytes | ((uint64_t)klen << 56), lang, c * mt);
+        if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += add_count_q(to, bytes | ((uint64_t)klen << 56), lang, c * mt);
         const int n = lev - 1;
-        if (n >= 1) {
+        if (n >= 1 && !(LDGPU_DIAG && (ablate & 2))) {
             const uint64_t sent = (1ull << (8 * n)) | (bytes & byte_mask(n));
-            add_count(t1, ((sent << lb) | (uint64_t)lang) | kDerived, 0, c);
+            n_t1 += add_count_q(t1, ((sent << lb) | (uint64_t)lang) | kDerived, 0, c);
         }
     }
+    flush_new_keys(to.size, n_to);
+    flush_new_keys(t1.size, n_t1);
 }
 
 // occupied T1 slots per key length (one-word and wide tables)
@@ -1797,14 +1850,14 @@ hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int64_t e0,
-                        int64_t n, bool pairs, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    const dim3 g((unsigned)((n + 1023) / 1024)), b(1024);
+hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int b0, int b1,
+                        bool pairs, hipStream_t stream) {
+    if (b1 <= b0) return hipSuccess;
+    const dim3 g((unsigned)(b1 - b0)), b(1024);
     const int pr = pairs && K == 1;
-    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, e0, n, pr);
-    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, e0, n, 0);
-    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, e0, n, 0);
+    if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, b0, pr);
+    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, b0, 0);
+    else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, b0, 0);
     return hipGetLastError();
 }
 
@@ -1827,10 +1880,10 @@ hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, bo
 }
 
 hipError_t launch_derive_pairs_level(const CountParams& t1, uint32_t lb, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
-                                     const CountParams& to, hipStream_t stream) {
+                                     const CountParams& to, int ablate, hipStream_t stream) {
     if (s1 <= s0) return hipSuccess;
     const unsigned g = (unsigned)std::min<uint64_t>(16384, (s1 - s0 + 255) / 256);
-    hipLaunchKernelGGL(derive_pairs_level_kernel, dim3(g), dim3(256), 0, stream, t1, lb, s0, s1, lev, mt, to);
+    hipLaunchKernelGGL(derive_pairs_level_kernel, dim3(g), dim3(256), 0, stream, t1, lb, s0, s1, lev, mt, to, ablate);
     return hipGetLastError();
 }
 
