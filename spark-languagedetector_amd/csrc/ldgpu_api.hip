@@ -2056,7 +2056,18 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         meta.insert(meta.end(), wg_doc.begin(), wg_doc.end());
         meta.insert(meta.end(), wg_rec.begin(), wg_rec.end());
         meta.insert(meta.end(), wg_dir.begin(), wg_dir.end());
+        // the documents' starts and lengths in perm order (emit prefetches a
+        // wave's next document with two independent loads)
         const size_t n_lang = wg_lang.size(), n_perm = perm.size();
+        for (size_t i = 0; i < n_perm; ++i) {
+            const int64_t dd = d0 + (nd ? perm[i] : 0);
+            meta.push_back(h_off[dd]);
+        }
+        std::vector<int32_t> plen(n_perm);
+        for (size_t i = 0; i < n_perm; ++i) {
+            const int64_t dd = d0 + (nd ? perm[i] : 0);
+            plen[i] = (int32_t)(h_off[dd + 1] - h_off[dd]);
+        }
         HIP_TRY(x->f_wg.ensure(sizeof(int64_t) * meta.size() + sizeof(int32_t) * (n_lang + n_perm) + 16));
         HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(acc, 1)));
         HIP_TRY(x->f_bstart.ensure(sizeof(int64_t) * (size_t)dirs));
@@ -2068,7 +2079,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         int32_t* d_perm = d_wg_lang + n_lang;
         HIP_TRY(hipMemcpyAsync(wgp, meta.data(), sizeof(int64_t) * meta.size(), hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(d_wg_lang, wg_lang.data(), sizeof(int32_t) * n_lang, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d_perm, perm.data(), sizeof(int32_t) * n_perm, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_perm, plen.data(), sizeof(int32_t) * n_perm, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemsetAsync(x->f_cnt3.p, 0, sizeof(uint32_t) * cnt3.size(), st));
         PartParams pp{};
         pp.bytes = d_bytes;
@@ -2083,11 +2094,12 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         pp.cb = c->cb;
         if (const char* ab = diag_env("LDGPU_FIT_EMIT_ABLATE")) pp.ablate = atoi(ab);
         pp.grid_a = grid_a;
-        pp.perm = d_perm;
+        pp.dlen = d_perm;
         pp.wg_lang = d_wg_lang;
         pp.wg_doc = (const int64_t*)wgp;
         pp.wg_rec = pp.wg_doc + grid_a + 1;
         pp.wg_dir = pp.wg_rec + grid_a + 1;
+        pp.dstart = pp.wg_dir + grid_a + 1;
         pp.rec = (uint64_t*)x->f_rec.p;
         pp.blk_start = (int64_t*)x->f_bstart.p;
         pp.blk_hdr = (uint32_t*)x->f_bhdr.p;

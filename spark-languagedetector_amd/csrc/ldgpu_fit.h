@@ -90,7 +90,9 @@ struct PartParams {
     // windows) and block ids [wg_dir[w], ...); blocks are sorted by q1 with a
     // kHdr header
     int32_t grid_a;             // emit workgroups (a multiple of kSplits)
-    const int32_t* perm;
+    const int64_t* dstart;      // perm order: each document's first byte (offsets[perm[i]]) ...
+    const int32_t* dlen;        // ... and length (> 0): a wave prefetches its next document's without a
+                                // dependent load
     const int32_t* wg_lang;
     const int64_t* wg_doc;
     const int64_t* wg_rec;

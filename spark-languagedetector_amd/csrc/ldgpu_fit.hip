@@ -1096,10 +1096,28 @@ template <int K>
 struct WaveState {
     static constexpr int kW = K == 3 ? 5 : 3;  // dwords per window position
     int64_t b, len, p0;
+    int64_t nb;                    // the next document (claimed a document early, its loads in flight)
+    int32_t nlen;                  // 0: none
     int32_t phase;
     bool pf;                       // pw holds the words of the next WIN step (issued a round early)
     uint32_t pw[emit_sub(K)][kW];
 };
+
+// claim the wave's next document and issue the loads of its start / length
+template <int K>
+__device__ __forceinline__ void claim_next(const PartParams& p, EmitLds<K>& S, WaveState<K>& w, int lane, int64_t d0,
+                                           int64_t d1) {
+    uint32_t k = 0;
+    if (lane == 0) k = __hip_atomic_fetch_add(&S.next_doc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // wave-uniform: scalar loads into SGPRs
+    const int64_t i = d0 + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(k, 0));
+    w.nb = 0;
+    w.nlen = 0;
+    if (i < d1) {
+        w.nb = p.dstart[i];
+        w.nlen = p.dlen[i];
+    }
+}
 
 // append the lanes' records (sub per lane) to the workgroup block with one
 // reservation (the round bound keeps it from overflowing); every lane of the
@@ -1164,30 +1182,27 @@ __device__ __forceinline__ uint64_t byte_mask(int n) { return n >= 8 ? ~0ull : (
 
 // One step of a wave: <= 64 sub positions of its document, one record each
 // -- the maximal window at the position, min(N, len - pos) bytes (N =
-// max(G)).  The positions' loads are all issued before any is used.
+// max(G)).  The positions' loads are all issued before any is used; the
+// next step's (or the next document's first step's) loads are issued at the
+// end, so they fly across the round barrier, and the document after the
+// next is claimed as a document starts.
 template <int K>
 __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, WaveState<K>& w, int lane, int64_t d0,
                                           int64_t d1, uint32_t lang) {
     constexpr int SUB = emit_sub(K);
-    if (w.phase == kNextDoc) {
-        uint32_t k = 0;
-        if (lane == 0) k = __hip_atomic_fetch_add(&S.next_doc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int64_t i = d0 + (int64_t)__shfl(k, 0);
-        if (i >= d1) {
+    if (w.phase == kNextDoc) {  // the wave's first document
+        claim_next<K>(p, S, w, lane, d0, d1);
+        if (w.nlen == 0) {
             w.phase = kDone;
             if (lane == 0) __hip_atomic_fetch_sub(&S.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
-        const int64_t d = p.perm[i];
-        const int64_t b = p.offsets[d];
-        const int64_t len = p.offsets[d + 1] - b;
-        if (len <= 0) return;
-        w.b = b;
-        w.len = len;
+        w.b = w.nb;
+        w.len = w.nlen;
         w.p0 = 0;
         w.pf = false;
         w.phase = kWin;
-        // fall through: the document's first positions in this step
+        claim_next<K>(p, S, w, lane, d0, d1);
     }
     if (!w.pf) window_loads<K>(p, w, lane, w.pw);
     w.pf = false;
@@ -1219,12 +1234,19 @@ __device__ __forceinline__ void emit_step(const PartParams& p, EmitLds<K>& S, Wa
     }
     emit_recs<K, SUB>(S, has, r, p, lane);
     w.p0 += 64 * SUB;
-    if (w.p0 >= w.len) {
-        w.phase = kNextDoc;
-    } else {  // the next step's loads fly across the round barrier
-        window_loads<K>(p, w, lane, w.pw);
-        w.pf = true;
+    if (w.p0 >= w.len) {  // the next document (claimed a document ago)
+        if (w.nlen == 0) {
+            w.phase = kDone;
+            if (lane == 0) __hip_atomic_fetch_sub(&S.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+        w.b = w.nb;
+        w.len = w.nlen;
+        w.p0 = 0;
+        claim_next<K>(p, S, w, lane, d0, d1);
     }
+    window_loads<K>(p, w, lane, w.pw);  // the next step's loads fly across the round barrier
+    w.pf = true;
 }
 
 // Write the block: counting sort by q1 in LDS, scattered stores into the
@@ -1255,8 +1277,9 @@ __device__ __forceinline__ void flush_block(const PartParams& p, EmitLds<K>& S, 
     lds_barrier();
 }
 
+// (HIP launch bound: >= 8 waves per SIMD, i.e. two workgroups per CU -- <= 64 VGPRs)
 template <int K>
-__global__ __launch_bounds__(kEmitWaves * 64, 2) void emit_kernel(const PartParams p) {
+__global__ __launch_bounds__(kEmitWaves * 64, 8) void emit_kernel(const PartParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t emit_smem[];
     EmitLds<K>& S = *reinterpret_cast<EmitLds<K>*>(emit_smem);
     constexpr uint32_t kThresh = (uint32_t)(emit_blk_recs(K) - emit_round_recs(K));
