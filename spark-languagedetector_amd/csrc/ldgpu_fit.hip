@@ -1541,17 +1541,28 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
     if (tid == 0) *n_out = 0u;
     __syncthreads();
     const int64_t beg = (int64_t)p.boff[blockIdx.x], end = (int64_t)p.boff[blockIdx.x + 1];
-    constexpr int kU = K == 1 ? 8 : 4;  // records per lane in flight; their probes advance together
+    constexpr int kU = 4;  // records per lane in flight (and 4 more loading); their probes advance together
+    // software pipeline: the next chunk's records load while this chunk probes
+    Rec<K> nx[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int64_t i = beg + (int64_t)wave * 64 * kU + 64 * u + lane;
+        nx[u] = i < end ? load_rec<K>(p.rec2, i) : Rec<K>{};
+    }
     for (int64_t i00 = beg + (int64_t)wave * 64 * kU; i00 < end; i00 += kEmitWaves * 64 * kU) {
         Rec<K> r[kU];
         uint32_t c[kU], slot[kU], tg[kU];
         bool pend[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
+            r[u] = nx[u];
+            const int64_t j = i00 + kEmitWaves * 64 * kU + 64 * u + lane;
+            nx[u] = j < end ? load_rec<K>(p.rec2, j) : Rec<K>{};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
             const int64_t i = i00 + 64 * u + lane;
             pend[u] = i < end;
-            if (pend[u]) r[u] = load_rec<K>(p.rec2, i);
-            else r[u] = Rec<K>{};
             c[u] = (uint32_t)rec_count<K>(r[u], p.cb);
             const uint64_t h = rec_hash<K>(r[u], p.cb);
             slot[u] = (uint32_t)(((uint64_t)(uint32_t)h * (uint64_t)N) >> 32);
