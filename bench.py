@@ -345,12 +345,18 @@ def fit_main(args, world, rank, local, dev, backend):
         t["total_s"] = time.perf_counter() - t0
         return t, distinct, table
 
-    for _ in range(args.warmup):
-        step()
+    def logged(tag):
+        r = step()
+        if rank == 0:  # progress on stderr (a long fit prints nothing else until its line)
+            print(f"fit {tag}: count {r[0]['count_s']:.3f} s, total {r[0]['total_s']:.3f} s", file=sys.stderr, flush=True)
+        return r
+
+    for i in range(args.warmup):
+        logged(f"warmup {i}")
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    parts = [step() for _ in range(args.steps)]
+    parts = [logged(f"step {i}") for i in range(args.steps)]
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

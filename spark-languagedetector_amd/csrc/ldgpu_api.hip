@@ -1822,7 +1822,9 @@ int derive_pending(ldgpu_counts* c) {
     const uint64_t L = (uint64_t)c->L;
     const char* dab = diag_env("LDGPU_FIT_DERIVE_ABLATE");  // timing only (counts wrong)
     const int derive_ablate = dab ? atoi(dab) : 0;
-    const bool pairs = c->K == 1;           // T1 of (window, language) pairs
+    // T1 of (window, language) pairs: one-word keys (K = 1) or a wide table of
+    // (packed key, lang + 1) (K = 2); dense rows otherwise
+    const int pairs = c->K == 1 ? 1 : (c->K == 2 ? 2 : 0);
     const uint64_t per_slot = pairs ? 1 : L;  // adds of one T1 slot (to T; to T1)
     // T1's occupied slots per key length
     unsigned long long cnt[16] = {};
@@ -1853,11 +1855,11 @@ int derive_pending(ldgpu_counts* c) {
         const uint32_t mt = mult[lev];
         const int n = lev - 1;
         if (!cnt[lev] || (!mt && n < 1)) continue;
-        const bool wide = lev > kMaxGram;
+        const bool wide = lev > kMaxGram || pairs == 2;  // the level's entries are in T1's wide table
         // T1 room for this level's prefixes (one per entry at most), within
         // 0.1 of its load limit (linear probes stay short)
         if (n >= 1) {
-            if (n <= kMaxGram) {
+            if (n <= kMaxGram && pairs != 2) {
                 const double need = (double)(t->size + cnt[lev]);
                 if (need > (max_load(t) + 0.1) * (double)t->cap) {
                     if (int rc = grow(t, next_pow2((uint64_t)(need / max_load(t)) + 16))) return rc;
@@ -1877,7 +1879,7 @@ int derive_pending(ldgpu_counts* c) {
             if (mt) {
                 const double room = std::max(1.0, (max_load(c) + 0.1) * (double)c->cap - (double)c->size);
                 slots = std::min<uint64_t>(slots, (uint64_t)(room / tload));
-                if (wide) {
+                if (lev > kMaxGram) {
                     const uint64_t occ = std::min<uint64_t>(cnt[lev], (uint64_t)(2.0 * tload * (double)slots) + 64);
                     if (int rc = wide_ensure(c, occ)) return rc;
                 }
@@ -1888,16 +1890,19 @@ int derive_pending(ldgpu_counts* c) {
             if (int rc = ensure_ovf(t, adds)) return rc;
             HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
             HIP_TRY(hipMemsetAsync(t->d_ovf_n, 0, sizeof(unsigned int), st));
-            if (pairs)
+            if (pairs == 2)
+                HIP_TRY(launch_derive_pairs2_level(wide_params(t), s0, s0 + slots, lev, mt, count_params(c), derive_ablate,
+                                                   st));
+            else if (pairs)
                 HIP_TRY(launch_derive_pairs_level(count_params(t), c->lb, s0, s0 + slots, lev, mt, count_params(c),
                                                   derive_ablate, st));
             else
                 HIP_TRY(launch_derive_level(count_params(t), wide_params(t), wide, s0, s0 + slots, lev, mt,
                                             count_params(c), wide_params(c), st));
-            if (wide && mt) {
+            if (lev > kMaxGram && mt) {
                 if (int rc = wide_after(c)) return rc;
             }
-            if (n > kMaxGram) {
+            if (n > kMaxGram || (pairs == 2 && n >= 1)) {
                 if (int rc = wide_after(t)) return rc;
             }
             if (int rc = after_batch(c)) return rc;
@@ -1962,9 +1967,10 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     }
     if (int rc = count_partial(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
     if (!c->pend) {
-        // one-word records: T1 keyed by (window, language) pairs, one counter
-        // each (a dense row of L counters per window otherwise)
-        if (int rc = counts_new(x, K == 1 ? 1 : c->L, c->G, c->nG, std::max<int64_t>(1 << 16, c->pend_hint), &c->pend))
+        // one- and two-word records: T1 keyed by (window, language) pairs, one
+        // counter each (K = 2: in its wide table, key (packed key, lang + 1));
+        // a dense row of L counters per window otherwise
+        if (int rc = counts_new(x, K <= 2 ? 1 : c->L, c->G, c->nG, std::max<int64_t>(1 << 16, c->pend_hint), &c->pend))
             return rc;
     }
     ldgpu_counts* t1 = c->pend;
@@ -2153,9 +2159,10 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         // grows with the keys actually inserted, not with the batch's entries
         // (most of which find their key; a slot holds a dense row of L
         // counters, 1.6 KB at L = 200).
-        const bool wide = K == 3 && maxg > kMaxGram;
+        // T1's wide table: windows of 8..15 bytes, or every pair (K = 2)
+        const bool wide = (K == 3 && maxg > kMaxGram) || K == 2;
         if (wide) {
-            if (int rc = wide_ensure(t1, 1)) return rc;
+            if (int rc = wide_ensure(t1, K == 2 ? (uint64_t)std::max<int64_t>(c->pend_hint, 1) : 1)) return rc;
         }
         // Projected growth: the batch adds about E x (the last batch's new
         // keys per entry) keys.  A table short of that grows once, here --
@@ -2190,9 +2197,12 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             int b1 = b0;
             int64_t n = 0;
             while (b1 < kQ * kQ && (b1 == b0 || n + (int64_t)nout[b1] <= room)) n += nout[b1++];
+            if (wide && 4 * (t1->wsize + (uint64_t)n) > 3 * t1->wcap) {  // one bucket beyond the room
+                if (int rc = wide_ensure(t1, (uint64_t)n)) return rc;
+            }
             if (int rc = ensure_ovf(t1, std::max<int64_t>(n, 1))) return rc;
             HIP_TRY(hipMemsetAsync(t1->d_ovf_n, 0, sizeof(unsigned int), st));
-            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), b0, b1, K == 1, st));
+            HIP_TRY(launch_merge(K, pp, count_params(t1), wide_params(t1), b0, b1, K <= 2, st));
             if (wide) {
                 if (int rc = wide_after(t1)) return rc;
             }

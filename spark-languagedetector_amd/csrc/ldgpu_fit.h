@@ -122,7 +122,9 @@ hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
 struct WideCountParams;
 // add the reduce output entries of buckets b0 .. b1 into the tables of T1
 // (K = 3: windows of 8..15 bytes into the wide table)
-// (buckets b0 .. b1; pairs, K = 1: T1 keyed by the entries' kl, one counter)
+// (buckets b0 .. b1; pairs: T1 of (window, language) pairs with one counter
+// each -- K = 1 keyed by the entries' kl, K = 2 a wide table of (packed key,
+// lang + 1))
 hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const WideCountParams& w, int b0, int b1,
                         bool pairs, hipStream_t stream);
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
@@ -181,8 +183,13 @@ hipError_t launch_derive_level(const CountParams& t1, const WideCountParams& t1w
 // (ablate: diagnostics build only, bit 0 no adds to T, bit 1 no prefix adds)
 hipError_t launch_derive_pairs_level(const CountParams& t1, uint32_t lb, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
                                      const CountParams& to, int ablate, hipStream_t stream);
-// out[t] += occupied T1 slots of t-byte keys (16 counters)
-hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, bool pairs, uint32_t lb,
+// the same for a two-word pair table T1 (K = 2: wide table, one counter,
+// lo = packed key, hi = lang + 1)
+hipError_t launch_derive_pairs2_level(const WideCountParams& t1w, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
+                                      const CountParams& to, int ablate, hipStream_t stream);
+// out[t] += occupied T1 slots of t-byte keys (16 counters); pairs: 0 dense
+// T1, 1 one-word pairs (lb language bits), 2 two-word pairs
+hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, int pairs, uint32_t lb,
                            unsigned long long* out, hipStream_t stream);
 // partial windows of docs[0 .. n) (documents shorter than some gram length)
 hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, const int64_t* docs,

@@ -1695,12 +1695,13 @@ __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const C
             const Rec<K> r = load_rec<K>(p.out, at);
             const int lang = (int)(r.w[K - 1] >> kCntBits);
             const unsigned long long cn = r.w[K - 1] & kCntMask;
-            if (K == 3 && r.w[1] != 0ull) nw += wide_add_q(w, r.w[0], r.w[1], lang, cn);
+            if (K == 2 && pairs) nw += wide_add_q(w, r.w[0], (uint64_t)lang + 1ull, 0, cn);  // (key, lang + 1)
+            else if (K == 3 && r.w[1] != 0ull) nw += wide_add_q(w, r.w[0], r.w[1], lang, cn);
             else nn += add_count_q(c, r.w[0], lang, cn);
         }
     }
     flush_new_keys(c.size, nn);
-    if (K == 3) flush_new_keys(w.size, nw);
+    if (K >= 2 && w.size) flush_new_keys(w.size, nw);
 }
 
 }  // namespace
@@ -1795,6 +1796,31 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
     flush_new_keys(t1.size, n_t1);
 }
 
+// the same for a two-word pair table T1 (K = 2 records: a wide table with
+// one counter, lo = the window's packed key, hi = lang + 1 | kDerived)
+__global__ __launch_bounds__(256) void derive_pairs2_level_kernel(const WideCountParams t1w, uint64_t s0, uint64_t s1,
+                                                                  int lev, uint32_t mt, const CountParams to,
+                                                                  int ablate) {
+    unsigned int n_to = 0, n_t1 = 0;
+    for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t hi = t1w.khi[s];
+        if (hi == kEmpty) continue;
+        const uint64_t key = t1w.klo[s];
+        const int klen = (int)(key >> 56);
+        if (klen != lev) continue;
+        const unsigned long long c = t1w.counts[s];
+        const int lang = (int)((hi & ~kDerived) - 1ull);
+        if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += add_count_q(to, key, lang, c * mt);
+        const int n = lev - 1;
+        if (n >= 1 && !(LDGPU_DIAG && (ablate & 2)))
+            n_t1 += wide_add_q(t1w, (key & byte_mask(n)) | ((uint64_t)n << 56), ((uint64_t)lang + 1ull) | kDerived, 0,
+                               c);
+    }
+    flush_new_keys(to.size, n_to);
+    flush_new_keys(t1w.size, n_t1);
+}
+
 // occupied T1 slots per key length (one-word and wide tables)
 __global__ __launch_bounds__(256) void len_hist_kernel(const CountParams t1, const WideCountParams t1w, int pairs,
                                                        uint32_t lb, unsigned long long* out) {
@@ -1805,7 +1831,12 @@ __global__ __launch_bounds__(256) void len_hist_kernel(const CountParams t1, con
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap + wcap;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t k = s < cap ? t1.keys[s] : t1w.khi[s - cap];
-        if (k != kEmpty) atomicAdd(&h[pairs ? kl_len(k & ~kDerived, lb) : (int)((k >> 56) & 15)], 1u);
+        if (k == kEmpty) continue;
+        int t;
+        if (pairs == 1) t = kl_len(k & ~kDerived, lb);
+        else if (pairs == 2) t = (int)((t1w.klo[s - cap] >> 56) & 15);  // two-word pairs: (packed key, lang + 1)
+        else t = (int)((k >> 56) & 15);
+        atomicAdd(&h[t], 1u);
     }
     __syncthreads();
     if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&out[threadIdx.x], (unsigned long long)h[threadIdx.x]);
@@ -1888,9 +1919,9 @@ hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const 
                         bool pairs, hipStream_t stream) {
     if (b1 <= b0) return hipSuccess;
     const dim3 g((unsigned)(b1 - b0)), b(1024);
-    const int pr = pairs && K == 1;
+    const int pr = pairs && K <= 2;
     if (K == 1) hipLaunchKernelGGL(merge_kernel<1>, g, b, 0, stream, p, c, w, b0, pr);
-    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, b0, 0);
+    else if (K == 2) hipLaunchKernelGGL(merge_kernel<2>, g, b, 0, stream, p, c, w, b0, pr);
     else hipLaunchKernelGGL(merge_kernel<3>, g, b, 0, stream, p, c, w, b0, 0);
     return hipGetLastError();
 }
@@ -1905,11 +1936,19 @@ hipError_t launch_derive_level(const CountParams& t1, const WideCountParams& t1w
     return hipGetLastError();
 }
 
-hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, bool pairs, uint32_t lb,
+hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, int pairs, uint32_t lb,
                            unsigned long long* out, hipStream_t stream) {
     const uint64_t n = t1.mask + 1 + (t1w.klo ? t1w.mask + 1 : 0);
     const unsigned g = (unsigned)std::min<uint64_t>(4096, (n + 255) / 256);
     hipLaunchKernelGGL(len_hist_kernel, dim3(g), dim3(256), 0, stream, t1, t1w, (int)pairs, lb, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_derive_pairs2_level(const WideCountParams& t1w, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
+                                      const CountParams& to, int ablate, hipStream_t stream) {
+    if (s1 <= s0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<uint64_t>(16384, (s1 - s0 + 255) / 256);
+    hipLaunchKernelGGL(derive_pairs2_level_kernel, dim3(g), dim3(256), 0, stream, t1w, s0, s1, lev, mt, to, ablate);
     return hipGetLastError();
 }
 
