@@ -519,24 +519,22 @@ int max_gram(const int32_t* G, int32_t nG) {
 int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ParsedTable& t,
                 ldgpu_model** out);
 
-// Place every key in nb 4-slot buckets (count mode).  Primary bucket while it
+// Place every key in nb 5-slot buckets (count mode).  Primary bucket while it
 // has room, else the secondary (raising the primary's overflow flag), else a
 // bounded random walk of evictions; false when it does not settle.
 bool bucket_place(const std::vector<uint64_t>& keys, const std::vector<uint64_t>& masks, int S,
                   const std::vector<uint8_t>& bad, uint64_t nb, std::vector<Bucket>& out) {
     out.assign(nb, Bucket{});
-    const int lg = log2u(nb);
-    auto prim = [&](uint64_t k) { return mix64(k) >> (64 - lg); };
-    auto sec = [&](uint64_t k) { return mix64(k) & (nb - 1); };
-    auto key_at = [&](uint64_t b, int s) { return out[b].k[s] & ~kBucketOverflow; };
-    auto put = [&](uint64_t b, int s, uint64_t k, uint64_t pay) {
-        out[b].k[s] = (out[b].k[s] & kBucketOverflow) | k;
+    auto prim = [&](uint64_t k) { return bucket_index((uint32_t)(mix64(k) >> 32), nb); };
+    auto sec = [&](uint64_t k) { return bucket_index((uint32_t)mix64(k), nb); };
+    auto put = [&](uint64_t b, int s, uint64_t k, uint32_t pay) {
+        out[b].k[s] = k;
         out[b].p[s] = pay;
-        if (b != prim(k)) out[prim(k)].k[0] |= kBucketOverflow;
+        if (b != prim(k)) out[prim(k)].flags |= kBucketOverflow;
     };
     auto free_slot = [&](uint64_t b) {
-        for (int s = 0; s < 4; ++s)
-            if (key_at(b, s) == kEmpty) return s;
+        for (int s = 0; s < 5; ++s)
+            if (out[b].k[s] == kEmpty) return s;
         return -1;
     };
     uint64_t rng = 0x9E3779B97F4A7C15ull;
@@ -548,11 +546,10 @@ bool bucket_place(const std::vector<uint64_t>& keys, const std::vector<uint64_t>
             if (w && !bits) lang = 64u * (uint32_t)s + (uint32_t)__builtin_ctzll(w);
             bits += __builtin_popcountll(w);
         }
-        if (bits != 1) lang = 0xffffffffu;
         uint64_t k = keys[i];
-        uint64_t pay = ((uint64_t)lang << 32) | (uint32_t)i | (bad[i] ? kBadRow : 0u);
+        uint32_t pay = (bits == 1 ? (kPayLang | lang) : (uint32_t)i) | (bad[i] ? kBadRow : 0u);
         bool placed = false;
-        for (int step = 0; step < 1000 && !placed; ++step) {
+        for (int step = 0; step < 2000 && !placed; ++step) {
             const uint64_t b1 = prim(k), b2 = sec(k);
             int s;
             if ((s = free_slot(b1)) >= 0) {
@@ -564,8 +561,9 @@ bool bucket_place(const std::vector<uint64_t>& keys, const std::vector<uint64_t>
             } else {
                 // evict a random resident of the secondary bucket; it retries its own buckets
                 rng = rng * 6364136223846793005ull + 1442695040888963407ull;
-                s = (int)(rng >> 62);
-                const uint64_t vk = key_at(b2, s), vp = out[b2].p[s];
+                s = (int)((rng >> 32) % 5u);
+                const uint64_t vk = out[b2].k[s];
+                const uint32_t vp = out[b2].p[s];
                 put(b2, s, k, pay);
                 k = vk;
                 pay = vp;
@@ -804,14 +802,17 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // (such a table's bloom never fits LDS: the keyed kernels, which alone read buckets)
     const bool use_buckets = m->mode == 3 && nn > (1 << 20);
     if (use_buckets) {
-        for (m->n_buckets = next_pow2(std::max<uint64_t>(16, (uint64_t)nn / 3 + 1));; m->n_buckets *= 2) {
+        // ~0.85 load (any bucket count); a placement that does not settle
+        // retries with 10 % more buckets
+        for (m->n_buckets = std::max<uint64_t>(16, (uint64_t)((double)nn / 4.25) + 1);;
+             m->n_buckets += m->n_buckets / 10 + 1) {
             if (bucket_place(keys, masks, S, t.bad, m->n_buckets, buckets)) break;
-            if (m->n_buckets >= (1ull << 32)) {
+            if (m->n_buckets >= (1ull << 31)) {
                 delete m;
                 return fail(LDGPU_ENOMEM, "key table: bucket placement failed");
             }
         }
-        m->slot_cap = m->n_buckets * 4;
+        m->slot_cap = m->n_buckets * 5;
         for (int64_t i = 0; i < nk; ++i) m->has_bad |= t.bad[i] != 0;
     }
     for (m->slot_cap = use_buckets ? m->slot_cap
@@ -1140,10 +1141,11 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.scores = d_scores;
     p.slots = m->d_slots;
     p.buckets = m->d_buckets;
-    // slot (bucket) 1 = h >> slot_shift, slot (bucket) 2 = h & slot_mask
+    // cuckoo slots: slot 1 = h >> slot_shift, slot 2 = h & slot_mask; buckets:
+    // bucket_index of h's halves over slot_mask = the bucket count
     const uint64_t n_index = m->d_buckets ? m->n_buckets : m->slot_cap;
     p.slot_shift = (uint32_t)(64 - log2u(n_index));
-    p.slot_mask = n_index - 1;
+    p.slot_mask = m->d_buckets ? m->n_buckets : n_index - 1;
     p.slot_shift32 = (uint32_t)(32 - log2u(n_index));  // cuckoo slots: slot_hash
     p.wslots = m->d_wslots;
     p.wslot_shift32 = m->d_wslots ? (uint32_t)(32 - log2u(m->wslot_cap)) : 0u;

@@ -200,16 +200,28 @@ struct alignas(16) WideSlot {
     uint32_t pad[2];
 };
 
-// Count-mode key table: 2-choice buckets of 4 slots, one 64-B line each.
-// p[i] = row | (the row's one language, or 0xffffffff) << 32.  A key goes
-// to its primary bucket (h >> (64 - log2 buckets)) while it has room, else to
-// its secondary one (h & (buckets - 1)), and then its primary bucket's
-// overflow flag (bit 63 of k[0]: never set in a key, whose top byte is its
-// length <= 7) is raised -- so most lookups read ONE line.
+// Count-mode key table of big models: 2-choice buckets of 5 slots, one 64-B
+// line each -- five packed keys, five 32-bit payloads, a flags word.  A
+// payload is kPayLang | the row's one language, or the row index (a row of
+// several languages: its mask words); kBadRow marks a row of the wrong
+// length.  A key goes to its primary bucket (bucket_index of the hash's high
+// half) while it has room, else to its secondary one (of the low half), and
+// then its primary bucket's overflow flag (flags bit 0) is raised -- so most
+// lookups read ONE line.  Any bucket count (not a power of two): the table is
+// sized for ~0.85 load, so config 5's 10M keys take 150 MB, which the
+// Infinity Cache holds beside the keyed bloom (4-slot buckets of 16-B slots at
+// a power-of-two count took 256 MiB).
 struct alignas(64) Bucket {
-    uint64_t k[4];
-    uint64_t p[4];
+    uint64_t k[5];
+    uint32_t p[5];
+    uint32_t flags;
 };
-constexpr uint64_t kBucketOverflow = 1ull << 63;
+static_assert(sizeof(Bucket) == 64, "one line per bucket");
+constexpr uint32_t kBucketOverflow = 1u;
+constexpr uint32_t kPayLang = 0x40000000u;
+
+__host__ __device__ __forceinline__ uint64_t bucket_index(uint32_t h, uint64_t nb) {
+    return ((uint64_t)h * nb) >> 32;
+}
 
 }  // namespace ldgpu

@@ -25,8 +25,8 @@ struct ScoreParams {
     int32_t* labels;            // [n_docs]
     double* scores;             // nullable [n_docs][L]
     const Slot* slots;          // open-addressed key -> row table (modes 0-2)
-    const Bucket* buckets;      // count mode: bucketed key -> (row, language) table; slot_shift/mask index it
-    uint32_t slot_shift;        // bucket = mix64(key) >> slot_shift (or & slot_mask)
+    const Bucket* buckets;      // count mode: bucketed key -> (row, language) table of slot_mask buckets
+    uint32_t slot_shift;        // (bucket_index of mix64(key)'s high / low half)
     uint64_t slot_mask;
     uint32_t slot_shift32;      // cuckoo slot = h1 (h2) >> slot_shift32 of slot_hash
     const WideSlot* wslots;     // wide keys (8..15 bytes), nullptr: none

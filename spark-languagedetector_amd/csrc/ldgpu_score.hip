@@ -21,7 +21,7 @@
 //              candidates to a per-wave LDS queue with mbcnt, so the queue is
 //              in reference order: n outer, position inner.
 //   verify     64 queued keys at a time probe the global table (2-choice
-//              cuckoo slots, 4-slot buckets for big count-mode tables, a
+//              cuckoo slots, 5-slot buckets for big count-mode tables, a
 //              two-word table for keys of 8..15 bytes).
 //   accumulate count mode (every row one shared value): per-language hit
 //              counts in LDS (order-free; 1-/2-byte keys counted straight from
@@ -222,17 +222,20 @@ __device__ __forceinline__ void hit_add(const uint4 (&e)[kHitQuads<S>], double (
 
 // Verify + accumulate the queued candidates (in queue order).
 // Look key up in one bucket (one 64-B line: 4 keys, then 4 payloads).
-__device__ __forceinline__ bool bucket_find(const Bucket* b, uint64_t key, uint64_t& pay) {
-    const uint4* q = reinterpret_cast<const uint4*>(b);
-    const uint4 k01 = q[0], k23 = q[1];
-    const uint64_t k0 = (((uint64_t)k01.y << 32) | k01.x) & ~kBucketOverflow;
-    const uint64_t k1 = ((uint64_t)k01.w << 32) | k01.z;
-    const uint64_t k2 = ((uint64_t)k23.y << 32) | k23.x;
-    const uint64_t k3 = ((uint64_t)k23.w << 32) | k23.z;
-    const int sl = k0 == key ? 0 : (k1 == key ? 1 : (k2 == key ? 2 : (k3 == key ? 3 : -1)));
-    if (sl < 0) return false;
-    pay = b->p[sl];
-    return true;
+// one bucket (one 64-B line, four independent 16-B loads): whether the key
+// is there (pay = its payload) and the bucket's overflow flag
+__device__ __forceinline__ bool bucket_find(const Bucket* b, uint64_t key, uint32_t& pay, bool& ovf) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(b);
+    const u32x4 a = q[0], c = q[1], d = q[2], e = q[3];
+    const uint64_t k0 = ((uint64_t)a.y << 32) | a.x;
+    const uint64_t k1 = ((uint64_t)a.w << 32) | a.z;
+    const uint64_t k2 = ((uint64_t)c.y << 32) | c.x;
+    const uint64_t k3 = ((uint64_t)c.w << 32) | c.z;
+    const uint64_t k4 = ((uint64_t)d.y << 32) | d.x;
+    // p[0..4] = d.z, d.w, e.x, e.y, e.z; flags = e.w
+    ovf = (e.w & kBucketOverflow) != 0u;
+    pay = k0 == key ? d.z : (k1 == key ? d.w : (k2 == key ? e.x : (k3 == key ? e.y : e.z)));
+    return k0 == key || k1 == key || k2 == key || k3 == key || k4 == key;
 }
 
 // A wide candidate (8..15 bytes): its own 2-choice table (WideSlot); value
@@ -379,16 +382,18 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             const uint64_t key = (win & (~0ull >> (64 - 8 * klen))) | ((uint64_t)klen << 56);
             if (MODE == 3 && KEYED && p.buckets) {  // (buckets only for tables beyond the caches)
                 const uint64_t h = mix64(key);
-                // 4-slot buckets, one 64-B line each: the key is in its primary
+                // 5-slot buckets, one 64-B line each: the key is in its primary
                 // bucket, or -- only if that bucket's overflow flag is set -- in
-                // its secondary one (Bucket, ldgpu_common.h)
-                uint64_t pay = 0;
-                bool found = bucket_find(p.buckets + (h >> p.slot_shift), key, pay);
-                if (!found && (p.buckets[h >> p.slot_shift].k[0] & kBucketOverflow))
-                    found = bucket_find(p.buckets + (h & p.slot_mask), key, pay);
+                // its secondary one (Bucket, ldgpu_common.h; slot_mask = buckets)
+                uint32_t pay = 0;
+                bool ovf = false;
+                bool found = bucket_find(p.buckets + bucket_index((uint32_t)(h >> 32), p.slot_mask), key, pay, ovf);
+                if (!found && ovf)
+                    found = bucket_find(p.buckets + bucket_index((uint32_t)h, p.slot_mask), key, pay, ovf);
                 if (found) {
-                    row = (uint32_t)pay;
-                    lang1 = (uint32_t)(pay >> 32);
+                    const bool one = (pay & kPayLang) != 0u;
+                    row = one ? (pay & kBadRow) : pay;
+                    lang1 = one ? (pay & 0xffffu) : 0xffffffffu;
                 }
             } else if constexpr (MODE == 3) {
                 // count mode reads only the slots' first halves (key, row,
