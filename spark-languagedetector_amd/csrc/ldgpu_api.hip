@@ -1983,9 +1983,19 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     std::vector<int64_t> lcnt(L + 1), lwin(L);
     std::vector<int32_t> perm;
     std::vector<int64_t> wg_doc, wg_rec, wg_dir;
-    std::vector<int32_t> wg_lang;
-    int64_t d0 = 0;
-    while (d0 < n_docs) {
+    // A batch's plan (documents in language order, emit workgroups, the
+    // documents' starts and lengths) is made on the host while the GPU runs
+    // the previous batch.
+    struct BatchPlan {
+        int64_t d0 = 0, d1 = 0, nd = 0, acc = 0, dirs = 0;
+        int grid_a = 0;
+        std::vector<int64_t> meta;
+        std::vector<int32_t> wg_lang, plen;
+    };
+    auto make_plan = [&](int64_t d0, BatchPlan& bp) {
+        std::vector<int64_t>& meta = bp.meta;
+        std::vector<int32_t>& wg_lang = bp.wg_lang;
+        std::vector<int32_t>& plen = bp.plen;
         // records of a document: one per byte position
         int64_t d1 = d0, W = 0;
         while (d1 < n_docs) {
@@ -2059,23 +2069,39 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         wg_doc.push_back(nd);
         wg_rec.push_back(acc);
         wg_dir.push_back(dirs);
-        std::vector<int64_t> meta;
+        meta.clear();
         meta.reserve(3 * wg_doc.size());
         meta.insert(meta.end(), wg_doc.begin(), wg_doc.end());
         meta.insert(meta.end(), wg_rec.begin(), wg_rec.end());
         meta.insert(meta.end(), wg_dir.begin(), wg_dir.end());
         // the documents' starts and lengths in perm order (emit prefetches a
         // wave's next document with two independent loads)
-        const size_t n_lang = wg_lang.size(), n_perm = perm.size();
+        const size_t n_perm = perm.size();
         for (size_t i = 0; i < n_perm; ++i) {
             const int64_t dd = d0 + (nd ? perm[i] : 0);
             meta.push_back(h_off[dd]);
         }
-        std::vector<int32_t> plen(n_perm);
+        plen.assign(n_perm, 0);
         for (size_t i = 0; i < n_perm; ++i) {
             const int64_t dd = d0 + (nd ? perm[i] : 0);
             plen[i] = (int32_t)(h_off[dd + 1] - h_off[dd]);
         }
+        bp.d0 = d0;
+        bp.d1 = d1;
+        bp.nd = nd;
+        bp.acc = acc;
+        bp.dirs = dirs;
+        bp.grid_a = grid_a;
+    };
+    BatchPlan cur, nxt;
+    make_plan(0, cur);
+    for (;;) {
+        const int64_t d0 = cur.d0, d1 = cur.d1, acc = cur.acc, dirs = cur.dirs;
+        const int grid_a = cur.grid_a;
+        const std::vector<int64_t>& meta = cur.meta;
+        const std::vector<int32_t>& wg_lang = cur.wg_lang;
+        const std::vector<int32_t>& plen = cur.plen;
+        const size_t n_lang = wg_lang.size(), n_perm = plen.size();
         HIP_TRY(x->f_wg.ensure(sizeof(int64_t) * meta.size() + sizeof(int32_t) * (n_lang + n_perm) + 16));
         HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(acc, 1)));
         HIP_TRY(x->f_bstart.ensure(sizeof(int64_t) * (size_t)dirs));
@@ -2113,40 +2139,35 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         pp.blk_hdr = (uint32_t*)x->f_bhdr.p;
         pp.nblk = (int32_t*)x->f_nblk.p;
         pp.cnt3 = (uint32_t*)x->f_cnt3.p;
-        HIP_TRY(launch_emit(K, pp, st));
-        HIP_TRY(hipMemcpyAsync(cnt3.data(), x->f_cnt3.p, sizeof(uint32_t) * cnt3.size(), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        // exact bucket offsets: (q1, q2) major, emit group minor
-        uint64_t off = 0;
-        for (int q = 0; q < kQ * kQ; ++q) {
-            boff[q] = off;
-            for (int s = 0; s < kSplits; ++s) {
-                p2off[(size_t)q * kSplits + s] = off;
-                off += cnt3[(size_t)q * kSplits + s];
-            }
-        }
-        boff[(size_t)kQ * kQ] = off;
-        const int64_t R = (int64_t)off;
-        if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld positions", (long long)R, (long long)acc);
+        // exact bucket offsets ((q1, q2) major, emit group minor) are scanned
+        // on the device, so emit, part2 and reduce run back to back; the
+        // bucket scratch is sized by the batch's positions (records <= them)
         HIP_TRY(x->f_p2.ensure(sizeof(uint64_t) * p2off.size()));
         HIP_TRY(x->f_boff.ensure(sizeof(uint64_t) * boff.size()));
-        HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(R, 1)));
-        HIP_TRY(x->f_okl.ensure(sizeof(uint64_t) * out_words(K) * (size_t)std::max<int64_t>(R, 1)));
+        HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(acc, 1)));
+        HIP_TRY(x->f_okl.ensure(sizeof(uint64_t) * out_words(K) * (size_t)std::max<int64_t>(acc, 1)));
         HIP_TRY(x->f_on.ensure(sizeof(uint32_t) * kQ * kQ + sizeof(uint64_t) * (kQ * kQ + 1)));
-        HIP_TRY(hipMemcpyAsync(x->f_p2.p, p2off.data(), sizeof(uint64_t) * p2off.size(), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(x->f_boff.p, boff.data(), sizeof(uint64_t) * boff.size(), hipMemcpyHostToDevice, st));
         pp.p2off = (const uint64_t*)x->f_p2.p;
         pp.rec2 = (uint64_t*)x->f_rec2.p;
         pp.boff = (const uint64_t*)x->f_boff.p;
         pp.out = (uint64_t*)x->f_okl.p;
         pp.nout = (uint32_t*)x->f_on.p;
         std::vector<uint32_t> nout((size_t)kQ * kQ, 0u);
-        if (R > 0) {
+        if (acc > 0) {
+            HIP_TRY(launch_emit(K, pp, st));
+            HIP_TRY(launch_fit_offsets(pp, st));
             HIP_TRY(launch_part2(K, pp, st));
             HIP_TRY(launch_reduce(K, pp, st));
             HIP_TRY(hipMemcpyAsync(nout.data(), pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(boff.data(), pp.boff, sizeof(uint64_t) * boff.size(), hipMemcpyDeviceToHost, st));
+        } else {
+            std::fill(boff.begin(), boff.end(), 0ull);
         }
+        const bool more = d1 < n_docs;
+        if (more) make_plan(d1, nxt);  // (host work while the GPU runs this batch)
         HIP_TRY(hipStreamSynchronize(st));
+        const int64_t R = (int64_t)boff[(size_t)kQ * kQ];
+        if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld positions", (long long)R, (long long)acc);
         unsigned long long E = 0;
         for (int b = 0; b < kQ * kQ; ++b) {
             if (nout[b] > boff[b + 1] - boff[b])
@@ -2212,7 +2233,8 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             b0 = b1;
         }
         if (E) t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - size0) / (double)E);
-        d0 = d1;
+        if (!more) break;
+        std::swap(cur, nxt);
     }
     // every gram length from the call's maximal windows; T1 back to the
     // context's block cache (the next call starts an empty one, sized by this)

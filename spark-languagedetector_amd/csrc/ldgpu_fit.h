@@ -117,6 +117,8 @@ size_t emit_lds_bytes(int K);
 size_t reduce_lds_bytes(int K);
 hipError_t fit3_prepare(int K);
 hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream);
+// p2off / boff from cnt3 on the device (one workgroup)
+hipError_t launch_fit_offsets(const PartParams& p, hipStream_t stream);
 hipError_t launch_part2(int K, const PartParams& p, hipStream_t stream);
 hipError_t launch_reduce(int K, const PartParams& p, hipStream_t stream);
 struct WideCountParams;

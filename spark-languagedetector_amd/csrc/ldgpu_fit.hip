@@ -1476,6 +1476,35 @@ __global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams
     }
 }
 
+// Exact bucket offsets from the emit histograms, on the device (no host
+// round trip between emit and part2): cnt3[(q1, q2)][group] counts ->
+// p2off = their exclusive prefix in that order, boff[b] = p2off[b][0],
+// boff[kQ * kQ] = the total.  One workgroup: each thread scans 32 counters.
+__global__ __launch_bounds__(1024) void fit_offsets_kernel(const uint32_t* cnt3, uint64_t* p2off, uint64_t* boff) {
+    constexpr int kN = kQ * kQ * kSplits, kPer = kN / 1024;
+    static_assert(kN % 1024 == 0 && kPer % kSplits == 0, "fit offsets");
+    __shared__ uint64_t part[1024];
+    const int t = threadIdx.x;
+    uint64_t sum = 0;
+    for (int i = 0; i < kPer; ++i) sum += cnt3[t * kPer + i];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan (Hillis-Steele)
+        const uint64_t v = t >= o ? part[t - o] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t acc = part[t] - sum;
+    for (int i = 0; i < kPer; ++i) {
+        const int j = t * kPer + i;
+        p2off[j] = acc;
+        if (j % kSplits == 0) boff[j / kSplits] = acc;
+        acc += cnt3[j];
+    }
+    if (t == 1023) boff[kQ * kQ] = acc;
+}
+
 // reduce: LDS hash slots per bucket (K u64 key words + a u32 count each, within
 // one workgroup's LDS)
 template <int K>
@@ -1896,6 +1925,12 @@ hipError_t launch_emit(int K, const PartParams& p, hipStream_t stream) {
     if (K == 1) hipLaunchKernelGGL(emit_kernel<1>, g, b, emit_lds_bytes(1), stream, p);
     else if (K == 2) hipLaunchKernelGGL(emit_kernel<2>, g, b, emit_lds_bytes(2), stream, p);
     else hipLaunchKernelGGL(emit_kernel<3>, g, b, emit_lds_bytes(3), stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_fit_offsets(const PartParams& p, hipStream_t stream) {
+    hipLaunchKernelGGL(fit_offsets_kernel, dim3(1), dim3(1024), 0, stream, p.cnt3, const_cast<uint64_t*>(p.p2off),
+                       const_cast<uint64_t*>(p.boff));
     return hipGetLastError();
 }
 
