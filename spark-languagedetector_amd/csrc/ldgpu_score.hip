@@ -1092,9 +1092,8 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
         // same window bytes and prefix-Bloom words.  Count mode (hit order
         // free): the host packs each DISTINCT length once and its hits count
         // its multiplicity in gramLengths.  The candidates of all lengths
-        // are verified together; a document whose candidates overflow the
-        // queue (nothing verified yet) restarts on the general path, so no
-        // verification state is live in this loop.
+        // are verified together, or in order whenever the next length's
+        // would overflow the queue.
         if (p.n_fast && !ablated(p, 2)) {
             Windows x;
             load_windows<STAGED>(p, src, 0, lane, x);
@@ -1119,9 +1118,13 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
                     test_sb<true, KEYED>(img, n, f, x, (int32_t)len - n + 1, m);
                 else
                     test_sb<false, KEYED>(img, n, f, x, (int32_t)len - n + 1, m);
-                if (qn + count_sb(m) > kQueueCap) {  // rare
-                    general = true;
-                    break;
+                if (qn + count_sb(m) > kQueueCap) {
+                    // verify and replay the queued candidates (they precede
+                    // this length's in reference order) and go on: a table
+                    // holding the 1-/2-byte grams of the text queues ~510
+                    // candidates per 256-B document, more than the queue
+                    flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
+                    qn = 0;
                 }
                 append_sb(wl.queue, qn, m, n, 0, lane);
             }
