@@ -154,7 +154,11 @@ int ldgpu_counts_destroy(ldgpu_counts* counts);
 
 /* Accumulate one batch of documents: every window of every gram length is
  * counted for doc_lang[d] (documents whose doc_lang is outside [0, n_langs)
- * are skipped, as reduceGrams filters unsupported languages). */
+ * are skipped, as reduceGrams filters unsupported languages).  Device
+ * scratch per call: the records of up to ~512 MB of corpus at a time (~16 GB,
+ * kept by the context for the next call) and a table of the call's maximal
+ * windows (one per byte position), from which every gram length's counts are
+ * derived before the call returns (FIT v4). */
 int ldgpu_count(ldgpu_counts* counts, const uint8_t* bytes, const int64_t* offsets,
                 const int32_t* doc_lang, int64_t n_docs);
 int ldgpu_count_device(ldgpu_counts* counts, const uint8_t* d_bytes, int64_t n_bytes,
