@@ -2,6 +2,7 @@
 // include/ldgpu.h (contexts, device tables, H2D/D2H staging, count-table
 // growth, probability / top-K table build).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -194,6 +195,8 @@ struct ldgpu_ctx {
     // context's count tables under `mu` and kept between fits: multi-GB
     // allocations per fit would cost more than the counting itself
     DevBuf f_rec, f_rec2, f_bstart, f_bhdr, f_nblk, f_cnt3, f_wg, f_p2, f_boff, f_okl, f_ocnt, f_on;
+    HostBuf h_fwg;                     // pinned staging of a batch's plan (one async copy to f_wg)
+    HostBuf h_fon;                     // pinned landing of a batch's nout / boff (an async copy back)
     // device blocks of destroyed / grown count tables and overflow lists,
     // reused by exact size: a Spark executor fits partition after partition,
     // and freeing and re-mapping ~10 GB per fit stalls the allocator
@@ -334,6 +337,8 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
     for (DevBuf* b : {&c->f_rec, &c->f_rec2, &c->f_bstart, &c->f_bhdr, &c->f_nblk, &c->f_cnt3, &c->f_wg, &c->f_p2,
                       &c->f_boff, &c->f_okl, &c->f_ocnt, &c->f_on})
         b->release();
+    c->h_fwg.release();
+    c->h_fon.release();
     for (ScorePipe* pp : c->pipes) pipe_destroy(pp);
     for (auto& b : c->cache) (void)hipFree(b.second);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2095,14 +2100,24 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     };
     BatchPlan cur, nxt;
     make_plan(0, cur);
+    // diagnostics build: host-side phase times per batch (LDGPU_FIT_TRACE)
+    const bool trace = diag_env("LDGPU_FIT_TRACE") != nullptr;
+    auto now_ms = [] {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    double tt[6] = {};
     for (;;) {
+        if (trace) tt[0] = now_ms();
         const int64_t d0 = cur.d0, d1 = cur.d1, acc = cur.acc, dirs = cur.dirs;
         const int grid_a = cur.grid_a;
         const std::vector<int64_t>& meta = cur.meta;
         const std::vector<int32_t>& wg_lang = cur.wg_lang;
         const std::vector<int32_t>& plen = cur.plen;
         const size_t n_lang = wg_lang.size(), n_perm = plen.size();
-        HIP_TRY(x->f_wg.ensure(sizeof(int64_t) * meta.size() + sizeof(int32_t) * (n_lang + n_perm) + 16));
+        const size_t wg_bytes = sizeof(int64_t) * meta.size() + sizeof(int32_t) * (n_lang + n_perm);
+        HIP_TRY(x->f_wg.ensure(wg_bytes + 16));
+        HIP_TRY(x->h_fwg.ensure(wg_bytes + 16));
+        HIP_TRY(x->h_fon.ensure(sizeof(uint32_t) * kQ * kQ + sizeof(uint64_t) * (kQ * kQ + 1)));
         HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * K * (size_t)std::max<int64_t>(acc, 1)));
         HIP_TRY(x->f_bstart.ensure(sizeof(int64_t) * (size_t)dirs));
         HIP_TRY(x->f_bhdr.ensure(sizeof(uint32_t) * kHdr * (size_t)dirs));
@@ -2111,9 +2126,15 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         uint8_t* wgp = (uint8_t*)x->f_wg.p;
         int32_t* d_wg_lang = (int32_t*)(wgp + sizeof(int64_t) * meta.size());
         int32_t* d_perm = d_wg_lang + n_lang;
-        HIP_TRY(hipMemcpyAsync(wgp, meta.data(), sizeof(int64_t) * meta.size(), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d_wg_lang, wg_lang.data(), sizeof(int32_t) * n_lang, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d_perm, plen.data(), sizeof(int32_t) * n_perm, hipMemcpyHostToDevice, st));
+        {  // the plan through pinned staging: one asynchronous copy (the
+           // previous batch's copy completed before its kernels, which the
+           // host waited for)
+            uint8_t* h = (uint8_t*)x->h_fwg.p;
+            memcpy(h, meta.data(), sizeof(int64_t) * meta.size());
+            memcpy(h + sizeof(int64_t) * meta.size(), wg_lang.data(), sizeof(int32_t) * n_lang);
+            memcpy(h + sizeof(int64_t) * meta.size() + sizeof(int32_t) * n_lang, plen.data(), sizeof(int32_t) * n_perm);
+            HIP_TRY(hipMemcpyAsync(wgp, h, wg_bytes, hipMemcpyHostToDevice, st));
+        }
         HIP_TRY(hipMemsetAsync(x->f_cnt3.p, 0, sizeof(uint32_t) * cnt3.size(), st));
         PartParams pp{};
         pp.bytes = d_bytes;
@@ -2158,14 +2179,24 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             HIP_TRY(launch_fit_offsets(pp, st));
             HIP_TRY(launch_part2(K, pp, st));
             HIP_TRY(launch_reduce(K, pp, st));
-            HIP_TRY(hipMemcpyAsync(nout.data(), pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(boff.data(), pp.boff, sizeof(uint64_t) * boff.size(), hipMemcpyDeviceToHost, st));
+            // into pinned memory: a copy to pageable memory would wait for the
+            // kernels here, before the next batch's plan
+            HIP_TRY(hipMemcpyAsync(x->h_fon.p, pp.nout, sizeof(uint32_t) * nout.size(), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync((uint8_t*)x->h_fon.p + sizeof(uint32_t) * nout.size(), pp.boff,
+                                   sizeof(uint64_t) * boff.size(), hipMemcpyDeviceToHost, st));
         } else {
             std::fill(boff.begin(), boff.end(), 0ull);
         }
         const bool more = d1 < n_docs;
+        if (trace) tt[1] = now_ms();
         if (more) make_plan(d1, nxt);  // (host work while the GPU runs this batch)
+        if (trace) tt[2] = now_ms();
         HIP_TRY(hipStreamSynchronize(st));
+        if (trace) tt[3] = now_ms();
+        if (acc > 0) {
+            memcpy(nout.data(), x->h_fon.p, sizeof(uint32_t) * nout.size());
+            memcpy(boff.data(), (uint8_t*)x->h_fon.p + sizeof(uint32_t) * nout.size(), sizeof(uint64_t) * boff.size());
+        }
         const int64_t R = (int64_t)boff[(size_t)kQ * kQ];
         if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld positions", (long long)R, (long long)acc);
         unsigned long long E = 0;
@@ -2206,6 +2237,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         }
         const uint64_t size0 = t1->size + t1->wsize;
         // (no entries: nout on the device is the last batch's, reduce did not run)
+        if (trace) tt[4] = now_ms();
         for (int b0 = E ? 0 : kQ * kQ; b0 < kQ * kQ;) {
             while ((double)t1->size > max_load(t1) * (double)t1->cap) {
                 if (int rc = grow(t1, 2 * t1->cap)) return rc;
@@ -2233,6 +2265,11 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             b0 = b1;
         }
         if (E) t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - size0) / (double)E);
+        if (trace) {
+            tt[5] = now_ms();
+            fprintf(stderr, "fit batch: upload+launch %.3f plan %.3f gpu-wait %.3f pre-merge %.3f merge %.3f ms\n",
+                    tt[1] - tt[0], tt[2] - tt[1], tt[3] - tt[2], tt[4] - tt[3], tt[5] - tt[4]);
+        }
         if (!more) break;
         std::swap(cur, nxt);
     }
