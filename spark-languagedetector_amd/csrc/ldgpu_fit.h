@@ -168,8 +168,8 @@ hipError_t launch_wide_add(const WideCountParams& p, const uint64_t* lo, const u
 hipError_t launch_wide_compact(const WideCountParams& p, uint64_t cap, uint64_t* out_lo, uint64_t* out_hi,
                                unsigned long long* out_counts, unsigned long long* out_n, hipStream_t stream);
 
-// ---- FIT v4 derive: the distinct gram lengths (ascending) and their
-// multiplicity in gramLengths
+// ---- FIT v4: the distinct gram lengths (ascending) and their multiplicity
+// in gramLengths (partial windows: partial_kernel)
 struct DeriveParams {
     int32_t n;
     int32_t len[kMaxGramLengths];
