@@ -398,9 +398,13 @@ def fit_main(args, world, rank, local, dev, backend):
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
                      "traffic": (traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}") or {}
                                  ).get("traffic_bytes_per_launch"),
-                     "kernel": "count (emit + part2 + reduce + merge)", "count_ms": round(count_s * 1e3, 3),
+                     "kernel": "count (emit + part2 + reduce + merge + derive)", "count_ms": round(count_s * 1e3, 3),
                      "algorithmic_bytes_per_count": int(algo)},
     }
+    if line["roofline"]["traffic"]:  # the counters' view: calibrated HBM bytes per count over the count time
+        tgbs = line["roofline"]["traffic"] / count_s / 1e9
+        line["roofline"]["traffic_GBps"] = round(tgbs, 1)
+        line["roofline"]["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
     if world > 1 and args.check_merge:
         # every rank's corpus regenerated on this GPU (same seeds), counted by
         # the oracle; the merged table (the same on every rank) must equal the
@@ -568,6 +572,12 @@ def main():
                 "traffic_scaled_from": prof.get("traffic_scaled_from"),
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "lookups_per_s": round(windows / (kernel_ms * 1e-3), 1)}
+    # the counters' view beside SURVEY's algorithmic one: calibrated HBM bytes
+    # per launch over the kernel time, as a fraction of the same peak
+    if roofline["traffic"]:
+        tgbs = roofline["traffic"] / (kernel_ms * 1e-3) / 1e9
+        roofline["traffic_GBps"] = round(tgbs, 1)
+        roofline["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
 
     cpu = None
     oracle_check = None
