@@ -160,20 +160,22 @@ def cpu_baseline(args, table, grams, data, off, packed=None):
 
 
 def cpu_baseline_fit(args, grams, data, off, lang):
-    """FIT on the oracle's C restatement (computeGrams + reduceGrams into a
-    host hash table, kind 'port', one thread), rank 0, bounded sample of the
-    same corpus; unit = corpus bytes/s like the line's value.  Also returns
-    the sample's oracle counts (key bytes, offsets, counts) for the parity
-    check of the GPU path on the same documents."""
+    """FIT on the oracle's C restatement (computeGrams per thread into private
+    host hash tables, then reduceGrams as a hash-partitioned merge: kind
+    'port', host_cores() pthreads, as the SCORE baseline), rank 0, bounded
+    sample of the same corpus; unit = corpus bytes/s like the line's value.
+    Also returns the sample's oracle counts (key bytes, offsets, counts) for
+    the parity check of the GPU path on the same documents."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ldoracle_c as OC
     L = OC.lib()
     g = np.asarray(grams, dtype=np.int32)
+    threads = host_cores()
 
     def run(n, keep=False):
         o = np.ascontiguousarray(off[:n + 1], dtype=np.int64)
         t0 = time.perf_counter()
-        h = L.ldo_count(OC._ptr(data), OC._ptr(o), OC._ptr(lang), n, args.langs, OC._ptr(g), len(g))
+        h = L.ldo_count_mt(OC._ptr(data), OC._ptr(o), OC._ptr(lang), n, args.langs, OC._ptr(g), len(g), threads)
         dt = time.perf_counter() - t0
         out = None
         if keep:
@@ -186,15 +188,15 @@ def cpu_baseline_fit(args, grams, data, off, lang):
         L.ldo_counts_destroy(h)
         return dt, out
 
-    probe = min(200, len(off) - 1)
+    probe = min(200 * threads, len(off) - 1)
     rate = int(off[probe]) / max(run(probe)[0], 1e-9)
     target = rate * args.cpu_seconds
     n = int(min(len(off) - 1, max(probe, np.searchsorted(off, target))))
     n = int(min(n, np.searchsorted(off, len(data), side="right") - 1))  # within the host copy of the corpus
     dt, exported = run(n, keep=True)
-    return {"value": round(int(off[n]) / dt, 1), "unit": "bytes/s", "cores": 1, "kind": "port",
+    return {"value": round(int(off[n]) / dt, 1), "unit": "bytes/s", "cores": threads, "kind": "port",
             "sample": f"first {n} documents ({int(off[n])} corpus bytes) of the GPU's corpus, "
-                      f"oracle/ldoracle.c ldo_count, 1 thread, {dt:.1f} s"}, n, exported
+                      f"oracle/ldoracle.c ldo_count_mt, {threads} pthreads, {dt:.1f} s"}, n, exported
 
 
 def host_path(model, data, off, acc_labels):
@@ -280,12 +282,44 @@ def traffic_from_profiles(workload_key):
     return same_shape
 
 
+# the kernels of one count call (ldgpu_count): the traffic the count's time covers
+COUNT_KERNELS = ("emit_kernel", "fit_offsets_kernel", "part2_kernel", "reduce_kernel", "merge_kernel",
+                 "derive_level_kernel", "derive_pairs_level_kernel", "derive_pairs2_level_kernel", "len_hist_kernel",
+                 "partial_kernel", "rehash_kernel", "wide_rehash_kernel", "sparse_rehash_kernel", "pair_rehash_kernel",
+                 "counts_add_kernel")
+
+
+def count_traffic(prof):
+    """Calibrated HBM bytes per count from a FIT PMC profile, summed over the
+    count's own kernels only (the profile's run also holds the table phase:
+    presence, select, top-K, stats)."""
+    if not prof:
+        return None
+    pk = prof.get("per_kernel_raw_bytes_per_count")
+    if not pk:
+        return prof.get("traffic_bytes_per_launch")
+    rf, wf = prof.get("read_factor", 1.0), prof.get("write_factor", 1.0)
+    tot = 0.0
+    for k, v in pk.items():
+        name = k.split("(")[0].split("<")[0]
+        if name in COUNT_KERNELS:
+            tot += rf * v.get("FETCH_SIZE", 0.0) + wf * v.get("WRITE_SIZE", 0.0)
+    return int(round(tot))
+
+
 def fit_corpus(args, ls, rank, dev):
     """This rank's config-3 shard: fit_bytes of 1-7 KB synthetic documents
     drawn on the GPU (synth.generate_device, seed per rank), untiled."""
     from languagedetection import synth as S
     n_docs = max(1, int(args.fit_bytes // 4096))  # U[1024, 7168]: 4096 B per document on average
     return S.generate_device(ls, n_docs, 1024, 7168, seed=S.SEED_BASE + 3 + 1000 * rank, device=dev)
+
+
+def masks_to_table(kb, ko, masks, vals, L):
+    """A mask-form fit table (DeviceCounts.fit_table_masks) as {gram: row}."""
+    b = kb.tobytes()
+    return {b[ko[i]:ko[i + 1]]: [float(vals[i]) if (int(masks[i, l // 64]) >> (l % 64)) & 1 else 0.0
+                                 for l in range(L)] for i in range(len(ko) - 1)}
 
 
 def topk_table_from_counts(kb, ko, cnt, K):
@@ -337,7 +371,7 @@ def fit_main(args, world, rank, local, dev, backend):
             t["merge_s"] = time.perf_counter() - t0 - t["create_s"] - t["count_s"]
         distinct = c.size()
         t1 = time.perf_counter()
-        table = c.fit_table(args.profile_size)
+        table = c.fit_table_masks(args.profile_size)   # packed mask form: no per-row Python objects
         t["table_s"] = time.perf_counter() - t1
         t2 = time.perf_counter()
         c.close()
@@ -386,7 +420,7 @@ def fit_main(args, world, rank, local, dev, backend):
                                f"grams {args.grams}, profile size {args.profile_size}",
                    "docs_per_gpu": n_docs, "corpus_bytes_per_gpu": n_bytes, "windows_per_gpu": windows,
                    "distinct_grams": parts[-1][1], "distinct_gram_language_pairs": st["pairs"],
-                   "table_rows": len(parts[-1][2]),
+                   "table_rows": len(parts[-1][2][1]) - 1,
                    "parallelism": f"dp{world} (corpus sharded; owner-exchange merge + distributed top-K)"},
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
                      for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
@@ -396,8 +430,7 @@ def fit_main(args, world, rank, local, dev, backend):
         "windows_counted_exactly_once": windows_ok,
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
-                     "traffic": (traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}") or {}
-                                 ).get("traffic_bytes_per_launch"),
+                     "traffic": count_traffic(traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}")),
                      "kernel": "count (emit + part2 + reduce + merge + derive)", "count_ms": round(count_s * 1e3, 3),
                      "algorithmic_bytes_per_count": int(algo)},
     }
@@ -425,7 +458,7 @@ def fit_main(args, world, rank, local, dev, backend):
         ko = np.zeros(len(okeys) + 1, dtype=np.int64)
         np.cumsum([len(k) for k in okeys], out=ko[1:])
         expect = topk_table_from_counts(kb, ko, ocnt, args.profile_size)
-        line["merged_table_matches_oracle"] = bool(parts[-1][2] == expect)
+        line["merged_table_matches_oracle"] = bool(masks_to_table(*parts[-1][2], args.langs) == expect)
         line["merge_check"] = {"ranks": world, "global_grams": len(okeys), "table_rows": len(expect)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         data_h = d_bytes[:min(n_bytes, 256 << 20)].cpu().numpy()

@@ -123,6 +123,9 @@ int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
 #define LDGPU_LAYOUT_PACKS              0x40
 #define LDGPU_LAYOUT_LANG_BLOCKS        0x80
 int ldgpu_model_layout(const ldgpu_model* model, int32_t* flags);
+/* The model's language count (a caller sizing score buffers, e.g. the JNI
+ * shim, takes it from the model rather than trusting its own). */
+int ldgpu_model_langs(const ldgpu_model* model, int32_t* n_langs);
 
 /* Host buffers in, host buffers out; synchronous.  out_scores is nullable
  * ([n_docs][n_langs] fp64).  out_labels[d] is the index into the supported
@@ -151,6 +154,8 @@ typedef struct ldgpu_counts ldgpu_counts;
 int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths,
                         int32_t n_grams, int64_t capacity_hint, ldgpu_counts** out);
 int ldgpu_counts_destroy(ldgpu_counts* counts);
+/* The table's language count. */
+int ldgpu_counts_langs(const ldgpu_counts* counts, int32_t* n_langs);
 
 /* Accumulate one batch of documents: every window of every gram length is
  * counted for doc_lang[d] (documents whose doc_lang is outside [0, n_langs)
@@ -266,6 +271,9 @@ int ldgpu_fit_table_size(ldgpu_counts* counts, int32_t profile_size, int64_t* n_
                          int64_t* key_bytes);
 int ldgpu_fit_table_export(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
                            double* rows);
+/* The cached table's rows and key bytes (what the last _size returned);
+ * LDGPU_EINVAL before any _size. */
+int ldgpu_fit_table_info(ldgpu_counts* counts, int64_t* n_rows, int64_t* key_bytes);
 /* The same table in mask form (masks [n_rows][ceil(L/64)], vals [n_rows]):
  * 8 (S + 1) bytes per row instead of 8 L -- what ldgpu_model_create_masks
  * takes (config-5 tables: 10M rows x 200 languages). */

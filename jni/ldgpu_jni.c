@@ -32,9 +32,14 @@ static void jclear(void) { jerr[0] = 0; }
 static void* addr(JNIEnv* env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
 
 /* LDGPU_OK when `buf` is a direct buffer of at least `bytes` bytes (or the
- * call touches none of it), else LDGPU_EINVAL with a message */
+ * call touches none of it), else LDGPU_EINVAL with a message.  A negative
+ * byte count (a size that went negative or overflowed on the way) fails. */
 static int need(JNIEnv* env, jobject buf, int64_t bytes, const char* what) {
-    if (bytes <= 0) return LDGPU_OK;
+    if (bytes < 0) {
+        snprintf(jerr, sizeof jerr, "%s: negative or overflowing size", what);
+        return LDGPU_EINVAL;
+    }
+    if (bytes == 0) return LDGPU_OK;
     if (!buf) {
         snprintf(jerr, sizeof jerr, "%s is null but %lld bytes are needed", what, (long long)bytes);
         return LDGPU_EINVAL;
@@ -52,10 +57,32 @@ static int need(JNIEnv* env, jobject buf, int64_t bytes, const char* what) {
     return LDGPU_OK;
 }
 
-/* offsets[n] of a checked int64 offsets buffer (its last entry), or -1 */
-static int64_t last_offset(JNIEnv* env, jobject offsets, int64_t n) {
+/* elem * a * b bytes, or -1 when a factor is negative or the product
+ * overflows int64 (need() then fails the call) */
+static int64_t bytes_of(int64_t elem, int64_t a, int64_t b) {
+    if (a < 0 || b < 0) return -1;
+    int64_t r;
+    if (__builtin_mul_overflow(elem, a, &r) || __builtin_mul_overflow(r, b, &r)) return -1;
+    return r;
+}
+
+/* an int64 offsets buffer of n + 1 entries (n >= 0) whose first entry is >= 0
+ * and whose last is >= the first; *last = offsets[n] (the bytes a call reads
+ * from the matching byte buffer).  (The library checks the entries between.) */
+static int need_offsets(JNIEnv* env, jobject offsets, int64_t n, const char* what, int64_t* last) {
+    const int rc = need(env, offsets, bytes_of(8, n < 0 || n == INT64_MAX ? -1 : n + 1, 1), what);
+    if (rc != LDGPU_OK) return rc;
     const int64_t* o = (const int64_t*)addr(env, offsets);
-    return o ? o[n] : -1;
+    if (!o) {
+        snprintf(jerr, sizeof jerr, "%s is not a direct buffer", what);
+        return LDGPU_EINVAL;
+    }
+    if (o[0] < 0 || o[n] < o[0]) {
+        snprintf(jerr, sizeof jerr, "%s: first entry %lld, last %lld", what, (long long)o[0], (long long)o[n]);
+        return LDGPU_EINVAL;
+    }
+    *last = o[n];
+    return LDGPU_OK;
 }
 
 #define CHECK(expr)                      \
@@ -117,9 +144,10 @@ JNIEXPORT jint JNICALL FN(modelCreate)(JNIEnv* env, jobject self, jlong ctx, jlo
     jclear();
     if (n_rows < 0 || n_langs < 1) return ldgpu_model_create((ldgpu_ctx*)(intptr_t)ctx, n_rows, NULL, NULL, NULL,
                                                              NULL, n_langs, NULL, 0, NULL);  /* its own EINVAL */
-    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
-    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n_rows), "keyBytes"));
-    CHECK(need(env, rows, 8 * n_rows * (int64_t)n_langs, "rows"));
+    int64_t nb = 0;
+    CHECK(need_offsets(env, key_offsets, n_rows, "keyOffsets", &nb));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, rows, bytes_of(8, n_rows, n_langs), "rows"));
     if (row_ok) CHECK(need(env, row_ok, n_rows, "rowOk"));
     jsize ng = 0;
     int32_t* g = ints(env, gram_lengths, &ng);
@@ -139,10 +167,11 @@ JNIEXPORT jint JNICALL FN(modelCreateMasks)(JNIEnv* env, jobject self, jlong ctx
     if (n_rows < 0 || n_langs < 1)
         return ldgpu_model_create_masks((ldgpu_ctx*)(intptr_t)ctx, n_rows, NULL, NULL, NULL, NULL, n_langs, NULL, 0,
                                         NULL);  /* its own EINVAL */
-    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
-    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n_rows), "keyBytes"));
-    CHECK(need(env, masks, 8 * n_rows * (int64_t)((n_langs + 63) / 64), "masks"));
-    CHECK(need(env, vals, 8 * n_rows, "vals"));
+    int64_t nb = 0;
+    CHECK(need_offsets(env, key_offsets, n_rows, "keyOffsets", &nb));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, masks, bytes_of(8, n_rows, ((int64_t)n_langs + 63) / 64), "masks"));
+    CHECK(need(env, vals, bytes_of(8, n_rows, 1), "vals"));
     jsize ng = 0;
     int32_t* g = ints(env, gram_lengths, &ng);
     ldgpu_model* m = NULL;
@@ -161,16 +190,24 @@ JNIEXPORT jint JNICALL FN(modelDestroy)(JNIEnv* env, jobject self, jlong model) 
     return ldgpu_model_destroy((ldgpu_model*)(intptr_t)model);
 }
 
-/* ldgpu_score: thread-safe; concurrent task threads run on their own streams */
+/* ldgpu_score: thread-safe; concurrent task threads run on their own streams.
+ * n_langs (the caller's) is unused: the scores buffer is sized by the model's
+ * own language count. */
 JNIEXPORT jint JNICALL FN(score)(JNIEnv* env, jobject self, jlong model, jobject bytes, jobject offsets,
                                  jlong n_docs, jobject labels, jobject scores, jint n_langs) {
     (void)self;
+    (void)n_langs;
     jclear();
     if (n_docs < 0) return ldgpu_score((ldgpu_model*)(intptr_t)model, NULL, NULL, n_docs, NULL, NULL);
-    CHECK(need(env, offsets, 8 * (n_docs + 1), "offsets"));
-    CHECK(need(env, bytes, last_offset(env, offsets, n_docs), "bytes"));
-    CHECK(need(env, labels, 4 * n_docs, "labels"));
-    if (scores) CHECK(need(env, scores, 8 * n_docs * (int64_t)n_langs, "scores"));
+    int64_t nb = 0;
+    CHECK(need_offsets(env, offsets, n_docs, "offsets", &nb));
+    CHECK(need(env, bytes, nb, "bytes"));
+    CHECK(need(env, labels, bytes_of(4, n_docs, 1), "labels"));
+    if (scores) {
+        int32_t L = 0;
+        CHECK(ldgpu_model_langs((const ldgpu_model*)(intptr_t)model, &L));
+        CHECK(need(env, scores, bytes_of(8, n_docs, L), "scores"));
+    }
     return ldgpu_score((ldgpu_model*)(intptr_t)model, (const uint8_t*)addr(env, bytes),
                        (const int64_t*)addr(env, offsets), n_docs, (int32_t*)addr(env, labels),
                        (double*)addr(env, scores));
@@ -200,9 +237,10 @@ JNIEXPORT jint JNICALL FN(count)(JNIEnv* env, jobject self, jlong counts, jobjec
     (void)self;
     jclear();
     if (n_docs < 0) return ldgpu_count((ldgpu_counts*)(intptr_t)counts, NULL, NULL, NULL, n_docs);
-    CHECK(need(env, offsets, 8 * (n_docs + 1), "offsets"));
-    CHECK(need(env, bytes, last_offset(env, offsets, n_docs), "bytes"));
-    CHECK(need(env, doc_lang, 4 * n_docs, "docLang"));
+    int64_t nb = 0;
+    CHECK(need_offsets(env, offsets, n_docs, "offsets", &nb));
+    CHECK(need(env, bytes, nb, "bytes"));
+    CHECK(need(env, doc_lang, bytes_of(4, n_docs, 1), "docLang"));
     return ldgpu_count((ldgpu_counts*)(intptr_t)counts, (const uint8_t*)addr(env, bytes),
                        (const int64_t*)addr(env, offsets), (const int32_t*)addr(env, doc_lang), n_docs);
 }
@@ -219,15 +257,19 @@ JNIEXPORT jint JNICALL FN(countsSize)(JNIEnv* env, jobject self, jlong counts, j
     return rc;
 }
 
+/* sizes from the table itself (n_langs, the caller's, is unused) */
 JNIEXPORT jint JNICALL FN(countsExport)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
                                         jobject key_offsets, jobject counts_out, jint n_langs) {
     (void)self;
+    (void)n_langs;
     jclear();
     int64_t n = 0, nb = 0;
+    int32_t L = 0;
+    CHECK(ldgpu_counts_langs((const ldgpu_counts*)(intptr_t)counts, &L));
     CHECK(ldgpu_counts_size((ldgpu_counts*)(intptr_t)counts, &n, &nb));
     CHECK(need(env, key_bytes, nb, "keyBytes"));
-    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
-    CHECK(need(env, counts_out, 8 * n * (int64_t)n_langs, "counts"));
+    CHECK(need(env, key_offsets, bytes_of(8, n + 1, 1), "keyOffsets"));
+    CHECK(need(env, counts_out, bytes_of(8, n, L), "counts"));
     return ldgpu_counts_export((ldgpu_counts*)(intptr_t)counts, (uint8_t*)addr(env, key_bytes),
                                (int64_t*)addr(env, key_offsets), (int64_t*)addr(env, counts_out));
 }
@@ -254,10 +296,10 @@ JNIEXPORT jint JNICALL FN(countsExportSparse)(JNIEnv* env, jobject self, jlong c
     int64_t nb = 0, np = 0;
     CHECK(ldgpu_counts_sparse_size((ldgpu_counts*)(intptr_t)counts, first, n, &nb, &np));
     CHECK(need(env, key_bytes, nb, "keyBytes"));
-    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
-    CHECK(need(env, pair_offsets, 8 * (n + 1), "pairOffsets"));
-    CHECK(need(env, pair_langs, 4 * np, "pairLangs"));
-    CHECK(need(env, pair_counts, 8 * np, "pairCounts"));
+    CHECK(need(env, key_offsets, bytes_of(8, n + 1, 1), "keyOffsets"));
+    CHECK(need(env, pair_offsets, bytes_of(8, n + 1, 1), "pairOffsets"));
+    CHECK(need(env, pair_langs, bytes_of(4, np, 1), "pairLangs"));
+    CHECK(need(env, pair_counts, bytes_of(8, np, 1), "pairCounts"));
     return ldgpu_counts_export_sparse((ldgpu_counts*)(intptr_t)counts, first, n, (uint8_t*)addr(env, key_bytes),
                                       (int64_t*)addr(env, key_offsets), (int64_t*)addr(env, pair_offsets),
                                       (int32_t*)addr(env, pair_langs), (int64_t*)addr(env, pair_counts));
@@ -270,26 +312,32 @@ JNIEXPORT jint JNICALL FN(countsAddSparse)(JNIEnv* env, jobject self, jlong coun
     jclear();
     if (n <= 0)
         return ldgpu_counts_add_sparse((ldgpu_counts*)(intptr_t)counts, n, NULL, NULL, NULL, NULL, NULL);
-    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
-    CHECK(need(env, pair_offsets, 8 * (n + 1), "pairOffsets"));
-    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n), "keyBytes"));
+    int64_t nb = 0, pl = 0;
+    CHECK(need_offsets(env, key_offsets, n, "keyOffsets", &nb));
+    CHECK(need_offsets(env, pair_offsets, n, "pairOffsets", &pl));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
     const int64_t* po = (const int64_t*)addr(env, pair_offsets);
-    const int64_t np = po[n] - po[0];
-    CHECK(need(env, pair_langs, 4 * np, "pairLangs"));
-    CHECK(need(env, pair_counts, 8 * np, "pairCounts"));
+    const int64_t np = pl - po[0];  /* the pairs are read from index 0 */
+    CHECK(need(env, pair_langs, bytes_of(4, np, 1), "pairLangs"));
+    CHECK(need(env, pair_counts, bytes_of(8, np, 1), "pairCounts"));
     return ldgpu_counts_add_sparse((ldgpu_counts*)(intptr_t)counts, n, (const uint8_t*)addr(env, key_bytes),
                                    (const int64_t*)addr(env, key_offsets), po, (const int32_t*)addr(env, pair_langs),
                                    (const int64_t*)addr(env, pair_counts));
 }
 
+/* rows are n x the table's own language count (n_langs, the caller's, is unused) */
 JNIEXPORT jint JNICALL FN(countsAdd)(JNIEnv* env, jobject self, jlong counts, jlong n, jobject key_bytes,
                                      jobject key_offsets, jobject rows, jint n_langs) {
     (void)self;
+    (void)n_langs;
     jclear();
     if (n <= 0) return ldgpu_counts_add((ldgpu_counts*)(intptr_t)counts, n, NULL, NULL, NULL);
-    CHECK(need(env, key_offsets, 8 * (n + 1), "keyOffsets"));
-    CHECK(need(env, key_bytes, last_offset(env, key_offsets, n), "keyBytes"));
-    CHECK(need(env, rows, 8 * n * (int64_t)n_langs, "rows"));
+    int64_t nb = 0;
+    int32_t L = 0;
+    CHECK(ldgpu_counts_langs((const ldgpu_counts*)(intptr_t)counts, &L));
+    CHECK(need_offsets(env, key_offsets, n, "keyOffsets", &nb));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, rows, bytes_of(8, n, L), "rows"));
     return ldgpu_counts_add((ldgpu_counts*)(intptr_t)counts, n, (const uint8_t*)addr(env, key_bytes),
                             (const int64_t*)addr(env, key_offsets), (const int64_t*)addr(env, rows));
 }
@@ -306,15 +354,28 @@ JNIEXPORT jint JNICALL FN(fitTableSize)(JNIEnv* env, jobject self, jlong counts,
     return rc;
 }
 
-/* n_rows / key_bytes_n: what fitTableSize returned for the cached table */
+/* The cached table's sizes come from the library (ldgpu_fit_table_info) and
+ * the table's own language count; n_rows / key_bytes_n / n_langs, the
+ * caller's, are unused. */
+static int table_sizes(jlong counts, int64_t* n_rows, int64_t* key_bytes, int32_t* L) {
+    CHECK(ldgpu_counts_langs((const ldgpu_counts*)(intptr_t)counts, L));
+    return ldgpu_fit_table_info((ldgpu_counts*)(intptr_t)counts, n_rows, key_bytes);
+}
+
 JNIEXPORT jint JNICALL FN(fitTableExport)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
                                           jobject key_offsets, jobject rows, jlong n_rows, jlong key_bytes_n,
                                           jint n_langs) {
     (void)self;
+    (void)n_rows;
+    (void)key_bytes_n;
+    (void)n_langs;
     jclear();
-    CHECK(need(env, key_bytes, key_bytes_n, "keyBytes"));
-    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
-    CHECK(need(env, rows, 8 * n_rows * (int64_t)n_langs, "rows"));
+    int64_t nr = 0, nb = 0;
+    int32_t L = 0;
+    CHECK(table_sizes(counts, &nr, &nb, &L));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, key_offsets, bytes_of(8, nr + 1, 1), "keyOffsets"));
+    CHECK(need(env, rows, bytes_of(8, nr, L), "rows"));
     return ldgpu_fit_table_export((ldgpu_counts*)(intptr_t)counts, (uint8_t*)addr(env, key_bytes),
                                   (int64_t*)addr(env, key_offsets), (double*)addr(env, rows));
 }
@@ -324,11 +385,17 @@ JNIEXPORT jint JNICALL FN(fitTableExportMasks)(JNIEnv* env, jobject self, jlong 
                                                jobject key_offsets, jobject masks, jobject vals, jlong n_rows,
                                                jlong key_bytes_n, jint n_langs) {
     (void)self;
+    (void)n_rows;
+    (void)key_bytes_n;
+    (void)n_langs;
     jclear();
-    CHECK(need(env, key_bytes, key_bytes_n, "keyBytes"));
-    CHECK(need(env, key_offsets, 8 * (n_rows + 1), "keyOffsets"));
-    CHECK(need(env, masks, 8 * n_rows * (int64_t)((n_langs + 63) / 64), "masks"));
-    CHECK(need(env, vals, 8 * n_rows, "vals"));
+    int64_t nr = 0, nb = 0;
+    int32_t L = 0;
+    CHECK(table_sizes(counts, &nr, &nb, &L));
+    CHECK(need(env, key_bytes, nb, "keyBytes"));
+    CHECK(need(env, key_offsets, bytes_of(8, nr + 1, 1), "keyOffsets"));
+    CHECK(need(env, masks, bytes_of(8, nr, ((int64_t)L + 63) / 64), "masks"));
+    CHECK(need(env, vals, bytes_of(8, nr, 1), "vals"));
     return ldgpu_fit_table_export_masks((ldgpu_counts*)(intptr_t)counts, (uint8_t*)addr(env, key_bytes),
                                         (int64_t*)addr(env, key_offsets), (uint64_t*)addr(env, masks),
                                         (double*)addr(env, vals));

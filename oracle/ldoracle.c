@@ -240,6 +240,100 @@ ldo_counts* ldo_count(const uint8_t* bytes, const int64_t* offsets, const int32_
     return c;
 }
 
+/* add `cnt` (a row of L) at key (p, len, h) */
+static void counts_add_row(ldo_counts* c, const uint8_t* p, int64_t len, uint64_t h, const int64_t* cnt) {
+    int ins;
+    int64_t idx = hm_upsert(&c->m, p, len, h, c->n, &ins);
+    if (ins) {
+        if (c->n + 1 > c->cap_rows) {
+            int64_t nc = c->cap_rows * 2;
+            c->counts = (int64_t*)realloc(c->counts, sizeof(int64_t) * (size_t)(nc * c->L));
+            memset(c->counts + c->cap_rows * c->L, 0, sizeof(int64_t) * (size_t)((nc - c->cap_rows) * c->L));
+            c->cap_rows = nc;
+        }
+        c->n++;
+    }
+    for (int32_t l = 0; l < c->L; ++l) c->counts[idx * c->L + l] += cnt[l];
+}
+
+static ldo_counts* counts_new(int32_t L) {
+    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
+    c->L = L; c->cap_rows = 1024;
+    c->counts = (int64_t*)calloc((size_t)(c->cap_rows * L), sizeof(int64_t));
+    hm_init(&c->m, 1024);
+    return c;
+}
+
+/* Multithreaded ldo_count (the CPU baseline of bench.py's FIT line, SURVEY
+ * §8d: N host threads): computeGrams per thread over a contiguous range of
+ * documents (balanced by bytes) into a private table -- Spark's map side --
+ * then reduceGrams: thread p sums every private table's keys of hash
+ * partition p (the shuffle), and the partitions (disjoint keys) are
+ * concatenated into one table.  Same counts as ldo_count. */
+typedef struct {
+    const uint8_t* bytes; const int64_t* off; const int32_t* lang; int64_t d0, d1; int32_t L; const int32_t* G;
+    int32_t nG; ldo_counts* local; ldo_counts** locals; int32_t nthreads, part; ldo_counts* out;
+} count_job;
+
+static void* count_map_worker(void* arg) {
+    count_job* j = (count_job*)arg;
+    j->local = ldo_count(j->bytes, j->off + j->d0, j->lang + j->d0, j->d1 - j->d0, j->L, j->G, j->nG);
+    return NULL;
+}
+
+static void* count_reduce_worker(void* arg) {
+    count_job* j = (count_job*)arg;
+    j->out = counts_new(j->L);
+    for (int32_t t = 0; t < j->nthreads; ++t) {
+        const ldo_counts* c = j->locals[t];
+        for (int64_t i = 0; i < c->m.cap; ++i) {
+            const entry* e = &c->m.e[i];
+            if (e->idx < 0 || (int32_t)((e->h >> 40) % (uint64_t)j->nthreads) != j->part) continue;
+            counts_add_row(j->out, e->p, e->len, e->h, c->counts + e->idx * c->L);
+        }
+    }
+    return NULL;
+}
+
+ldo_counts* ldo_count_mt(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, int64_t n_docs,
+                         int32_t L, const int32_t* G, int32_t nG, int32_t nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if (nthreads == 1 || n_docs < 2 * nthreads) return ldo_count(bytes, offsets, doc_lang, n_docs, L, G, nG);
+    pthread_t th[256]; count_job jobs[256]; ldo_counts* locals[256];
+    const int64_t b0 = offsets[0], nb = offsets[n_docs] - b0;
+    int64_t d = 0;
+    for (int32_t t = 0; t < nthreads; ++t) {
+        const int64_t goal = b0 + nb * (t + 1) / nthreads;
+        int64_t d1 = d;
+        while (d1 < n_docs && (offsets[d1] < goal || t + 1 == nthreads)) ++d1;
+        jobs[t] = (count_job){bytes, offsets, doc_lang, d, d1, L, G, nG, NULL, locals, nthreads, t, NULL};
+        d = d1;
+        pthread_create(&th[t], NULL, count_map_worker, &jobs[t]);
+    }
+    for (int32_t t = 0; t < nthreads; ++t) { pthread_join(th[t], NULL); locals[t] = jobs[t].local; }
+    for (int32_t t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, count_reduce_worker, &jobs[t]);
+    for (int32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    int64_t total = 0;
+    for (int32_t t = 0; t < nthreads; ++t) total += jobs[t].out->n;
+    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
+    c->L = L; c->cap_rows = total > 0 ? total : 1;
+    c->counts = (int64_t*)calloc((size_t)(c->cap_rows * L), sizeof(int64_t));
+    hm_init(&c->m, c->cap_rows);
+    for (int32_t t = 0; t < nthreads; ++t) {
+        const ldo_counts* o = jobs[t].out;
+        for (int64_t i = 0; i < o->m.cap; ++i) {
+            const entry* e = &o->m.e[i];
+            if (e->idx >= 0) counts_add_row(c, e->p, e->len, e->h, o->counts + e->idx * L);
+        }
+    }
+    for (int32_t t = 0; t < nthreads; ++t) {
+        free(locals[t]->m.e); free(locals[t]->counts); free(locals[t]);
+        free(jobs[t].out->m.e); free(jobs[t].out->counts); free(jobs[t].out);
+    }
+    return c;
+}
+
 int64_t ldo_counts_size(const ldo_counts* c) { return c->n; }
 
 int64_t ldo_counts_key_bytes(const ldo_counts* c) {

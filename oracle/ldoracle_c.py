@@ -42,6 +42,8 @@ def lib():
         L.ldo_score.argtypes = [_p, _p, _i32, _p, _p, _i64, _p, _p, _i32]
         L.ldo_count.restype = _p
         L.ldo_count.argtypes = [_p, _p, _p, _i64, _i32, _p, _i32]
+        L.ldo_count_mt.restype = _p
+        L.ldo_count_mt.argtypes = [_p, _p, _p, _i64, _i32, _p, _i32, _i32]
         L.ldo_counts_size.restype = _i64
         L.ldo_counts_size.argtypes = [_p]
         L.ldo_counts_key_bytes.restype = _i64
@@ -111,15 +113,20 @@ class Table:
 
 
 def count(data: np.ndarray, offsets: np.ndarray, doc_lang: np.ndarray, n_langs: int,
-          gram_lengths: Sequence[int]) -> Tuple[List[bytes], np.ndarray]:
+          gram_lengths: Sequence[int], nthreads: int = 1) -> Tuple[List[bytes], np.ndarray]:
     """computeGrams + reduceGrams: distinct grams sorted by (len, bytes) and raw
-    int64 counts [n_grams, L] (apply the JVM Int wrap separately)."""
+    int64 counts [n_grams, L] (apply the JVM Int wrap separately).  nthreads > 1:
+    ldo_count_mt (per-thread tables, then a hash-partitioned reduce)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.int64)
     doc_lang = np.ascontiguousarray(doc_lang, dtype=np.int32)
     g = np.asarray(gram_lengths, dtype=np.int32)
     L = lib()
-    h = L.ldo_count(_ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1, n_langs, _ptr(g), len(g))
+    if nthreads > 1:
+        h = L.ldo_count_mt(_ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1, n_langs, _ptr(g), len(g),
+                           nthreads)
+    else:
+        h = L.ldo_count(_ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1, n_langs, _ptr(g), len(g))
     try:
         n = L.ldo_counts_size(h)
         nb = L.ldo_counts_key_bytes(h)

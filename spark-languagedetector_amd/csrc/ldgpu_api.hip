@@ -1088,6 +1088,12 @@ extern "C" int ldgpu_model_info(const ldgpu_model* m, int32_t* mode, int64_t* n_
     return ok();
 }
 
+extern "C" int ldgpu_model_langs(const ldgpu_model* m, int32_t* n_langs) {
+    if (!m || !n_langs) return fail(LDGPU_EINVAL, "model/n_langs is NULL");
+    *n_langs = m->L;
+    return ok();
+}
+
 extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
     if (!m || !flags) return fail(LDGPU_EINVAL, "model/flags is NULL");
     const ldgpu_model* b = m->blocks.empty() ? m : m->blocks[0];  // blocks share one layout
@@ -1381,8 +1387,20 @@ struct ldgpu_counts {
     int32_t nGw = 0, Gw[kMaxGramLengths] = {};
     uint64_t cap = 0;
     uint64_t* d_keys = nullptr;
-    unsigned long long* d_counts = nullptr;
+    unsigned long long* d_counts = nullptr;  // [cap][L] (dense tables: T1 of the count calls)
     unsigned long long* d_size = nullptr;
+    // The final table T of a count table is sparse (ldgpu_fit.h CountParams):
+    // the grams in d_keys with presence bits d_masks[cap][S], the counts in a
+    // table of (gram slot, language) pairs -- the reduceGrams rows
+    // (LanguageDetector.scala:57-65), ~1.3 per gram on the fit corpora, where a
+    // dense row of L counters per gram took 1.6 KB at L = 200.
+    bool sparse = false;
+    int32_t S = 0;
+    uint64_t* d_masks = nullptr;
+    uint64_t pcap = 0, psize = 0;
+    uint64_t* d_pkeys = nullptr;
+    unsigned long long* d_pcounts = nullptr;
+    unsigned long long* d_psize = nullptr;
     uint64_t* d_ovf_keys = nullptr;
     int32_t* d_ovf_lang = nullptr;
     unsigned long long* d_ovf_cnt = nullptr;
@@ -1435,6 +1453,10 @@ struct ldgpu_counts {
 };
 
 namespace {
+// u64 words per gram slot besides the key: dense rows of L counters, or the
+// sparse table's S presence words
+uint64_t row_words(const ldgpu_counts* c) { return c->sparse ? (uint64_t)c->S : (uint64_t)c->L; }
+
 CountParams count_params(const ldgpu_counts* c) {
     CountParams p{};
     p.keys = c->d_keys;
@@ -1451,6 +1473,25 @@ CountParams count_params(const ldgpu_counts* c) {
     p.L = c->L;
     p.nG = c->nGn;
     for (int i = 0; i < c->nGn; ++i) p.G[i] = c->Gn[i];
+    if (c->sparse) {
+        p.masks = c->d_masks;
+        p.S = c->S;
+        p.pkeys = c->d_pkeys;
+        p.pcounts = c->d_pcounts;
+        p.pshift = (uint32_t)(64 - log2u(c->pcap));
+        p.pmask = c->pcap - 1;
+        p.psize = c->d_psize;
+    }
+    return p;
+}
+
+// the sparse table's pairs seen as a dense table of one counter per slot
+// (stats_kernel: occupied pairs and the sum of their counts)
+CountParams pair_view(const ldgpu_counts* c) {
+    CountParams p{};
+    p.keys = c->d_pkeys;
+    p.counts = c->d_pcounts;
+    p.L = 1;
     return p;
 }
 
@@ -1466,34 +1507,78 @@ void counts_free(ldgpu_counts* c) {
         (void)hipStreamSynchronize(c->ctx->stream);
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
+        cache_free(c->ctx, c->d_masks, c->cap * (size_t)c->S * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
         cache_free(c->ctx, c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
         cache_free(c->ctx, c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
         cache_free(c->ctx, c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
     } else {
-        for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_ovf_keys, (void*)c->d_ovf_lang,
-                        (void*)c->d_ovf_cnt})
+        for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_masks, (void*)c->d_pkeys,
+                        (void*)c->d_pcounts, (void*)c->d_ovf_keys, (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt})
             if (p) (void)hipFree(p);
     }
-    for (void* p : {(void*)c->d_size, (void*)c->d_ovf_n, (void*)c->d_ovf2_keys, (void*)c->d_ovf2_lang,
-                    (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
+    for (void* p : {(void*)c->d_size, (void*)c->d_psize, (void*)c->d_ovf_n, (void*)c->d_ovf2_keys,
+                    (void*)c->d_ovf2_lang, (void*)c->d_ovf2_cnt, (void*)c->d_ovf2_n})
         if (p) (void)hipFree(p);
     delete c;
 }
 
-int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, unsigned long long** counts) {
+// a gram table of cap slots: keys and rows of row_words(c) u64 words (dense
+// counters, or the sparse table's presence masks), zeroed
+int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, unsigned long long** rows) {
+    const size_t rb = cap * (size_t)row_words(c) * sizeof(unsigned long long);
     HIP_TRY(cache_alloc(c->ctx, (void**)keys, cap * sizeof(uint64_t)));
-    hipError_t e = cache_alloc(c->ctx, (void**)counts, cap * (size_t)c->L * sizeof(unsigned long long));
+    hipError_t e = cache_alloc(c->ctx, (void**)rows, rb);
     if (e != hipSuccess) {
         cache_free(c->ctx, *keys, cap * sizeof(uint64_t));
         *keys = nullptr;
         return fail(LDGPU_ENOMEM, "count table of %llu slots: %s", (unsigned long long)cap, hipGetErrorString(e));
     }
     HIP_TRY(hipMemsetAsync(*keys, 0, cap * sizeof(uint64_t), c->ctx->stream));
-    HIP_TRY(hipMemsetAsync(*counts, 0, cap * (size_t)c->L * sizeof(unsigned long long), c->ctx->stream));
+    HIP_TRY(hipMemsetAsync(*rows, 0, rb, c->ctx->stream));
     return LDGPU_OK;
 }
 
-// grow to new_cap (power of two) by rehashing on the device
+// the sparse table's pair table of pcap slots, zeroed
+int alloc_pairs(ldgpu_counts* c, uint64_t pcap, uint64_t** pkeys, unsigned long long** pcounts) {
+    HIP_TRY(cache_alloc(c->ctx, (void**)pkeys, pcap * sizeof(uint64_t)));
+    hipError_t e = cache_alloc(c->ctx, (void**)pcounts, pcap * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        cache_free(c->ctx, *pkeys, pcap * sizeof(uint64_t));
+        *pkeys = nullptr;
+        return fail(LDGPU_ENOMEM, "pair table of %llu slots: %s", (unsigned long long)pcap, hipGetErrorString(e));
+    }
+    HIP_TRY(hipMemsetAsync(*pkeys, 0, pcap * sizeof(uint64_t), c->ctx->stream));
+    HIP_TRY(hipMemsetAsync(*pcounts, 0, pcap * sizeof(unsigned long long), c->ctx->stream));
+    return LDGPU_OK;
+}
+
+// the sparse table's pairs into a fresh pair table of new_pcap slots, their
+// gram slots through remap (a grown gram table) or kept (remap null)
+int rebuild_pairs(ldgpu_counts* c, uint64_t new_pcap, const uint64_t* remap) {
+    uint64_t* nk = nullptr;
+    unsigned long long* nc = nullptr;
+    if (int rc = alloc_pairs(c, new_pcap, &nk, &nc)) return rc;
+    ldgpu_counts tmp;
+    tmp.sparse = true;
+    tmp.cap = c->cap;
+    tmp.pcap = new_pcap;
+    tmp.d_pkeys = nk;
+    tmp.d_pcounts = nc;
+    HIP_TRY(launch_pair_rehash(count_params(c), count_params(&tmp), c->pcap, remap, c->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
+    cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
+    c->d_pkeys = nk;
+    c->d_pcounts = nc;
+    c->pcap = new_pcap;
+    return LDGPU_OK;
+}
+
+// grow to new_cap (power of two) by rehashing on the device (the sparse
+// table: its grams with their masks, then its pairs re-keyed by the grams'
+// new slots)
 int grow(ldgpu_counts* c, uint64_t new_cap) {
     if (new_cap <= c->cap) return LDGPU_OK;
     uint64_t* nk = nullptr;
@@ -1502,8 +1587,34 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
     CountParams from = count_params(c);
     ldgpu_counts tmp;
     tmp.L = c->L;
+    tmp.sparse = c->sparse;
+    tmp.S = c->S;
     tmp.cap = new_cap;
     tmp.d_keys = nk;
+    if (c->sparse) {
+        tmp.d_masks = reinterpret_cast<uint64_t*>(nc);
+        uint64_t* remap = nullptr;
+        hipError_t e = cache_alloc(c->ctx, (void**)&remap, c->cap * sizeof(uint64_t));
+        if (e == hipSuccess) e = launch_sparse_rehash(from, count_params(&tmp), c->cap, remap, c->ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
+        if (e != hipSuccess) {
+            if (remap) cache_free(c->ctx, remap, c->cap * sizeof(uint64_t));
+            cache_free(c->ctx, nk, new_cap * sizeof(uint64_t));
+            cache_free(c->ctx, nc, new_cap * (size_t)c->S * sizeof(uint64_t));
+            return fail(LDGPU_ENOMEM, "count table grow: %s", hipGetErrorString(e));
+        }
+        const uint64_t old_cap = c->cap;
+        uint64_t* old_keys = c->d_keys;
+        uint64_t* old_masks = c->d_masks;
+        c->d_keys = nk;
+        c->d_masks = tmp.d_masks;
+        c->cap = new_cap;
+        cache_free(c->ctx, old_keys, old_cap * sizeof(uint64_t));
+        cache_free(c->ctx, old_masks, old_cap * (size_t)c->S * sizeof(uint64_t));
+        const int rc = rebuild_pairs(c, c->pcap, remap);
+        cache_free(c->ctx, remap, old_cap * sizeof(uint64_t));
+        return rc;
+    }
     tmp.d_counts = nc;
     CountParams to = count_params(&tmp);
     HIP_TRY(launch_rehash(from, to, c->cap, c->ctx->stream));
@@ -1516,17 +1627,41 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
     return LDGPU_OK;
 }
 
+// the sparse table's pair table to new_pcap slots
+int pgrow(ldgpu_counts* c, uint64_t new_pcap) {
+    if (!c->sparse || new_pcap <= c->pcap) return LDGPU_OK;
+    return rebuild_pairs(c, new_pcap, nullptr);
+}
+
 // Load a count table may reach before it doubles: 1/2, or 0.8 once the
-// doubled table would pass kBigTableBytes -- a slot holds a dense row of L
-// counters (1.6 KB at L = 200), so config 5's fit of 45M grams would need 2^27
-// slots (216 GB) at load 1/2, more than the device holds next to the old table
-// during the rehash.  (A rare insert that meets a linear-probe cluster longer
-// than kMaxProbe goes to the overflow list and is re-inserted by the host.)
+// doubled table would pass kBigTableBytes -- a dense slot holds a row of L
+// counters (1.6 KB at L = 200: T1 of a K = 3 fit), so a dense table of 45M grams
+// would need 2^27 slots (216 GB) at load 1/2, more than the device holds next to
+// the old table during the rehash.  The sparse table's slots are small (key +
+// S mask words; 16-B pairs): load 1/2.  (A rare insert that meets a linear-probe
+// cluster longer than kMaxProbe goes to the overflow list and is re-inserted
+// by the host.)
 constexpr uint64_t kBigTableBytes = 96ull << 30;
 
 double max_load(const ldgpu_counts* c) {
-    const uint64_t slot = 8ull + 8ull * (uint64_t)c->L;
+    const uint64_t slot = 8ull + 8ull * row_words(c);
     return 2 * c->cap * slot > kBigTableBytes ? 0.8 : 0.5;
+}
+
+// the sparse table's pair table doubles past load 1/2
+double pair_load() { return 0.5; }
+
+// room for `grams` more grams and `pairs` more pairs within the load limits
+// (grow / pgrow to the next fitting power of two)
+int reserve(ldgpu_counts* c, uint64_t grams, uint64_t pairs) {
+    if ((double)(c->size + grams) > max_load(c) * (double)c->cap) {
+        uint64_t target = next_pow2((uint64_t)((double)(c->size + grams) / max_load(c)) + 16);
+        if (int rc = grow(c, target)) return rc;
+    }
+    if (c->sparse && (double)(c->psize + pairs) > pair_load() * (double)c->pcap) {
+        if (int rc = pgrow(c, next_pow2((uint64_t)((double)(c->psize + pairs) / pair_load()) + 16))) return rc;
+    }
+    return LDGPU_OK;
 }
 
 // after a batch: read size / overflow, grow, re-insert overflow entries
@@ -1534,20 +1669,25 @@ double max_load(const ldgpu_counts* c) {
 // slots: entries are re-inserted in place; the caller keeps it within 0.9
 // load)
 int after_batch(ldgpu_counts* c, bool may_grow = true) {
-    unsigned long long size = 0;
+    unsigned long long size = 0, psize = 0;
     unsigned int novf = 0;
     HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
+    if (c->sparse) HIP_TRY(hipMemcpyAsync(&psize, c->d_psize, sizeof psize, hipMemcpyDeviceToHost, c->ctx->stream));
     HIP_TRY(hipMemcpyAsync(&novf, c->d_ovf_n, sizeof novf, hipMemcpyDeviceToHost, c->ctx->stream));
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
     if (novf > c->ovf_cap)  // cannot happen: sub-launches hold <= ovf_cap windows
         return fail(LDGPU_ENOMEM, "count table overflow (%u entries lost)", novf);
     c->size = size;
+    c->psize = psize;
+    c->tbl_valid = false;
+    c->sp_valid = false;
     if (novf == 0) {
         while (may_grow && (double)c->size > max_load(c) * (double)c->cap) {  // past the load limit: double
             if (int rc = grow(c, 2 * c->cap)) return rc;
         }
-        c->tbl_valid = false;
-        c->sp_valid = false;
+        while (may_grow && c->sparse && (double)c->psize > pair_load() * (double)c->pcap) {
+            if (int rc = pgrow(c, 2 * c->pcap)) return rc;
+        }
         return LDGPU_OK;
     }
     // Entries whose key found no slot are on the overflow list: grow, then
@@ -1586,14 +1726,18 @@ int after_batch(ldgpu_counts* c, bool may_grow = true) {
     // (kReinsertProbe: an overflow is a long linear-probe cluster, not a full
     // table); otherwise the table grows to the load limit first.  The list may
     // count windows, duplicates included (legacy count kernel), so a grow is
-    // sized within 8x the table.
-    uint64_t target = c->cap;
-    if (may_grow && (double)(size + novf) > 0.9 * (double)c->cap) {
-        target = next_pow2((uint64_t)((double)(size + novf) / max_load(c)) + 16);
-        target = std::max<uint64_t>(std::min<uint64_t>(target, 8 * c->cap), 2 * c->cap);
-    }
+    // sized within 8x the table.  (The sparse table: its gram and pair tables
+    // alike.)
+    auto target_of = [&](uint64_t sz, uint64_t cap, double load) {
+        if (!may_grow || (double)(sz + novf) <= 0.9 * (double)cap) return cap;
+        const uint64_t t = next_pow2((uint64_t)((double)(sz + novf) / load) + 16);
+        return std::max<uint64_t>(std::min<uint64_t>(t, 8 * cap), 2 * cap);
+    };
+    uint64_t target = target_of(size, c->cap, max_load(c));
+    uint64_t ptarget = c->sparse ? target_of(psize, c->pcap, pair_load()) : 0;
     for (unsigned int n = novf; n > 0;) {
         if (int rc = grow(c, target)) return rc;
+        if (int rc = pgrow(c, ptarget)) return rc;
         CountParams p = count_params(c);
         p.max_probe = kReinsertProbe;
         p.ovf_keys = dst_k;
@@ -1606,8 +1750,11 @@ int after_batch(ldgpu_counts* c, bool may_grow = true) {
         unsigned int again = 0;
         HIP_TRY(hipMemcpyAsync(&again, dst_n, sizeof again, hipMemcpyDeviceToHost, c->ctx->stream));
         HIP_TRY(hipMemcpyAsync(&size, c->d_size, sizeof size, hipMemcpyDeviceToHost, c->ctx->stream));
+        if (c->sparse)
+            HIP_TRY(hipMemcpyAsync(&psize, c->d_psize, sizeof psize, hipMemcpyDeviceToHost, c->ctx->stream));
         HIP_TRY(hipStreamSynchronize(c->ctx->stream));
         c->size = size;
+        c->psize = psize;
         n = again;
         std::swap(src_k, dst_k);
         std::swap(src_l, dst_l);
@@ -1616,9 +1763,8 @@ int after_batch(ldgpu_counts* c, bool may_grow = true) {
         std::swap(src_cap, dst_cap);
         if (!may_grow && n > 0) return fail(LDGPU_EDEVICE, "count table: %u entries found no slot", n);
         target = 2 * c->cap;
+        ptarget = 2 * c->pcap;
     }
-    c->tbl_valid = false;
-    c->sp_valid = false;
     return LDGPU_OK;
 }
 
@@ -1760,9 +1906,7 @@ int wide_count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, 
         }
         if (int rc = wide_ensure(c, (uint64_t)wide)) return rc;
         if (int rc = ensure_ovf(c, std::max<int64_t>(part, 1))) return rc;
-        if (2 * (c->size + (uint64_t)part) > c->cap) {
-            if (int rc = grow(c, next_pow2(4 * (c->size + (uint64_t)part) + 16))) return rc;
-        }
+        if (int rc = reserve(c, (uint64_t)part, (uint64_t)part)) return rc;
         WideCountParams p = wide_params(c);
         p.bytes = d_bytes;
         p.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
@@ -1791,7 +1935,7 @@ constexpr int64_t kBatchRecords = 1ll << 29;
 int out_words(int K) { return K == 1 ? 2 : K; }
 
 int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, int64_t capacity_hint,
-               ldgpu_counts** out);
+               ldgpu_counts** out, bool sparse = false);
 
 // distinct gram lengths, ascending, with their multiplicity in gramLengths
 DeriveParams derive_params(const ldgpu_counts* c) {
@@ -1845,14 +1989,24 @@ int derive_pending(ldgpu_counts* c) {
         cache_free(c->ctx, d_h, sizeof cnt);
     }
     // T's projected growth: the N-byte windows (most of T1) are new keys
-    // (a pair table holds ~2 languages per window on multilingual corpora)
+    // (a pair table holds ~2 languages per window on multilingual corpora);
+    // every T1 entry of a level is one (gram, language) pair of T
     {
-        const double est = (double)c->size + (pairs ? 0.55 : 1.1) * (double)(t->size + t->wsize);
+        const double tn = (double)(t->size + t->wsize);
+        const double est = (double)c->size + (pairs ? 0.55 : 1.1) * tn;
         if (est > max_load(c) * (double)c->cap) {
-            const uint64_t slot = 8ull + 8ull * L;
+            const uint64_t slot = 8ull + 8ull * row_words(c);
             uint64_t target = next_pow2((uint64_t)(est / 0.5) + 1);
             if (target * slot > kBigTableBytes) target = next_pow2((uint64_t)(est / 0.8) + 1);
             if (target > c->cap && grow(c, target) != LDGPU_OK) {
+                (void)hipGetLastError();
+                (void)ok();
+            }
+        }
+        const double pest = (double)c->psize + 1.1 * tn;
+        if (c->sparse && pest > pair_load() * (double)c->pcap) {
+            const uint64_t target = next_pow2((uint64_t)(pest / pair_load()) + 1);
+            if (pgrow(c, target) != LDGPU_OK) {
                 (void)hipGetLastError();
                 (void)ok();
             }
@@ -1882,10 +2036,18 @@ int derive_pending(ldgpu_counts* c) {
             while ((double)c->size > max_load(c) * (double)c->cap) {
                 if (int rc = grow(c, 2 * c->cap)) return rc;
             }
+            while (c->sparse && (double)c->psize > pair_load() * (double)c->pcap) {
+                if (int rc = pgrow(c, 2 * c->pcap)) return rc;
+            }
             uint64_t slots = kOvfMax / per_slot;
             if (mt) {
+                // every occupied T1 slot adds at most one gram and per_slot pairs to T
                 const double room = std::max(1.0, (max_load(c) + 0.1) * (double)c->cap - (double)c->size);
                 slots = std::min<uint64_t>(slots, (uint64_t)(room / tload));
+                if (c->sparse) {
+                    const double proom = std::max(1.0, (pair_load() + 0.1) * (double)c->pcap - (double)c->psize);
+                    slots = std::min<uint64_t>(slots, (uint64_t)(proom / (tload * (double)per_slot)));
+                }
                 if (lev > kMaxGram) {
                     const uint64_t occ = std::min<uint64_t>(cnt[lev], (uint64_t)(2.0 * tload * (double)slots) + 64);
                     if (int rc = wide_ensure(c, occ)) return rc;
@@ -1939,9 +2101,7 @@ int count_partial(ldgpu_counts* c, const uint8_t* d_bytes, const int64_t* d_offs
     hipStream_t st = x->stream;
     const int64_t n = (int64_t)docs.size();
     if (int rc = ensure_ovf(c, n)) return rc;
-    if ((double)(c->size + (uint64_t)n) > max_load(c) * (double)c->cap) {
-        if (int rc = grow(c, next_pow2((uint64_t)((double)(c->size + (uint64_t)n) / max_load(c)) + 16))) return rc;
-    }
+    if (int rc = reserve(c, (uint64_t)n, (uint64_t)n)) return rc;
     if (any_wide) {
         if (int rc = wide_ensure(c, (uint64_t)n)) return rc;
     }
@@ -2295,6 +2455,10 @@ int count_launch_narrow(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes
 int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
                  const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, const int32_t* h_lang, hipStream_t st) {
     if (st != c->ctx->stream) HIP_TRY(hipStreamSynchronize(st));  // inputs were written on the caller's stream
+    // the cached fit table and sparse copy describe the counts before this
+    // call, which may fail part-way through changing them
+    c->tbl_valid = false;
+    c->sp_valid = false;
     if (c->v3) return count_launch_v3(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, h_lang);
     if (c->nGn > 0) {
         if (int rc = count_launch_narrow(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, c->ctx->stream))
@@ -2354,17 +2518,19 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
                     LDGPU_MAX_LANGS);
     if (int rc = check_grams(gram_lengths, n_grams, kMaxWideGram)) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
-    if (int rc = counts_new(ctx, n_langs, gram_lengths, n_grams, capacity_hint, out)) return rc;
+    if (int rc = counts_new(ctx, n_langs, gram_lengths, n_grams, capacity_hint, out, true)) return rc;
     return ok();
 }
 
 namespace {
 // a count table (validated arguments; the caller has set the device)
 int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, int64_t capacity_hint,
-               ldgpu_counts** out) {
+               ldgpu_counts** out, bool sparse) {
     auto* c = new ldgpu_counts();
     c->ctx = ctx;
     c->L = n_langs;
+    c->sparse = sparse;
+    c->S = sparse ? (n_langs + 63) / 64 : 0;
     c->nG = n_grams;
     for (int i = 0; i < n_grams; ++i) {
         c->G[i] = gram_lengths[i];
@@ -2397,9 +2563,16 @@ int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int
             }
         }
     }
-    int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
+    int rc = sparse ? alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<unsigned long long**>(&c->d_masks))
+                    : alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
+    if (!rc && sparse) {
+        c->pcap = c->cap;
+        rc = alloc_pairs(c, c->pcap, &c->d_pkeys, &c->d_pcounts);
+    }
     hipError_t e = hipSuccess;
     if (!rc) e = hipMalloc((void**)&c->d_size, sizeof(unsigned long long));
+    if (!rc && e == hipSuccess && sparse) e = hipMalloc((void**)&c->d_psize, sizeof(unsigned long long));
+    if (!rc && e == hipSuccess && sparse) e = hipMemsetAsync(c->d_psize, 0, sizeof(unsigned long long), ctx->stream);
     if (!rc && e == hipSuccess) e = cache_alloc(c->ctx, (void**)&c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
     if (!rc && e == hipSuccess) e = cache_alloc(c->ctx, (void**)&c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
     if (!rc && e == hipSuccess)
@@ -2416,6 +2589,12 @@ int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int
     return LDGPU_OK;
 }
 }  // namespace
+
+extern "C" int ldgpu_counts_langs(const ldgpu_counts* c, int32_t* n_langs) {
+    if (!c || !n_langs) return fail(LDGPU_EINVAL, "counts/n_langs is NULL");
+    *n_langs = c->L;
+    return ok();
+}
 
 extern "C" int ldgpu_counts_destroy(ldgpu_counts* c) {
     counts_free(c);
@@ -2550,34 +2729,72 @@ std::vector<uint64_t> wide_order(const std::vector<uint64_t>& wlo, const std::ve
     return word;
 }
 
-// compacted host copy: keys + counts rows, sorted by (length, bytes)
-int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsigned long long>& cnt) {
-    const uint64_t n = c->size;
-    uint64_t* d_k = nullptr;
-    unsigned long long *d_c = nullptr, *d_n = nullptr;
-    HIP_TRY(hipMalloc((void**)&d_k, std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
-    hipError_t e = hipMalloc((void**)&d_c, std::max<uint64_t>(n, 1) * c->L * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc((void**)&d_n, sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemsetAsync(d_n, 0, sizeof(unsigned long long), c->ctx->stream);
-    if (e == hipSuccess) e = launch_compact(count_params(c), c->cap, d_k, d_c, d_n, c->ctx->stream);
-    unsigned long long got = 0;
-    std::vector<uint64_t> k(n);
-    std::vector<unsigned long long> cc((size_t)n * c->L);
-    if (e == hipSuccess) e = hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, c->ctx->stream);
-    if (e == hipSuccess && n)
-        e = hipMemcpyAsync(k.data(), d_k, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->ctx->stream);
-    if (e == hipSuccess && n)
-        e = hipMemcpyAsync(cc.data(), d_c, n * c->L * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                           c->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
-    for (void* p : {(void*)d_k, (void*)d_c, (void*)d_n})
-        if (p) (void)hipFree(p);
-    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "count export: %s", hipGetErrorString(e));
-    if (got != n) return fail(LDGPU_EDEVICE, "count export: %llu slots occupied, %llu expected", got,
-                              (unsigned long long)n);
-    std::vector<std::pair<uint64_t, uint64_t>> sk(n);
-    for (uint64_t i = 0; i < n; ++i) sk[i] = {sort_key(k[i]), i};
-    std::sort(sk.begin(), sk.end());
+// the packed key of a sort_key (ldgpu_common.h): length in the top byte,
+// bytes big-endian below it
+uint64_t unsort_key(uint64_t s) {
+    const int len = key_len(s);
+    uint64_t k = (uint64_t)len << 56;
+    for (int i = 0; i < len; ++i) k |= ((s >> (48 - 8 * i)) & 0xffull) << (8 * i);
+    return k;
+}
+
+// The table pulled to the host in (length, bytes) order -- the rows of
+// reduceGrams (LanguageDetector.scala:57-65): every gram (one-word key, or a
+// wide stand-in kWideTag << 56 | rank, c->wide_sorted[rank]) and its nonzero
+// (language, count) pairs in language order (pairs of gram i: [poff[i],
+// poff[i + 1])).  with_pairs = false: the keys only.
+struct Pulled {
+    std::vector<uint64_t> keys;
+    std::vector<int64_t> poff;
+    std::vector<int32_t> lang;
+    std::vector<int64_t> cnt;
+};
+
+int counts_pull(ldgpu_counts* c, Pulled& out, bool with_pairs = true) {
+    const uint64_t n = c->size, np = c->psize;
+    hipStream_t st = c->ctx->stream;
+    std::vector<uint64_t> sk(n), pk;
+    std::vector<unsigned long long> pc;
+    if (n) {
+        // the grams' sort keys ordered on the device, each gram slot's rank, then
+        // the pairs keyed (rank, language) and ordered the same way
+        DevBufs db;
+        db.ctx = c->ctx;
+        uint64_t *d_sk, *d_slot;
+        uint32_t* d_rank;
+        unsigned long long* d_n;
+        HIP_TRY(db.alloc(&d_sk, n));
+        HIP_TRY(db.alloc(&d_slot, n));
+        HIP_TRY(db.alloc(&d_rank, c->cap));
+        HIP_TRY(db.alloc(&d_n, 2));
+        HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
+        HIP_TRY(launch_gram_compact(count_params(c), c->cap, d_sk, d_slot, d_n, true, st));
+        unsigned long long got = 0;
+        HIP_TRY(hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (got != n)
+            return fail(LDGPU_EDEVICE, "count export: %llu grams, %llu expected", got, (unsigned long long)n);
+        HIP_TRY(sort_pairs_u64((int64_t)n, d_sk, reinterpret_cast<unsigned long long*>(d_slot), 59, st));
+        HIP_TRY(hipMemcpyAsync(sk.data(), d_sk, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        if (with_pairs && np) {
+            uint64_t* d_pk;
+            unsigned long long* d_pc;
+            HIP_TRY(db.alloc(&d_pk, np));
+            HIP_TRY(db.alloc(&d_pc, np));
+            HIP_TRY(launch_rank_scatter((int64_t)n, d_slot, d_rank, st));
+            HIP_TRY(launch_pair_compact(count_params(c), c->pcap, d_rank, d_pk, d_pc, d_n + 1, st));
+            HIP_TRY(hipMemcpyAsync(&got, d_n + 1, sizeof got, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (got != np)
+                return fail(LDGPU_EDEVICE, "count export: %llu pairs, %llu expected", got, (unsigned long long)np);
+            HIP_TRY(sort_pairs_u64((int64_t)np, d_pk, d_pc, (int)kPairLangBits + log2u(n + 1) + 1, st));
+            pk.resize(np);
+            pc.resize(np);
+            HIP_TRY(hipMemcpyAsync(pk.data(), d_pk, np * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(pc.data(), d_pc, np * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     // the wide grams (8..15 bytes) after them, in (length, bytes) order, as
     // stand-in keys kWideTag << 56 | rank (c->wide_sorted[rank])
     std::vector<uint64_t> wlo, whi;
@@ -2586,16 +2803,37 @@ int counts_pull(ldgpu_counts* c, std::vector<uint64_t>& keys, std::vector<unsign
     const uint64_t nw = wlo.size();
     const std::vector<uint64_t> word = wide_order(wlo, whi);
     c->wide_sorted.resize(nw);
-    keys.resize(n + nw);
-    cnt.resize((size_t)(n + nw) * c->L);
-    for (uint64_t i = 0; i < n; ++i) {
-        keys[i] = k[sk[i].second];
-        memcpy(&cnt[(size_t)i * c->L], &cc[(size_t)sk[i].second * c->L], sizeof(unsigned long long) * c->L);
-    }
+    out.keys.resize(n + nw);
+    for (uint64_t i = 0; i < n; ++i) out.keys[i] = unsort_key(sk[i]);
     for (uint64_t r = 0; r < nw; ++r) {
         c->wide_sorted[r] = {wlo[word[r]], whi[word[r]]};
-        keys[n + r] = (kWideTag << 56) | r;
-        memcpy(&cnt[(size_t)(n + r) * c->L], &wc[(size_t)word[r] * c->L], sizeof(unsigned long long) * c->L);
+        out.keys[n + r] = (kWideTag << 56) | r;
+    }
+    out.poff.clear();
+    out.lang.clear();
+    out.cnt.clear();
+    if (!with_pairs) return LDGPU_OK;
+    const int L = c->L;
+    out.poff.assign(n + nw + 1, 0);
+    out.lang.resize(pk.size());
+    out.cnt.resize(pk.size());
+    for (size_t j = 0; j < pk.size(); ++j) {
+        const uint64_t r = pk[j] >> kPairLangBits;
+        if (r >= n) return fail(LDGPU_EDEVICE, "count export: pair of gram %llu, %llu grams", (unsigned long long)r,
+                                (unsigned long long)n);
+        out.poff[r + 1]++;
+        out.lang[j] = (int32_t)(pk[j] & ((1ull << kPairLangBits) - 1ull));
+        out.cnt[j] = (int64_t)pc[j];
+    }
+    for (uint64_t i = 0; i < n; ++i) out.poff[i + 1] += out.poff[i];
+    for (uint64_t r = 0; r < nw; ++r) {
+        const unsigned long long* row = &wc[(size_t)word[r] * L];
+        for (int l = 0; l < L; ++l) {
+            if (!row[l]) continue;
+            out.lang.push_back(l);
+            out.cnt.push_back((int64_t)row[l]);
+        }
+        out.poff[n + r + 1] = (int64_t)out.lang.size();
     }
     return LDGPU_OK;
 }
@@ -2632,11 +2870,10 @@ extern "C" int ldgpu_counts_size(ldgpu_counts* c, int64_t* n_grams, int64_t* key
     HIP_TRY(hipSetDevice(c->ctx->device));
     if (n_grams) *n_grams = (int64_t)(c->size + c->wsize);
     if (key_bytes) {
-        std::vector<uint64_t> k;
-        std::vector<unsigned long long> cc;
-        if (int rc = counts_pull(c, k, cc)) return rc;
+        Pulled t;
+        if (int rc = counts_pull(c, t, false)) return rc;
         int64_t s = 0;
-        for (uint64_t x : k) s += gram_bytes(c, x, nullptr);
+        for (uint64_t x : t.keys) s += gram_bytes(c, x, nullptr);
         *key_bytes = s;
     }
     return ok();
@@ -2650,7 +2887,8 @@ extern "C" int ldgpu_counts_stats(ldgpu_counts* c, int64_t* n_grams, int64_t* n_
     unsigned long long h[2] = {0, 0};
     HIP_TRY(hipMalloc((void**)&d, sizeof h));
     hipError_t e = hipMemsetAsync(d, 0, sizeof h, c->ctx->stream);
-    if (e == hipSuccess) e = launch_stats(count_params(c), c->cap, d, c->ctx->stream);
+    // the sparse table's pairs (one counter each), the wide table's rows
+    if (e == hipSuccess) e = launch_stats(pair_view(c), c->pcap, d, c->ctx->stream);
     if (e == hipSuccess && c->wcap) {  // the wide table, through the same kernel (hi != 0: occupied)
         CountParams w{};
         w.keys = c->d_whi;
@@ -2672,11 +2910,14 @@ extern "C" int ldgpu_counts_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t*
     if (!c || !key_offsets || !counts_out) return fail(LDGPU_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    std::vector<uint64_t> k;
-    std::vector<unsigned long long> cc;
-    if (int rc = counts_pull(c, k, cc)) return rc;
-    write_keys(c, k, key_bytes, key_offsets);
-    for (size_t i = 0; i < cc.size(); ++i) counts_out[i] = (int64_t)cc[i];
+    Pulled t;
+    if (int rc = counts_pull(c, t)) return rc;
+    write_keys(c, t.keys, key_bytes, key_offsets);
+    const int L = c->L;
+    const size_t n = t.keys.size();
+    memset(counts_out, 0, sizeof(int64_t) * n * (size_t)L);
+    for (size_t i = 0; i < n; ++i)
+        for (int64_t j = t.poff[i]; j < t.poff[i + 1]; ++j) counts_out[i * L + t.lang[j]] = t.cnt[j];
     return ok();
 }
 
@@ -2684,26 +2925,15 @@ namespace {
 // the sparse host copy (ldgpu_counts::sp_*), pulled once per table state
 int sparse_pull(ldgpu_counts* c) {
     if (c->sp_valid) return LDGPU_OK;
-    std::vector<uint64_t> k;
-    std::vector<unsigned long long> cc;
-    if (int rc = counts_pull(c, k, cc)) return rc;
-    const int L = c->L;
-    const size_t n = k.size();
-    c->sp_keys = std::move(k);
+    Pulled t;
+    if (int rc = counts_pull(c, t)) return rc;
+    const size_t n = t.keys.size();
+    c->sp_keys = std::move(t.keys);
     c->sp_koff.assign(n + 1, 0);
-    c->sp_poff.assign(n + 1, 0);
-    c->sp_lang.clear();
-    c->sp_cnt.clear();
-    for (size_t i = 0; i < n; ++i) {
-        c->sp_koff[i + 1] = c->sp_koff[i] + gram_bytes(c, c->sp_keys[i], nullptr);
-        for (int l = 0; l < L; ++l) {
-            const unsigned long long v = cc[i * (size_t)L + l];
-            if (!v) continue;
-            c->sp_lang.push_back(l);
-            c->sp_cnt.push_back((int64_t)v);
-        }
-        c->sp_poff[i + 1] = (int64_t)c->sp_lang.size();
-    }
+    for (size_t i = 0; i < n; ++i) c->sp_koff[i + 1] = c->sp_koff[i] + gram_bytes(c, c->sp_keys[i], nullptr);
+    c->sp_poff = std::move(t.poff);
+    c->sp_lang = std::move(t.lang);
+    c->sp_cnt = std::move(t.cnt);
     c->sp_valid = true;
     return LDGPU_OK;
 }
@@ -2714,6 +2944,56 @@ int check_range(const ldgpu_counts* c, int64_t first, int64_t n) {
         return fail(LDGPU_EINVAL, "gram range [%lld, %lld) outside [0, %lld)", (long long)first,
                     (long long)(first + n), (long long)total);
     return LDGPU_OK;
+}
+
+// (key, language, count) triples of one-word keys into the sparse table
+// (nonzero counts; probe-limit overflows are re-inserted by after_batch)
+int add_triples(ldgpu_counts* c, const std::vector<uint64_t>& tk, const std::vector<int32_t>& tl,
+                const std::vector<unsigned long long>& tc) {
+    const int64_t nt = (int64_t)tk.size();
+    if (!nt) return LDGPU_OK;
+    hipStream_t st = c->ctx->stream;
+    if (int rc = reserve(c, (uint64_t)nt, (uint64_t)nt)) return rc;
+    if (int rc = ensure_ovf(c, nt)) return rc;
+    DevBufs tb;
+    uint64_t* d_k;
+    int32_t* d_l;
+    unsigned long long* d_c;
+    HIP_TRY(tb.alloc(&d_k, nt));
+    HIP_TRY(tb.alloc(&d_l, nt));
+    HIP_TRY(tb.alloc(&d_c, nt));
+    HIP_TRY(hipMemcpyAsync(d_k, tk.data(), nt * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_l, tl.data(), nt * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_c, tc.data(), nt * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+    HIP_TRY(launch_counts_add(count_params(c), d_k, nullptr, d_l, d_c, nt, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return after_batch(c);
+}
+
+// dense rows of wide keys (8..15 bytes) into the wide table
+int add_wide_rows(ldgpu_counts* c, const std::vector<uint64_t>& wlo, const std::vector<uint64_t>& whi,
+                  const std::vector<unsigned long long>& wrows) {
+    const int64_t nw = (int64_t)wlo.size();
+    if (!nw) return LDGPU_OK;
+    hipStream_t st = c->ctx->stream;
+    if (int rc = wide_ensure(c, (uint64_t)nw)) return rc;
+    DevBufs wb;
+    uint64_t *d_lo, *d_hi;
+    unsigned long long* d_r;
+    HIP_TRY(wb.alloc(&d_lo, nw));
+    HIP_TRY(wb.alloc(&d_hi, nw));
+    HIP_TRY(wb.alloc(&d_r, (size_t)nw * c->L));
+    HIP_TRY(hipMemcpyAsync(d_lo, wlo.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_hi, whi.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_r, wrows.data(), wrows.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_wide_add(wide_params(c), d_lo, d_hi, d_r, nw, st));
+    return wide_after(c);
+}
+
+uint64_t wide_lo_host(const uint8_t* kb) { return (pack_key_host(kb, 8) & ((1ull << 56) - 1)) | ((uint64_t)kb[7] << 56); }
+uint64_t wide_hi_host(const uint8_t* kb, int64_t len) {
+    return (pack_key_host(kb + 8, (int)len - 8) & ((1ull << 56) - 1)) | ((uint64_t)len << 56);
 }
 }  // namespace
 
@@ -2789,8 +3069,8 @@ extern "C" int ldgpu_counts_add_sparse(ldgpu_counts* c, int64_t n, const uint8_t
                 tc.push_back((unsigned long long)pair_counts[q]);
             }
         } else {
-            wlo.push_back((pack_key_host(kb, 8) & ((1ull << 56) - 1)) | ((uint64_t)kb[7] << 56));
-            whi.push_back((pack_key_host(kb + 8, (int)len - 8) & ((1ull << 56) - 1)) | ((uint64_t)len << 56));
+            wlo.push_back(wide_lo_host(kb));
+            whi.push_back(wide_hi_host(kb, len));
             wrows.resize(wrows.size() + c->L, 0ull);
             for (int64_t j = pair_offsets[i]; j < pair_offsets[i + 1]; ++j) {
                 const int64_t q = j - pair_offsets[0];
@@ -2800,42 +3080,10 @@ extern "C" int ldgpu_counts_add_sparse(ldgpu_counts* c, int64_t n, const uint8_t
     }
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    hipStream_t st = c->ctx->stream;
-    if (!wlo.empty()) {
-        const int64_t nw = (int64_t)wlo.size();
-        if (int rc = wide_ensure(c, (uint64_t)nw)) return rc;
-        DevBufs wb;
-        uint64_t *d_lo, *d_hi;
-        unsigned long long* d_r;
-        HIP_TRY(wb.alloc(&d_lo, nw));
-        HIP_TRY(wb.alloc(&d_hi, nw));
-        HIP_TRY(wb.alloc(&d_r, (size_t)nw * c->L));
-        HIP_TRY(hipMemcpyAsync(d_lo, wlo.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d_hi, whi.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d_r, wrows.data(), wrows.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_wide_add(wide_params(c), d_lo, d_hi, d_r, nw, st));
-        if (int rc = wide_after(c)) return rc;
-    }
-    const int64_t nt = (int64_t)tk.size();
-    if (!nt) return ok();
-    if (2 * (c->size + (uint64_t)nt) > c->cap) {
-        if (int rc = grow(c, next_pow2(4 * (c->size + nt) + 16))) return rc;
-    }
-    if (int rc = ensure_ovf(c, nt)) return rc;
-    DevBufs tb;
-    uint64_t* d_k;
-    int32_t* d_l;
-    unsigned long long* d_c;
-    HIP_TRY(tb.alloc(&d_k, nt));
-    HIP_TRY(tb.alloc(&d_l, nt));
-    HIP_TRY(tb.alloc(&d_c, nt));
-    HIP_TRY(hipMemcpyAsync(d_k, tk.data(), nt * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_l, tl.data(), nt * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_c, tc.data(), nt * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
-    HIP_TRY(launch_counts_add(count_params(c), d_k, nullptr, d_l, d_c, nt, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (int rc = after_batch(c)) return rc;
+    c->tbl_valid = false;
+    c->sp_valid = false;
+    if (int rc = add_wide_rows(c, wlo, whi, wrows)) return rc;
+    if (int rc = add_triples(c, tk, tl, tc)) return rc;
     return ok();
 }
 
@@ -2846,72 +3094,41 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     if (n < 0) return fail(LDGPU_EINVAL, "n < 0");
     if (n == 0) return ok();
     if (!key_bytes || !key_offsets || !counts_in) return fail(LDGPU_EINVAL, "NULL argument");
-    // one-word keys (1..7 bytes) and wide keys (8..15 bytes: two words)
-    std::vector<uint64_t> keys, wlo, whi;
-    std::vector<int64_t> narrow_rows, wide_rows;
+    // one-word keys (1..7 bytes): their nonzero counts as (key, language,
+    // count) triples; wide keys (8..15 bytes: two words) as dense rows
+    const int L = c->L;
+    std::vector<uint64_t> tk, wlo, whi;
+    std::vector<int32_t> tl;
+    std::vector<unsigned long long> tc, wrows;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = key_offsets[i + 1] - key_offsets[i];
         if (len < 1 || len > LDGPU_MAX_FIT_GRAM)
             return fail(LDGPU_EINVAL, "key %lld has length %lld outside [1, %d]", (long long)i, (long long)len,
                         LDGPU_MAX_FIT_GRAM);
         const uint8_t* kb = key_bytes + key_offsets[i];
+        const int64_t* row = counts_in + (size_t)i * L;
+        for (int l = 0; l < L; ++l)
+            if (row[l] < 0) return fail(LDGPU_EINVAL, "key %lld: negative count", (long long)i);
         if (len <= kMaxGram) {
-            keys.push_back(pack_key_host(kb, (int)len));
-            narrow_rows.push_back(i);
+            const uint64_t key = pack_key_host(kb, (int)len);
+            for (int l = 0; l < L; ++l) {
+                if (!row[l]) continue;
+                tk.push_back(key);
+                tl.push_back(l);
+                tc.push_back((unsigned long long)row[l]);
+            }
         } else {
-            wlo.push_back((pack_key_host(kb, 8) & ((1ull << 56) - 1)) | ((uint64_t)kb[7] << 56));
-            whi.push_back((pack_key_host(kb + 8, (int)len - 8) & ((1ull << 56) - 1)) | ((uint64_t)len << 56));
-            wide_rows.push_back(i);
+            wlo.push_back(wide_lo_host(kb));
+            whi.push_back(wide_hi_host(kb, len));
+            wrows.insert(wrows.end(), row, row + L);
         }
     }
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    if (!wide_rows.empty()) {
-        const int64_t nw = (int64_t)wide_rows.size();
-        if (int rc = wide_ensure(c, (uint64_t)nw)) return rc;
-        std::vector<int64_t> wrows((size_t)nw * c->L);
-        for (int64_t j = 0; j < nw; ++j)
-            memcpy(&wrows[(size_t)j * c->L], counts_in + (size_t)wide_rows[j] * c->L, sizeof(int64_t) * c->L);
-        DevBufs wb;
-        uint64_t *d_lo, *d_hi;
-        unsigned long long* d_r;
-        HIP_TRY(wb.alloc(&d_lo, nw));
-        HIP_TRY(wb.alloc(&d_hi, nw));
-        HIP_TRY(wb.alloc(&d_r, (size_t)nw * c->L));
-        HIP_TRY(hipMemcpyAsync(d_lo, wlo.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, c->ctx->stream));
-        HIP_TRY(hipMemcpyAsync(d_hi, whi.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice, c->ctx->stream));
-        HIP_TRY(hipMemcpyAsync(d_r, wrows.data(), (size_t)nw * c->L * sizeof(int64_t), hipMemcpyHostToDevice,
-                               c->ctx->stream));
-        HIP_TRY(launch_wide_add(wide_params(c), d_lo, d_hi, d_r, nw, c->ctx->stream));
-        if (int rc = wide_after(c)) return rc;
-    }
-    if (keys.empty()) return ok();
-    std::vector<int64_t> nrows;
-    if ((int64_t)keys.size() != n) {
-        nrows.resize(keys.size() * (size_t)c->L);
-        for (size_t j = 0; j < keys.size(); ++j)
-            memcpy(&nrows[j * c->L], counts_in + (size_t)narrow_rows[j] * c->L, sizeof(int64_t) * c->L);
-        counts_in = nrows.data();
-        n = (int64_t)keys.size();
-    }
-    if (2 * (c->size + (uint64_t)n) > c->cap) {
-        if (int rc = grow(c, next_pow2(4 * (c->size + n) + 16))) return rc;
-    }
-    uint64_t* d_k = nullptr;
-    unsigned long long* d_c = nullptr;
-    HIP_TRY(hipMalloc((void**)&d_k, n * sizeof(uint64_t)));
-    hipError_t e = hipMalloc((void**)&d_c, (size_t)n * c->L * sizeof(unsigned long long));
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d_k, keys.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, c->ctx->stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d_c, counts_in, (size_t)n * c->L * sizeof(int64_t), hipMemcpyHostToDevice, c->ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream);
-    if (e == hipSuccess) e = launch_counts_add(count_params(c), d_k, d_c, nullptr, nullptr, n, c->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
-    (void)hipFree(d_k);
-    if (d_c) (void)hipFree(d_c);
-    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "counts_add: %s", hipGetErrorString(e));
-    if (int rc = after_batch(c)) return rc;
+    c->tbl_valid = false;
+    c->sp_valid = false;
+    if (int rc = add_wide_rows(c, wlo, whi, wrows)) return rc;
+    if (int rc = add_triples(c, tk, tl, tc)) return rc;
     return ok();
 }
 
@@ -2928,17 +3145,28 @@ extern "C" int ldgpu_counts_export_device(ldgpu_counts* c, int64_t capacity, uin
         return fail(LDGPU_EINVAL, "export_device: %llu grams exceed the capacity %lld", (unsigned long long)c->size,
                     (long long)capacity);
     if (c->size && (!d_keys || !d_counts)) return fail(LDGPU_EINVAL, "device pointer is NULL");
+    if (!c->size) return ok();
     hipStream_t st = (hipStream_t)stream;
-    unsigned long long* d_n = nullptr;
-    HIP_TRY(hipMalloc((void**)&d_n, sizeof(unsigned long long)));
-    hipError_t e = hipMemsetAsync(d_n, 0, sizeof(unsigned long long), st);
-    if (e == hipSuccess)
-        e = launch_compact(count_params(c), c->cap, d_keys, reinterpret_cast<unsigned long long*>(d_counts), d_n, st);
+    hipStream_t cs = c->ctx->stream;
+    HIP_TRY(hipStreamSynchronize(st));  // the caller's buffers may be in use on its stream
+    // the grams (unordered) with their slots, each slot's output row, then the
+    // pairs into the zeroed dense rows
+    DevBufs db;
+    db.ctx = c->ctx;
+    uint64_t* d_slot;
+    uint32_t* d_rank;
+    unsigned long long* d_n;
+    HIP_TRY(db.alloc(&d_slot, c->size));
+    HIP_TRY(db.alloc(&d_rank, c->cap));
+    HIP_TRY(db.alloc(&d_n, 1));
+    HIP_TRY(hipMemsetAsync(d_n, 0, sizeof(unsigned long long), cs));
+    HIP_TRY(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * c->size * (size_t)c->L, cs));
+    HIP_TRY(launch_gram_compact(count_params(c), c->cap, d_keys, d_slot, d_n, false, cs));
+    HIP_TRY(launch_rank_scatter((int64_t)c->size, d_slot, d_rank, cs));
+    HIP_TRY(launch_pair_dense(count_params(c), c->pcap, d_rank, reinterpret_cast<unsigned long long*>(d_counts), cs));
     unsigned long long got = 0;
-    if (e == hipSuccess) e = hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(d_n);
-    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "export_device: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
     if (got != c->size) return fail(LDGPU_EDEVICE, "export_device: %llu grams, %llu expected", got,
                                     (unsigned long long)c->size);
     return ok();
@@ -2953,15 +3181,29 @@ extern "C" int ldgpu_counts_add_device(ldgpu_counts* c, int64_t n, const uint64_
     if (!d_keys || !d_counts) return fail(LDGPU_EINVAL, "device pointer is NULL");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
+    c->tbl_valid = false;
+    c->sp_valid = false;
     hipStream_t st = (hipStream_t)stream;
+    hipStream_t cs = c->ctx->stream;
     HIP_TRY(hipStreamSynchronize(st));
-    if (2 * (c->size + (uint64_t)n) > c->cap) {
-        if (int rc = grow(c, next_pow2(4 * (c->size + n) + 16))) return rc;
+    // room for the block's nonzero counts (pairs) and keys
+    unsigned long long nnz = 0;
+    {
+        DevBufs db;
+        db.ctx = c->ctx;
+        unsigned long long* d_nz;
+        HIP_TRY(db.alloc(&d_nz, 1));
+        HIP_TRY(hipMemsetAsync(d_nz, 0, sizeof(unsigned long long), cs));
+        HIP_TRY(launch_nnz(reinterpret_cast<const unsigned long long*>(d_counts), n * (int64_t)c->L, d_nz, cs));
+        HIP_TRY(hipMemcpyAsync(&nnz, d_nz, sizeof nnz, hipMemcpyDeviceToHost, cs));
+        HIP_TRY(hipStreamSynchronize(cs));
     }
-    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), c->ctx->stream));
-    HIP_TRY(launch_counts_add(count_params(c), d_keys, reinterpret_cast<const unsigned long long*>(d_counts), nullptr, nullptr,
-                              n, c->ctx->stream));
-    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    if (int rc = reserve(c, (uint64_t)n, nnz)) return rc;
+    if (int rc = ensure_ovf(c, (int64_t)std::max<unsigned long long>(nnz, 1))) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), cs));
+    HIP_TRY(launch_counts_add(count_params(c), d_keys, reinterpret_cast<const unsigned long long*>(d_counts), nullptr,
+                              nullptr, n, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
     if (int rc = after_batch(c)) return rc;
     return ok();
 }
@@ -3043,15 +3285,14 @@ int table_from_presence(ldgpu_counts* c, const std::vector<uint64_t>& keys, cons
 // Host build from the full count table (used when some language has fewer
 // than K present grams: the zero-valued fill needs every gram).
 int fit_table_host(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_bytes) {
-    std::vector<uint64_t> keys;
-    std::vector<unsigned long long> cnt;
-    if (int rc = counts_pull(c, keys, cnt)) return rc;
+    Pulled t;
+    if (int rc = counts_pull(c, t)) return rc;
     const int L = c->L, S = (L + 63) / 64;
-    std::vector<uint64_t> masks(keys.size() * S, 0);
-    for (size_t i = 0; i < keys.size(); ++i)
-        for (int l = 0; l < L; ++l)
-            if (cnt[i * L + l]) masks[i * S + l / 64] |= 1ull << (l % 64);
-    return table_from_presence(c, keys, masks, K, n_rows, key_bytes);
+    std::vector<uint64_t> masks(t.keys.size() * S, 0);
+    for (size_t i = 0; i < t.keys.size(); ++i)
+        for (int64_t j = t.poff[i]; j < t.poff[i + 1]; ++j)
+            if (t.cnt[j]) masks[i * S + t.lang[j] / 64] |= 1ull << (t.lang[j] % 64);
+    return table_from_presence(c, t.keys, masks, K, n_rows, key_bytes);
 }
 }  // namespace
 
@@ -3303,7 +3544,7 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
         HIP_TRY(db.alloc(&d_nof, W));
         HIP_TRY(db.alloc(&d_cur, W));
         HIP_TRY(hipMemsetAsync(d_nof, 0, sizeof(unsigned long long) * W, st));
-        HIP_TRY(launch_owner_pair_count(count_params(c), c->cap, (uint32_t)W, d_nof, st));
+        HIP_TRY(launch_owner_pair_count(count_params(c), c->pcap, (uint32_t)W, d_nof, st));
         HIP_TRY(hipMemcpyAsync(nof.data(), d_nof, sizeof(unsigned long long) * W, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         unsigned long long acc = 0;
@@ -3314,7 +3555,7 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
         }
         HIP_TRY(db.alloc(&d_pairs, 2 * (size_t)acc));
         HIP_TRY(hipMemcpyAsync(d_cur, cur.data(), sizeof(unsigned long long) * W, hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_owner_pair_scatter(count_params(c), c->cap, (uint32_t)W, d_cur, d_pairs, st));
+        HIP_TRY(launch_owner_pair_scatter(count_params(c), c->pcap, (uint32_t)W, d_cur, d_pairs, st));
         HIP_TRY(hipStreamSynchronize(st));
         return LDGPU_OK;
     };
@@ -3338,16 +3579,23 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     if (int rc = comm_alltoallv_dev(m, (const uint8_t*)d_pairs, sb, (uint8_t*)d_rpairs, rb)) return rc;
     // the owned shard, rebuilt: one key may arrive from several ranks
     auto rebuild = [&]() -> int {
+        HIP_TRY(hipStreamSynchronize(st));
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
-        cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
-        c->d_keys = nullptr;
-        c->d_counts = nullptr;
-        c->cap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
-        if (int rc = alloc_table(c, c->cap, &c->d_keys, &c->d_counts)) return rc;
+        cache_free(c->ctx, c->d_masks, c->cap * (size_t)c->S * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
+        c->d_keys = c->d_masks = c->d_pkeys = nullptr;
+        c->d_pcounts = nullptr;
+        c->cap = c->pcap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
+        if (int rc = alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<unsigned long long**>(&c->d_masks)))
+            return rc;
+        if (int rc = alloc_pairs(c, c->pcap, &c->d_pkeys, &c->d_pcounts)) return rc;
         if (int rc = ensure_ovf(c, R)) return rc;
         HIP_TRY(hipMemsetAsync(c->d_size, 0, sizeof(unsigned long long), st));
+        HIP_TRY(hipMemsetAsync(c->d_psize, 0, sizeof(unsigned long long), st));
         HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
         c->size = 0;
+        c->psize = 0;
         HIP_TRY(launch_pairs_add(count_params(c), d_rpairs, R, st));
         HIP_TRY(hipStreamSynchronize(st));
         return after_batch(c);
@@ -3661,6 +3909,15 @@ extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows,
     if (fallback) {
         if (int rc = fit_table_host(c, K, n_rows, key_bytes)) return rc;
     }
+    return ok();
+}
+
+extern "C" int ldgpu_fit_table_info(ldgpu_counts* c, int64_t* n_rows, int64_t* key_bytes) {
+    if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    if (!c->tbl_valid) return fail(LDGPU_EINVAL, "call ldgpu_fit_table_size first");
+    const size_t n = c->tbl_off.size() - 1;
+    if (n_rows) *n_rows = (int64_t)n;
+    if (key_bytes) *key_bytes = c->tbl_off[n];
     return ok();
 }
 

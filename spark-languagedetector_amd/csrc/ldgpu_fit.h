@@ -29,7 +29,23 @@ struct CountParams {
     int32_t L;
     int32_t nG;
     int32_t G[kMaxGramLengths];
+
+    // Sparse table (the final count table T of ldgpu_counts; pkeys != null,
+    // counts == null): the reference's reduceGrams rows (LanguageDetector.
+    // scala:57-65) -- one (gram, language) -> count pair per row, not a dense
+    // row of L counters per gram.  keys[cap] holds the grams with their
+    // presence bits masks[cap][S] (bit l: the pair (gram, l) exists); the pair
+    // table pkeys[pcap] / pcounts[pcap] is keyed (gram slot + 1) << 12 | lang.
+    uint64_t* masks;
+    int32_t S;
+    uint64_t* pkeys;
+    unsigned long long* pcounts;
+    uint32_t pshift;            // pair slot = mix64(pair key) >> pshift
+    uint64_t pmask;             // pcap - 1
+    unsigned long long* psize;  // distinct pairs inserted
 };
+
+constexpr uint32_t kPairLangBits = 12;  // pair key: (gram slot + 1) << 12 | lang (L <= 4096)
 
 constexpr int kCountWaves = 16;
 constexpr uint32_t kMaxProbe = 128;
@@ -132,6 +148,29 @@ hipError_t launch_merge(int K, const PartParams& p, const CountParams& c, const 
 // rehash all occupied slots of `from` into `to` (keys unique), moving the count rows
 hipError_t launch_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap,
                          hipStream_t stream);
+// sparse table: grams of `from` into `to` with their presence masks,
+// remap[old slot] = new slot; then every pair of `from` into the pair table of
+// `to` (gram slots through remap, or kept when remap is null)
+hipError_t launch_sparse_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap, uint64_t* remap,
+                                hipStream_t stream);
+hipError_t launch_pair_rehash(const CountParams& from, const CountParams& to, uint64_t from_pcap,
+                              const uint64_t* remap, hipStream_t stream);
+// sparse table exports: the grams (out_keys[o], out_slot[o] = gram slot);
+// rank_of[slot[r]] = r; every pair as (rank_of[gram] << 12 | lang, count)
+// (sort_keys: out_keys holds each gram's sort_key, ldgpu_common.h)
+hipError_t launch_gram_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys, uint64_t* out_slot,
+                               unsigned long long* out_n, bool sort_keys, hipStream_t stream);
+hipError_t launch_rank_scatter(int64_t n, const uint64_t* slot, uint32_t* rank_of, hipStream_t stream);
+hipError_t launch_pair_compact(const CountParams& p, uint64_t pcap, const uint32_t* rank_of, uint64_t* out_pk,
+                               unsigned long long* out_cnt, unsigned long long* out_n, hipStream_t stream);
+// every pair's count into dense rows: rows[rank_of[gram]][lang] (rows zeroed by the caller)
+hipError_t launch_pair_dense(const CountParams& p, uint64_t pcap, const uint32_t* rank_of, unsigned long long* rows,
+                             hipStream_t stream);
+// sort (key, value) u64 pairs by the low `bits` bits of the key (hipcub radix;
+// scratch allocated and freed here; synchronises `stream`)
+hipError_t sort_pairs_u64(int64_t n, uint64_t* keys, unsigned long long* vals, int bits, hipStream_t stream);
+// nonzero entries of n u64 counters: *out += them
+hipError_t launch_nnz(const unsigned long long* v, int64_t n, unsigned long long* out, hipStream_t stream);
 // out[0] += distinct (gram, language) pairs, out[1] += sum of all counts
 hipError_t launch_stats(const CountParams& p, uint64_t cap, unsigned long long* out, hipStream_t stream);
 // compact occupied slots: out_keys[i], out_counts[i][L]; *out_n = number written

@@ -128,6 +128,57 @@ __device__ __forceinline__ void flush_new_keys(unsigned long long* size, unsigne
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(size, (unsigned long long)v);
 }
 
+// Sparse table T (CountParams::pkeys): find-or-insert of a pair key in the
+// pair table; the slot or -1 at the probe limit
+__device__ __forceinline__ int64_t pair_find_or_insert(const CountParams& p, uint64_t pk, bool& new_pair) {
+    uint64_t s = mix64(pk) >> p.pshift;
+    for (uint32_t probe = 0; probe < p.max_probe; ++probe) {
+        uint64_t k = __hip_atomic_load(&p.pkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == pk) return (int64_t)s;
+        if (k == kEmpty) {
+            const unsigned long long old =
+                atomicCAS(reinterpret_cast<unsigned long long*>(&p.pkeys[s]), 0ull, (unsigned long long)pk);
+            if (old == 0ull) {
+                new_pair = true;
+                return (int64_t)s;
+            }
+            if (old == pk) return (int64_t)s;
+        }
+        s = (s + 1) & p.pmask;
+    }
+    return -1;
+}
+
+// c of (key, lang) into the sparse table: the gram's slot (its presence bit
+// set when the pair is new), then the pair's counter.  An add that reaches a
+// probe limit in either table goes to the overflow list as (key, lang, c) --
+// re-adding it finds the gram if it was placed.  A zero count adds nothing
+// (a reduceGrams row has count >= 1).  Returns new gram | new pair << 32.
+__device__ __forceinline__ uint64_t sparse_add_q(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
+    if (!c) return 0;
+    bool new_gram = false, new_pair = false;
+    const int64_t g = find_or_insert(p, key, new_gram);
+    int64_t s = -1;
+    if (g >= 0) {
+        s = pair_find_or_insert(p, ((uint64_t)(g + 1) << kPairLangBits) | (uint64_t)lang, new_pair);
+        if (s >= 0) {
+            atomicAdd(&p.pcounts[s], c);
+            if (new_pair)
+                atomicOr(reinterpret_cast<unsigned long long*>(&p.masks[(size_t)g * p.S + (lang >> 6)]),
+                         1ull << (lang & 63));
+        }
+    }
+    if (s < 0) {
+        const unsigned int at = atomicAdd(p.ovf_n, 1u);
+        if (at < p.ovf_cap) {
+            p.ovf_keys[at] = key;
+            p.ovf_lang[at] = lang;
+            p.ovf_cnt[at] = c;
+        }
+    }
+    return (uint64_t)new_gram | ((uint64_t)new_pair << 32);
+}
+
 // add_count without the counter update: returns whether the key is new
 __device__ __forceinline__ bool add_count_q(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
     bool new_key = false;
@@ -145,8 +196,29 @@ __device__ __forceinline__ bool add_count_q(const CountParams& p, uint64_t key, 
     return new_key;
 }
 
+// an add into T (sparse) or a dense table without the counter updates: new
+// keys | new pairs << 32 (t_flush adds them up)
+__device__ __forceinline__ uint64_t t_add_q(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
+    if (p.pkeys) return sparse_add_q(p, key, lang, c);
+    return add_count_q(p, key, lang, c) ? 1ull : 0ull;
+}
+
+// a thread's t_add_q results into the table's counters (every lane of the wave calls it)
+__device__ __forceinline__ void t_flush(const CountParams& p, uint64_t n) {
+    flush_new_keys(p.size, (unsigned int)n);
+    if (p.pkeys) flush_new_keys(p.psize, (unsigned int)(n >> 32));
+}
+
 __device__ __forceinline__ void add_count(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
     if (LDGPU_FIT_ABLATE & 2) return;
+    if (p.pkeys) {  // sparse T: one atomic per ballot on each counter
+        const uint64_t r = sparse_add_q(p, key, lang, c);
+        const uint64_t mg = __ballot(r & 1ull), mp = __ballot(r >> 32);
+        const uint32_t lane = threadIdx.x & 63;
+        if (mg && lane == (uint32_t)__builtin_ctzll(mg)) atomicAdd(p.size, (unsigned long long)__popcll(mg));
+        if (mp && lane == (uint32_t)__builtin_ctzll(mp)) atomicAdd(p.psize, (unsigned long long)__popcll(mp));
+        return;
+    }
     bool new_key = false;
     const int64_t s = find_or_insert(p, key, new_key);
     count_new_keys(p, new_key);
@@ -269,6 +341,17 @@ __global__ void counts_add_kernel(const CountParams p, const uint64_t* keys, con
                                   const int32_t* lang_of, const unsigned long long* cnt_of, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (p.pkeys) {  // sparse T: every nonzero (key, language, count) as one add (overflow: the list)
+        if (lang_of) {
+            add_count(p, keys[i], lang_of[i], cnt_of ? cnt_of[i] : 1ull);
+        } else {
+            uint64_t r = 0;
+            for (int l = 0; l < p.L; ++l) r += sparse_add_q(p, keys[i], l, rows[(size_t)i * p.L + l]);
+            if (r & 0xffffffffull) atomicAdd(p.size, (unsigned long long)(r & 0xffffffffull));
+            if (r >> 32) atomicAdd(p.psize, (unsigned long long)(r >> 32));
+        }
+        return;
+    }
     bool new_key = false;
     const int64_t s = find_or_insert(p, keys[i], new_key);
     count_new_keys(p, new_key);
@@ -357,7 +440,172 @@ __global__ __launch_bounds__(kScanThreads) void compact_kernel(const CountParams
     }
 }
 
+// ---- sparse table T (CountParams::pkeys): grow, export
+__global__ void sparse_rehash_kernel(const CountParams from, const CountParams to, uint64_t from_cap, uint64_t* remap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= from_cap) return;
+    const uint64_t key = from.keys[i];
+    if (key == kEmpty) return;
+    uint64_t s = mix64(key) >> to.shift;
+    while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.keys[s]), 0ull, (unsigned long long)key) != 0ull)
+        s = (s + 1) & to.mask;
+    for (int w = 0; w < from.S; ++w) to.masks[s * to.S + w] = from.masks[i * from.S + w];
+    remap[i] = s;
+}
+
+__global__ void pair_rehash_kernel(const CountParams from, const CountParams to, uint64_t from_pcap,
+                                   const uint64_t* remap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= from_pcap) return;
+    uint64_t pk = from.pkeys[i];
+    if (pk == kEmpty) return;
+    if (remap) {
+        const uint64_t g = (pk >> kPairLangBits) - 1ull;
+        pk = ((remap[g] + 1ull) << kPairLangBits) | (pk & ((1ull << kPairLangBits) - 1ull));
+    }
+    uint64_t s = mix64(pk) >> to.pshift;
+    while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.pkeys[s]), 0ull, (unsigned long long)pk) != 0ull)
+        s = (s + 1) & to.pmask;
+    to.pcounts[s] = from.pcounts[i];
+}
+
+__global__ __launch_bounds__(kScanThreads) void gram_compact_kernel(const CountParams p, uint64_t cap,
+                                                                    uint64_t* out_keys, uint64_t* out_slot,
+                                                                    unsigned long long* out_n, int sort_keys) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < cap; c0 += (uint64_t)gridDim.x * kScanThreads) {
+        const uint64_t i = c0 + threadIdx.x;
+        const bool occ = i < cap && p.keys[i] != kEmpty;
+        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
+        if (!occ) continue;
+        out_keys[o] = sort_keys ? sort_key(p.keys[i]) : p.keys[i];
+        out_slot[o] = i;
+    }
+}
+
+__global__ void rank_scatter_kernel(int64_t n, const uint64_t* slot, uint32_t* rank_of) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) rank_of[slot[r]] = (uint32_t)r;
+}
+
+__global__ __launch_bounds__(kScanThreads) void pair_compact_kernel(const CountParams p, uint64_t pcap,
+                                                                    const uint32_t* rank_of, uint64_t* out_pk,
+                                                                    unsigned long long* out_cnt,
+                                                                    unsigned long long* out_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < pcap; c0 += (uint64_t)gridDim.x * kScanThreads) {
+        const uint64_t i = c0 + threadIdx.x;
+        const uint64_t pk = i < pcap ? p.pkeys[i] : kEmpty;
+        const bool occ = pk != kEmpty;
+        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
+        if (!occ) continue;
+        const uint64_t g = (pk >> kPairLangBits) - 1ull;
+        out_pk[o] = ((uint64_t)rank_of[g] << kPairLangBits) | (pk & ((1ull << kPairLangBits) - 1ull));
+        out_cnt[o] = p.pcounts[i];
+    }
+}
+
+__global__ void pair_dense_kernel(const CountParams p, uint64_t pcap, const uint32_t* rank_of,
+                                  unsigned long long* rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= pcap) return;
+    const uint64_t pk = p.pkeys[i];
+    if (pk == kEmpty) return;
+    const uint64_t g = (pk >> kPairLangBits) - 1ull;
+    rows[(uint64_t)rank_of[g] * p.L + (pk & ((1ull << kPairLangBits) - 1ull))] = p.pcounts[i];
+}
+
+__global__ __launch_bounds__(256) void nnz_kernel(const unsigned long long* v, int64_t n, unsigned long long* out) {
+    unsigned long long k = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        k += v[i] != 0ull;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) k += __shfl_xor(k, o);
+    if ((threadIdx.x & 63) == 0 && k) atomicAdd(out, k);
+}
+
 }  // namespace
+
+hipError_t launch_sparse_rehash(const CountParams& from, const CountParams& to, uint64_t from_cap, uint64_t* remap,
+                                hipStream_t stream) {
+    if (from_cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(sparse_rehash_kernel, dim3((unsigned)((from_cap + 255) / 256)), dim3(256), 0, stream, from, to,
+                       from_cap, remap);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_rehash(const CountParams& from, const CountParams& to, uint64_t from_pcap,
+                              const uint64_t* remap, hipStream_t stream) {
+    if (from_pcap == 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_rehash_kernel, dim3((unsigned)((from_pcap + 255) / 256)), dim3(256), 0, stream, from, to,
+                       from_pcap, remap);
+    return hipGetLastError();
+}
+
+hipError_t launch_gram_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys, uint64_t* out_slot,
+                               unsigned long long* out_n, bool sort_keys, hipStream_t stream) {
+    hipLaunchKernelGGL(gram_compact_kernel, dim3(scan_grid(cap)), dim3(kScanThreads), 0, stream, p, cap, out_keys,
+                       out_slot, out_n, (int)sort_keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_rank_scatter(int64_t n, const uint64_t* slot, uint32_t* rank_of, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rank_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, slot, rank_of);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_compact(const CountParams& p, uint64_t pcap, const uint32_t* rank_of, uint64_t* out_pk,
+                               unsigned long long* out_cnt, unsigned long long* out_n, hipStream_t stream) {
+    hipLaunchKernelGGL(pair_compact_kernel, dim3(scan_grid(pcap)), dim3(kScanThreads), 0, stream, p, pcap, rank_of,
+                       out_pk, out_cnt, out_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_dense(const CountParams& p, uint64_t pcap, const uint32_t* rank_of, unsigned long long* rows,
+                             hipStream_t stream) {
+    if (pcap == 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_dense_kernel, dim3((unsigned)((pcap + 255) / 256)), dim3(256), 0, stream, p, pcap, rank_of,
+                       rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_nnz(const unsigned long long* v, int64_t n, unsigned long long* out, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(nnz_kernel, dim3(g), dim3(256), 0, stream, v, n, out);
+    return hipGetLastError();
+}
+
+hipError_t sort_pairs_u64(int64_t n, uint64_t* keys, unsigned long long* vals, int bits, hipStream_t stream) {
+    if (n <= 1) return hipSuccess;
+    uint64_t* k2 = nullptr;
+    unsigned long long* v2 = nullptr;
+    void* tmp = nullptr;
+    size_t tb = 0;
+    hipcub::DoubleBuffer<uint64_t> kb(keys, nullptr);
+    hipcub::DoubleBuffer<unsigned long long> vb(vals, nullptr);
+    hipError_t e = hipMalloc((void**)&k2, sizeof(uint64_t) * n);
+    if (e == hipSuccess) e = hipMalloc((void**)&v2, sizeof(unsigned long long) * n);
+    if (e == hipSuccess) {
+        kb = hipcub::DoubleBuffer<uint64_t>(keys, k2);
+        vb = hipcub::DoubleBuffer<unsigned long long>(vals, v2);
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, vb, (int)n, 0, bits, stream);
+    }
+    if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tb, 16));
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kb, vb, (int)n, 0, bits, stream);
+    if (e == hipSuccess && kb.Current() != keys)
+        e = hipMemcpyAsync(keys, kb.Current(), sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess && vb.Current() != vals)
+        e = hipMemcpyAsync(vals, vb.Current(), sizeof(unsigned long long) * n, hipMemcpyDeviceToDevice, stream);
+    const hipError_t s = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = s;
+    for (void* q : {(void*)k2, (void*)v2, tmp})
+        if (q) (void)hipFree(q);
+    return e;
+}
 
 hipError_t launch_count(const CountParams& p, int grid, hipStream_t stream) {
     hipLaunchKernelGGL(count_kernel, dim3(grid), dim3(kCountWaves * 64), 0, stream, p);
@@ -431,13 +679,15 @@ __global__ __launch_bounds__(kScanThreads) void presence_kernel(const CountParam
         const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
         if (!occ) continue;
         const unsigned long long* row = p.counts + i * L;
-        // the row's presence bits, 64 languages a word, 8 counters per batch of
-        // independent loads; then the histogram from the bits (one read of the row)
+        // the row's presence bits, 64 languages a word (sparse T: kept per
+        // gram; dense: 8 counters per batch of independent loads); then the
+        // histogram from the bits
         int k = 0;
         for (int s = 0; s < S; ++s) {
             const int l0 = 64 * s, nl = min(64, L - l0);
             uint64_t w = 0;
-            for (int b0 = 0; b0 < nl; b0 += 8) {
+            if (p.masks) w = p.masks[i * p.S + s];
+            else for (int b0 = 0; b0 < nl; b0 += 8) {
                 unsigned long long v[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[u] = b0 + u < nl ? row[l0 + b0 + u] : 0ull;
@@ -563,8 +813,17 @@ __global__ void owner_scatter_kernel(const CountParams p, uint64_t cap, uint32_t
 // pairs, 16 B each -- (key, lang << 52 | count) -- instead of its dense row of
 // L counters (1.3 pairs per gram against L = 20..200 counters on the fit
 // corpora)
+// (sparse T: cap is the pair table's; one thread per pair)
+__device__ __forceinline__ uint64_t pair_gram(const CountParams& p, uint64_t pk) {
+    return p.keys[(pk >> kPairLangBits) - 1ull];
+}
+
 __global__ void owner_pair_count_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* n_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p.pkeys) {
+        if (i < cap && p.pkeys[i] != kEmpty) atomicAdd(&n_of[owner_of(pair_gram(p, p.pkeys[i]), world)], 1ull);
+        return;
+    }
     if (i >= cap || p.keys[i] == kEmpty) return;
     unsigned long long k = 0;
     for (int l = 0; l < p.L; ++l) k += p.counts[i * p.L + l] != 0ull;
@@ -574,6 +833,14 @@ __global__ void owner_pair_count_kernel(const CountParams p, uint64_t cap, uint3
 __global__ void owner_pair_scatter_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* cursor,
                                           uint64_t* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p.pkeys) {
+        if (i >= cap || p.pkeys[i] == kEmpty) return;
+        const uint64_t pk = p.pkeys[i], key = pair_gram(p, pk);
+        const unsigned long long o = atomicAdd(&cursor[owner_of(key, world)], 1ull);
+        out[2 * o] = key;
+        out[2 * o + 1] = ((pk & ((1ull << kPairLangBits) - 1ull)) << kPairCntBits) | p.pcounts[i];
+        return;
+    }
     if (i >= cap || p.keys[i] == kEmpty) return;
     const uint64_t key = p.keys[i];
     const unsigned long long* row = p.counts + i * p.L;
@@ -1756,7 +2023,8 @@ __global__ __launch_bounds__(256) void derive_level_kernel(const CountParams t1,
                                                            uint64_t s0, uint64_t s1, int lev, uint32_t mt,
                                                            const CountParams to, const WideCountParams tow) {
     const int L = t1.L;
-    unsigned int n_to = 0, n_tow = 0, n_t1 = 0, n_t1w = 0;
+    uint64_t n_to = 0;
+    unsigned int n_tow = 0, n_t1 = 0, n_t1w = 0;
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
          s += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t lo, hi = 0;
@@ -1778,7 +2046,7 @@ __global__ __launch_bounds__(256) void derive_level_kernel(const CountParams t1,
             const unsigned long long c = row[l];
             if (!c) continue;
             if (mt) {
-                if (lev <= kMaxGram) n_to += add_count_q(to, lo | ((uint64_t)lev << 56), l, c * mt);
+                if (lev <= kMaxGram) n_to += t_add_q(to, lo | ((uint64_t)lev << 56), l, c * mt);
                 else n_tow += wide_add_q(tow, lo, hi | ((uint64_t)lev << 56), l, c * mt);
             }
             if (n >= 1) {
@@ -1787,7 +2055,7 @@ __global__ __launch_bounds__(256) void derive_level_kernel(const CountParams t1,
             }
         }
     }
-    flush_new_keys(to.size, n_to);
+    t_flush(to, n_to);
     flush_new_keys(t1.size, n_t1);
     if (tow.size) flush_new_keys(tow.size, n_tow);
     if (t1w.size) flush_new_keys(t1w.size, n_t1w);
@@ -1803,7 +2071,8 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
                                                                  uint64_t s1, int lev, uint32_t mt,
                                                                  const CountParams to, int ablate) {
     const uint64_t lmask = (1ull << lb) - 1ull;
-    unsigned int n_to = 0, n_t1 = 0;
+    uint64_t n_to = 0;
+    unsigned int n_t1 = 0;
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t key = t1.keys[s];
@@ -1814,14 +2083,14 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
         const unsigned long long c = t1.counts[s];
         const int lang = (int)(kl & lmask);
         const uint64_t bytes = (kl >> lb) ^ (1ull << (8 * klen));
-        if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += add_count_q(to, bytes | ((uint64_t)klen << 56), lang, c * mt);
+        if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += t_add_q(to, bytes | ((uint64_t)klen << 56), lang, c * mt);
         const int n = lev - 1;
         if (n >= 1 && !(LDGPU_DIAG && (ablate & 2))) {
             const uint64_t sent = (1ull << (8 * n)) | (bytes & byte_mask(n));
             n_t1 += add_count_q(t1, ((sent << lb) | (uint64_t)lang) | kDerived, 0, c);
         }
     }
-    flush_new_keys(to.size, n_to);
+    t_flush(to, n_to);
     flush_new_keys(t1.size, n_t1);
 }
 
@@ -1830,7 +2099,8 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
 __global__ __launch_bounds__(256) void derive_pairs2_level_kernel(const WideCountParams t1w, uint64_t s0, uint64_t s1,
                                                                   int lev, uint32_t mt, const CountParams to,
                                                                   int ablate) {
-    unsigned int n_to = 0, n_t1 = 0;
+    uint64_t n_to = 0;
+    unsigned int n_t1 = 0;
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t hi = t1w.khi[s];
@@ -1840,13 +2110,13 @@ __global__ __launch_bounds__(256) void derive_pairs2_level_kernel(const WideCoun
         if (klen != lev) continue;
         const unsigned long long c = t1w.counts[s];
         const int lang = (int)((hi & ~kDerived) - 1ull);
-        if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += add_count_q(to, key, lang, c * mt);
+        if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += t_add_q(to, key, lang, c * mt);
         const int n = lev - 1;
         if (n >= 1 && !(LDGPU_DIAG && (ablate & 2)))
             n_t1 += wide_add_q(t1w, (key & byte_mask(n)) | ((uint64_t)n << 56), ((uint64_t)lang + 1ull) | kDerived, 0,
                                c);
     }
-    flush_new_keys(to.size, n_to);
+    t_flush(to, n_to);
     flush_new_keys(t1w.size, n_t1);
 }
 

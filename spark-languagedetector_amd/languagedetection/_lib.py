@@ -59,10 +59,12 @@ SIGNATURES = [
     ("ldgpu_model_destroy", ctypes.c_int, [_p]),
     ("ldgpu_model_info", ctypes.c_int, [_p, _pi32, _pi64, _pi64, _pi64, _pi64]),
     ("ldgpu_model_layout", ctypes.c_int, [_p, _pi32]),
+    ("ldgpu_model_langs", ctypes.c_int, [_p, _pi32]),
     ("ldgpu_score", ctypes.c_int, [_p, _p, _p, _i64, _p, _p]),
     ("ldgpu_score_device", ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _p, _p]),
     ("ldgpu_counts_create", ctypes.c_int, [_p, _i32, _p, _i32, _i64, _pp]),
     ("ldgpu_counts_destroy", ctypes.c_int, [_p]),
+    ("ldgpu_counts_langs", ctypes.c_int, [_p, _pi32]),
     ("ldgpu_count", ctypes.c_int, [_p, _p, _p, _p, _i64]),
     ("ldgpu_count_device", ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p]),
     ("ldgpu_counts_size", ctypes.c_int, [_p, _pi64, _pi64]),
@@ -80,6 +82,7 @@ SIGNATURES = [
     ("ldgpu_comm_destroy", ctypes.c_int, [_p]),
     ("ldgpu_counts_merge", ctypes.c_int, [_p, _p]),
     ("ldgpu_fit_table_size", ctypes.c_int, [_p, _i32, _pi64, _pi64]),
+    ("ldgpu_fit_table_info", ctypes.c_int, [_p, _pi64, _pi64]),
     ("ldgpu_fit_table_export", ctypes.c_int, [_p, _p, _p, _p]),
     ("ldgpu_fit_table_export_masks", ctypes.c_int, [_p, _p, _p, _p, _p]),
 ]
