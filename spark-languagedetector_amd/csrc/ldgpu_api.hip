@@ -801,11 +801,19 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     std::vector<Slot> slots;
     std::vector<Bucket> buckets;
     // count mode with a table beyond the caches (> 2^20 keys: 32 MiB of slots):
-    // 2-choice buckets of 4 slots (Bucket, ldgpu_common.h) at load 0.4-0.75,
-    // so most lookups read ONE HBM line instead of two slots; cache-resident
-    // tables keep the two independent slot loads (one dependent step less)
-    // (such a table's bloom never fits LDS: the keyed kernels, which alone read buckets)
+    // 2-choice buckets of 5 slots (Bucket, ldgpu_common.h: one 64-B line) at
+    // about 0.85 load, so most lookups read ONE HBM line instead of two slots;
+    // cache-resident tables keep the two independent slot loads (one dependent
+    // step less) (such a table's bloom never fits LDS: the keyed kernels, which
+    // alone read buckets)
     const bool use_buckets = m->mode == 3 && nn > (1 << 20);
+    if (use_buckets && (uint64_t)nk >= (uint64_t)kPayLang) {
+        // a bucket payload holds a multi-language row's index below kPayLang
+        // (bit 30 marks a one-language payload, bit 31 a bad row)
+        delete m;
+        return fail(LDGPU_EUNSUPPORTED, "key table: %lld one-word keys, bucket payloads hold row indices < 2^30",
+                    (long long)nk);
+    }
     if (use_buckets) {
         // ~0.85 load (any bucket count); a placement that does not settle
         // retries with 10 % more buckets

@@ -6,9 +6,10 @@ kernels run on gfx950 through libldgpu.so (include/ldgpu.h).
 """
 from .api import (FitValidationError, LanguageDetector, LanguageDetectorModel, LanguageDetectorModelReader,
                   LanguageDetectorModelWriter, NullPointerException, save_grams)
+from .language import Language
 from .preprocessing import LowerCasePreprocessor, PatternSyntaxException, SpecialCharPreprocessor
 from .runtime import DeviceCounts, DeviceModel
 
 __all__ = ["LanguageDetector", "LanguageDetectorModel", "LanguageDetectorModelReader", "LanguageDetectorModelWriter",
            "FitValidationError", "NullPointerException", "DeviceCounts", "DeviceModel", "save_grams",
-           "LowerCasePreprocessor", "SpecialCharPreprocessor", "PatternSyntaxException"]
+           "LowerCasePreprocessor", "SpecialCharPreprocessor", "PatternSyntaxException", "Language"]

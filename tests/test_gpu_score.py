@@ -323,6 +323,41 @@ def test_long_documents_and_hot_keys():
     check_parity(table, L, [1, 3, 2, 1], data, off)
 
 
+@pytest.mark.parametrize("form", ["mask", "dense", "uniform"])
+def test_fast_path_queue_flush_mid_document(form, uniform_path):
+    """Documents of max(G)..256 bytes (the single-superblock fast path) whose
+    windows nearly all hit -- every 1-byte gram and most 2-/3-byte grams of a
+    small alphabet are keys, gram lengths ordered with a duplicate -- so the
+    per-wave candidate queue fills before the next gram length: the kernel
+    verifies and replays it in order mid-document.  Labels and the bits of the
+    fp64 scores equal the oracle's, on the ordered (replay) and count paths."""
+    rng = np.random.default_rng({"mask": 41, "dense": 42, "uniform": 43}[form])
+    L = 7
+    alphabet = np.frombuffer(b"abcde", dtype=np.uint8)
+    keys = [bytes([c]) for c in range(256)]
+    keys += [bytes([a, b]) for a in b"abcde" for b in b"abcde"]
+    keys += [bytes(rng.choice(alphabet, size=3)) for _ in range(100)]
+    table = {}
+    for k in keys:
+        if form == "dense":
+            table[k] = rng.normal(size=L).tolist()
+        else:
+            m = rng.random(L) < 0.4
+            m[int(rng.integers(0, L))] = True
+            v = 0.25 if form == "uniform" else math.log(1.0 + 1.0 / int(m.sum()))
+            table[k] = [v if b else 0.0 for b in m]
+    lens = rng.integers(150, 257, size=3000)
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, [1, 3, 2, 1], data, off, variant=uniform_path[1])
+    if form == "dense":
+        assert m.info()["mode"] == 1
+    elif form == "mask":
+        assert m.info()["mode"] == 0
+    else:
+        assert m.info()["mode"] == uniform_path[0]
+
+
 def test_unaligned_offsets_and_nonzero_start():
     rng = np.random.default_rng(9)
     alphabet = np.frombuffer(b"xyz", dtype=np.uint8)

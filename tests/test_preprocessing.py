@@ -84,3 +84,17 @@ def test_pipeline_lowercase_then_model_schema():
     df = LowerCasePreprocessor().transform(pd.DataFrame({"fulltext": ["Die"], "lang": ["de"]}))
     m = LanguageDetectorModel({"die": [1.0, 0.0]}, [3], ["de", "en"]).setOutputCol("pred")
     assert m.transformSchema(m._schema_of(df)) == {"lang": "string", "fulltext": "string", "pred": "string"}
+
+
+def test_language_enumeration():
+    """LanguageSpecs.scala:10-13: Language.withName("de").toString == "de";
+    ids are positions in isoLanguageCodes (Language.scala:13-200)."""
+    from languagedetection import Language
+    de = Language.withName("de")
+    assert str(de) == "de"
+    assert Language.isoLanguageCodes[de.id] == "de"
+    assert Language.maxId == len(Language.isoLanguageCodes) == 182
+    assert len(set(Language.isoLanguageCodes)) == 182
+    assert Language(0).name == "ab" and str(Language(181)) == "zu"
+    with pytest.raises(KeyError, match="No value found for 'xx'"):
+        Language.withName("xx")
