@@ -52,10 +52,13 @@ enum ldgpu_status {
 /* Device-path limits.  Gram lengths 1..LDGPU_MAX_GRAM for SCORE tables and
  * LDGPU_MAX_FIT_GRAM for FIT counting: keys of up to 7 bytes pack into one
  * u64 (7 payload bytes + a length byte); keys of 8..15 bytes take two words,
- * in a table of their own (SCORE and FIT alike).  1..LDGPU_MAX_LANGS
+ * in a table of their own (SCORE and FIT alike); a SCORE table with a gram
+ * length beyond 15 keeps every key in a general table (hash + key bytes
+ * compared on the device: any length, as the reference), and FIT counts grams
+ * of more than 15 bytes in a table of such keys (up to 2^24 - 1 bytes).  1..LDGPU_MAX_LANGS
  * languages (SCORE scores more than 256 in blocks of 256 languages). */
-#define LDGPU_MAX_GRAM 15      /* SCORE tables: keys of 8..15 bytes take two words */
-#define LDGPU_MAX_FIT_GRAM 15  /* FIT counting: keys of 8..15 bytes in a two-word table */
+#define LDGPU_MAX_GRAM 2147483647  /* SCORE tables: any gram length */
+#define LDGPU_MAX_FIT_GRAM 16777215  /* FIT counting: lengths beyond 15 in a general-key table */
 #define LDGPU_MAX_LANGS 4096
 #define LDGPU_MAX_GRAM_LENGTHS 32
 
@@ -122,6 +125,7 @@ int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
 #define LDGPU_LAYOUT_DIRECT             0x20
 #define LDGPU_LAYOUT_PACKS              0x40
 #define LDGPU_LAYOUT_LANG_BLOCKS        0x80
+#define LDGPU_LAYOUT_GENERAL_KEYS       0x100  /* keys of any length (a gram length > 15) */
 int ldgpu_model_layout(const ldgpu_model* model, int32_t* flags);
 /* The model's language count (a caller sizing score buffers, e.g. the JNI
  * shim, takes it from the model rather than trusting its own). */

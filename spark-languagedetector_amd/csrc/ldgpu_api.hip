@@ -406,6 +406,13 @@ struct ldgpu_model {
     bool pack_ok = false;           // mode 3: short documents may be scored in packs (score_pack)
     int32_t* d_err = nullptr;
     unsigned long long* d_stats = nullptr;  // LDGPU_STATS diagnostics (printed at destroy)
+    // general keys (a gram length beyond kMaxWideGram: ldgpu_general.hip):
+    // every key in one GenSlot table, its bytes in the arena
+    bool general = false;
+    GenSlot* d_gslots = nullptr;
+    uint64_t gslot_cap = 0;
+    uint8_t* d_arena = nullptr;
+    int64_t* d_koff = nullptr;
     // L > kBlockLangs: one sub-model per block of kBlockLangs languages
     // (model_build_blocked); this model then holds no table of its own
     std::vector<ldgpu_model*> blocks;
@@ -426,7 +433,7 @@ void model_free(ldgpu_model* m) {
         (void)hipFree(m->d_stats);
     }
     for (void* p : {(void*)m->d_slots, (void*)m->d_wslots, (void*)m->d_buckets, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
-                    (void*)m->d_fold, (void*)m->d_err})
+                    (void*)m->d_fold, (void*)m->d_err, (void*)m->d_gslots, (void*)m->d_arena, (void*)m->d_koff})
         if (p) (void)hipFree(p);
     delete m;
 }
@@ -464,7 +471,7 @@ int check_model_args(ldgpu_ctx* ctx, ldgpu_model** out, int64_t n_rows, int32_t 
         return fail(LDGPU_EUNSUPPORTED, "%d languages exceed the device path's limit of %d", n_langs,
                     LDGPU_MAX_LANGS);
     if (n_rows < 0) return fail(LDGPU_EINVAL, "n_rows < 0");
-    return check_grams(gram_lengths, n_grams, kMaxWideGram);  // SCORE tables: two-word keys up to 15 bytes
+    return check_grams(gram_lengths, n_grams, LDGPU_MAX_GRAM);  // SCORE: any length (beyond 15: general keys)
 }
 
 // unique keys -> source row index (later duplicates win); wide keys (8..15
@@ -580,12 +587,144 @@ bool bucket_place(const std::vector<uint64_t>& keys, const std::vector<uint64_t>
 }
 }  // namespace
 
+namespace {
+// A model with a gram length beyond kMaxWideGram (ldgpu_general.hip): every
+// key of 1..max(G) bytes (longer keys can never be hit) in one GenSlot table
+// with its bytes in an arena; Scala toMap semantics (a later duplicate key
+// wins).  Rows in mask form (masks [rows][S], vals) or dense (rows [rows][L]);
+// row_ok (nullable) marks wrong-length rows.  src_row: row i of the table is
+// source row src_row[i] of the caller's arrays.
+int model_create_general(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes, const int64_t* key_offsets,
+                         const double* rows, const uint8_t* row_ok, const uint64_t* masks, const double* vals,
+                         int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams, ldgpu_model** out) {
+    const int maxg = max_gram(gram_lengths, n_grams);
+    const int S = (n_langs + 63) / 64;
+    std::unordered_map<std::string, int64_t> idx;
+    idx.reserve((size_t)n_rows * 2 + 1);
+    std::vector<int64_t> src;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t len = key_offsets[r + 1] - key_offsets[r];
+        if (len < 0) return fail(LDGPU_EINVAL, "key_offsets decrease at row %lld", (long long)r);
+        if (len == 0 || len > maxg) continue;
+        std::string k((const char*)key_bytes + key_offsets[r], (size_t)len);
+        auto it = idx.find(k);
+        if (it == idx.end()) {
+            idx.emplace(std::move(k), (int64_t)src.size());
+            src.push_back(r);
+        } else {
+            src[it->second] = r;
+        }
+    }
+    const int64_t nk = (int64_t)src.size();
+    if (nk >= (int64_t)kBadRow) return fail(LDGPU_EUNSUPPORTED, "%lld keys exceed the general table", (long long)nk);
+    std::vector<uint8_t> arena;
+    std::vector<int64_t> koff(1, 0);
+    for (int64_t i = 0; i < nk; ++i) {
+        const int64_t r = src[i];
+        arena.insert(arena.end(), key_bytes + key_offsets[r], key_bytes + key_offsets[r + 1]);
+        koff.push_back((int64_t)arena.size());
+    }
+    const uint64_t cap = next_pow2(std::max<uint64_t>(16, 2 * (uint64_t)nk + 1));
+    std::vector<GenSlot> slots(cap, GenSlot{0, 0, 0});
+    const uint32_t shift = (uint32_t)(64 - log2u(cap));
+    for (int64_t i = 0; i < nk; ++i) {
+        const int64_t len = koff[i + 1] - koff[i];
+        const uint64_t h = gen_hash(arena.data() + koff[i], len);
+        uint64_t sl = h >> shift;
+        while (slots[sl].len) sl = (sl + 1) & (cap - 1);
+        const bool bad = row_ok && !row_ok[src[i]];
+        slots[sl] = GenSlot{h, (uint32_t)len, (uint32_t)i | (bad ? kBadRow : 0u)};
+    }
+    auto* m = new ldgpu_model();
+    m->ctx = ctx;
+    m->L = n_langs;
+    m->nG = n_grams;
+    for (int i = 0; i < n_grams; ++i) m->G[i] = gram_lengths[i];
+    m->slices = S;
+    m->general = true;
+    m->n_keys = nk;
+    m->gslot_cap = cap;
+    m->slot_cap = cap;
+    for (int64_t i = 0; i < nk; ++i) {
+        const int64_t len = koff[i + 1] - koff[i];
+        if (len < 32) m->len_mask |= 1u << len;
+        m->has_bad |= row_ok && !row_ok[src[i]];
+    }
+    // mask form unless some row has two different nonzero values (as
+    // ldgpu_model_create decides)
+    std::vector<uint64_t> mk;
+    std::vector<double> vv, dr;
+    bool dense = false;
+    if (rows) {
+        for (int64_t i = 0; i < nk && !dense; ++i) {
+            const double* rw = rows + src[i] * (int64_t)n_langs;
+            uint64_t v = 0;
+            bool have = false;
+            for (int l = 0; l < n_langs && !dense; ++l) {
+                if (rw[l] == 0.0) continue;
+                uint64_t b;
+                memcpy(&b, &rw[l], 8);
+                if (!have) {
+                    v = b;
+                    have = true;
+                } else {
+                    dense = b != v;
+                }
+            }
+        }
+    }
+    m->dense = dense;
+    m->mode = dense ? 2 : 0;
+    if (dense) {
+        dr.resize((size_t)nk * n_langs);
+        for (int64_t i = 0; i < nk; ++i)
+            memcpy(&dr[(size_t)i * n_langs], rows + src[i] * (int64_t)n_langs, sizeof(double) * n_langs);
+    } else {
+        mk.assign((size_t)nk * S, 0);
+        vv.assign((size_t)nk, 0.0);
+        for (int64_t i = 0; i < nk; ++i) {
+            if (rows) {
+                const double* rw = rows + src[i] * (int64_t)n_langs;
+                for (int l = 0; l < n_langs; ++l) {
+                    if (rw[l] == 0.0) continue;
+                    mk[(size_t)i * S + l / 64] |= 1ull << (l % 64);
+                    vv[i] = rw[l];
+                }
+            } else {
+                memcpy(&mk[(size_t)i * S], masks + src[i] * S, sizeof(uint64_t) * S);
+                if (n_langs % 64) mk[(size_t)i * S + S - 1] &= (1ull << (n_langs % 64)) - 1ull;
+                vv[i] = vals[src[i]];
+                if (vv[i] == 0.0)  // the all-zero row
+                    for (int w = 0; w < S; ++w) mk[(size_t)i * S + w] = 0;
+            }
+        }
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = upload(&m->d_gslots, slots, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_arena, arena, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_koff, koff, &m->device_bytes);
+    if (e == hipSuccess && dense) e = upload(&m->d_rows, dr, &m->device_bytes);
+    if (e == hipSuccess && !dense) e = upload(&m->d_masks, mk, &m->device_bytes);
+    if (e == hipSuccess && !dense) e = upload(&m->d_vals, vv, &m->device_bytes);
+    if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
+    if (e != hipSuccess) {
+        model_free(m);
+        return fail(LDGPU_ENOMEM, "model upload: %s", hipGetErrorString(e));
+    }
+    *out = m;
+    return ok();
+}
+}  // namespace
+
 extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
                                   const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
                                   int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
                                   ldgpu_model** out) {
     if (int rc = check_model_args(ctx, out, n_rows, n_langs, gram_lengths, n_grams)) return rc;
     if (n_rows > 0 && (!key_bytes || !key_offsets || !rows)) return fail(LDGPU_EINVAL, "table pointer is NULL");
+    if (max_gram(gram_lengths, n_grams) > kMaxWideGram)
+        return model_create_general(ctx, n_rows, key_bytes, key_offsets, rows, row_ok, nullptr, nullptr, n_langs,
+                                    gram_lengths, n_grams, out);
     ParsedTable t;
     std::vector<int64_t> src_row;
     if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row,
@@ -640,6 +779,9 @@ extern "C" int ldgpu_model_create_masks(ldgpu_ctx* ctx, int64_t n_rows, const ui
     if (int rc = check_model_args(ctx, out, n_rows, n_langs, gram_lengths, n_grams)) return rc;
     if (n_rows > 0 && (!key_bytes || !key_offsets || !masks || !vals))
         return fail(LDGPU_EINVAL, "table pointer is NULL");
+    if (max_gram(gram_lengths, n_grams) > kMaxWideGram)
+        return model_create_general(ctx, n_rows, key_bytes, key_offsets, nullptr, nullptr, masks, vals, n_langs,
+                                    gram_lengths, n_grams, out);
     ParsedTable t;
     std::vector<int64_t> src_row;
     if (int rc = unique_keys(n_rows, key_bytes, key_offsets, max_gram(gram_lengths, n_grams), t.keys, src_row,
@@ -1114,6 +1256,7 @@ extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
     if (b->direct_words) f |= LDGPU_LAYOUT_DIRECT;
     if (b->pack_ok) f |= LDGPU_LAYOUT_PACKS;
     if (!m->blocks.empty()) f |= LDGPU_LAYOUT_LANG_BLOCKS;
+    if (m->general) f = LDGPU_LAYOUT_GENERAL_KEYS;
     *flags = f;
     return ok();
 }
@@ -1123,6 +1266,30 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
                  int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st, double* d_best = nullptr,
                  int block = 0, int64_t score_stride = 0) {
     if (n_docs == 0) return LDGPU_OK;
+    if (m->general) {
+        GenScoreParams g{};
+        g.bytes = d_bytes;
+        g.offsets = d_offsets;
+        g.n_docs = n_docs;
+        g.labels = d_labels;
+        g.scores = d_scores;
+        g.slots = m->d_gslots;
+        g.slot_mask = m->gslot_cap - 1;
+        g.slot_shift = (uint32_t)(64 - log2u(m->gslot_cap));
+        g.arena = m->d_arena;
+        g.koff = m->d_koff;
+        g.masks = m->dense ? nullptr : m->d_masks;
+        g.vals = m->d_vals;
+        g.rows = m->d_rows;
+        g.err = d_err;
+        g.L = m->L;
+        g.nG = m->nG;
+        for (int i = 0; i < m->nG; ++i) g.G[i] = m->G[i];
+        const int64_t want = (n_docs + kGenWaves - 1) / kGenWaves;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * 8));
+        HIP_TRY(launch_general_score(g, grid, st));
+        return LDGPU_OK;
+    }
     if (!m->blocks.empty()) {
         // one launch per language block (block labels and maxima in stream-
         // ordered scratch), then the first maximum across blocks
@@ -1440,9 +1607,23 @@ struct ldgpu_counts {
     unsigned long long* d_wcounts = nullptr;
     unsigned long long* d_wsize = nullptr;
     unsigned int* d_wfull = nullptr;
-    // the wide grams (lo, hi) in (length, bytes) order, as of the last
-    // counts_pull: key kWideTag << 56 | r of a pulled key list is wide[r]
-    std::vector<std::pair<uint64_t, uint64_t>> wide_sorted;
+    // grams longer than kMaxWideGram (ldgpu_long.hip): gram slots with a key
+    // arena, presence masks and a pair table, as the sparse T; Gall = the
+    // caller's gram lengths, G (above) its lengths <= 15 (FIT v4), Gl the
+    // longer ones
+    int32_t nGall = 0, Gall[kMaxGramLengths] = {};
+    int32_t nGl = 0, Gl[kMaxGramLengths] = {};
+    uint64_t lcap = 0, lsize = 0, lpcap = 0, lpsize = 0, larena_cap = 0, larena_n = 0;
+    LongSlot* d_lslots = nullptr;
+    uint64_t* d_lmasks = nullptr;
+    uint8_t* d_larena = nullptr;
+    uint64_t* d_lpkeys = nullptr;
+    unsigned long long* d_lpcounts = nullptr;
+    unsigned long long* d_lctr = nullptr;  // [0] grams, [1] pairs, [2] arena bytes, [3] full flag
+    // the grams of 8 or more bytes (wide and long) in (length, bytes) order, as
+    // of the last counts_pull: key kWideTag << 56 | r of a pulled key list is
+    // ext_sorted[r]
+    std::vector<std::string> ext_sorted;
     // cached fit table (ldgpu_fit_table_size -> _export)
     bool tbl_valid = false;
     // sparse host copy of the table for ranged exports (ldgpu_counts_export_sparse),
@@ -1495,18 +1676,22 @@ CountParams count_params(const ldgpu_counts* c) {
 
 // the sparse table's pairs seen as a dense table of one counter per slot
 // (stats_kernel: occupied pairs and the sum of their counts)
-CountParams pair_view(const ldgpu_counts* c) {
+CountParams pair_view_of(uint64_t* pkeys, unsigned long long* pcounts) {
     CountParams p{};
-    p.keys = c->d_pkeys;
-    p.counts = c->d_pcounts;
+    p.keys = pkeys;
+    p.counts = pcounts;
     p.L = 1;
     return p;
 }
 
+CountParams pair_view(const ldgpu_counts* c) { return pair_view_of(c->d_pkeys, c->d_pcounts); }
+
 void counts_free(ldgpu_counts* c) {
     if (!c) return;
     if (c->pend) counts_free(c->pend);
-    for (void* p : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts, (void*)c->d_wsize, (void*)c->d_wfull})
+    for (void* p : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts, (void*)c->d_wsize, (void*)c->d_wfull,
+                    (void*)c->d_lslots, (void*)c->d_lmasks, (void*)c->d_larena, (void*)c->d_lpkeys,
+                    (void*)c->d_lpcounts, (void*)c->d_lctr})
         if (p) (void)hipFree(p);
     if (c->ctx) {
         (void)hipSetDevice(c->ctx->device);
@@ -1888,6 +2073,219 @@ int wide_after(ldgpu_counts* c) {
     return LDGPU_OK;
 }
 
+// ---- grams longer than kMaxWideGram (ldgpu_long.hip)
+LongCountParams long_params(const ldgpu_counts* c) {
+    LongCountParams p{};
+    p.slots = c->d_lslots;
+    p.masks = c->d_lmasks;
+    p.S = (c->L + 63) / 64;
+    p.shift = c->lcap ? (uint32_t)(64 - log2u(c->lcap)) : 63u;
+    p.mask = c->lcap ? c->lcap - 1 : 0;
+    p.size = c->d_lctr;
+    p.psize = c->d_lctr ? c->d_lctr + 1 : nullptr;
+    p.arena_n = c->d_lctr ? c->d_lctr + 2 : nullptr;
+    p.full = c->d_lctr ? reinterpret_cast<unsigned int*>(c->d_lctr + 3) : nullptr;
+    p.arena = c->d_larena;
+    p.arena_cap = c->larena_cap;
+    p.pkeys = c->d_lpkeys;
+    p.pcounts = c->d_lpcounts;
+    p.pshift = c->lpcap ? (uint32_t)(64 - log2u(c->lpcap)) : 63u;
+    p.pmask = c->lpcap ? c->lpcap - 1 : 0;
+    p.L = c->L;
+    return p;
+}
+
+// the long table's pairs as a sparse-T pair view (launch_pair_rehash / _compact)
+CountParams long_pair_view(const ldgpu_counts* c, uint64_t* pkeys, unsigned long long* pcounts, uint64_t pcap) {
+    CountParams v{};
+    v.pkeys = pkeys;
+    v.pcounts = pcounts;
+    v.pshift = pcap ? (uint32_t)(64 - log2u(pcap)) : 63u;
+    v.pmask = pcap ? pcap - 1 : 0;
+    v.L = 1;
+    return v;
+}
+
+// room for `grams` more long grams, `pairs` more pairs (load <= 1/2) and
+// `bytes` more arena bytes: allocate, or grow by device rehash (pairs re-keyed
+// through the slot remap) / a copy of the arena
+int long_reserve(ldgpu_counts* c, uint64_t grams, uint64_t pairs, uint64_t bytes) {
+    hipStream_t st = c->ctx->stream;
+    const int S = (c->L + 63) / 64;
+    if (!c->d_lctr) {
+        HIP_TRY(hipMalloc((void**)&c->d_lctr, 4 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(c->d_lctr, 0, 4 * sizeof(unsigned long long), st));
+    }
+    uint64_t* remap = nullptr;
+    if (2 * (c->lsize + grams) > c->lcap) {
+        const uint64_t cap = next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->lsize + grams)));
+        ldgpu_counts t;
+        t.L = c->L;
+        t.lcap = cap;
+        hipError_t e = hipMalloc((void**)&t.d_lslots, cap * sizeof(LongSlot));
+        if (e == hipSuccess) e = hipMalloc((void**)&t.d_lmasks, cap * (size_t)S * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemsetAsync(t.d_lslots, 0, cap * sizeof(LongSlot), st);
+        if (e == hipSuccess) e = hipMemsetAsync(t.d_lmasks, 0, cap * (size_t)S * sizeof(uint64_t), st);
+        if (e == hipSuccess && c->lcap) e = hipMalloc((void**)&remap, c->lcap * sizeof(uint64_t));
+        if (e == hipSuccess && c->lcap) e = launch_long_rehash(long_params(c), long_params(&t), c->lcap, remap, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            for (void* q : {(void*)t.d_lslots, (void*)t.d_lmasks, (void*)remap})
+                if (q) (void)hipFree(q);
+            return fail(LDGPU_ENOMEM, "long gram table of %llu slots: %s", (unsigned long long)cap,
+                        hipGetErrorString(e));
+        }
+        for (void* q : {(void*)c->d_lslots, (void*)c->d_lmasks})
+            if (q) (void)hipFree(q);
+        c->d_lslots = t.d_lslots;
+        c->d_lmasks = t.d_lmasks;
+        c->lcap = cap;
+    }
+    if (remap || 2 * (c->lpsize + pairs) > c->lpcap) {
+        const uint64_t pcap = std::max<uint64_t>(c->lpcap, next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->lpsize + pairs))));
+        uint64_t* nk = nullptr;
+        unsigned long long* nc = nullptr;
+        hipError_t e = hipMalloc((void**)&nk, pcap * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&nc, pcap * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemsetAsync(nk, 0, pcap * sizeof(uint64_t), st);
+        if (e == hipSuccess) e = hipMemsetAsync(nc, 0, pcap * sizeof(unsigned long long), st);
+        if (e == hipSuccess && c->lpcap)
+            e = launch_pair_rehash(long_pair_view(c, c->d_lpkeys, c->d_lpcounts, c->lpcap),
+                                   long_pair_view(c, nk, nc, pcap), c->lpcap, remap, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (remap) (void)hipFree(remap);
+        if (e != hipSuccess) {
+            for (void* q : {(void*)nk, (void*)nc})
+                if (q) (void)hipFree(q);
+            return fail(LDGPU_ENOMEM, "long gram pair table of %llu slots: %s", (unsigned long long)pcap,
+                        hipGetErrorString(e));
+        }
+        for (void* q : {(void*)c->d_lpkeys, (void*)c->d_lpcounts})
+            if (q) (void)hipFree(q);
+        c->d_lpkeys = nk;
+        c->d_lpcounts = nc;
+        c->lpcap = pcap;
+    }
+    if (c->larena_n + bytes > c->larena_cap) {
+        const uint64_t cap = next_pow2(std::max<uint64_t>(1 << 16, 2 * (c->larena_n + bytes)));
+        uint8_t* a = nullptr;
+        hipError_t e = hipMalloc((void**)&a, cap);
+        if (e == hipSuccess && c->larena_n) e = hipMemcpyAsync(a, c->d_larena, c->larena_n, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            if (a) (void)hipFree(a);
+            return fail(LDGPU_ENOMEM, "long gram key arena of %llu bytes: %s", (unsigned long long)cap,
+                        hipGetErrorString(e));
+        }
+        if (c->d_larena) (void)hipFree(c->d_larena);
+        c->d_larena = a;
+        c->larena_cap = cap;
+    }
+    return LDGPU_OK;
+}
+
+// after a long launch: the counters, and no insert left without room
+int long_after(ldgpu_counts* c) {
+    unsigned long long ctr[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(ctr, c->d_lctr, sizeof ctr, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(c->ctx->stream));
+    c->tbl_valid = false;
+    c->sp_valid = false;
+    if ((unsigned int)ctr[3]) return fail(LDGPU_EDEVICE, "long gram table: an insert found no room");
+    c->lsize = ctr[0];
+    c->lpsize = ctr[1];
+    c->larena_n = ctr[2];
+    return LDGPU_OK;
+}
+
+// the long gram lengths (distinct, with their multiplicity in gramLengths)
+DeriveParams long_lengths(const ldgpu_counts* c) {
+    DeriveParams d{};
+    for (int i = 0; i < c->nGl; ++i) {
+        int j = 0;
+        while (j < d.n && d.len[j] != c->Gl[i]) ++j;
+        if (j == d.n) {
+            d.len[d.n] = c->Gl[i];
+            d.mult[d.n++] = 0;
+        }
+        d.mult[j]++;
+    }
+    return d;
+}
+
+// Count the long gram lengths of documents [0, n_docs) (h_off, h_lang: their
+// offsets and languages on the host): launches of at most kLongLaunchWindows
+// windows, the tables sized for each up front.
+constexpr int64_t kLongLaunchWindows = 1ll << 24;
+
+int long_count_launch(ldgpu_counts* c, const uint8_t* d_bytes, const int64_t* d_offsets, const int32_t* d_lang,
+                      int64_t n_docs, const int64_t* h_off, const int32_t* h_lang) {
+    const DeriveParams d = long_lengths(c);
+    if (!d.n) return LDGPU_OK;
+    int64_t d0 = 0;
+    while (d0 < n_docs) {
+        int64_t d1 = d0, win = 0, bytes = 0;
+        while (d1 < n_docs) {
+            const int64_t len = h_off[d1 + 1] - h_off[d1];
+            int64_t w = 0, b = 0;
+            if (h_lang[d1] >= 0 && h_lang[d1] < c->L) {
+                bool part = false;
+                for (int j = 0; j < d.n; ++j) {
+                    if (len >= d.len[j]) {
+                        w += len - d.len[j] + 1;
+                        b += (len - d.len[j] + 1) * (int64_t)d.len[j];
+                    } else {
+                        part = true;
+                    }
+                }
+                if (part && len > kMaxWideGram) {
+                    w += 1;
+                    b += len;
+                }
+            }
+            if (d1 > d0 && win + w > kLongLaunchWindows) break;
+            win += w;
+            bytes += b;
+            ++d1;
+        }
+        if (win) {
+            if (int rc = long_reserve(c, (uint64_t)win, (uint64_t)win, (uint64_t)bytes)) return rc;
+            HIP_TRY(launch_long_count(long_params(c), d_bytes, d_offsets + d0, d_lang + d0, d1 - d0, d, c->ctx->stream));
+            if (int rc = long_after(c)) return rc;
+        }
+        d0 = d1;
+    }
+    return LDGPU_OK;
+}
+
+// add (key, language, count) triples of long keys (their bytes: kb[ko[i] ..
+// ko[i + 1]), host memory) to the long table
+int long_add_triples(ldgpu_counts* c, const std::vector<uint8_t>& kb, const std::vector<int64_t>& ko,
+                     const std::vector<int32_t>& tl, const std::vector<unsigned long long>& tc) {
+    const int64_t n = (int64_t)tl.size();
+    if (!n) return LDGPU_OK;
+    if (int rc = long_reserve(c, (uint64_t)n, (uint64_t)n, (uint64_t)kb.size())) return rc;
+    hipStream_t st = c->ctx->stream;
+    uint8_t* d_kb = nullptr;
+    int64_t* d_ko = nullptr;
+    int32_t* d_l = nullptr;
+    unsigned long long* d_c = nullptr;
+    hipError_t e = hipMalloc((void**)&d_kb, std::max<size_t>(kb.size(), 1));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_ko, sizeof(int64_t) * (n + 1));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_l, sizeof(int32_t) * n);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_c, sizeof(unsigned long long) * n);
+    if (e == hipSuccess && !kb.empty()) e = hipMemcpyAsync(d_kb, kb.data(), kb.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_ko, ko.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_l, tl.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_c, tc.data(), sizeof(unsigned long long) * n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = launch_long_add(long_params(c), d_kb, d_ko, d_l, d_c, n, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    for (void* q : {(void*)d_kb, (void*)d_ko, (void*)d_l, (void*)d_c})
+        if (q) (void)hipFree(q);
+    if (e != hipSuccess) return fail(LDGPU_EDEVICE, "long gram add: %s", hipGetErrorString(e));
+    return long_after(c);
+}
+
 // Count the wide gram lengths of documents [0, n_docs): sub-launches of at
 // most kWideLaunchWindows wide windows, the table grown for each up front;
 // partial windows shorter than 8 bytes go to the one-word table through its
@@ -1946,14 +2344,19 @@ int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int
                ldgpu_counts** out, bool sparse = false);
 
 // distinct gram lengths, ascending, with their multiplicity in gramLengths
+// (every gramLengths entry, long ones included: partial_kernel counts the
+// partial window of a short document once per n above its length)
 DeriveParams derive_params(const ldgpu_counts* c) {
     DeriveParams d{};
-    for (int n = 1; n <= kMaxWideGram; ++n) {
-        uint32_t m = 0;
-        for (int i = 0; i < c->nG; ++i) m += c->G[i] == n;
-        if (!m) continue;
-        d.len[d.n] = n;
-        d.mult[d.n] = m;
+    std::vector<int32_t> lens(c->Gall, c->Gall + c->nGall);
+    std::sort(lens.begin(), lens.end());
+    for (size_t i = 0; i < lens.size(); ++i) {
+        if (d.n && d.len[d.n - 1] == lens[i]) {
+            d.mult[d.n - 1]++;
+            continue;
+        }
+        d.len[d.n] = lens[i];
+        d.mult[d.n] = 1;
         ++d.n;
     }
     return d;
@@ -2095,7 +2498,7 @@ int derive_pending(ldgpu_counts* c) {
 int count_partial(ldgpu_counts* c, const uint8_t* d_bytes, const int64_t* d_offsets, const int32_t* d_lang,
                   int64_t n_docs, const int64_t* h_off, const int32_t* h_lang) {
     int maxg = 0;
-    for (int i = 0; i < c->nG; ++i) maxg = std::max(maxg, c->G[i]);
+    for (int i = 0; i < c->nGall; ++i) maxg = std::max(maxg, c->Gall[i]);
     std::vector<int64_t> docs;
     bool any_wide = false;
     for (int64_t d = 0; d < n_docs; ++d) {
@@ -2141,6 +2544,9 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         c->pend = nullptr;
     }
     if (int rc = count_partial(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
+    // gram lengths beyond 15 bytes: their own table (ldgpu_long.hip)
+    if (int rc = long_count_launch(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
+    if (c->nG == 0) return LDGPU_OK;  // no gram length of <= 15 bytes: no maximal windows
     if (!c->pend) {
         // one- and two-word records: T1 keyed by (window, language) pairs, one
         // counter each (K = 2: in its wide table, key (packed key, lang + 1));
@@ -2524,7 +2930,7 @@ extern "C" int ldgpu_counts_create(ldgpu_ctx* ctx, int32_t n_langs, const int32_
     if (n_langs < 1 || n_langs > LDGPU_MAX_LANGS)
         return fail(n_langs < 1 ? LDGPU_EINVAL : LDGPU_EUNSUPPORTED, "n_langs %d outside [1, %d]", n_langs,
                     LDGPU_MAX_LANGS);
-    if (int rc = check_grams(gram_lengths, n_grams, kMaxWideGram)) return rc;
+    if (int rc = check_grams(gram_lengths, n_grams, LDGPU_MAX_FIT_GRAM)) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = counts_new(ctx, n_langs, gram_lengths, n_grams, capacity_hint, out, true)) return rc;
     return ok();
@@ -2539,9 +2945,16 @@ int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int
     c->L = n_langs;
     c->sparse = sparse;
     c->S = sparse ? (n_langs + 63) / 64 : 0;
-    c->nG = n_grams;
+    // G: the lengths of <= 15 bytes (FIT v4: maximal windows); Gl: longer
+    // ones (ldgpu_long.hip); Gall: all, in the caller's order
+    c->nGall = n_grams;
     for (int i = 0; i < n_grams; ++i) {
-        c->G[i] = gram_lengths[i];
+        c->Gall[i] = gram_lengths[i];
+        if (gram_lengths[i] > kMaxWideGram) {
+            c->Gl[c->nGl++] = gram_lengths[i];
+            continue;
+        }
+        c->G[c->nG++] = gram_lengths[i];
         if (gram_lengths[i] <= kMaxGram)
             c->Gn[c->nGn++] = gram_lengths[i];
         else
@@ -2746,9 +3159,94 @@ uint64_t unsort_key(uint64_t s) {
     return k;
 }
 
+// The grams of 8 or more bytes (the wide table's, 8..15, and the long
+// table's, 16..), unordered, as byte strings with their nonzero (language,
+// count) pairs in language order (gram i: [poff[i], poff[i + 1])).
+struct Ext {
+    std::vector<std::string> keys;
+    std::vector<int64_t> poff{0};
+    std::vector<int32_t> lang;
+    std::vector<int64_t> cnt;
+};
+
+std::string wide_bytes(uint64_t lo, uint64_t hi) {
+    const int len = key_len(hi);
+    std::string k((size_t)len, '\0');
+    for (int j = 0; j < len; ++j) k[j] = (char)(uint8_t)((j < 8 ? lo : hi) >> (8 * (j & 7)));
+    return k;
+}
+
+// the long table on the host: its grams (slot order) and pairs
+int long_export(ldgpu_counts* c, Ext& x, bool with_pairs) {
+    if (!c->lsize) return LDGPU_OK;
+    hipStream_t st = c->ctx->stream;
+    std::vector<LongSlot> slots(c->lcap);
+    std::vector<uint8_t> arena(std::max<uint64_t>(c->larena_n, 1));
+    HIP_TRY(hipMemcpyAsync(slots.data(), c->d_lslots, c->lcap * sizeof(LongSlot), hipMemcpyDeviceToHost, st));
+    if (c->larena_n) HIP_TRY(hipMemcpyAsync(arena.data(), c->d_larena, c->larena_n, hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> pk;
+    std::vector<unsigned long long> pc;
+    if (with_pairs) {
+        pk.resize(c->lpcap);
+        pc.resize(c->lpcap);
+        HIP_TRY(hipMemcpyAsync(pk.data(), c->d_lpkeys, c->lpcap * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(pc.data(), c->d_lpcounts, c->lpcap * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int64_t> idx(c->lcap, -1);
+    const size_t base = x.keys.size();
+    for (uint64_t s = 0; s < c->lcap; ++s) {
+        if (!slots[s].h) continue;
+        const uint64_t off = slots[s].meta >> kLongLenBits, len = slots[s].meta & ((1ull << kLongLenBits) - 1);
+        if (off + len > c->larena_n) return fail(LDGPU_EDEVICE, "long gram table: slot %llu outside the arena",
+                                                 (unsigned long long)s);
+        idx[s] = (int64_t)(x.keys.size() - base);
+        x.keys.emplace_back((const char*)arena.data() + off, (size_t)len);
+    }
+    const size_t ng = x.keys.size() - base;
+    if (ng != c->lsize) return fail(LDGPU_EDEVICE, "long gram table: %zu grams, %llu expected", ng,
+                                    (unsigned long long)c->lsize);
+    std::vector<std::vector<std::pair<int32_t, int64_t>>> per(ng);
+    for (uint64_t i = 0; i < pk.size(); ++i) {
+        if (!pk[i]) continue;
+        const uint64_t g = (pk[i] >> kPairLangBits) - 1;
+        if (g >= c->lcap || idx[g] < 0) return fail(LDGPU_EDEVICE, "long gram table: pair of an empty slot");
+        per[idx[g]].push_back({(int32_t)(pk[i] & ((1ull << kPairLangBits) - 1)), (int64_t)pc[i]});
+    }
+    for (size_t g = 0; g < ng; ++g) {
+        std::sort(per[g].begin(), per[g].end());
+        for (auto& q : per[g]) {
+            x.lang.push_back(q.first);
+            x.cnt.push_back(q.second);
+        }
+        x.poff.push_back((int64_t)x.lang.size());
+    }
+    return LDGPU_OK;
+}
+
+// the wide and long grams (unordered), with their pairs when with_pairs
+int ext_export(ldgpu_counts* c, Ext& x, bool with_pairs) {
+    std::vector<uint64_t> wlo, whi;
+    std::vector<unsigned long long> wc;
+    if (int rc = wide_export(c, wlo, whi, wc)) return rc;
+    const int L = c->L;
+    for (size_t i = 0; i < wlo.size(); ++i) {
+        x.keys.push_back(wide_bytes(wlo[i], whi[i]));
+        if (with_pairs)
+            for (int l = 0; l < L; ++l) {
+                if (!wc[i * L + l]) continue;
+                x.lang.push_back(l);
+                x.cnt.push_back((int64_t)wc[i * L + l]);
+            }
+        x.poff.push_back((int64_t)x.lang.size());
+    }
+    return long_export(c, x, with_pairs);
+}
+
 // The table pulled to the host in (length, bytes) order -- the rows of
 // reduceGrams (LanguageDetector.scala:57-65): every gram (one-word key, or a
-// wide stand-in kWideTag << 56 | rank, c->wide_sorted[rank]) and its nonzero
+// stand-in kWideTag << 56 | rank, c->ext_sorted[rank]) and its nonzero
 // (language, count) pairs in language order (pairs of gram i: [poff[i],
 // poff[i + 1])).  with_pairs = false: the keys only.
 struct Pulled {
@@ -2803,26 +3301,30 @@ int counts_pull(ldgpu_counts* c, Pulled& out, bool with_pairs = true) {
         }
         HIP_TRY(hipStreamSynchronize(st));
     }
-    // the wide grams (8..15 bytes) after them, in (length, bytes) order, as
-    // stand-in keys kWideTag << 56 | rank (c->wide_sorted[rank])
-    std::vector<uint64_t> wlo, whi;
-    std::vector<unsigned long long> wc;
-    if (int rc = wide_export(c, wlo, whi, wc)) return rc;
-    const uint64_t nw = wlo.size();
-    const std::vector<uint64_t> word = wide_order(wlo, whi);
-    c->wide_sorted.resize(nw);
-    out.keys.resize(n + nw);
+    // the grams of 8 or more bytes (wide: 8..15, long: 16..) after them, in
+    // (length, bytes) order, as stand-in keys kWideTag << 56 | rank
+    // (c->ext_sorted[rank])
+    Ext ext;
+    if (int rc = ext_export(c, ext, with_pairs)) return rc;
+    const uint64_t nx = ext.keys.size();
+    std::vector<uint64_t> ord(nx);
+    for (uint64_t i = 0; i < nx; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) {
+        const std::string &x = ext.keys[a], &y = ext.keys[b];
+        return x.size() != y.size() ? x.size() < y.size() : x < y;  // unsigned bytes: char_traits compares as unsigned
+    });
+    c->ext_sorted.resize(nx);
+    out.keys.resize(n + nx);
     for (uint64_t i = 0; i < n; ++i) out.keys[i] = unsort_key(sk[i]);
-    for (uint64_t r = 0; r < nw; ++r) {
-        c->wide_sorted[r] = {wlo[word[r]], whi[word[r]]};
+    for (uint64_t r = 0; r < nx; ++r) {
+        c->ext_sorted[r] = ext.keys[ord[r]];
         out.keys[n + r] = (kWideTag << 56) | r;
     }
     out.poff.clear();
     out.lang.clear();
     out.cnt.clear();
     if (!with_pairs) return LDGPU_OK;
-    const int L = c->L;
-    out.poff.assign(n + nw + 1, 0);
+    out.poff.assign(n + nx + 1, 0);
     out.lang.resize(pk.size());
     out.cnt.resize(pk.size());
     for (size_t j = 0; j < pk.size(); ++j) {
@@ -2834,12 +3336,11 @@ int counts_pull(ldgpu_counts* c, Pulled& out, bool with_pairs = true) {
         out.cnt[j] = (int64_t)pc[j];
     }
     for (uint64_t i = 0; i < n; ++i) out.poff[i + 1] += out.poff[i];
-    for (uint64_t r = 0; r < nw; ++r) {
-        const unsigned long long* row = &wc[(size_t)word[r] * L];
-        for (int l = 0; l < L; ++l) {
-            if (!row[l]) continue;
-            out.lang.push_back(l);
-            out.cnt.push_back((int64_t)row[l]);
+    for (uint64_t r = 0; r < nx; ++r) {
+        const uint64_t i = ord[r];
+        for (int64_t j = ext.poff[i]; j < ext.poff[i + 1]; ++j) {
+            out.lang.push_back(ext.lang[j]);
+            out.cnt.push_back(ext.cnt[j]);
         }
         out.poff[n + r + 1] = (int64_t)out.lang.size();
     }
@@ -2847,7 +3348,7 @@ int counts_pull(ldgpu_counts* c, Pulled& out, bool with_pairs = true) {
 }
 
 // bytes of a pulled key (one-word, or a wide stand-in resolved through
-// c->wide_sorted): returns the length, writes the bytes when out != nullptr
+// c->ext_sorted): returns the length, writes the bytes when out != nullptr
 int gram_bytes(const ldgpu_counts* c, uint64_t k, uint8_t* out) {
     if (key_len(k) < (int)kWideTag) {
         const int len = key_len(k);
@@ -2855,11 +3356,9 @@ int gram_bytes(const ldgpu_counts* c, uint64_t k, uint8_t* out) {
             for (int j = 0; j < len; ++j) out[j] = (uint8_t)(k >> (8 * j));
         return len;
     }
-    const auto& w = c->wide_sorted[k & ((1ull << 56) - 1)];
-    const int len = key_len(w.second);
-    if (out)
-        for (int j = 0; j < len; ++j) out[j] = (uint8_t)((j < 8 ? w.first : w.second) >> (8 * (j & 7)));
-    return len;
+    const std::string& w = c->ext_sorted[k & ((1ull << 56) - 1)];
+    if (out) memcpy(out, w.data(), w.size());
+    return (int)w.size();
 }
 
 void write_keys(const ldgpu_counts* c, const std::vector<uint64_t>& keys, uint8_t* key_bytes, int64_t* key_offsets) {
@@ -2876,7 +3375,7 @@ extern "C" int ldgpu_counts_size(ldgpu_counts* c, int64_t* n_grams, int64_t* key
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    if (n_grams) *n_grams = (int64_t)(c->size + c->wsize);
+    if (n_grams) *n_grams = (int64_t)(c->size + c->wsize + c->lsize);
     if (key_bytes) {
         Pulled t;
         if (int rc = counts_pull(c, t, false)) return rc;
@@ -2897,6 +3396,8 @@ extern "C" int ldgpu_counts_stats(ldgpu_counts* c, int64_t* n_grams, int64_t* n_
     hipError_t e = hipMemsetAsync(d, 0, sizeof h, c->ctx->stream);
     // the sparse table's pairs (one counter each), the wide table's rows
     if (e == hipSuccess) e = launch_stats(pair_view(c), c->pcap, d, c->ctx->stream);
+    if (e == hipSuccess && c->lpcap)  // the long grams' pairs
+        e = launch_stats(pair_view_of(c->d_lpkeys, c->d_lpcounts), c->lpcap, d, c->ctx->stream);
     if (e == hipSuccess && c->wcap) {  // the wide table, through the same kernel (hi != 0: occupied)
         CountParams w{};
         w.keys = c->d_whi;
@@ -2908,7 +3409,7 @@ extern "C" int ldgpu_counts_stats(ldgpu_counts* c, int64_t* n_grams, int64_t* n_
     if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(LDGPU_EDEVICE, "counts_stats: %s", hipGetErrorString(e));
-    if (n_grams) *n_grams = (int64_t)(c->size + c->wsize);
+    if (n_grams) *n_grams = (int64_t)(c->size + c->wsize + c->lsize);
     if (n_pairs) *n_pairs = (int64_t)h[0];
     if (total) *total = (int64_t)h[1];
     return ok();
@@ -3050,10 +3551,13 @@ extern "C" int ldgpu_counts_add_sparse(ldgpu_counts* c, int64_t n, const uint8_t
     if (!key_bytes || !key_offsets || !pair_offsets) return fail(LDGPU_EINVAL, "NULL argument");
     const int64_t np = pair_offsets[n] - pair_offsets[0];
     if (np < 0 || (np && (!pair_langs || !pair_counts))) return fail(LDGPU_EINVAL, "bad pair offsets / NULL pairs");
-    // one-word keys as (key, language, count) triples; wide keys as dense rows
+    // one-word keys as (key, language, count) triples; wide keys as dense
+    // rows; longer keys as triples with their bytes
     std::vector<uint64_t> tk, wlo, whi;
-    std::vector<int32_t> tl;
-    std::vector<unsigned long long> tc, wrows;
+    std::vector<int32_t> tl, ll;
+    std::vector<unsigned long long> tc, wrows, lc;
+    std::vector<uint8_t> lkb;
+    std::vector<int64_t> lko(1, 0);
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = key_offsets[i + 1] - key_offsets[i];
         if (len < 1 || len > LDGPU_MAX_FIT_GRAM)
@@ -3076,6 +3580,15 @@ extern "C" int ldgpu_counts_add_sparse(ldgpu_counts* c, int64_t n, const uint8_t
                 tl.push_back(pair_langs[q]);
                 tc.push_back((unsigned long long)pair_counts[q]);
             }
+        } else if (len > kMaxWideGram) {
+            for (int64_t j = pair_offsets[i]; j < pair_offsets[i + 1]; ++j) {
+                const int64_t q = j - pair_offsets[0];
+                if (!pair_counts[q]) continue;
+                lkb.insert(lkb.end(), kb, kb + len);
+                lko.push_back((int64_t)lkb.size());
+                ll.push_back(pair_langs[q]);
+                lc.push_back((unsigned long long)pair_counts[q]);
+            }
         } else {
             wlo.push_back(wide_lo_host(kb));
             whi.push_back(wide_hi_host(kb, len));
@@ -3091,6 +3604,7 @@ extern "C" int ldgpu_counts_add_sparse(ldgpu_counts* c, int64_t n, const uint8_t
     c->tbl_valid = false;
     c->sp_valid = false;
     if (int rc = add_wide_rows(c, wlo, whi, wrows)) return rc;
+    if (int rc = long_add_triples(c, lkb, lko, ll, lc)) return rc;
     if (int rc = add_triples(c, tk, tl, tc)) return rc;
     return ok();
 }
@@ -3106,8 +3620,10 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     // count) triples; wide keys (8..15 bytes: two words) as dense rows
     const int L = c->L;
     std::vector<uint64_t> tk, wlo, whi;
-    std::vector<int32_t> tl;
-    std::vector<unsigned long long> tc, wrows;
+    std::vector<int32_t> tl, ll;
+    std::vector<unsigned long long> tc, wrows, lc;
+    std::vector<uint8_t> lkb;
+    std::vector<int64_t> lko(1, 0);
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = key_offsets[i + 1] - key_offsets[i];
         if (len < 1 || len > LDGPU_MAX_FIT_GRAM)
@@ -3125,6 +3641,14 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
                 tl.push_back(l);
                 tc.push_back((unsigned long long)row[l]);
             }
+        } else if (len > kMaxWideGram) {
+            for (int l = 0; l < L; ++l) {
+                if (!row[l]) continue;
+                lkb.insert(lkb.end(), kb, kb + len);
+                lko.push_back((int64_t)lkb.size());
+                ll.push_back(l);
+                lc.push_back((unsigned long long)row[l]);
+            }
         } else {
             wlo.push_back(wide_lo_host(kb));
             whi.push_back(wide_hi_host(kb, len));
@@ -3136,6 +3660,7 @@ extern "C" int ldgpu_counts_add(ldgpu_counts* c, int64_t n, const uint8_t* key_b
     c->tbl_valid = false;
     c->sp_valid = false;
     if (int rc = add_wide_rows(c, wlo, whi, wrows)) return rc;
+    if (int rc = long_add_triples(c, lkb, lko, ll, lc)) return rc;
     if (int rc = add_triples(c, tk, tl, tc)) return rc;
     return ok();
 }
@@ -3145,8 +3670,8 @@ extern "C" int ldgpu_counts_export_device(ldgpu_counts* c, int64_t capacity, uin
     if (!c || !n_out) return fail(LDGPU_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
-    if (c->wsize)
-        return fail(LDGPU_EUNSUPPORTED, "export_device: the table holds grams of 8..15 bytes, which have no packed "
+    if (c->wsize || c->lsize)
+        return fail(LDGPU_EUNSUPPORTED, "export_device: the table holds grams of 8 or more bytes, which have no packed "
                                         "u64 form (use ldgpu_counts_export)");
     *n_out = (int64_t)c->size;
     if ((int64_t)c->size > capacity)
@@ -3508,6 +4033,77 @@ int merge_wide(ldgpu_counts* c, ldgpu_comm* m) {
 }  // namespace
 
 namespace {
+// The merge's long grams (16 bytes or more, their own table): as the wide
+// ones, every rank's (key, language, count) triples reach every rank over the
+// host all-gather and each keeps those it owns (gen_hash of the bytes), summed
+// into a fresh long table.  Raises c->merged_wide on every rank alike when any
+// rank held one (the top-K then runs on the host over every rank's rows).
+int merge_long(ldgpu_counts* c, ldgpu_comm* m) {
+    Ext x;
+    if (int rc = long_export(c, x, true)) return rc;
+    std::vector<uint8_t> blob;
+    const uint64_t nx = x.keys.size();
+    put(blob, &nx, 1);
+    for (uint64_t i = 0; i < nx; ++i) {
+        const uint64_t len = x.keys[i].size(), np = (uint64_t)(x.poff[i + 1] - x.poff[i]);
+        put(blob, &len, 1);
+        put(blob, (const uint8_t*)x.keys[i].data(), len);
+        put(blob, &np, 1);
+        put(blob, x.lang.data() + x.poff[i], np);
+        put(blob, x.cnt.data() + x.poff[i], np);
+    }
+    std::vector<std::vector<uint8_t>> all;
+    if (int rc = comm_allgatherv_host(m, blob, all)) return rc;
+    std::vector<uint8_t> kb;
+    std::vector<int64_t> ko(1, 0);
+    std::vector<int32_t> tl;
+    std::vector<unsigned long long> tc;
+    bool any = false;
+    for (int r = 0; r < m->world; ++r) {
+        const uint8_t* q = all[r].data();
+        uint64_t cnt;
+        memcpy(&cnt, q, 8);
+        q += 8;
+        any |= cnt > 0;
+        for (uint64_t i = 0; i < cnt; ++i) {
+            uint64_t len, np;
+            memcpy(&len, q, 8);
+            const uint8_t* key = q + 8;
+            q += 8 + len;
+            memcpy(&np, q, 8);
+            q += 8;
+            const int32_t* ls = reinterpret_cast<const int32_t*>(q);
+            std::vector<int64_t> cs(np);
+            memcpy(cs.data(), q + 4 * np, 8 * np);
+            q += 12 * np;
+            const uint64_t h = gen_hash(key, (int64_t)len);
+            if ((uint32_t)(((h & 0xffffffffull) * (uint64_t)m->world) >> 32) != (uint32_t)m->rank) continue;
+            for (uint64_t j = 0; j < np; ++j) {
+                kb.insert(kb.end(), key, key + len);
+                ko.push_back((int64_t)kb.size());
+                int32_t l;
+                memcpy(&l, ls + j, 4);
+                tl.push_back(l);
+                tc.push_back((unsigned long long)cs[j]);
+            }
+        }
+    }
+    c->merged_wide = c->merged_wide || any;
+    // this rank's long table, rebuilt from the owned triples
+    for (void* q : {(void*)c->d_lslots, (void*)c->d_lmasks, (void*)c->d_larena, (void*)c->d_lpkeys,
+                    (void*)c->d_lpcounts})
+        if (q) (void)hipFree(q);
+    c->d_lslots = nullptr;
+    c->d_lmasks = nullptr;
+    c->d_larena = nullptr;
+    c->d_lpkeys = nullptr;
+    c->d_lpcounts = nullptr;
+    c->lcap = c->lpcap = c->larena_cap = 0;
+    c->lsize = c->lpsize = c->larena_n = 0;
+    if (c->d_lctr) HIP_TRY(hipMemsetAsync(c->d_lctr, 0, 4 * sizeof(unsigned long long), c->ctx->stream));
+    return long_add_triples(c, kb, ko, tl, tc);
+}
+
 // Every rank's status before a collective phase: a failure that one rank
 // alone meets (an allocation, a count check) ends the merge on EVERY rank
 // instead of leaving the others waiting in the next exchange.  Returns the
@@ -3610,6 +4206,7 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     };
     if (int rc = comm_agree(m, rebuild())) return rc;
     if (int rc = comm_agree(m, merge_wide(c, m))) return rc;
+    if (int rc = comm_agree(m, merge_long(c, m))) return rc;
     c->comm = m;
     c->tbl_valid = false;
     c->sp_valid = false;
@@ -3708,34 +4305,50 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
             keys[j] = rk[order[j].second.first][order[j].second.second];
             memcpy(&masks[j * S], rm[order[j].second.first] + order[j].second.second * S, 8 * S);
         }
-        if (c->merged_wide) {  // every rank's wide grams after them, in (length, bytes) order
-            std::vector<uint64_t> wlo, whi;
-            std::vector<unsigned long long> wc;
-            if (int rc = wide_export(c, wlo, whi, wc)) return rc;
-            std::vector<uint64_t> wm(wlo.size() * S, 0);
-            for (size_t i = 0; i < wlo.size(); ++i)
-                for (int l = 0; l < L; ++l)
-                    if (wc[i * L + l]) wm[i * S + l / 64] |= 1ull << (l % 64);
+        if (c->merged_wide) {  // every rank's grams of 8 or more bytes after them, in (length, bytes) order
+            Ext x;
+            if (int rc = ext_export(c, x, true)) return rc;
+            // blob: count, then per gram its length, bytes and S mask words
             std::vector<uint8_t> wblob;
-            put(wblob, wlo.data(), wlo.size());
-            put(wblob, whi.data(), whi.size());
-            put(wblob, wm.data(), wm.size());
+            const uint64_t nx = x.keys.size();
+            put(wblob, &nx, 1);
+            for (uint64_t i = 0; i < nx; ++i) {
+                const uint64_t len = x.keys[i].size();
+                std::vector<uint64_t> m(S, 0);
+                for (int64_t j = x.poff[i]; j < x.poff[i + 1]; ++j)
+                    if (x.cnt[j]) m[x.lang[j] / 64] |= 1ull << (x.lang[j] % 64);
+                put(wblob, &len, 1);
+                put(wblob, (const uint8_t*)x.keys[i].data(), len);
+                put(wblob, m.data(), m.size());
+            }
             std::vector<std::vector<uint8_t>> wall;
             if (int rc = comm_allgatherv_host(cm, wblob, wall)) return rc;
-            std::vector<uint64_t> glo, ghi, gm;
+            std::vector<std::pair<std::string, std::vector<uint64_t>>> g;
             for (int r = 0; r < cm->world; ++r) {
-                const size_t nr = wall[r].size() / (8 * (2 + (size_t)S));
-                const uint64_t* lo = reinterpret_cast<const uint64_t*>(wall[r].data());
-                glo.insert(glo.end(), lo, lo + nr);
-                ghi.insert(ghi.end(), lo + nr, lo + 2 * nr);
-                gm.insert(gm.end(), lo + 2 * nr, lo + 2 * nr + nr * S);
+                const uint8_t* q = wall[r].data();
+                uint64_t cnt;
+                memcpy(&cnt, q, 8);
+                q += 8;
+                for (uint64_t i = 0; i < cnt; ++i) {
+                    uint64_t len;
+                    memcpy(&len, q, 8);
+                    q += 8;
+                    std::string k((const char*)q, (size_t)len);
+                    q += len;
+                    std::vector<uint64_t> m(S);
+                    memcpy(m.data(), q, 8 * (size_t)S);
+                    q += 8 * (size_t)S;
+                    g.emplace_back(std::move(k), std::move(m));
+                }
             }
-            const std::vector<uint64_t> word = wide_order(glo, ghi);
-            c->wide_sorted.resize(word.size());
-            for (size_t r = 0; r < word.size(); ++r) {
-                c->wide_sorted[r] = {glo[word[r]], ghi[word[r]]};
+            std::sort(g.begin(), g.end(), [](const auto& u, const auto& v) {
+                return u.first.size() != v.first.size() ? u.first.size() < v.first.size() : u.first < v.first;
+            });
+            c->ext_sorted.resize(g.size());
+            for (size_t r = 0; r < g.size(); ++r) {
+                c->ext_sorted[r] = g[r].first;
                 keys.push_back((kWideTag << 56) | r);
-                masks.insert(masks.end(), gm.begin() + word[r] * S, gm.begin() + (word[r] + 1) * S);
+                masks.insert(masks.end(), g[r].second.begin(), g[r].second.end());
             }
         }
         *fallback = false;
@@ -3898,7 +4511,7 @@ extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows,
     // must match), even for K <= 0 or an empty shard
     // (tables holding grams of 8..15 bytes take the host top-K over the
     // pulled table, whose keys stay in (length, bytes) order)
-    if (!c->comm && (K <= 0 || c->size == 0 || c->wsize > 0)) {
+    if (!c->comm && (K <= 0 || c->size == 0 || c->wsize > 0 || c->lsize > 0)) {
         if (int rc = fit_table_host(c, K, n_rows, key_bytes)) return rc;
         return ok();
     }

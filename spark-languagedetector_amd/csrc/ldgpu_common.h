@@ -149,6 +149,24 @@ __host__ __device__ __forceinline__ void wide_hash(uint64_t lo, uint64_t hi, uin
 
 __host__ __device__ __forceinline__ int key_len(uint64_t key) { return (int)(key >> 56); }
 
+// General keys (any length; tables with a gram length beyond kMaxWideGram):
+// a 64-bit hash of the key's bytes and length (FNV-1a, then mix64), host and
+// device alike; the key itself is compared byte for byte against the table's
+// key arena on a hash match.
+__host__ __device__ __forceinline__ uint64_t gen_hash(const uint8_t* p, int64_t len) {
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)len;
+    for (int64_t i = 0; i < len; ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return mix64(h);
+}
+
+// Slot of the general key table (open addressing, linear probes): the key's
+// hash, its length (0: empty slot) and its row (kBadRow: wrong length).
+struct alignas(16) GenSlot {
+    uint64_t h;
+    uint32_t len;
+    uint32_t row;
+};
+
 inline uint64_t pack_key_host(const uint8_t* p, int len) {
     uint64_t k = (uint64_t)len << 56;
     for (int i = 0; i < len; ++i) k |= (uint64_t)p[i] << (8 * i);

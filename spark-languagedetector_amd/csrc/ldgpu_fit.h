@@ -237,6 +237,49 @@ hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const in
                           int64_t n_docs, const CountParams& to, const WideCountParams& tow, const DeriveParams& d,
                           hipStream_t stream);
 
+// ---- FIT of gram lengths beyond kMaxWideGram (ldgpu_long.hip): keys of any
+// length in a table of their own -- a slot per gram holds the hash of its
+// bytes and length (gen_hash, ldgpu_common.h) and where its bytes sit in the
+// table's key arena -- with presence masks and a pair table of (gram slot,
+// language) -> count as the sparse T (CountParams).  The host sizes every
+// table and the arena for a launch up front, so an insert always finds room.
+struct alignas(16) LongSlot {
+    uint64_t h;       // gen_hash | 1 (0: empty)
+    uint64_t meta;    // arena offset << 24 | length (0: being written)
+};
+constexpr uint64_t kLongLenBits = 24;  // gram lengths < 2^24
+
+struct LongCountParams {
+    LongSlot* slots;
+    uint64_t* masks;            // [cap][S] presence bits
+    int32_t S;
+    uint32_t shift;             // slot = h >> shift
+    uint64_t mask;              // cap - 1
+    unsigned long long* size;   // distinct grams
+    uint8_t* arena;             // key bytes
+    unsigned long long* arena_n;  // arena bytes used
+    uint64_t arena_cap;
+    uint64_t* pkeys;            // pair table: (slot + 1) << kPairLangBits | lang
+    unsigned long long* pcounts;
+    uint32_t pshift;
+    uint64_t pmask;
+    unsigned long long* psize;
+    unsigned int* full;         // set if an insert found no room (never: the host sizes the tables)
+    int32_t L;
+};
+
+// every window of the long gram lengths d (duplicates: mult) of documents
+// [0, n_docs), and the partial window (the whole text) of each document of
+// 16 <= len < n, counted for its language
+hipError_t launch_long_count(const LongCountParams& p, const uint8_t* bytes, const int64_t* offsets,
+                             const int32_t* doc_lang, int64_t n_docs, const DeriveParams& d, hipStream_t stream);
+// add n (key, language, count) triples: key i = kbytes[koff[i] .. koff[i + 1])
+hipError_t launch_long_add(const LongCountParams& p, const uint8_t* kbytes, const int64_t* koff, const int32_t* lang,
+                           const unsigned long long* cnt, int64_t n, hipStream_t stream);
+// grow: slots (and masks) of `from` into `to`, remap[old] = new slot
+hipError_t launch_long_rehash(const LongCountParams& from, const LongCountParams& to, uint64_t from_cap,
+                              uint64_t* remap, hipStream_t stream);
+
 // ---- device probability / top-K (computeProbabilities + filterTopGrams)
 // presence: compact occupied slots into keys[n], masks[n][S] (count > 0 per
 // language) and k[n] (= popcount), and histogram hist[l][k] over (gram, l).

@@ -1,0 +1,131 @@
+// ldgpu_general.hip -- SCORE for tables with keys of any length (gfx950).
+//
+// Semantic target: LanguageDetectorModel.detect(Array[Byte], ...),
+// LanguageDetectorModel.scala:131-156, for models whose gram lengths go beyond
+// the packed one- and two-word keys (1..15 bytes): the reference accepts any n
+// (:139-147).  For n in gramLengths (order, duplicates repeat), for every
+// window of the Scala sliding(n) (0 < len < n: one window, the whole text) in
+// position order, a table hit adds its row to the scores (s[l] = s[l] +
+// row[l], F2J daxpy with a = 1.0); then breeze's argmax (first maximum; a NaN
+// first score keeps index 0).
+//
+// One wave per document.  Lanes take 64 consecutive windows: each hashes its
+// window (gen_hash), probes the key table (linear probes over GenSlot) and, on
+// a hash and length match, compares the window with the key's bytes in the
+// arena.  The hits of the 64 windows are then replayed in position order --
+// the reference's order, so the fp64 sums are bit-identical: lane j adds
+// row[l] for its languages l = j, j + 64, ... into the wave's score vector in
+// LDS.  A mask-form row adds v at its set languages (adding 0.0 elsewhere is
+// exact: a score is never -0.0).  This path favours generality over speed:
+// tables with every gram length <= 15 take the LDS-filtered kernels of
+// ldgpu_score.hip.
+#include "ldgpu_internal.h"
+
+namespace ldgpu {
+namespace {
+
+__device__ __forceinline__ bool key_equal(const uint8_t* a, const uint8_t* b, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// the row of the key window[0 .. klen), or -1
+__device__ __forceinline__ int64_t gen_lookup(const GenScoreParams& p, const uint8_t* w, int64_t klen) {
+    const uint64_t h = gen_hash(w, klen);
+    uint64_t s = h >> p.slot_shift;
+    for (;;) {
+        const GenSlot e = p.slots[s];
+        if (e.len == 0) return -1;
+        if (e.h == h && e.len == (uint32_t)klen) {
+            const uint32_t r = e.row & ~kBadRow;
+            if (key_equal(w, p.arena + p.koff[r], klen)) return (int64_t)e.row;
+        }
+        s = (s + 1) & p.slot_mask;
+    }
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double u = __shfl_xor(v, o);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kGenWaves * 64) void general_score_kernel(const GenScoreParams p) {
+    extern __shared__ double gen_acc[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    double* acc = gen_acc + (size_t)wave * p.L;
+    const int S = (p.L + 63) / 64;
+    const int64_t stride = (int64_t)gridDim.x * kGenWaves;
+    for (int64_t doc = (int64_t)blockIdx.x * kGenWaves + wave; doc < p.n_docs; doc += stride) {
+        for (int l = lane; l < p.L; l += 64) acc[l] = 0.0;
+        const int64_t b = p.offsets[doc];
+        const int64_t len = p.offsets[doc + 1] - b;
+        const uint8_t* d = p.bytes + b;
+        for (int gi = 0; gi < p.nG; ++gi) {
+            const int64_t n = p.G[gi];
+            const int64_t nw = n_windows(len, (int)(n > 0x7fffffff ? 0x7fffffff : n));
+            const int64_t klen = len < n ? len : n;
+            for (int64_t p0 = 0; p0 < nw; p0 += 64) {
+                const int64_t pos = p0 + lane;
+                const int64_t row = pos < nw ? gen_lookup(p, d + pos, klen) : -1;
+                uint64_t hits = __ballot(row >= 0);
+                while (hits) {  // in window order
+                    const int j = __builtin_ctzll(hits);
+                    hits &= hits - 1;
+                    const uint32_t r = (uint32_t)__shfl((int)row, j);
+                    if (r & kBadRow) {
+                        if (lane == 0) atomicOr(p.err, 1);
+                        continue;
+                    }
+                    if (p.masks) {
+                        const double v = p.vals[r];
+                        for (int s = 0; s < S; ++s) {
+                            const int l = s * 64 + lane;
+                            if (l < p.L && ((p.masks[(size_t)r * S + s] >> lane) & 1ull)) acc[l] = acc[l] + v;
+                        }
+                    } else {
+                        const double* rw = p.rows + (size_t)r * p.L;
+                        for (int l = lane; l < p.L; l += 64) acc[l] = acc[l] + rw[l];
+                    }
+                }
+            }
+        }
+        // breeze argmax: the first index of the maximum of the non-NaN scores;
+        // a NaN first score keeps index 0
+        double lv = -__builtin_inf();
+        for (int l = lane; l < p.L; l += 64)
+            if (!__builtin_isnan(acc[l]) && acc[l] > lv) lv = acc[l];
+        const double M = wave_max(lv);
+        int first = 0x7fffffff;
+        for (int l = lane; l < p.L; l += 64)
+            if (acc[l] == M) {
+                first = l;
+                break;
+            }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o));
+        const int label = (__builtin_isnan(acc[0]) || first == 0x7fffffff) ? 0 : first;
+        if (lane == 0) p.labels[doc] = label;
+        if (p.scores)
+            for (int l = lane; l < p.L; l += 64) p.scores[doc * p.L + l] = acc[l];
+    }
+}
+
+}  // namespace
+
+hipError_t launch_general_score(const GenScoreParams& p, int grid, hipStream_t stream) {
+    const size_t lds = sizeof(double) * kGenWaves * p.L;  // <= 64 KiB (L <= 4096)
+    hipError_t e = hipFuncSetAttribute((const void*)&general_score_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(general_score_kernel, dim3(grid), dim3(kGenWaves * 64), sizeof(double) * kGenWaves * p.L,
+                       stream, p);
+    return hipGetLastError();
+}
+
+}  // namespace ldgpu

@@ -127,6 +127,34 @@ inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool p
 // (fma accumulate), 2 = dense fp64 rows, 3 = mask rows sharing one finite
 // value (per-language hit counts); lds_bloom = bloom staged in LDS
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream);
+// General-key scoring (ldgpu_general.hip): models with a gram length beyond
+// kMaxWideGram -- keys of any length in one table (GenSlot), compared byte for
+// byte against the key arena on a hash match.  One wave per document; the
+// reference's loop order (n outer, window position inner), each hit's row
+// added in that order by the lanes (language l: lane l mod 64), the scores in
+// LDS; the breeze argmax.
+struct GenScoreParams {
+    const uint8_t* bytes;
+    const int64_t* offsets;     // [n_docs + 1]
+    int64_t n_docs;
+    int32_t* labels;
+    double* scores;             // nullable [n_docs][L]
+    const GenSlot* slots;
+    uint64_t slot_mask;         // slots - 1 (power of two)
+    uint32_t slot_shift;        // first slot = h >> slot_shift
+    const uint8_t* arena;       // key bytes
+    const int64_t* koff;        // [rows + 1] key offsets into the arena
+    const uint64_t* masks;      // mask form: [rows][S] (null: dense rows)
+    const double* vals;         // mask form: [rows]
+    const double* rows;         // dense form: [rows][L]
+    int32_t* err;               // bit 0: a window hit a wrong-length row
+    int32_t L;
+    int32_t nG;
+    int32_t G[kMaxGramLengths];
+};
+constexpr int kGenWaves = 2;    // waves per workgroup (LDS: 2 x L doubles)
+hipError_t launch_general_score(const GenScoreParams& p, int grid, hipStream_t stream);
+
 // label[i] = the first block maximum over nb language blocks (block b's
 // labels / maxima at lab + b n, best + b n)
 hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out,

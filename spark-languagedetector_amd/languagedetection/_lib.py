@@ -29,12 +29,13 @@ LDGPU_ENOMEM = 3
 LDGPU_EDEVICE = 4
 LDGPU_EUNSUPPORTED = 5
 LDGPU_ENODEV = 6
-MAX_GRAM = 15  # SCORE tables (keys of 8..15 bytes take two words)
-MAX_FIT_GRAM = 15  # FIT counting (grams of 8..15 bytes in a two-word table)
+MAX_GRAM = 2147483647  # SCORE tables: any gram length (beyond 15: the general-key table)
+MAX_FIT_GRAM = 16777215  # FIT counting (grams of 8..15 bytes: two words; longer: the general-key table)
 MAX_LANGS = 4096
 # ldgpu_model_layout flags
 LAYOUT_FLAGS = {"lds_bloom": 0x01, "keyed_bloom": 0x02, "keyed_bloom_lines": 0x04, "buckets": 0x08,
-                "wide_keys": 0x10, "direct": 0x20, "packs": 0x40, "lang_blocks": 0x80}
+                "wide_keys": 0x10, "direct": 0x20, "packs": 0x40, "lang_blocks": 0x80,
+                "general_keys": 0x100}
 
 _p = ctypes.c_void_p
 _pp = ctypes.POINTER(ctypes.c_void_p)

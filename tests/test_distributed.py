@@ -144,14 +144,16 @@ def _check_fit(tmp_path, world, K, grams):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,grams", [(80, [1, 2, 3]), (5000, [2, 3]), (60, [2, 9]), (5000, [1, 8, 12])])
+@pytest.mark.parametrize("K,grams", [(80, [1, 2, 3]), (5000, [2, 3]), (60, [2, 9]), (5000, [1, 8, 12]),
+                                     (60, [2, 17]), (5000, [1, 16, 9])])
 def test_fit_distributed_matches_single_process(tmp_path, K, grams):
     """Two ranks (cuda:0 each), host transport over gloo: the library's owner
     exchange leaves disjoint shards with the oracle's global counts, and the
     distributed top-K gives every rank the oracle's table -- also with K above
     some language's present grams (the zero-valued fill), and with gram
-    lengths 8..15 (wide grams: every rank's entries all-gathered, each rank
-    keeping those it owns; the top-K over every rank's presence rows)."""
+    lengths 8..15 (wide grams) or beyond (long grams): every rank's entries
+    all-gathered, each rank keeping those it owns; the top-K over every rank's
+    presence rows."""
     mp.spawn(_fit_worker, args=(2, free_port(), str(tmp_path), K, grams, "host"), nprocs=2, join=True)
     _check_fit(tmp_path, 2, K, grams)
 

@@ -361,7 +361,8 @@ def _wide_corpus(grams, L, seed):
     return data, off, lang
 
 
-@pytest.mark.parametrize("grams", [[8], [1, 3, 9, 12], [15, 2, 9, 9], [5, 10], [7, 8]])
+@pytest.mark.parametrize("grams", [[8], [1, 3, 9, 12], [15, 2, 9, 9], [5, 10], [7, 8], [16], [3, 20], [31],
+                                   [2, 17, 9, 17]])
 def test_wide_gram_counts_table_and_model(grams):
     """Gram lengths 8..15 (computeGrams, LanguageDetector.scala:32-43, any n):
     windows of 8..15 bytes count in a two-word-key table of their own; the
@@ -415,10 +416,23 @@ def test_wide_gram_counts_add_and_limits():
     extra = np.zeros_like(cnt)
     extra[::2] = cnt[::2]
     assert k2 == keys and np.array_equal(c2, cnt + extra)
-    with pytest.raises(NotImplementedError, match="8..15 bytes"):
+    with pytest.raises(NotImplementedError, match="8 or more bytes"):
         a.export_device()
-    with pytest.raises(NotImplementedError):
-        DeviceCounts(L, [16])
+    # gram lengths beyond 15: the long-key table; its keys take counts_add too
+    c = DeviceCounts(L, [2, 18])
+    c.count(data, off, lang)
+    lk, lc = c.export()
+    okeys, ocnt = OC.count(data, off, lang, L, [2, 18])
+    assert lk == okeys and np.array_equal(lc, ocnt)
+    d = DeviceCounts(L, [1])
+    d.add(lk, lc)
+    d.add(lk[::3], lc[::3])
+    dk, dc = d.export()
+    extra = np.zeros_like(lc)
+    extra[::3] = lc[::3]
+    assert dk == lk and np.array_equal(dc, lc + extra)
+    with pytest.raises(NotImplementedError, match="8 or more bytes"):
+        c.export_device()
 
 
 @pytest.mark.parametrize("grams", [[1, 2, 3], [2, 9]])

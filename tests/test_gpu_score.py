@@ -302,6 +302,53 @@ def test_wide_keys(grams, form):
     assert np.array_equal(labels, ol)
 
 
+@pytest.mark.parametrize("grams", [[16], [3, 20], [31], [1, 40, 2, 40], [17, 5, 9]])
+@pytest.mark.parametrize("form", ["count", "mask", "dense"])
+def test_long_keys_general_table(grams, form):
+    """Gram lengths beyond 15 (the reference accepts any n,
+    LanguageDetectorModel.scala:139-147): every key in the general table (hash
+    + key bytes compared on the device), the reference's window order, labels
+    and fp64 score bits equal to the oracle's; partial windows of documents
+    shorter than n make keys of every length up to n."""
+    rng = np.random.default_rng(sum(grams) * 13 + len(form))
+    alphabet = np.frombuffer(b"ab ", dtype=np.uint8)
+    L = 70 if form == "mask" else 9
+    lens_k = sorted(set(grams) | {max(1, g - 3) for g in grams} | {1, 2})
+    if form == "dense":
+        table = _random_table(rng, L, 600, lens_k, alphabet, False)
+    else:
+        table = _random_table(rng, L, 600, lens_k, alphabet, True, uniform=math.log(2.0) if form == "count" else None)
+    lens = rng.integers(0, 140, size=800)
+    lens[:10] = [0, 1, 7, 8, 15, 16, 17, 31, 40, 300]
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, grams, data, off)
+    assert m.info()["layout"] == ["general_keys"]
+    labels, _ = m.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(labels, ol)
+
+
+def test_long_keys_wrong_length_row_and_masks():
+    """A 20-byte key whose row has the wrong length fails only when hit; a
+    mask-form table of long keys scores as its dense rows."""
+    m = LanguageDetectorModel({"abcdefghijklmnopqrst": [1.0], "xy": [0.0, 1.0]}, [2, 20], ["a", "b"])
+    assert m.predict_indices(["xyxy"])[0].tolist() == [1]
+    with pytest.raises(ValueError, match="requirement failed"):
+        m.predict_indices(["zzabcdefghijklmnopqrstzz"])
+    kb = np.frombuffer(b"0123456789abcdefgh" + b"xy", dtype=np.uint8).copy()
+    ko = np.array([0, 18, 20], np.int64)
+    masks = np.array([[0b10], [0b01]], np.uint64)
+    vals = np.array([0.75, 0.5])
+    dm = DeviceModel.from_masks(kb, ko, masks, vals, 2, [18, 2])
+    docs = [b"0123456789abcdefgh", b"xyxy0123456789abcdefgh", b"zz", b""]
+    data, off = encoding.pack(docs)
+    labels, scores = dm.score(data, off, want_scores=True)
+    table = {b"0123456789abcdefgh": [0.0, 0.75], b"xy": [0.5, 0.0]}
+    ol, os_ = oracle_c(table, 2, [18, 2], data, off)
+    assert np.array_equal(labels, ol) and np.array_equal(bits(scores), bits(os_))
+
+
 def test_wide_keys_wrong_length_row():
     """A wide key whose row has the wrong length fails only when hit."""
     m = LanguageDetectorModel({"abcdefghij": [1.0], "xy": [0.0, 1.0]}, [2, 10], ["a", "b"])
@@ -401,8 +448,7 @@ def test_duplicate_keys_last_wins():
 def test_invalid_arguments():
     with pytest.raises(ValueError, match="both must be positive"):
         DeviceModel({b"a": [1.0]}, 1, [0])
-    with pytest.raises(NotImplementedError):
-        DeviceModel({b"a": [1.0]}, 1, [16])  # SCORE keys: up to 15 bytes
+    assert DeviceModel({b"a": [1.0]}, 1, [16]).info()["layout"] == ["general_keys"]  # any gram length
     m = DeviceModel({b"a": [1.0]}, 1, [1])
     with pytest.raises(ValueError, match="offsets decrease"):
         m.score(np.zeros(8, dtype=np.uint8), np.array([0, 4, 2], dtype=np.int64))
