@@ -13,6 +13,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -381,6 +382,7 @@ struct ldgpu_model {
     int mode = 0;             // kernel mode: 0 mask, 1 mask + finite values, 2 dense, 3 mask + one finite value
     bool lds_filter = true;
     bool kb_lines = false;   // keyed bloom in the line layout (kKbLineBytes)
+    bool kb_chunks = false;  // count mode: keyed bloom in the chunk layout (kb_chunk)
     bool has_bad = false;
     int64_t n_keys = 0;
     uint64_t slot_cap = 0;
@@ -1121,9 +1123,10 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         } else {
             const uint32_t lo = (uint32_t)kw;
             const uint32_t hi = (uint32_t)(kw >> 32) & ((1u << (8 * std::min(3, std::max(0, kl - 4)))) - 1u);
-            if (m->lds_filter) {  // prefix bloom
+            if (m->lds_filter) {  // prefix bloom (LDGPU_BLOOM_BITS bits per key)
                 const uint32_t b = pf_bit(kl, lo, hi);
                 filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (b & 31u);
+                if (LDGPU_BLOOM_BITS == 2) filter[kBloomBase + pf_word(lo, bshift)] |= 1u << (pf_bit2(kl, lo, hi) & 31u);
             } else {  // keyed bloom (kb_hash; keys of >= 4 bytes in their position's line)
                 const uint32_t h = kb_hash(lo, hi, (uint32_t)kl);
                 const bool ln = m->kb_lines && kl >= 4;
@@ -1131,6 +1134,50 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                 filter[kBloomBase + w] |= 1u << ((h >> kb_sbit(kl, m->kb_lines, bshift)) & 31u);
             }
         }
+    }
+
+    // Count mode, keyed bloom that stays L2-resident: the chunk layout
+    // (kb_chunk, ldgpu_common.h) when its false-candidate estimate is at most
+    // 1.5x the word layout's: a position then costs one L2 request for every
+    // key length instead of one per length.  The estimates stand in for text
+    // windows that are not keys: the word layout's, its overall fill (a
+    // window's word is random); the chunk layout's, the mean of (filled bits /
+    // 128)^2 over the chunks of the keys' distinct 3-byte prefixes (a window
+    // whose prefix many keys share is mostly a key itself: weighting chunks
+    // by key count overstates it ~6x on config 4's table).
+    if (!m->lds_filter && !m->kb_lines && m->mode == 3 && bwords >= 4) {
+        const uint64_t chunks = bwords / 4;
+        const uint32_t cshift = 32u - (uint32_t)log2u(chunks);
+        std::vector<uint32_t> cf(bwords, 0u);
+        std::unordered_set<uint32_t> prefixes;
+        for (int64_t i = 0; i < nn + nw; ++i) {
+            const int kl = i < nn ? key_len(keys[i]) : key_len(t.whi[i - nn]);
+            if (kl < 3) continue;
+            const uint64_t kw = i < nn ? keys[i] : t.wlo[i - nn];
+            const uint32_t lo = (uint32_t)kw;
+            const uint32_t hi = (uint32_t)(kw >> 32) & ((1u << (8 * std::min(3, std::max(0, kl - 4)))) - 1u);
+            const uint32_t h = kb_hash(lo, hi, (uint32_t)kl);
+            const uint32_t c = kb_chunk(lo) >> cshift;
+            for (uint32_t q : {h >> 25, (h >> 18) & 127u}) cf[4 * c + (q >> 5)] |= 1u << (q & 31u);
+            prefixes.insert(lo & 0xffffffu);
+        }
+        uint64_t set = 0;
+        for (uint64_t w = 0; w < bwords; ++w) set += __builtin_popcount(filter[kBloomBase + w]);
+        const double ew = (double)set / (32.0 * (double)bwords);
+        double ec = 0.0;
+        for (uint32_t pr : prefixes) {
+            const uint32_t* q = &cf[4 * (kb_chunk(pr) >> cshift)];
+            const double fc = (__builtin_popcount(q[0]) + __builtin_popcount(q[1]) + __builtin_popcount(q[2]) +
+                               __builtin_popcount(q[3])) / 128.0;
+            ec += fc * fc;
+        }
+        ec /= (double)std::max<size_t>(prefixes.size(), 1);
+        m->kb_chunks = ec <= 1.5 * ew;
+#ifdef LDGPU_NO_KB_CHUNKS  // A/B builds (tools/build_variant.sh)
+        m->kb_chunks = false;
+#endif
+        if (const char* kc = diag_env("LDGPU_KB_CHUNKS")) m->kb_chunks = atoi(kc) != 0;  // tests: either layout
+        if (m->kb_chunks) std::copy(cf.begin(), cf.end(), filter.begin() + kBloomBase);
     }
 
     // count mode with every 1-/2-byte key naming ONE language (fit tables of
@@ -1197,7 +1244,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         }
     }
     int resident = 0;
-    if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->lds_bytes, &resident);
+    if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->kb_chunks, m->lds_bytes, &resident);
     // persistent grid = what is resident; never more workgroups than the LDS admits
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
     if (const char* ov = diag_env("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
@@ -1249,7 +1296,8 @@ extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
     const ldgpu_model* b = m->blocks.empty() ? m : m->blocks[0];  // blocks share one layout
     int32_t f = 0;
     if (b->lds_filter) f |= LDGPU_LAYOUT_LDS_BLOOM;
-    if (!b->lds_filter && !b->kb_lines) f |= LDGPU_LAYOUT_KEYED_BLOOM;
+    if (!b->lds_filter && !b->kb_lines && !b->kb_chunks) f |= LDGPU_LAYOUT_KEYED_BLOOM;
+    if (b->kb_chunks) f |= LDGPU_LAYOUT_KEYED_BLOOM_CHUNKS;
     if (b->kb_lines) f |= LDGPU_LAYOUT_KEYED_BLOOM_LINES;
     if (b->d_buckets) f |= LDGPU_LAYOUT_BUCKETS;
     if (b->d_wslots) f |= LDGPU_LAYOUT_WIDE_KEYS;
@@ -1338,6 +1386,8 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.filter = m->d_filter;
     p.bloom_shift = (uint32_t)(32 - m->filter_log2);
     p.kb_lines = m->kb_lines ? 1 : 0;
+    p.kb_chunks = m->kb_chunks ? 1 : 0;
+    if (m->kb_chunks) p.bloom_shift += 2;  // chunk index = kb_chunk >> (32 - log2(words / 4))
     p.bloom_words = (uint32_t)((uint64_t)1 << m->filter_log2);
     p.len_mask = m->len_mask;
     p.masks = m->d_masks;

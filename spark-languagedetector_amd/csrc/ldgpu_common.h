@@ -66,6 +66,22 @@ __host__ __device__ __forceinline__ uint32_t pf_bit(int klen, uint32_t lo, uint3
     return pf_bit_c(lo, hi, pf_shift(klen), pf_mult(klen));
 }
 
+// Bits per key of the prefix Bloom (LDGPU_BLOOM_BITS, 1 or 2).  With two, a
+// key sets a second bit of its word, from a second multiplier over the same
+// three bytes, and a window is a candidate only when both bits are set: at
+// ~2.5 keys per word the false candidates fall ~4x (every false candidate is
+// an L2 verify) for two more VALU ops per test -- the word is already in a
+// register.
+#ifndef LDGPU_BLOOM_BITS
+#define LDGPU_BLOOM_BITS 2
+#endif
+__host__ __device__ __forceinline__ constexpr uint32_t pf_mult2_of(uint32_t m) {
+    return ((m ^ 0xA5A5A5u) * 0x2Fu + 0x1B873Du) & 0xFFFFFFu;
+}
+__host__ __device__ __forceinline__ uint32_t pf_bit2(int klen, uint32_t lo, uint32_t hi) {
+    return pf_bit_c(lo, hi, pf_shift(klen), pf_mult2_of(pf_mult(klen)));
+}
+
 // Keyed bloom (tables whose bloom exceeds LDS): for a key of klen >= 3 bytes
 // (lo / hi = its bytes, masked to klen) word = h >> (32 - wlog), bit =
 // (h >> (27 - wlog)) mod 32 of h = kb_hash -- three 24-bit multiplies over
@@ -103,6 +119,15 @@ __host__ __device__ __forceinline__ uint32_t kb_sbit(uint32_t klen, bool lines, 
 __host__ __device__ __forceinline__ uint32_t kb_line16(uint32_t lo, uint32_t wshift) {
     return (kb_line(lo) >> (wshift + 4)) << 4;
 }
+
+// Keyed bloom, chunk layout (count-mode tables whose keyed bloom stays
+// L2-resident, chosen at build when its false-candidate estimate is no worse):
+// every key of >= 3 bytes sets TWO bits of ONE 16-B chunk chosen by the first
+// three bytes of its window position -- q1 = h >> 25 and q2 = (h >> 18) mod
+// 128 of h = kb_hash(key) -- so a position's tests of every length read one
+// 16-B chunk (one L2 request) instead of a word per length.  chunk =
+// kb_chunk(lo) >> shift (shift = 32 - log2 chunks).
+__host__ __device__ __forceinline__ uint32_t kb_chunk(uint32_t lo) { return kb_line(lo & 0xffffffu); }
 
 // Filter image (host-built, staged whole into LDS): a direct 256-bit bitmap
 // of the 1-byte keys, a direct 65536-bit bitmap of the 2-byte keys, then the

@@ -35,6 +35,7 @@ struct ScoreParams {
     uint32_t bloom_words;       // power of two
     uint32_t bloom_shift;       // bloom word = hash >> bloom_shift (>= 10)
     int32_t kb_lines;           // keyed bloom in the line layout (kb_line16: blooms beyond kKbLineBytes)
+    int32_t kb_chunks;          // count mode: keyed bloom in the chunk layout (kb_chunk; chunk = kb_chunk >> bloom_shift)
     uint32_t len_mask;          // bit k set: the table holds keys of k bytes
     const uint64_t* masks;      // mask mode: [rows][S] language bitmasks
     const double* vals;         // mask mode: [rows] the row's one nonzero value
@@ -160,6 +161,7 @@ hipError_t launch_general_score(const GenScoreParams& p, int grid, hipStream_t s
 hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out,
                                  hipStream_t stream);
 // sets the dynamic-LDS limit and returns the resident workgroups per CU
-hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu);
+// (chunks: a count-mode table's keyed bloom in the chunk layout)
+hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu);
 
 }  // namespace ldgpu

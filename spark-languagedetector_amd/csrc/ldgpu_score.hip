@@ -354,7 +354,7 @@ __device__ __forceinline__ void verify_complete(const ScoreParams& p, const Wave
 // PACK (MODE 3, packed short documents, score_pack): an entry's position is
 // its low 8 bits and bits 8..9 name the document of the pack, whose (u16)
 // counter block it counts into.
-template <int S, int MODE, bool STAGED, bool KEYED, bool PACK = false, bool WIDE = false>
+template <int S, int MODE, bool STAGED, int KEYED, bool PACK = false, bool WIDE = false>
 __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, int qn, const DocSrc& src,
                                       double (&acc)[S], int lane, bool weighted = false, int q_begin = 0) {
     __builtin_amdgcn_wave_barrier();
@@ -590,15 +590,29 @@ __device__ __forceinline__ int count_argmax(const ScoreParams& p, C* cnt, int la
 // would saturate prefix words; gb / gshift locate that bloom.
 struct FWords {
     uint32_t w3[kSub];  // prefix bloom: the position's word; keyed line layout: its line << 4 (kb_line16)
+    u32x4 ck[kSub];     // keyed chunk layout (KEYED == 2): the position's 16-B chunk
     const uint32_t* gb;
     uint32_t gshift;
     bool lines;         // keyed bloom in the line layout (ScoreParams::kb_lines)
 };
 
-template <bool KEYED>
+// Bloom layout of a kernel instantiation (KEYED): 0 = prefix Bloom in LDS,
+// 1 = keyed bloom in global memory (a word per key, or the line layout),
+// 2 = keyed chunk layout (count mode: a 16-B chunk per window position, every
+// length's bits in it, kb_chunk16).  kind_of: the filter_word KIND of keys
+// of >= 3 bytes.
+constexpr int kind_of(int keyed) { return keyed == 2 ? 5 : (keyed ? 4 : 3); }
+
+template <int KEYED>
 __device__ __forceinline__ void load_fwords(const ScoreParams& p, const uint32_t* bloom, const Windows& x,
                                             FWords& f) {
-    if constexpr (KEYED) {
+    if constexpr (KEYED == 2) {
+        // one 16-B load per position: its chunk holds the bits of every key
+        // length starting there
+        const u32x4* c4 = reinterpret_cast<const u32x4*>(bloom);
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) f.ck[k] = c4[kb_chunk(x.lo[k]) >> p.bloom_shift];
+    } else if constexpr (KEYED) {
         f.gb = bloom;
         f.gshift = p.bloom_shift;
         f.lines = p.kb_lines != 0;
@@ -630,19 +644,32 @@ __device__ __forceinline__ uint64_t lanes_below(int32_t n) {  // n in [1, 64]
     return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
 }
 
-// the filter word and bit position of sub-block k's window
+// the filter word and bit positions of sub-block k's window: a candidate has
+// bits bit and bit2 of w set (bit2 = bit except for a two-bit prefix Bloom)
 template <int KIND>
 __device__ __forceinline__ void filter_word(const uint32_t* img, uint32_t sh, uint32_t mul, const FWords& f,
-                                            const Windows& x, int k, uint32_t& w, uint32_t& bit) {
+                                            const Windows& x, int k, uint32_t& w, uint32_t& bit, uint32_t& bit2) {
     if constexpr (KIND == 1) {
         w = img[(x.lo[k] >> 5) & 7u];
-        bit = x.lo[k];
+        bit = bit2 = x.lo[k];
     } else if constexpr (KIND == 2) {
         w = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
-        bit = x.lo[k];
+        bit = bit2 = x.lo[k];
     } else if constexpr (KIND == 3) {
         w = f.w3[k];
-        bit = mulhi24(__builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh), mul);
+        const uint32_t in = __builtin_amdgcn_alignbit(x.hi[k], x.lo[k], sh);
+        bit = mulhi24(in, mul);
+        bit2 = LDGPU_BLOOM_BITS == 2 ? mulhi24(in, pf_mult2_of(mul)) : bit;
+    } else if constexpr (KIND == 5) {  // keyed chunk layout: sh = key length
+        const uint32_t lo = sh >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * sh)) - 1u);
+        const uint32_t hi = sh <= 4 ? 0u : x.hi[k] & ((1u << (8 * (sh < 7 ? sh - 4 : 3))) - 1u);
+        const uint32_t h = kb_hash(lo, hi, sh);
+        const uint32_t q1 = h >> 25, q2 = (h >> 18) & 127u;
+        const u32x4 c = f.ck[k];
+        const uint32_t w1 = q1 < 64 ? (q1 < 32 ? c.x : c.y) : (q1 < 96 ? c.z : c.w);
+        const uint32_t w2 = q2 < 64 ? (q2 < 32 ? c.x : c.y) : (q2 < 96 ? c.z : c.w);
+        w = (w1 >> (q1 & 31u)) & (w2 >> (q2 & 31u));  // bit 0: both bits set
+        bit = bit2 = 0;
     } else {  // KIND 4, keyed bloom: sh = key length, mul = unused
         const uint32_t lo = sh >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * sh)) - 1u);
         // (a wide key hashes its first seven bytes)
@@ -650,21 +677,22 @@ __device__ __forceinline__ void filter_word(const uint32_t* img, uint32_t sh, ui
         const uint32_t h = kb_hash(lo, hi, sh);
         // (f.w3 is 0 outside the line layout)
         w = f.gb[(sh >= 4 ? f.w3[k] : 0u) + (h >> kb_sword(sh, f.lines, f.gshift))];
-        bit = h >> kb_sbit(sh, f.lines, f.gshift);
+        bit = bit2 = h >> kb_sbit(sh, f.lines, f.gshift);
     }
+}
+
+__device__ __forceinline__ bool filter_hit(uint32_t w, uint32_t bit, uint32_t bit2) {
+    return (__builtin_amdgcn_ubfe(w, bit, 1) & __builtin_amdgcn_ubfe(w, bit2, 1)) != 0u;
 }
 
 template <int KIND, int NSB>
 __device__ __forceinline__ void test_len(const uint32_t* img, uint32_t sh, uint32_t mul, const FWords& f,
                                          const Windows& x, int32_t nw, uint64_t (&m)[kSub]) {
-    uint32_t w[NSB], bit[NSB];
+    uint32_t w[NSB], bit[NSB], bit2[NSB];
 #pragma unroll
-    for (int k = 0; k < NSB; ++k) filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
+    for (int k = 0; k < NSB; ++k) filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k], bit2[k]);
 #pragma unroll
-    for (int k = 0; k < NSB; ++k) {
-        const uint32_t c = __builtin_amdgcn_ubfe(w[k], bit[k], 1);
-        m[k] = __builtin_amdgcn_ballot_w64(c != 0u);
-    }
+    for (int k = 0; k < NSB; ++k) m[k] = __builtin_amdgcn_ballot_w64(filter_hit(w[k], bit[k], bit2[k]));
     m[NSB - 1] &= lanes_below(nw - 64 * (NSB - 1));
 #pragma unroll
     for (int k = NSB; k < kSub; ++k) m[k] = 0;
@@ -684,11 +712,11 @@ __device__ __forceinline__ void test_nsb(const uint32_t* img, uint32_t sh, uint3
 }
 
 // FULL: every length has more than 192 windows (NSB = 4, no dispatch)
-template <bool FULL, bool KEYED>
+template <bool FULL, int KEYED>
 __device__ __forceinline__ void test_sb(const uint32_t* img, int klen, const FWords& f, const Windows& x, int32_t nw,
                                         uint64_t (&m)[kSub]) {
     const uint32_t sh = KEYED ? (uint32_t)klen : pf_shift(klen), mul = pf_mult(klen);
-    constexpr int K3 = KEYED ? 4 : 3;
+    constexpr int K3 = kind_of(KEYED);
     if (klen == 1) {
         if (FULL) test_len<1, 4>(img, sh, mul, f, x, nw, m); else test_nsb<1>(img, sh, mul, f, x, nw, m);
     } else if (klen == 2) {
@@ -844,7 +872,7 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 // Count-mode verify of a full queue in the middle of a document's probe
 // (hit-dense tables: config 5's 10M keys); counts are order-free, so the
 // probe just continues.
-template <int S, bool STAGED, bool KEYED, bool WIDE>
+template <int S, bool STAGED, int KEYED, bool WIDE>
 __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds& wl, int qn, const DocSrc& src,
                                             int lane) {
     double acc[S];  // unused in count mode
@@ -880,7 +908,7 @@ __device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x,
 // probe_count_all)
 constexpr int kFmDirect = 16;
 
-template <int N, bool FULL, int S, bool STAGED, bool KEYED, bool WIDE>
+template <int N, bool FULL, int S, bool STAGED, int KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                             const DocSrc& src, uint32_t fm) {
@@ -892,7 +920,7 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
             return;
         }
     }
-    constexpr int KIND = N < 3 ? N : (KEYED ? 4 : 3);
+    constexpr int KIND = N < 3 ? N : kind_of(KEYED);
     constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
     uint64_t m[kSub];
     if constexpr (FULL) {
@@ -907,7 +935,7 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
     append_sb(wl.queue, qn, m, N, 0, lane);
 }
 
-template <bool FULL, int S, bool STAGED, bool KEYED, bool WIDE>
+template <bool FULL, int S, bool STAGED, int KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                                 const DocSrc& src) {
@@ -935,7 +963,7 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {
         const int n = 8 + __builtin_ctz(wm);
         const uint32_t sh = KEYED ? (uint32_t)n : pf_shift(n), mul = pf_mult(n);
-        constexpr int K3 = KEYED ? 4 : 3;
+        constexpr int K3 = kind_of(KEYED);
         uint64_t m[kSub];
         if constexpr (FULL)
             test_len<K3, 4>(img, sh, mul, f, x, len - n + 1, m);
@@ -973,7 +1001,7 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
 // each document's label is its block's count argmax.  Three 64-B documents
 // per wave-pass instead of one: the lanes a lone short document leaves idle
 // do the next documents' windows.
-template <int N, int S, bool KEYED, bool WIDE>
+template <int N, int S, int KEYED, bool WIDE>
 __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
                                            const DocSrc& src, uint32_t dummy_a, uint32_t fm,
@@ -986,21 +1014,21 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
             return;
         }
     }
-    constexpr int KIND = N < 3 ? N : (KEYED ? 4 : 3);
+    constexpr int KIND = N < 3 ? N : kind_of(KEYED);
     constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
     uint64_t m[kSub];
-    uint32_t w[kSub], bit[kSub];
+    uint32_t w[kSub], bit[kSub], bit2[kSub];
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
         if constexpr (KIND == 4 && N - 3 < kPreN) {
             w[k] = kw[N - 3][k];
-            bit[k] = keyed_hash<N>(x, k) >> kb_sbit(N, f.lines, f.gshift);
+            bit[k] = bit2[k] = keyed_hash<N>(x, k) >> kb_sbit(N, f.lines, f.gshift);
         } else {
-            filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k]);
+            filter_word<KIND>(img, sh, mul, f, x, k, w[k], bit[k], bit2[k]);
         }
     }
 #pragma unroll
-    for (int k = 0; k < kSub; ++k) m[k] = __ballot(__builtin_amdgcn_ubfe(w[k], bit[k], 1) != 0u && pk.rem[k] >= N);
+    for (int k = 0; k < kSub; ++k) m[k] = __ballot(filter_hit(w[k], bit[k], bit2[k]) && pk.rem[k] >= N);
     if (qn + count_sb(m) > kQueueCap) {
         double acc[S];  // unused in count mode
         flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
@@ -1012,7 +1040,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
 // One pack: documents [i, i + nd) of the staged group, ends e1 < e2 < e3 <=
 // tot relative to the pack's first byte (unused ends = tot); labels to
 // wl.labels[i ..).
-template <int S, bool KEYED, bool WIDE>
+template <int S, int KEYED, bool WIDE>
 __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                         const uint32_t* bloom, const DocSrc& src, int32_t e1, int32_t e2,
                                         int32_t e3, int32_t tot, int nd, int i, int lane) {
@@ -1035,7 +1063,7 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
     if (ablated(p, 2)) fm = 0;
     const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
     uint32_t kw[kPreN][kSub];
-    if constexpr (KEYED) {
+    if constexpr (KEYED == 1) {
         keyed_preload<3>(f, x, fm, kw);
         keyed_preload<4>(f, x, fm, kw);
         keyed_preload<5>(f, x, fm, kw);
@@ -1049,15 +1077,14 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
     probe_pack<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {  // wide lengths 8..15
         const int n = 8 + __builtin_ctz(wm);
-        constexpr int K3 = KEYED ? 4 : 3;
+        constexpr int K3 = kind_of(KEYED);
         const uint32_t sh = KEYED ? (uint32_t)n : pf_shift(n), mul = pf_mult(n);
         uint64_t m[kSub];
-        uint32_t w[kSub], bit[kSub];
+        uint32_t w[kSub], bit[kSub], bit2[kSub];
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) filter_word<K3>(img, sh, mul, f, x, k, w[k], bit[k]);
+        for (int k = 0; k < kSub; ++k) filter_word<K3>(img, sh, mul, f, x, k, w[k], bit[k], bit2[k]);
 #pragma unroll
-        for (int k = 0; k < kSub; ++k)
-            m[k] = __ballot(__builtin_amdgcn_ubfe(w[k], bit[k], 1) != 0u && pk.rem[k] >= n);
+        for (int k = 0; k < kSub; ++k) m[k] = __ballot(filter_hit(w[k], bit[k], bit2[k]) && pk.rem[k] >= n);
         if (qn + count_sb(m) > kQueueCap) {
             double acc[S];
             flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
@@ -1077,7 +1104,7 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
 }
 
 // Score one document (probe -> verify/accumulate -> argmax -> outputs).
-template <int S, int MODE, bool STAGED, bool KEYED, bool WIDE>
+template <int S, int MODE, bool STAGED, int KEYED, bool WIDE>
 __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                           const uint32_t* bloom, int64_t doc, int64_t b, int64_t len,
                                           const DocSrc& src, int lane) {
@@ -1245,8 +1272,11 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
 
 // PACK (count mode only): a separate instantiation with the pack path, so the
 // pack path's registers never burden the single-document kernels
-template <int S, int MODE, bool FLDS, bool PACK = false, bool WIDE = false>
+// BL: the bloom layout (KEYED of the device functions): 0 = prefix Bloom in
+// LDS, 1 = keyed bloom (words / lines), 2 = keyed chunks
+template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false>
 __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
+    constexpr bool FLDS = BL == 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1342,14 +1372,14 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                         }
                         if (nd > 1) {
                             const int32_t tot = e[nd - 1];
-                            score_pack<S, !FLDS, WIDE>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
+                            score_pack<S, BL, WIDE>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
                                                  nd > 3 ? e[2] : tot, tot, nd, i, lane);
                             i += nd;
                             continue;
                         }
                     }
                 }
-                const int lab = score_doc<S, MODE, true, !FLDS, WIDE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, true, BL, WIDE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
                 ++i;
             }
@@ -1358,7 +1388,7 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                 const int64_t b = rdlane_i64(offv, i);
                 const int64_t len = rdlane_i64(offv, i + 1) - b;
                 const DocSrc src{nullptr, b};
-                const int lab = score_doc<S, MODE, false, !FLDS, WIDE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
+                const int lab = score_doc<S, MODE, false, BL, WIDE>(p, wl, lds, bloom, g0 + i, b, len, src, lane);
                 if (lane == 0) wl.labels[i] = lab;
             }
         }
@@ -1372,30 +1402,30 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     if (lane < prev_cnt) p.labels[prev_g0 + lane] = (int32_t)wl.labels[lane];
 }
 
-template <int S, int MODE, bool FLDS, bool WIDE>
+template <int S, int MODE, int BL, bool WIDE>
 hipError_t launch_w(const ScoreParams& p, int grid, hipStream_t stream) {
     const bool pack = MODE == 3 && p.pack;
-    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words, pack);
+    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (BL == 0 ? p.bloom_words : 0u) + p.direct_words, pack);
     if constexpr (MODE == 3) {
         if (pack) {
-            hipLaunchKernelGGL((score_kernel<S, MODE, FLDS, true, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds,
+            hipLaunchKernelGGL((score_kernel<S, MODE, BL, true, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds,
                                stream, p);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((score_kernel<S, MODE, FLDS, false, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
+    hipLaunchKernelGGL((score_kernel<S, MODE, BL, false, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
 
 // tables with wide keys (8..15 bytes) run the WIDE instantiations
-template <int S, int MODE, bool FLDS>
+template <int S, int MODE, int BL>
 hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
-    return p.wslots ? launch_w<S, MODE, FLDS, true>(p, grid, stream) : launch_w<S, MODE, FLDS, false>(p, grid, stream);
+    return p.wslots ? launch_w<S, MODE, BL, true>(p, grid, stream) : launch_w<S, MODE, BL, false>(p, grid, stream);
 }
 
-template <int S, int MODE, bool FLDS, bool PACK = false, bool WIDE = false>
+template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false>
 hipError_t prepare_k(size_t lds, int* blocks) {
-    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, FLDS, PACK, WIDE>);
+    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, BL, PACK, WIDE>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, kScoreWaves * 64, lds);
@@ -1403,51 +1433,60 @@ hipError_t prepare_k(size_t lds, int* blocks) {
 
 // count mode prepares both instantiations (single documents, packs); the
 // resident workgroups are the smaller of the two
-template <int S, int MODE, bool FLDS>
+template <int S, int MODE, int BL>
 hipError_t prepare_t(size_t lds, int* blocks) {
-    hipError_t e = prepare_k<S, MODE, FLDS>(lds, blocks);
+    hipError_t e = prepare_k<S, MODE, BL>(lds, blocks);
     int b2 = 0;
-    if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, false, true>(lds, &b2);
+    if (e == hipSuccess) e = prepare_k<S, MODE, BL, false, true>(lds, &b2);
     if (e == hipSuccess) *blocks = std::min(*blocks, b2);
     if constexpr (MODE == 3) {
-        if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, true>(lds, &b2);
+        if (e == hipSuccess) e = prepare_k<S, MODE, BL, true>(lds, &b2);
         if (e == hipSuccess) *blocks = std::min(*blocks, b2);
-        if (e == hipSuccess) e = prepare_k<S, MODE, FLDS, true, true>(lds, &b2);
+        if (e == hipSuccess) e = prepare_k<S, MODE, BL, true, true>(lds, &b2);
         if (e == hipSuccess) *blocks = std::min(*blocks, b2);
     }
     return e;
 }
 
-template <int MODE, bool FLDS>
+template <int MODE, int BL>
 hipError_t launch_s(const ScoreParams& p, int slices, int grid, hipStream_t stream) {
     switch (slices) {
-        case 1: return launch_t<1, MODE, FLDS>(p, grid, stream);
-        case 2: return launch_t<2, MODE, FLDS>(p, grid, stream);
-        case 3: return launch_t<3, MODE, FLDS>(p, grid, stream);
-        case 4: return launch_t<4, MODE, FLDS>(p, grid, stream);
+        case 1: return launch_t<1, MODE, BL>(p, grid, stream);
+        case 2: return launch_t<2, MODE, BL>(p, grid, stream);
+        case 3: return launch_t<3, MODE, BL>(p, grid, stream);
+        case 4: return launch_t<4, MODE, BL>(p, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
-template <int MODE, bool FLDS>
+template <int MODE, int BL>
 hipError_t prepare_s(int slices, size_t lds, int* blocks) {
     switch (slices) {
-        case 1: return prepare_t<1, MODE, FLDS>(lds, blocks);
-        case 2: return prepare_t<2, MODE, FLDS>(lds, blocks);
-        case 3: return prepare_t<3, MODE, FLDS>(lds, blocks);
-        case 4: return prepare_t<4, MODE, FLDS>(lds, blocks);
+        case 1: return prepare_t<1, MODE, BL>(lds, blocks);
+        case 2: return prepare_t<2, MODE, BL>(lds, blocks);
+        case 3: return prepare_t<3, MODE, BL>(lds, blocks);
+        case 4: return prepare_t<4, MODE, BL>(lds, blocks);
         default: return hipErrorInvalidValue;
     }
 }
 
+// the chunk layout is built for count-mode tables only (MODE 3)
 template <int MODE>
 hipError_t launch_m(const ScoreParams& p, int slices, bool lds_bloom, int grid, hipStream_t stream) {
-    return lds_bloom ? launch_s<MODE, true>(p, slices, grid, stream) : launch_s<MODE, false>(p, slices, grid, stream);
+    if (lds_bloom) return launch_s<MODE, 0>(p, slices, grid, stream);
+    if constexpr (MODE == 3) {
+        if (p.kb_chunks) return launch_s<MODE, 2>(p, slices, grid, stream);
+    }
+    return launch_s<MODE, 1>(p, slices, grid, stream);
 }
 
 template <int MODE>
-hipError_t prepare_m(int slices, bool lds_bloom, size_t lds, int* blocks) {
-    return lds_bloom ? prepare_s<MODE, true>(slices, lds, blocks) : prepare_s<MODE, false>(slices, lds, blocks);
+hipError_t prepare_m(int slices, bool lds_bloom, bool chunks, size_t lds, int* blocks) {
+    if (lds_bloom) return prepare_s<MODE, 0>(slices, lds, blocks);
+    if constexpr (MODE == 3) {
+        if (chunks) return prepare_s<MODE, 2>(slices, lds, blocks);
+    }
+    return prepare_s<MODE, 1>(slices, lds, blocks);
 }
 
 // first maximum across language blocks: block maxima compared with '>' in
@@ -1487,12 +1526,12 @@ hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_blo
     }
 }
 
-hipError_t score_prepare(int slices, int mode, bool lds_bloom, size_t lds_bytes, int* blocks_per_cu) {
+hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu) {
     switch (mode) {
-        case 0: return prepare_m<0>(slices, lds_bloom, lds_bytes, blocks_per_cu);
-        case 1: return prepare_m<1>(slices, lds_bloom, lds_bytes, blocks_per_cu);
-        case 2: return prepare_m<2>(slices, lds_bloom, lds_bytes, blocks_per_cu);
-        case 3: return prepare_m<3>(slices, lds_bloom, lds_bytes, blocks_per_cu);
+        case 0: return prepare_m<0>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
+        case 1: return prepare_m<1>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
+        case 2: return prepare_m<2>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
+        case 3: return prepare_m<3>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
         default: return hipErrorInvalidValue;
     }
 }

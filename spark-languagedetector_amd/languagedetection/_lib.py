@@ -35,7 +35,7 @@ MAX_LANGS = 4096
 # ldgpu_model_layout flags
 LAYOUT_FLAGS = {"lds_bloom": 0x01, "keyed_bloom": 0x02, "keyed_bloom_lines": 0x04, "buckets": 0x08,
                 "wide_keys": 0x10, "direct": 0x20, "packs": 0x40, "lang_blocks": 0x80,
-                "general_keys": 0x100}
+                "general_keys": 0x100, "keyed_bloom_chunks": 0x200}
 
 _p = ctypes.c_void_p
 _pp = ctypes.POINTER(ctypes.c_void_p)
