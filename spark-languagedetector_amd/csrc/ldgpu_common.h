@@ -70,10 +70,12 @@ __host__ __device__ __forceinline__ uint32_t pf_bit(int klen, uint32_t lo, uint3
 // key sets a second bit of its word, from a second multiplier over the same
 // three bytes, and a window is a candidate only when both bits are set: at
 // ~2.5 keys per word the false candidates fall ~4x (every false candidate is
-// an L2 verify) for two more VALU ops per test -- the word is already in a
-// register.
+// an L2 verify) for two more VALU ops per test.  Measured on config 2 (same
+// box, tools/ab.sh): 5.47 ms with two bits against 5.34 ms with one -- the
+// verify of a 256-B document's candidates is one 64-lane batch either way, so
+// the VALU cost outweighs the fewer candidates.  One bit it is.
 #ifndef LDGPU_BLOOM_BITS
-#define LDGPU_BLOOM_BITS 2
+#define LDGPU_BLOOM_BITS 1
 #endif
 __host__ __device__ __forceinline__ constexpr uint32_t pf_mult2_of(uint32_t m) {
     return ((m ^ 0xA5A5A5u) * 0x2Fu + 0x1B873Du) & 0xFFFFFFu;
