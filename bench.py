@@ -164,8 +164,9 @@ def cpu_baseline_fit(args, grams, data, off, lang):
     host hash tables, then reduceGrams as a hash-partitioned merge: kind
     'port', host_cores() pthreads, as the SCORE baseline), rank 0, bounded
     sample of the same corpus; unit = corpus bytes/s like the line's value.
-    Also returns the sample's oracle counts (key bytes, offsets, counts) for
-    the parity check of the GPU path on the same documents."""
+    Also returns the sample's oracle counts in sparse form (key bytes, key
+    offsets, pair offsets, languages, counts) for the parity check of the GPU
+    path on the same documents."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ldoracle_c as OC
     L = OC.lib()
@@ -177,14 +178,7 @@ def cpu_baseline_fit(args, grams, data, off, lang):
         t0 = time.perf_counter()
         h = L.ldo_count_mt(OC._ptr(data), OC._ptr(o), OC._ptr(lang), n, args.langs, OC._ptr(g), len(g), threads)
         dt = time.perf_counter() - t0
-        out = None
-        if keep:
-            k = L.ldo_counts_size(h)
-            kb = np.zeros(max(L.ldo_counts_key_bytes(h), 1), dtype=np.uint8)
-            ko = np.zeros(k + 1, dtype=np.int64)
-            cnt = np.zeros((k, args.langs), dtype=np.int64)
-            L.ldo_counts_export(h, OC._ptr(kb), OC._ptr(ko), OC._ptr(cnt))
-            out = (kb[:int(ko[-1])], ko, cnt)
+        out = OC.export_sparse(h) if keep else None   # (gram, language) pairs: no dense row of L per gram
         L.ldo_counts_destroy(h)
         return dt, out
 
@@ -463,16 +457,18 @@ def fit_main(args, world, rank, local, dev, backend):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         data_h = d_bytes[:min(n_bytes, 256 << 20)].cpu().numpy()
         lang_h = d_lang.cpu().numpy()
-        line["cpu_baseline"], n_s, (okb, oko, ocnt) = cpu_baseline_fit(args, grams, data_h, off, lang_h)
-        # the GPU count of the same sample documents against the oracle's
+        line["cpu_baseline"], n_s, expect = cpu_baseline_fit(args, grams, data_h, off, lang_h)
+        # the GPU count of the same sample documents against the oracle's, as
+        # sorted (gram, language, count) pairs
         c = DeviceCounts(args.langs, grams, device=local)
         c.count_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), d_lang.data_ptr(), n_s, stream.cuda_stream)
         torch.cuda.synchronize(dev)
-        gkb, gko, gcnt = c.export_arrays()
+        got = c.export_sparse()
         c.close()
-        ok = (np.array_equal(gko, oko) and np.array_equal(gkb, okb) and np.array_equal(gcnt, ocnt))
+        ok = len(got) == len(expect) and all(np.array_equal(a, b) for a, b in zip(got, expect))
         line["counts_match_oracle"] = bool(ok)
-        line["oracle_check"] = {"docs_checked": int(n_s), "grams_checked": int(len(oko) - 1)}
+        line["oracle_check"] = {"docs_checked": int(n_s), "grams_checked": int(len(expect[1]) - 1),
+                                "pairs_checked": int(len(expect[3]))}
     if rank == 0:
         print(json.dumps(line), flush=True)
         if args.json_out:

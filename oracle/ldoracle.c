@@ -202,16 +202,58 @@ int ldo_score(const ldo_table* t, const int32_t* G, int32_t nG, const uint8_t* b
 }
 
 /* -------------------------------------------------------------------- count */
+/* reduceGrams keys its sums by (language, gram) (LanguageDetector.scala:57-65):
+ * so does this table -- one slot per distinct (gram, language) pair holding
+ * its count; the gram rows of an export are assembled from the sorted pairs. */
+typedef struct { uint64_t h; const uint8_t* p; int64_t len; int32_t lang; int64_t cnt; } pentry;
+
 typedef struct {
-    hmap m; int32_t L; int64_t n; int64_t cap_rows; int64_t* counts;
+    pentry* e; int64_t cap; int64_t n; int32_t L;
+    const pentry** sorted; int64_t n_grams, key_bytes; /* export view (built on demand) */
 } ldo_counts;
+
+static uint64_t pair_hash(uint64_t h, int32_t lang) {
+    uint64_t x = h ^ ((uint64_t)(uint32_t)lang * 0x9e3779b97f4a7c15ull);
+    x ^= x >> 31; x *= 0xd6e8feb86659fd93ull; x ^= x >> 32;
+    return x;
+}
+
+static ldo_counts* counts_new(int32_t L, int64_t want) {
+    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
+    int64_t cap = 1024;
+    while (cap < 2 * want) cap <<= 1;
+    c->L = L; c->cap = cap;
+    c->e = (pentry*)calloc((size_t)cap, sizeof(pentry));
+    return c;
+}
+
+static void pm_add(ldo_counts* c, const uint8_t* p, int64_t len, uint64_t h, int32_t lang, int64_t cnt);
+
+static void pm_grow(ldo_counts* c) {
+    pentry* old = c->e;
+    const int64_t oc = c->cap;
+    c->cap *= 2; c->n = 0;
+    c->e = (pentry*)calloc((size_t)c->cap, sizeof(pentry));
+    for (int64_t i = 0; i < oc; ++i) if (old[i].p) pm_add(c, old[i].p, old[i].len, old[i].h, old[i].lang, old[i].cnt);
+    free(old);
+}
+
+/* count of (gram p[0..len), lang) += cnt; h = hbytes of the gram */
+static void pm_add(ldo_counts* c, const uint8_t* p, int64_t len, uint64_t h, int32_t lang, int64_t cnt) {
+    if (2 * (c->n + 1) > c->cap) pm_grow(c);
+    const int64_t mask = c->cap - 1;
+    int64_t s = (int64_t)(pair_hash(h, lang) & (uint64_t)mask);
+    for (;;) {
+        pentry* e = &c->e[s];
+        if (!e->p) { *e = (pentry){h, p, len, lang, cnt}; c->n++; return; }
+        if (e->h == h && e->lang == lang && e->len == len && memcmp(e->p, p, (size_t)len) == 0) { e->cnt += cnt; return; }
+        s = (s + 1) & mask;
+    }
+}
 
 ldo_counts* ldo_count(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, int64_t n_docs,
                       int32_t L, const int32_t* G, int32_t nG) {
-    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
-    c->L = L; c->cap_rows = 1024;
-    c->counts = (int64_t*)calloc((size_t)(c->cap_rows * L), sizeof(int64_t));
-    hm_init(&c->m, 1024);
+    ldo_counts* c = counts_new(L, 1024);
     for (int64_t d = 0; d < n_docs; ++d) {
         const uint8_t* p = bytes + offsets[d];
         int64_t len = offsets[d + 1] - offsets[d];
@@ -221,54 +263,17 @@ ldo_counts* ldo_count(const uint8_t* bytes, const int64_t* offsets, const int32_
             int64_t n = G[gi];
             int64_t nw = len == 0 ? 0 : (len < n ? 1 : len - n + 1);
             int64_t wl = len < n ? len : n;
-            for (int64_t i = 0; i < nw; ++i) {
-                int ins;
-                int64_t idx = hm_upsert(&c->m, p + i, wl, hbytes(p + i, wl), c->n, &ins);
-                if (ins) {
-                    if (c->n + 1 > c->cap_rows) {
-                        int64_t nc = c->cap_rows * 2;
-                        c->counts = (int64_t*)realloc(c->counts, sizeof(int64_t) * (size_t)(nc * L));
-                        memset(c->counts + c->cap_rows * L, 0, sizeof(int64_t) * (size_t)((nc - c->cap_rows) * L));
-                        c->cap_rows = nc;
-                    }
-                    c->n++;
-                }
-                c->counts[idx * L + lang] += 1;
-            }
+            for (int64_t i = 0; i < nw; ++i) pm_add(c, p + i, wl, hbytes(p + i, wl), lang, 1);
         }
     }
-    return c;
-}
-
-/* add `cnt` (a row of L) at key (p, len, h) */
-static void counts_add_row(ldo_counts* c, const uint8_t* p, int64_t len, uint64_t h, const int64_t* cnt) {
-    int ins;
-    int64_t idx = hm_upsert(&c->m, p, len, h, c->n, &ins);
-    if (ins) {
-        if (c->n + 1 > c->cap_rows) {
-            int64_t nc = c->cap_rows * 2;
-            c->counts = (int64_t*)realloc(c->counts, sizeof(int64_t) * (size_t)(nc * c->L));
-            memset(c->counts + c->cap_rows * c->L, 0, sizeof(int64_t) * (size_t)((nc - c->cap_rows) * c->L));
-            c->cap_rows = nc;
-        }
-        c->n++;
-    }
-    for (int32_t l = 0; l < c->L; ++l) c->counts[idx * c->L + l] += cnt[l];
-}
-
-static ldo_counts* counts_new(int32_t L) {
-    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
-    c->L = L; c->cap_rows = 1024;
-    c->counts = (int64_t*)calloc((size_t)(c->cap_rows * L), sizeof(int64_t));
-    hm_init(&c->m, 1024);
     return c;
 }
 
 /* Multithreaded ldo_count (the CPU baseline of bench.py's FIT line, SURVEY
  * §8d: N host threads): computeGrams per thread over a contiguous range of
  * documents (balanced by bytes) into a private table -- Spark's map side --
- * then reduceGrams: thread p sums every private table's keys of hash
- * partition p (the shuffle), and the partitions (disjoint keys) are
+ * then reduceGrams: thread p sums every private table's pairs of hash
+ * partition p (the shuffle), and the partitions (disjoint pairs) are
  * concatenated into one table.  Same counts as ldo_count. */
 typedef struct {
     const uint8_t* bytes; const int64_t* off; const int32_t* lang; int64_t d0, d1; int32_t L; const int32_t* G;
@@ -281,18 +286,28 @@ static void* count_map_worker(void* arg) {
     return NULL;
 }
 
+static int32_t part_of(const pentry* e, int32_t nthreads) {
+    return (int32_t)((pair_hash(e->h, e->lang) >> 40) % (uint64_t)nthreads);
+}
+
 static void* count_reduce_worker(void* arg) {
     count_job* j = (count_job*)arg;
-    j->out = counts_new(j->L);
+    int64_t want = 0;
+    for (int32_t t = 0; t < j->nthreads; ++t) want += j->locals[t]->n / j->nthreads;
+    j->out = counts_new(j->L, want);
     for (int32_t t = 0; t < j->nthreads; ++t) {
         const ldo_counts* c = j->locals[t];
-        for (int64_t i = 0; i < c->m.cap; ++i) {
-            const entry* e = &c->m.e[i];
-            if (e->idx < 0 || (int32_t)((e->h >> 40) % (uint64_t)j->nthreads) != j->part) continue;
-            counts_add_row(j->out, e->p, e->len, e->h, c->counts + e->idx * c->L);
+        for (int64_t i = 0; i < c->cap; ++i) {
+            const pentry* e = &c->e[i];
+            if (e->p && part_of(e, j->nthreads) == j->part) pm_add(j->out, e->p, e->len, e->h, e->lang, e->cnt);
         }
     }
     return NULL;
+}
+
+static void counts_free(ldo_counts* c) {
+    if (!c) return;
+    free(c->e); free(c->sorted); free(c);
 }
 
 ldo_counts* ldo_count_mt(const uint8_t* bytes, const int64_t* offsets, const int32_t* doc_lang, int64_t n_docs,
@@ -314,57 +329,87 @@ ldo_counts* ldo_count_mt(const uint8_t* bytes, const int64_t* offsets, const int
     for (int32_t t = 0; t < nthreads; ++t) { pthread_join(th[t], NULL); locals[t] = jobs[t].local; }
     for (int32_t t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, count_reduce_worker, &jobs[t]);
     for (int32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    for (int32_t t = 0; t < nthreads; ++t) counts_free(locals[t]);
     int64_t total = 0;
     for (int32_t t = 0; t < nthreads; ++t) total += jobs[t].out->n;
-    ldo_counts* c = (ldo_counts*)calloc(1, sizeof(ldo_counts));
-    c->L = L; c->cap_rows = total > 0 ? total : 1;
-    c->counts = (int64_t*)calloc((size_t)(c->cap_rows * L), sizeof(int64_t));
-    hm_init(&c->m, c->cap_rows);
+    ldo_counts* c = counts_new(L, total);
     for (int32_t t = 0; t < nthreads; ++t) {
         const ldo_counts* o = jobs[t].out;
-        for (int64_t i = 0; i < o->m.cap; ++i) {
-            const entry* e = &o->m.e[i];
-            if (e->idx >= 0) counts_add_row(c, e->p, e->len, e->h, o->counts + e->idx * L);
+        for (int64_t i = 0; i < o->cap; ++i) {
+            const pentry* e = &o->e[i];
+            if (e->p) pm_add(c, e->p, e->len, e->h, e->lang, e->cnt);
         }
-    }
-    for (int32_t t = 0; t < nthreads; ++t) {
-        free(locals[t]->m.e); free(locals[t]->counts); free(locals[t]);
-        free(jobs[t].out->m.e); free(jobs[t].out->counts); free(jobs[t].out);
+        counts_free(jobs[t].out);
     }
     return c;
 }
 
-int64_t ldo_counts_size(const ldo_counts* c) { return c->n; }
-
-int64_t ldo_counts_key_bytes(const ldo_counts* c) {
-    int64_t s = 0;
-    for (int64_t i = 0; i < c->m.cap; ++i) if (c->m.e[i].idx >= 0) s += c->m.e[i].len;
-    return s;
-}
-
-static int cmp_entry(const void* a, const void* b) {
-    const entry* x = *(const entry* const*)a; const entry* y = *(const entry* const*)b;
+static int cmp_pentry(const void* a, const void* b) {
+    const pentry* x = *(const pentry* const*)a; const pentry* y = *(const pentry* const*)b;
     if (x->len != y->len) return x->len < y->len ? -1 : 1;
-    return memcmp(x->p, y->p, (size_t)x->len);
+    const int m = memcmp(x->p, y->p, (size_t)x->len);
+    if (m) return m;
+    return x->lang < y->lang ? -1 : (x->lang > y->lang);
 }
 
-/* export sorted by (length, unsigned bytes): key_bytes, key_offsets[n+1], counts[n][L] */
-void ldo_counts_export(const ldo_counts* c, uint8_t* key_bytes, int64_t* key_offsets, int64_t* counts) {
-    const entry** v = (const entry**)malloc(sizeof(entry*) * (size_t)(c->n > 0 ? c->n : 1));
+/* the pairs sorted by (gram length, unsigned bytes, language); distinct grams */
+static void sorted_view(ldo_counts* c) {
+    if (c->sorted) return;
+    c->sorted = (const pentry**)malloc(sizeof(pentry*) * (size_t)(c->n > 0 ? c->n : 1));
     int64_t k = 0;
-    for (int64_t i = 0; i < c->m.cap; ++i) if (c->m.e[i].idx >= 0) v[k++] = &c->m.e[i];
-    qsort(v, (size_t)k, sizeof(entry*), cmp_entry);
-    int64_t o = 0;
-    key_offsets[0] = 0;
+    for (int64_t i = 0; i < c->cap; ++i) if (c->e[i].p) c->sorted[k++] = &c->e[i];
+    qsort(c->sorted, (size_t)k, sizeof(pentry*), cmp_pentry);
+    c->n_grams = c->key_bytes = 0;
     for (int64_t i = 0; i < k; ++i) {
-        memcpy(key_bytes + o, v[i]->p, (size_t)v[i]->len);
-        o += v[i]->len; key_offsets[i + 1] = o;
-        memcpy(counts + i * c->L, c->counts + v[i]->idx * c->L, sizeof(int64_t) * (size_t)c->L);
+        const pentry* e = c->sorted[i];
+        if (i && e->len == c->sorted[i - 1]->len && memcmp(e->p, c->sorted[i - 1]->p, (size_t)e->len) == 0) continue;
+        c->n_grams++;
+        c->key_bytes += e->len;
     }
-    free(v);
 }
 
-void ldo_counts_destroy(ldo_counts* c) {
-    if (!c) return;
-    free(c->m.e); free(c->counts); free(c);
+int64_t ldo_counts_size(ldo_counts* c) { sorted_view(c); return c->n_grams; }
+int64_t ldo_counts_key_bytes(ldo_counts* c) { sorted_view(c); return c->key_bytes; }
+int64_t ldo_counts_pairs(const ldo_counts* c) { return c->n; }
+
+/* export sorted by (length, unsigned bytes); sparse: key_bytes, key_offsets
+ * [n+1], pair_offsets [n+1], the pairs' languages (ascending per gram) and
+ * counts; dense (ldo_counts_export): counts[n][L] */
+void ldo_counts_export_sparse(ldo_counts* c, uint8_t* key_bytes, int64_t* key_offsets, int64_t* pair_offsets,
+                              int32_t* langs, int64_t* counts) {
+    sorted_view(c);
+    int64_t o = 0, g = -1;
+    key_offsets[0] = 0;
+    pair_offsets[0] = 0;
+    for (int64_t i = 0; i < c->n; ++i) {
+        const pentry* e = c->sorted[i];
+        if (!(i && e->len == c->sorted[i - 1]->len && memcmp(e->p, c->sorted[i - 1]->p, (size_t)e->len) == 0)) {
+            ++g;
+            memcpy(key_bytes + o, e->p, (size_t)e->len);
+            o += e->len;
+            key_offsets[g + 1] = o;
+        }
+        pair_offsets[g + 1] = i + 1;
+        langs[i] = e->lang;
+        counts[i] = e->cnt;
+    }
 }
+
+void ldo_counts_export(ldo_counts* c, uint8_t* key_bytes, int64_t* key_offsets, int64_t* counts) {
+    sorted_view(c);
+    int64_t o = 0, g = -1;
+    key_offsets[0] = 0;
+    memset(counts, 0, sizeof(int64_t) * (size_t)(c->n_grams * c->L));
+    for (int64_t i = 0; i < c->n; ++i) {
+        const pentry* e = c->sorted[i];
+        if (!(i && e->len == c->sorted[i - 1]->len && memcmp(e->p, c->sorted[i - 1]->p, (size_t)e->len) == 0)) {
+            ++g;
+            memcpy(key_bytes + o, e->p, (size_t)e->len);
+            o += e->len;
+            key_offsets[g + 1] = o;
+        }
+        counts[g * c->L + e->lang] = e->cnt;
+    }
+}
+
+void ldo_counts_destroy(ldo_counts* c) { counts_free(c); }

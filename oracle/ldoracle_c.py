@@ -49,6 +49,9 @@ def lib():
         L.ldo_counts_key_bytes.restype = _i64
         L.ldo_counts_key_bytes.argtypes = [_p]
         L.ldo_counts_export.argtypes = [_p, _p, _p, _p]
+        L.ldo_counts_pairs.restype = _i64
+        L.ldo_counts_pairs.argtypes = [_p]
+        L.ldo_counts_export_sparse.argtypes = [_p, _p, _p, _p, _p, _p]
         L.ldo_counts_destroy.argtypes = [_p]
         _lib = L
     return _lib
@@ -138,3 +141,37 @@ def count(data: np.ndarray, offsets: np.ndarray, doc_lang: np.ndarray, n_langs: 
         L.ldo_counts_destroy(h)
     keys = [bytes(blob[off[i]:off[i + 1]]) for i in range(n)]
     return keys, cnt
+
+
+def export_sparse(h):
+    """The (gram, language) pairs of an ldo_counts handle in (length, bytes,
+    language) order: (key_bytes, key_offsets [n+1], pair_offsets [n+1],
+    pair_langs int32, pair_counts int64) -- the form of
+    ldgpu_counts_export_sparse."""
+    L = lib()
+    n = L.ldo_counts_size(h)
+    nb = L.ldo_counts_key_bytes(h)
+    npairs = L.ldo_counts_pairs(h)
+    kb = np.zeros(max(nb, 1), dtype=np.uint8)
+    ko = np.zeros(n + 1, dtype=np.int64)
+    po = np.zeros(n + 1, dtype=np.int64)
+    pl = np.zeros(max(npairs, 1), dtype=np.int32)
+    pc = np.zeros(max(npairs, 1), dtype=np.int64)
+    L.ldo_counts_export_sparse(h, _ptr(kb), _ptr(ko), _ptr(po), _ptr(pl), _ptr(pc))
+    return kb[:nb], ko, po, pl[:npairs], pc[:npairs]
+
+
+def count_sparse(data: np.ndarray, offsets: np.ndarray, doc_lang: np.ndarray, n_langs: int,
+                 gram_lengths: Sequence[int], nthreads: int = 1):
+    """count() in sparse form (export_sparse): no dense row of L per gram."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    doc_lang = np.ascontiguousarray(doc_lang, dtype=np.int32)
+    g = np.asarray(gram_lengths, dtype=np.int32)
+    L = lib()
+    h = L.ldo_count_mt(_ptr(data), _ptr(offsets), _ptr(doc_lang), len(offsets) - 1, n_langs, _ptr(g), len(g),
+                       max(nthreads, 1))
+    try:
+        return export_sparse(h)
+    finally:
+        L.ldo_counts_destroy(h)

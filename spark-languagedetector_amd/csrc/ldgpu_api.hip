@@ -1615,13 +1615,12 @@ struct ldgpu_counts {
     unsigned long long* d_counts = nullptr;  // [cap][L] (dense tables: T1 of the count calls)
     unsigned long long* d_size = nullptr;
     // The final table T of a count table is sparse (ldgpu_fit.h CountParams):
-    // the grams in d_keys with presence bits d_masks[cap][S], the counts in a
-    // table of (gram slot, language) pairs -- the reduceGrams rows
-    // (LanguageDetector.scala:57-65), ~1.3 per gram on the fit corpora, where a
-    // dense row of L counters per gram took 1.6 KB at L = 200.
+    // the grams in d_keys with their language counts d_kcnt[cap] (the pairs
+    // each has), the counts in a table of (gram slot, language) pairs -- the
+    // reduceGrams rows (LanguageDetector.scala:57-65), ~1.3 per gram on the fit
+    // corpora, where a dense row of L counters per gram took 1.6 KB at L = 200.
     bool sparse = false;
-    int32_t S = 0;
-    uint64_t* d_masks = nullptr;
+    uint32_t* d_kcnt = nullptr;
     uint64_t pcap = 0, psize = 0;
     uint64_t* d_pkeys = nullptr;
     unsigned long long* d_pcounts = nullptr;
@@ -1658,14 +1657,13 @@ struct ldgpu_counts {
     unsigned long long* d_wsize = nullptr;
     unsigned int* d_wfull = nullptr;
     // grams longer than kMaxWideGram (ldgpu_long.hip): gram slots with a key
-    // arena, presence masks and a pair table, as the sparse T; Gall = the
+    // arena and a pair table, as the sparse T; Gall = the
     // caller's gram lengths, G (above) its lengths <= 15 (FIT v4), Gl the
     // longer ones
     int32_t nGall = 0, Gall[kMaxGramLengths] = {};
     int32_t nGl = 0, Gl[kMaxGramLengths] = {};
     uint64_t lcap = 0, lsize = 0, lpcap = 0, lpsize = 0, larena_cap = 0, larena_n = 0;
     LongSlot* d_lslots = nullptr;
-    uint64_t* d_lmasks = nullptr;
     uint8_t* d_larena = nullptr;
     uint64_t* d_lpkeys = nullptr;
     unsigned long long* d_lpcounts = nullptr;
@@ -1692,9 +1690,9 @@ struct ldgpu_counts {
 };
 
 namespace {
-// u64 words per gram slot besides the key: dense rows of L counters, or the
-// sparse table's S presence words
-uint64_t row_words(const ldgpu_counts* c) { return c->sparse ? (uint64_t)c->S : (uint64_t)c->L; }
+// bytes per gram slot besides the key: dense rows of L u64 counters, or the
+// sparse table's u32 language count
+uint64_t row_bytes(const ldgpu_counts* c) { return c->sparse ? 4ull : 8ull * (uint64_t)c->L; }
 
 CountParams count_params(const ldgpu_counts* c) {
     CountParams p{};
@@ -1713,8 +1711,7 @@ CountParams count_params(const ldgpu_counts* c) {
     p.nG = c->nGn;
     for (int i = 0; i < c->nGn; ++i) p.G[i] = c->Gn[i];
     if (c->sparse) {
-        p.masks = c->d_masks;
-        p.S = c->S;
+        p.kcnt = c->d_kcnt;
         p.pkeys = c->d_pkeys;
         p.pcounts = c->d_pcounts;
         p.pshift = (uint32_t)(64 - log2u(c->pcap));
@@ -1740,7 +1737,7 @@ void counts_free(ldgpu_counts* c) {
     if (!c) return;
     if (c->pend) counts_free(c->pend);
     for (void* p : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts, (void*)c->d_wsize, (void*)c->d_wfull,
-                    (void*)c->d_lslots, (void*)c->d_lmasks, (void*)c->d_larena, (void*)c->d_lpkeys,
+                    (void*)c->d_lslots, (void*)c->d_larena, (void*)c->d_lpkeys,
                     (void*)c->d_lpcounts, (void*)c->d_lctr})
         if (p) (void)hipFree(p);
     if (c->ctx) {
@@ -1750,14 +1747,14 @@ void counts_free(ldgpu_counts* c) {
         (void)hipStreamSynchronize(c->ctx->stream);
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
-        cache_free(c->ctx, c->d_masks, c->cap * (size_t)c->S * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_kcnt, c->cap * sizeof(uint32_t));
         cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
         cache_free(c->ctx, c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
         cache_free(c->ctx, c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
         cache_free(c->ctx, c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
     } else {
-        for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_masks, (void*)c->d_pkeys,
+        for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_kcnt, (void*)c->d_pkeys,
                         (void*)c->d_pcounts, (void*)c->d_ovf_keys, (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt})
             if (p) (void)hipFree(p);
     }
@@ -1767,10 +1764,10 @@ void counts_free(ldgpu_counts* c) {
     delete c;
 }
 
-// a gram table of cap slots: keys and rows of row_words(c) u64 words (dense
-// counters, or the sparse table's presence masks), zeroed
-int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, unsigned long long** rows) {
-    const size_t rb = cap * (size_t)row_words(c) * sizeof(unsigned long long);
+// a gram table of cap slots: keys and rows of row_bytes(c) (dense counters,
+// or the sparse table's language counts), zeroed
+int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, void** rows) {
+    const size_t rb = cap * (size_t)row_bytes(c);
     HIP_TRY(cache_alloc(c->ctx, (void**)keys, cap * sizeof(uint64_t)));
     hipError_t e = cache_alloc(c->ctx, (void**)rows, rb);
     if (e != hipSuccess) {
@@ -1825,17 +1822,16 @@ int rebuild_pairs(ldgpu_counts* c, uint64_t new_pcap, const uint64_t* remap) {
 int grow(ldgpu_counts* c, uint64_t new_cap) {
     if (new_cap <= c->cap) return LDGPU_OK;
     uint64_t* nk = nullptr;
-    unsigned long long* nc = nullptr;
-    if (int rc = alloc_table(c, new_cap, &nk, &nc)) return rc;
+    void* nr = nullptr;
+    if (int rc = alloc_table(c, new_cap, &nk, &nr)) return rc;
     CountParams from = count_params(c);
     ldgpu_counts tmp;
     tmp.L = c->L;
     tmp.sparse = c->sparse;
-    tmp.S = c->S;
     tmp.cap = new_cap;
     tmp.d_keys = nk;
     if (c->sparse) {
-        tmp.d_masks = reinterpret_cast<uint64_t*>(nc);
+        tmp.d_kcnt = static_cast<uint32_t*>(nr);
         uint64_t* remap = nullptr;
         hipError_t e = cache_alloc(c->ctx, (void**)&remap, c->cap * sizeof(uint64_t));
         if (e == hipSuccess) e = launch_sparse_rehash(from, count_params(&tmp), c->cap, remap, c->ctx->stream);
@@ -1843,29 +1839,29 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
         if (e != hipSuccess) {
             if (remap) cache_free(c->ctx, remap, c->cap * sizeof(uint64_t));
             cache_free(c->ctx, nk, new_cap * sizeof(uint64_t));
-            cache_free(c->ctx, nc, new_cap * (size_t)c->S * sizeof(uint64_t));
+            cache_free(c->ctx, nr, new_cap * sizeof(uint32_t));
             return fail(LDGPU_ENOMEM, "count table grow: %s", hipGetErrorString(e));
         }
         const uint64_t old_cap = c->cap;
         uint64_t* old_keys = c->d_keys;
-        uint64_t* old_masks = c->d_masks;
+        uint32_t* old_kcnt = c->d_kcnt;
         c->d_keys = nk;
-        c->d_masks = tmp.d_masks;
+        c->d_kcnt = tmp.d_kcnt;
         c->cap = new_cap;
         cache_free(c->ctx, old_keys, old_cap * sizeof(uint64_t));
-        cache_free(c->ctx, old_masks, old_cap * (size_t)c->S * sizeof(uint64_t));
+        cache_free(c->ctx, old_kcnt, old_cap * sizeof(uint32_t));
         const int rc = rebuild_pairs(c, c->pcap, remap);
         cache_free(c->ctx, remap, old_cap * sizeof(uint64_t));
         return rc;
     }
-    tmp.d_counts = nc;
+    tmp.d_counts = static_cast<unsigned long long*>(nr);
     CountParams to = count_params(&tmp);
     HIP_TRY(launch_rehash(from, to, c->cap, c->ctx->stream));
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
     cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
     cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
     c->d_keys = nk;
-    c->d_counts = nc;
+    c->d_counts = static_cast<unsigned long long*>(nr);
     c->cap = new_cap;
     return LDGPU_OK;
 }
@@ -1876,33 +1872,40 @@ int pgrow(ldgpu_counts* c, uint64_t new_pcap) {
     return rebuild_pairs(c, new_pcap, nullptr);
 }
 
-// Load a count table may reach before it doubles: 1/2, or 0.8 once the
-// doubled table would pass kBigTableBytes -- a dense slot holds a row of L
-// counters (1.6 KB at L = 200: T1 of a K = 3 fit), so a dense table of 45M grams
-// would need 2^27 slots (216 GB) at load 1/2, more than the device holds next to
-// the old table during the rehash.  The sparse table's slots are small (key +
-// S mask words; 16-B pairs): load 1/2.  (A rare insert that meets a linear-probe
-// cluster longer than kMaxProbe goes to the overflow list and is re-inserted
-// by the host.)
-constexpr uint64_t kBigTableBytes = 96ull << 30;
+// Load a table may reach before it doubles: 1/2, or 0.8 once the doubled
+// table would pass kBigTableBytes -- the device must hold the old and the new
+// table during a rehash, next to the others of the fit.  A dense slot holds a
+// row of L counters (1.6 KB at L = 200: T1 of a K = 3 fit); the sparse T's
+// gram slots are 12 B and its pairs 16 B, but a 1 GB fit at L = 200 holds
+// ~1.4G grams and ~1.7G pairs (2^31 slots each at load 0.8: 26 + 34 GB;
+// 2^32 at load 1/2 would take twice that, and three times during the grow).
+// (A rare insert that meets a linear-probe cluster longer than kMaxProbe goes
+// to the overflow list and is re-inserted by the host.)
+constexpr uint64_t kBigTableBytes = 48ull << 30;
 
-double max_load(const ldgpu_counts* c) {
-    const uint64_t slot = 8ull + 8ull * row_words(c);
-    return 2 * c->cap * slot > kBigTableBytes ? 0.8 : 0.5;
+double load_limit(uint64_t cap, uint64_t slot_bytes) { return 2 * cap * slot_bytes > kBigTableBytes ? 0.8 : 0.5; }
+
+double max_load(const ldgpu_counts* c) { return load_limit(c->cap, 8ull + row_bytes(c)); }
+
+// the sparse table's pair table (16-B slots)
+double pair_load(const ldgpu_counts* c) { return load_limit(c->pcap, 16ull); }
+
+// the smallest power-of-two table of slot_bytes slots that holds `need` keys
+// within its load limit
+uint64_t cap_for(double need, uint64_t slot_bytes) {
+    uint64_t cap = 1ull << 12;
+    while (need > load_limit(cap, slot_bytes) * (double)cap) cap <<= 1;
+    return cap;
 }
-
-// the sparse table's pair table doubles past load 1/2
-double pair_load() { return 0.5; }
 
 // room for `grams` more grams and `pairs` more pairs within the load limits
 // (grow / pgrow to the next fitting power of two)
 int reserve(ldgpu_counts* c, uint64_t grams, uint64_t pairs) {
     if ((double)(c->size + grams) > max_load(c) * (double)c->cap) {
-        uint64_t target = next_pow2((uint64_t)((double)(c->size + grams) / max_load(c)) + 16);
-        if (int rc = grow(c, target)) return rc;
+        if (int rc = grow(c, cap_for((double)(c->size + grams) + 16, 8ull + row_bytes(c)))) return rc;
     }
-    if (c->sparse && (double)(c->psize + pairs) > pair_load() * (double)c->pcap) {
-        if (int rc = pgrow(c, next_pow2((uint64_t)((double)(c->psize + pairs) / pair_load()) + 16))) return rc;
+    if (c->sparse && (double)(c->psize + pairs) > pair_load(c) * (double)c->pcap) {
+        if (int rc = pgrow(c, cap_for((double)(c->psize + pairs) + 16, 16ull))) return rc;
     }
     return LDGPU_OK;
 }
@@ -1928,7 +1931,7 @@ int after_batch(ldgpu_counts* c, bool may_grow = true) {
         while (may_grow && (double)c->size > max_load(c) * (double)c->cap) {  // past the load limit: double
             if (int rc = grow(c, 2 * c->cap)) return rc;
         }
-        while (may_grow && c->sparse && (double)c->psize > pair_load() * (double)c->pcap) {
+        while (may_grow && c->sparse && (double)c->psize > pair_load(c) * (double)c->pcap) {
             if (int rc = pgrow(c, 2 * c->pcap)) return rc;
         }
         return LDGPU_OK;
@@ -1977,7 +1980,7 @@ int after_batch(ldgpu_counts* c, bool may_grow = true) {
         return std::max<uint64_t>(std::min<uint64_t>(t, 8 * cap), 2 * cap);
     };
     uint64_t target = target_of(size, c->cap, max_load(c));
-    uint64_t ptarget = c->sparse ? target_of(psize, c->pcap, pair_load()) : 0;
+    uint64_t ptarget = c->sparse ? target_of(psize, c->pcap, pair_load(c)) : 0;
     for (unsigned int n = novf; n > 0;) {
         if (int rc = grow(c, target)) return rc;
         if (int rc = pgrow(c, ptarget)) return rc;
@@ -2071,8 +2074,10 @@ WideCountParams wide_params(const ldgpu_counts* c) {
     return p;
 }
 
-// room for `extra` more wide keys at load <= 1/2 (so an insert's probe always
-// ends): allocate or grow (device rehash) the wide table
+// room for `extra` more wide keys within the load limit (1/2; 0.8 for a big
+// table, as load_limit -- an insert's probe always ends, the table never
+// fills): allocate or grow (device rehash) the wide table, to 4x the keys (a
+// big table: to load <= 0.7)
 int wide_ensure(ldgpu_counts* c, uint64_t extra) {
     hipStream_t st = c->ctx->stream;
     if (!c->d_wsize) {
@@ -2081,8 +2086,10 @@ int wide_ensure(ldgpu_counts* c, uint64_t extra) {
         HIP_TRY(hipMemsetAsync(c->d_wsize, 0, sizeof(unsigned long long), st));
         HIP_TRY(hipMemsetAsync(c->d_wfull, 0, sizeof(unsigned int), st));
     }
-    if (c->wcap && 2 * (c->wsize + extra) <= c->wcap) return LDGPU_OK;
-    const uint64_t cap = next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->wsize + extra)));
+    const uint64_t slot = 16ull + 8ull * (uint64_t)c->L, need = c->wsize + extra;
+    if (c->wcap && (double)need <= load_limit(c->wcap, slot) * (double)c->wcap) return LDGPU_OK;
+    uint64_t cap = next_pow2(std::max<uint64_t>(1 << 12, 4 * need));
+    if (cap * slot > kBigTableBytes) cap = std::max(c->wcap, next_pow2((uint64_t)((double)need / 0.7) + 1));
     ldgpu_counts t;
     t.L = c->L;
     t.wcap = cap;
@@ -2127,8 +2134,6 @@ int wide_after(ldgpu_counts* c) {
 LongCountParams long_params(const ldgpu_counts* c) {
     LongCountParams p{};
     p.slots = c->d_lslots;
-    p.masks = c->d_lmasks;
-    p.S = (c->L + 63) / 64;
     p.shift = c->lcap ? (uint32_t)(64 - log2u(c->lcap)) : 63u;
     p.mask = c->lcap ? c->lcap - 1 : 0;
     p.size = c->d_lctr;
@@ -2161,7 +2166,6 @@ CountParams long_pair_view(const ldgpu_counts* c, uint64_t* pkeys, unsigned long
 // through the slot remap) / a copy of the arena
 int long_reserve(ldgpu_counts* c, uint64_t grams, uint64_t pairs, uint64_t bytes) {
     hipStream_t st = c->ctx->stream;
-    const int S = (c->L + 63) / 64;
     if (!c->d_lctr) {
         HIP_TRY(hipMalloc((void**)&c->d_lctr, 4 * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(c->d_lctr, 0, 4 * sizeof(unsigned long long), st));
@@ -2173,22 +2177,18 @@ int long_reserve(ldgpu_counts* c, uint64_t grams, uint64_t pairs, uint64_t bytes
         t.L = c->L;
         t.lcap = cap;
         hipError_t e = hipMalloc((void**)&t.d_lslots, cap * sizeof(LongSlot));
-        if (e == hipSuccess) e = hipMalloc((void**)&t.d_lmasks, cap * (size_t)S * sizeof(uint64_t));
         if (e == hipSuccess) e = hipMemsetAsync(t.d_lslots, 0, cap * sizeof(LongSlot), st);
-        if (e == hipSuccess) e = hipMemsetAsync(t.d_lmasks, 0, cap * (size_t)S * sizeof(uint64_t), st);
         if (e == hipSuccess && c->lcap) e = hipMalloc((void**)&remap, c->lcap * sizeof(uint64_t));
         if (e == hipSuccess && c->lcap) e = launch_long_rehash(long_params(c), long_params(&t), c->lcap, remap, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) {
-            for (void* q : {(void*)t.d_lslots, (void*)t.d_lmasks, (void*)remap})
+            for (void* q : {(void*)t.d_lslots, (void*)remap})
                 if (q) (void)hipFree(q);
             return fail(LDGPU_ENOMEM, "long gram table of %llu slots: %s", (unsigned long long)cap,
                         hipGetErrorString(e));
         }
-        for (void* q : {(void*)c->d_lslots, (void*)c->d_lmasks})
-            if (q) (void)hipFree(q);
+        if (c->d_lslots) (void)hipFree(c->d_lslots);
         c->d_lslots = t.d_lslots;
-        c->d_lmasks = t.d_lmasks;
         c->lcap = cap;
     }
     if (remap || 2 * (c->lpsize + pairs) > c->lpcap) {
@@ -2456,23 +2456,32 @@ int derive_pending(ldgpu_counts* c) {
         const double tn = (double)(t->size + t->wsize);
         const double est = (double)c->size + (pairs ? 0.55 : 1.1) * tn;
         if (est > max_load(c) * (double)c->cap) {
-            const uint64_t slot = 8ull + 8ull * row_words(c);
-            uint64_t target = next_pow2((uint64_t)(est / 0.5) + 1);
-            if (target * slot > kBigTableBytes) target = next_pow2((uint64_t)(est / 0.8) + 1);
+            const uint64_t target = cap_for(est, 8ull + row_bytes(c));
             if (target > c->cap && grow(c, target) != LDGPU_OK) {
                 (void)hipGetLastError();
                 (void)ok();
             }
         }
         const double pest = (double)c->psize + 1.1 * tn;
-        if (c->sparse && pest > pair_load() * (double)c->pcap) {
-            const uint64_t target = next_pow2((uint64_t)(pest / pair_load()) + 1);
-            if (pgrow(c, target) != LDGPU_OK) {
+        if (c->sparse && pest > pair_load(c) * (double)c->pcap) {
+            if (pgrow(c, cap_for(pest, 16ull)) != LDGPU_OK) {
                 (void)hipGetLastError();
                 (void)ok();
             }
         }
     }
+    // two-word pair T1 (K = 2): each level writes its prefixes and the shorter
+    // entries into a fresh table (derive_pairs2_level_kernel's split), sized
+    // for all of them, and T1 is freed after the level: a level's scan reads
+    // only the entries still to derive, and T1 never holds the grown table
+    // next to the old one (diagnostics: LDGPU_FIT_DERIVE_INPLACE keeps one T1)
+    const bool split = pairs == 2 && !diag_env("LDGPU_FIT_DERIVE_INPLACE");
+    struct Owned {
+        ldgpu_counts* p = nullptr;
+        ~Owned() {
+            if (p) counts_free(p);
+        }
+    };
     for (int lev = maxg; lev >= 1; --lev) {
         const uint32_t mt = mult[lev];
         const int n = lev - 1;
@@ -2480,7 +2489,14 @@ int derive_pending(ldgpu_counts* c) {
         const bool wide = lev > kMaxGram || pairs == 2;  // the level's entries are in T1's wide table
         // T1 room for this level's prefixes (one per entry at most), within
         // 0.1 of its load limit (linear probes stay short)
-        if (n >= 1) {
+        Owned nx;
+        if (n >= 1 && split) {
+            uint64_t keep = cnt[lev];
+            for (int j = 1; j < lev; ++j) keep += cnt[j];
+            if (int rc = counts_new(c->ctx, 1, c->G, c->nG, 1 << 12, &nx.p)) return rc;
+            if (int rc = wide_ensure(nx.p, keep)) return rc;
+            cnt[n] += cnt[lev];
+        } else if (n >= 1) {
             if (n <= kMaxGram && pairs != 2) {
                 const double need = (double)(t->size + cnt[lev]);
                 if (need > (max_load(t) + 0.1) * (double)t->cap) {
@@ -2497,7 +2513,7 @@ int derive_pending(ldgpu_counts* c) {
             while ((double)c->size > max_load(c) * (double)c->cap) {
                 if (int rc = grow(c, 2 * c->cap)) return rc;
             }
-            while (c->sparse && (double)c->psize > pair_load() * (double)c->pcap) {
+            while (c->sparse && (double)c->psize > pair_load(c) * (double)c->pcap) {
                 if (int rc = pgrow(c, 2 * c->pcap)) return rc;
             }
             uint64_t slots = kOvfMax / per_slot;
@@ -2506,7 +2522,7 @@ int derive_pending(ldgpu_counts* c) {
                 const double room = std::max(1.0, (max_load(c) + 0.1) * (double)c->cap - (double)c->size);
                 slots = std::min<uint64_t>(slots, (uint64_t)(room / tload));
                 if (c->sparse) {
-                    const double proom = std::max(1.0, (pair_load() + 0.1) * (double)c->pcap - (double)c->psize);
+                    const double proom = std::max(1.0, (pair_load(c) + 0.1) * (double)c->pcap - (double)c->psize);
                     slots = std::min<uint64_t>(slots, (uint64_t)(proom / (tload * (double)per_slot)));
                 }
                 if (lev > kMaxGram) {
@@ -2521,8 +2537,8 @@ int derive_pending(ldgpu_counts* c) {
             HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
             HIP_TRY(hipMemsetAsync(t->d_ovf_n, 0, sizeof(unsigned int), st));
             if (pairs == 2)
-                HIP_TRY(launch_derive_pairs2_level(wide_params(t), s0, s0 + slots, lev, mt, count_params(c), derive_ablate,
-                                                   st));
+                HIP_TRY(launch_derive_pairs2_level(wide_params(t), s0, s0 + slots, lev, mt, count_params(c),
+                                                   nx.p ? wide_params(nx.p) : WideCountParams{}, derive_ablate, st));
             else if (pairs)
                 HIP_TRY(launch_derive_pairs_level(count_params(t), c->lb, s0, s0 + slots, lev, mt, count_params(c),
                                                   derive_ablate, st));
@@ -2533,11 +2549,16 @@ int derive_pending(ldgpu_counts* c) {
                 if (int rc = wide_after(c)) return rc;
             }
             if (n > kMaxGram || (pairs == 2 && n >= 1)) {
-                if (int rc = wide_after(t)) return rc;
+                if (int rc = wide_after(nx.p ? nx.p : t)) return rc;
             }
             if (int rc = after_batch(c)) return rc;
             if (int rc = after_batch(t, false)) return rc;
             s0 += slots;
+        }
+        if (nx.p) {  // the next level's T1
+            counts_free(t);
+            c->pend = t = nx.p;
+            nx.p = nullptr;
         }
     }
     return LDGPU_OK;
@@ -2866,17 +2887,19 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             while ((double)t1->size > max_load(t1) * (double)t1->cap) {
                 if (int rc = grow(t1, 2 * t1->cap)) return rc;
             }
-            if (wide && 2 * t1->wsize > t1->wcap) {
-                if (int rc = wide_ensure(t1, 0)) return rc;
+            if (wide) {
+                if (int rc = wide_ensure(t1, 0)) return rc;  // past its load limit: grows
             }
+            // the wide table's ceiling for a chunk: 3/4 (load limit 1/2), 0.9 (0.8)
+            const double wceil = wide ? std::min(0.9, 1.5 * load_limit(t1->wcap, 16ull + 8ull * (uint64_t)t1->L)) : 0.0;
             const double ceil_load = max_load(t1) + 0.1;
             int64_t room = (int64_t)(ceil_load * (double)t1->cap) - (int64_t)t1->size;
-            if (wide) room = std::min<int64_t>(room, (int64_t)(3 * (t1->wcap / 4) - t1->wsize));
+            if (wide) room = std::min<int64_t>(room, (int64_t)(wceil * (double)t1->wcap) - (int64_t)t1->wsize);
             // buckets b0 .. b1 (at least one) whose entries fit the room
             int b1 = b0;
             int64_t n = 0;
             while (b1 < kQ * kQ && (b1 == b0 || n + (int64_t)nout[b1] <= room)) n += nout[b1++];
-            if (wide && 4 * (t1->wsize + (uint64_t)n) > 3 * t1->wcap) {  // one bucket beyond the room
+            if (wide && (double)(t1->wsize + (uint64_t)n) > wceil * (double)t1->wcap) {  // one bucket beyond the room
                 if (int rc = wide_ensure(t1, (uint64_t)n)) return rc;
             }
             if (int rc = ensure_ovf(t1, std::max<int64_t>(n, 1))) return rc;
@@ -2994,7 +3017,6 @@ int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int
     c->ctx = ctx;
     c->L = n_langs;
     c->sparse = sparse;
-    c->S = sparse ? (n_langs + 63) / 64 : 0;
     // G: the lengths of <= 15 bytes (FIT v4: maximal windows); Gl: longer
     // ones (ldgpu_long.hip); Gall: all, in the caller's order
     c->nGall = n_grams;
@@ -3034,8 +3056,8 @@ int counts_new(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, int
             }
         }
     }
-    int rc = sparse ? alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<unsigned long long**>(&c->d_masks))
-                    : alloc_table(c, c->cap, &c->d_keys, &c->d_counts);
+    int rc = sparse ? alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<void**>(&c->d_kcnt))
+                    : alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<void**>(&c->d_counts));
     if (!rc && sparse) {
         c->pcap = c->cap;
         rc = alloc_pairs(c, c->pcap, &c->d_pkeys, &c->d_pcounts);
@@ -4140,11 +4162,10 @@ int merge_long(ldgpu_counts* c, ldgpu_comm* m) {
     }
     c->merged_wide = c->merged_wide || any;
     // this rank's long table, rebuilt from the owned triples
-    for (void* q : {(void*)c->d_lslots, (void*)c->d_lmasks, (void*)c->d_larena, (void*)c->d_lpkeys,
+    for (void* q : {(void*)c->d_lslots, (void*)c->d_larena, (void*)c->d_lpkeys,
                     (void*)c->d_lpcounts})
         if (q) (void)hipFree(q);
     c->d_lslots = nullptr;
-    c->d_lmasks = nullptr;
     c->d_larena = nullptr;
     c->d_lpkeys = nullptr;
     c->d_lpcounts = nullptr;
@@ -4235,13 +4256,14 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
     auto rebuild = [&]() -> int {
         HIP_TRY(hipStreamSynchronize(st));
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
-        cache_free(c->ctx, c->d_masks, c->cap * (size_t)c->S * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_kcnt, c->cap * sizeof(uint32_t));
         cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
-        c->d_keys = c->d_masks = c->d_pkeys = nullptr;
+        c->d_keys = c->d_pkeys = nullptr;
+        c->d_kcnt = nullptr;
         c->d_pcounts = nullptr;
         c->cap = c->pcap = next_pow2((uint64_t)std::max<int64_t>(1 << 12, 2 * R + 16));
-        if (int rc = alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<unsigned long long**>(&c->d_masks)))
+        if (int rc = alloc_table(c, c->cap, &c->d_keys, reinterpret_cast<void**>(&c->d_kcnt)))
             return rc;
         if (int rc = alloc_pairs(c, c->pcap, &c->d_pkeys, &c->d_pcounts)) return rc;
         if (int rc = ensure_ovf(c, R)) return rc;
@@ -4264,10 +4286,12 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
 }
 
 namespace {
-// Device build (SURVEY §8f "next" #3): presence masks, k and the (language,
-// k) histogram on the device; the host picks each language's threshold
-// class; the device flags the grams below it and resolves the threshold
-// class's (length, bytes) ties.  Only the chosen grams (<= L*K) cross PCIe.
+// Device build (SURVEY §8f "next" #3): from the sparse table's pairs the
+// (language, k) histogram (k = the gram's language count, kept by the count
+// kernels); the host picks each language's threshold class; the device flags
+// the grams below it, resolves the threshold class's (length, bytes) ties and
+// builds the chosen rows' presence masks from the pairs.  Only the chosen
+// grams (<= L*K) cross PCIe.
 // On a merged table (c->comm) the histogram is summed over the ranks, the
 // ties are resolved against the ranks' candidate prefixes, and the chosen
 // rows of every rank are gathered: every rank builds the same global table.
@@ -4279,18 +4303,22 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     hipStream_t st = c->ctx->stream;
     DevBufs db;
     db.ctx = c->ctx;
-    uint64_t *d_keys, *d_masks;
+    if (n > (int64_t)0xffffffffll) return fail(LDGPU_EUNSUPPORTED, "fit table: %lld grams", (long long)n);
+    const CountParams cp = count_params(c);
+    uint64_t* d_keys;
+    uint32_t* d_rowof;
     int32_t* d_k;
     unsigned long long* d_n;
     unsigned int* d_hist;
     HIP_TRY(db.alloc(&d_keys, n));
-    HIP_TRY(db.alloc(&d_masks, (size_t)n * S));
     HIP_TRY(db.alloc(&d_k, n));
+    HIP_TRY(db.alloc(&d_rowof, c->cap));
     HIP_TRY(db.alloc(&d_n, 2));
     HIP_TRY(db.alloc(&d_hist, (size_t)L * (L + 1)));
     HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(unsigned int) * L * (L + 1), st));
-    HIP_TRY(launch_presence(count_params(c), c->cap, S, d_keys, d_masks, d_k, d_n, d_hist, st));
+    HIP_TRY(launch_gram_rows(cp, c->cap, d_keys, d_k, d_rowof, d_n, st));
+    HIP_TRY(launch_pair_hist(cp, c->pcap, d_rowof, d_k, L, d_hist, st));
     std::vector<unsigned int> hist((size_t)L * (L + 1));
     unsigned long long got = 0;
     HIP_TRY(hipMemcpyAsync(hist.data(), d_hist, sizeof(unsigned int) * hist.size(), hipMemcpyDeviceToHost, st));
@@ -4332,6 +4360,10 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         // merged table: gather every rank's presence rows, select on the host
         std::vector<uint64_t> hk(n), hm((size_t)n * S);
         if (n) {
+            uint64_t* d_masks;
+            HIP_TRY(db.alloc(&d_masks, (size_t)n * S));
+            HIP_TRY(hipMemsetAsync(d_masks, 0, sizeof(uint64_t) * n * S, st));
+            HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, nullptr, S, d_masks, st));
             HIP_TRY(hipMemcpyAsync(hk.data(), d_keys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(hm.data(), d_masks, sizeof(uint64_t) * n * S, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -4419,7 +4451,9 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(hipMemcpyAsync(d_kstar, kstar.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d_need, need.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(d_cn, 0, sizeof(unsigned int), st));
-    HIP_TRY(launch_select(n, L, S, d_keys, d_masks, d_k, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn, st));
+    HIP_TRY(hipMemsetAsync(d_chosen, 0, (size_t)n, st));
+    HIP_TRY(launch_pair_select(cp, c->pcap, d_rowof, d_keys, d_k, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn,
+                               st));
     unsigned int cn = 0;
     HIP_TRY(hipMemcpyAsync(&cn, d_cn, sizeof cn, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -4486,16 +4520,20 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     const int64_t cap_out = std::min<int64_t>(n, (int64_t)L * std::max<int32_t>(K, 0));
     uint64_t *d_ok, *d_om;
     int32_t* d_okk;
+    uint32_t* d_outrow;
     HIP_TRY(db.alloc(&d_ok, cap_out));
-    HIP_TRY(db.alloc(&d_om, (size_t)cap_out * S));
     HIP_TRY(db.alloc(&d_okk, cap_out));
+    HIP_TRY(db.alloc(&d_outrow, n));
     HIP_TRY(hipMemsetAsync(d_n + 1, 0, sizeof(unsigned long long), st));
-    HIP_TRY(launch_gather_chosen(n, S, d_chosen, d_keys, d_masks, d_k, d_ok, d_om, d_okk, d_n + 1, st));
+    HIP_TRY(launch_gather_rows(n, d_chosen, d_keys, d_k, d_ok, d_okk, d_outrow, d_n + 1, cap_out, st));
     unsigned long long m = 0;
     HIP_TRY(hipMemcpyAsync(&m, d_n + 1, sizeof m, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if ((int64_t)m > cap_out) return fail(LDGPU_EDEVICE, "top-K: %llu grams chosen, at most %lld expected", m,
                                          (long long)cap_out);
+    HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
+    HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
+    HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, d_outrow, S, d_om, st));
     std::vector<uint64_t> ok(m), om((size_t)m * S);
     std::vector<int32_t> okk(m);
     if (m) {

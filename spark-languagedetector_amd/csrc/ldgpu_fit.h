@@ -33,11 +33,10 @@ struct CountParams {
     // Sparse table (the final count table T of ldgpu_counts; pkeys != null,
     // counts == null): the reference's reduceGrams rows (LanguageDetector.
     // scala:57-65) -- one (gram, language) -> count pair per row, not a dense
-    // row of L counters per gram.  keys[cap] holds the grams with their
-    // presence bits masks[cap][S] (bit l: the pair (gram, l) exists); the pair
-    // table pkeys[pcap] / pcounts[pcap] is keyed (gram slot + 1) << 12 | lang.
-    uint64_t* masks;
-    int32_t S;
+    // row of L counters per gram.  keys[cap] holds the grams with kcnt[cap],
+    // the number of languages each occurs in (its pairs: k of computeProbabilities);
+    // the pair table pkeys[pcap] / pcounts[pcap] is keyed (gram slot + 1) << 12 | lang.
+    uint32_t* kcnt;
     uint64_t* pkeys;
     unsigned long long* pcounts;
     uint32_t pshift;            // pair slot = mix64(pair key) >> pshift
@@ -226,8 +225,11 @@ hipError_t launch_derive_pairs_level(const CountParams& t1, uint32_t lb, uint64_
                                      const CountParams& to, int ablate, hipStream_t stream);
 // the same for a two-word pair table T1 (K = 2: wide table, one counter,
 // lo = packed key, hi = lang + 1)
+// nx.khi != null (split): the prefixes and T1's shorter entries go to nx, the
+// next level's T1 (t1w is then read only); else the prefixes go to t1w
 hipError_t launch_derive_pairs2_level(const WideCountParams& t1w, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
-                                      const CountParams& to, int ablate, hipStream_t stream);
+                                      const CountParams& to, const WideCountParams& nx, int ablate,
+                                      hipStream_t stream);
 // out[t] += occupied T1 slots of t-byte keys (16 counters); pairs: 0 dense
 // T1, 1 one-word pairs (lb language bits), 2 two-word pairs
 hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, int pairs, uint32_t lb,
@@ -240,8 +242,8 @@ hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const in
 // ---- FIT of gram lengths beyond kMaxWideGram (ldgpu_long.hip): keys of any
 // length in a table of their own -- a slot per gram holds the hash of its
 // bytes and length (gen_hash, ldgpu_common.h) and where its bytes sit in the
-// table's key arena -- with presence masks and a pair table of (gram slot,
-// language) -> count as the sparse T (CountParams).  The host sizes every
+// table's key arena -- with a pair table of (gram slot, language) -> count as
+// the sparse T (CountParams).  The host sizes every
 // table and the arena for a launch up front, so an insert always finds room.
 struct alignas(16) LongSlot {
     uint64_t h;       // gen_hash | 1 (0: empty)
@@ -251,8 +253,6 @@ constexpr uint64_t kLongLenBits = 24;  // gram lengths < 2^24
 
 struct LongCountParams {
     LongSlot* slots;
-    uint64_t* masks;            // [cap][S] presence bits
-    int32_t S;
     uint32_t shift;             // slot = h >> shift
     uint64_t mask;              // cap - 1
     unsigned long long* size;   // distinct grams
@@ -276,22 +276,36 @@ hipError_t launch_long_count(const LongCountParams& p, const uint8_t* bytes, con
 // add n (key, language, count) triples: key i = kbytes[koff[i] .. koff[i + 1])
 hipError_t launch_long_add(const LongCountParams& p, const uint8_t* kbytes, const int64_t* koff, const int32_t* lang,
                            const unsigned long long* cnt, int64_t n, hipStream_t stream);
-// grow: slots (and masks) of `from` into `to`, remap[old] = new slot
+// grow: slots of `from` into `to`, remap[old] = new slot
 hipError_t launch_long_rehash(const LongCountParams& from, const LongCountParams& to, uint64_t from_cap,
                               uint64_t* remap, hipStream_t stream);
 
-// ---- device probability / top-K (computeProbabilities + filterTopGrams)
-// presence: compact occupied slots into keys[n], masks[n][S] (count > 0 per
-// language) and k[n] (= popcount), and histogram hist[l][k] over (gram, l).
-hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
-                           int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream);
-// select: chosen[j] = 1 when k_j < kstar[l] for some l in the gram's mask;
-// grams with k_j == kstar[l] (need[l] > 0) are appended as threshold
-// candidates (lang, sort key, index).
-hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
-                         const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
-                         uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream);
-// chosen[idx[i]] = 1
+// ---- top-K over the sparse table's pairs (computeProbabilities +
+// filterTopGrams, LanguageDetector.scala:75-132): the grams compacted
+// (out_keys[o], out_k[o] = k, rowof[slot] = o); the (language, k) histogram,
+// the selection and the chosen rows' presence masks all from the pairs
+hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint32_t* rowof,
+                            unsigned long long* out_n, hipStream_t stream);
+hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const int32_t* ks, int L,
+                            unsigned int* hist, hipStream_t stream);
+// chosen[j] = 1 when the gram is below its language's threshold class; the
+// threshold-class pairs (need[l] > 0) appended as candidates (lang, sort key, j)
+hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
+                              const int32_t* ks, const int32_t* kstar, const int32_t* need, uint8_t* chosen,
+                              int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n,
+                              hipStream_t stream);
+// the chosen rows: out_keys[r], out_k[r], outrow[j] = r (0xffffffff: not
+// chosen); rows from out_cap on are counted in out_n, not written
+hipError_t launch_gather_rows(int64_t n, const uint8_t* chosen, const uint64_t* keys, const int32_t* ks,
+                              uint64_t* out_keys, int32_t* out_k, uint32_t* outrow, unsigned long long* out_n,
+                              int64_t out_cap, hipStream_t stream);
+// presence masks: masks[row][l / 64] |= bit l for every pair, row = outrow[rowof[g]]
+// (outrow null: rowof[g]); masks zeroed by the caller
+hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow, int S,
+                             uint64_t* masks, hipStream_t stream);
+
+// threshold-class ties: per language the need[l] smallest (length, bytes)
+// candidates get chosen[idx] = 1
 // sorted_keys (nullable): instead of marking, write the candidates' sort keys
 // in (language, key) order (the distributed top-K takes each segment's prefix)
 hipError_t launch_topk_candidates(int64_t cn, int L, const int32_t* cand_lang, const uint64_t* cand_key,
@@ -316,9 +330,5 @@ hipError_t launch_owner_pair_scatter(const CountParams& p, uint64_t cap, uint32_
                                      uint64_t* out, hipStream_t stream);
 hipError_t launch_pairs_add(const CountParams& p, const uint64_t* pairs, int64_t n, hipStream_t stream);
 hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream);
-// gather the chosen grams: out_keys[m], out_masks[m][S], out_k[m]
-hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,
-                                const int32_t* ks, uint64_t* out_keys, uint64_t* out_masks, int32_t* out_k,
-                                unsigned long long* out_n, hipStream_t stream);
 
 }  // namespace ldgpu

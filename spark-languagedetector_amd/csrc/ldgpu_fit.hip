@@ -149,8 +149,8 @@ __device__ __forceinline__ int64_t pair_find_or_insert(const CountParams& p, uin
     return -1;
 }
 
-// c of (key, lang) into the sparse table: the gram's slot (its presence bit
-// set when the pair is new), then the pair's counter.  An add that reaches a
+// c of (key, lang) into the sparse table: the gram's slot (its language
+// count up when the pair is new), then the pair's counter.  An add that reaches a
 // probe limit in either table goes to the overflow list as (key, lang, c) --
 // re-adding it finds the gram if it was placed.  A zero count adds nothing
 // (a reduceGrams row has count >= 1).  Returns new gram | new pair << 32.
@@ -163,9 +163,7 @@ __device__ __forceinline__ uint64_t sparse_add_q(const CountParams& p, uint64_t 
         s = pair_find_or_insert(p, ((uint64_t)(g + 1) << kPairLangBits) | (uint64_t)lang, new_pair);
         if (s >= 0) {
             atomicAdd(&p.pcounts[s], c);
-            if (new_pair)
-                atomicOr(reinterpret_cast<unsigned long long*>(&p.masks[(size_t)g * p.S + (lang >> 6)]),
-                         1ull << (lang & 63));
+            if (new_pair) atomicAdd(&p.kcnt[g], 1u);
         }
     }
     if (s < 0) {
@@ -449,7 +447,7 @@ __global__ void sparse_rehash_kernel(const CountParams from, const CountParams t
     uint64_t s = mix64(key) >> to.shift;
     while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.keys[s]), 0ull, (unsigned long long)key) != 0ull)
         s = (s + 1) & to.mask;
-    for (int w = 0; w < from.S; ++w) to.masks[s * to.S + w] = from.masks[i * from.S + w];
+    to.kcnt[s] = from.kcnt[i];
     remap[i] = s;
 }
 
@@ -650,120 +648,17 @@ hipError_t launch_compact(const CountParams& p, uint64_t cap, uint64_t* out_keys
 // language mask of g.  filterTopGrams ranks, per language l, ALL grams by v_l
 // descending and keeps K (:113-119); since log(1 + 1/k) falls with k, the
 // order is: present grams by k ascending, then absent ones; ties by the
-// build's (length, bytes) rule.  The device computes masks, k and the
-// (language, k) histogram; the host turns the histogram into a threshold
-// class per language; the device flags every gram below a threshold and
-// emits the threshold-class candidates, whose (length, bytes) order the host
-// resolves with nth_element.
+// build's (length, bytes) rule.  From the sparse table's pairs the device
+// builds the (language, k) histogram (k kept per gram by the count kernels);
+// the host turns it into a threshold class per language; the device flags
+// every gram below a threshold and sorts the threshold-class candidates by
+// (language, length, bytes), then builds the chosen rows' masks.
 namespace ldgpu {
 namespace {
-
-// grid-stride over the table in chunks of kScanThreads slots; the (language,
-// k) histogram in LDS (L <= 88), flushed once per block
-__global__ __launch_bounds__(kScanThreads) void presence_kernel(const CountParams p, uint64_t cap, int S,
-                                                                uint64_t* out_keys, uint64_t* out_masks,
-                                                                int32_t* out_k, unsigned long long* out_n,
-                                                                unsigned int* hist) {
-    extern __shared__ unsigned int lhist[];
-    __shared__ unsigned int wcnt[kScanThreads / 64];
-    __shared__ unsigned long long bbase;
-    const int L = p.L;
-    const bool lds_hist = L <= 88;  // L * (L + 1) * 4 B <= 31 KiB
-    if (lds_hist) {
-        for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x) lhist[i] = 0u;
-        __syncthreads();
-    }
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < cap; c0 += (uint64_t)gridDim.x * kScanThreads) {
-        const uint64_t i = c0 + threadIdx.x;
-        const bool occ = i < cap && p.keys[i] != kEmpty;
-        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
-        if (!occ) continue;
-        const unsigned long long* row = p.counts + i * L;
-        // the row's presence bits, 64 languages a word (sparse T: kept per
-        // gram; dense: 8 counters per batch of independent loads); then the
-        // histogram from the bits
-        int k = 0;
-        for (int s = 0; s < S; ++s) {
-            const int l0 = 64 * s, nl = min(64, L - l0);
-            uint64_t w = 0;
-            if (p.masks) w = p.masks[i * p.S + s];
-            else for (int b0 = 0; b0 < nl; b0 += 8) {
-                unsigned long long v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = b0 + u < nl ? row[l0 + b0 + u] : 0ull;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) w |= (uint64_t)(v[u] != 0ull) << (b0 + u);
-            }
-            out_masks[o * S + s] = w;
-            k += __popcll(w);
-        }
-        out_keys[o] = p.keys[i];
-        out_k[o] = k;
-        for (int s = 0; s < S; ++s) {
-            uint64_t w = out_masks[o * S + s];
-            while (w) {
-                const int l = 64 * s + __builtin_ctzll(w);
-                w &= w - 1;
-                if (lds_hist)
-                    atomicAdd(&lhist[l * (L + 1) + k], 1u);
-                else
-                    atomicAdd(&hist[l * (L + 1) + k], 1u);
-            }
-        }
-    }
-    if (lds_hist) {
-        __syncthreads();
-        for (int t = threadIdx.x; t < L * (L + 1); t += blockDim.x)
-            if (lhist[t]) atomicAdd(&hist[t], lhist[t]);
-    }
-}
-
-__global__ void select_kernel(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
-                              const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
-                              uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const int k = ks[j];
-    uint8_t ch = 0;
-    for (int s = 0; s < S; ++s) {
-        uint64_t w = masks[j * S + s];
-        while (w) {
-            const int l = s * 64 + __builtin_ctzll(w);
-            w &= w - 1;
-            if (k < kstar[l]) {
-                ch = 1;
-            } else if (k == kstar[l] && need[l] > 0) {
-                const unsigned int at = atomicAdd(cand_n, 1u);
-                cand_lang[at] = l;
-                cand_key[at] = sort_key(keys[j]);
-                cand_idx[at] = (uint32_t)j;
-            }
-        }
-    }
-    chosen[j] = ch;
-}
 
 __global__ void mark_kernel(const uint32_t* idx, int64_t n, uint8_t* chosen) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) chosen[idx[i]] = 1;
-}
-
-__global__ __launch_bounds__(kScanThreads) void gather_chosen_kernel(int64_t n, int S, const uint8_t* chosen,
-                                                                     const uint64_t* keys, const uint64_t* masks,
-                                                                     const int32_t* ks, uint64_t* out_keys,
-                                                                     uint64_t* out_masks, int32_t* out_k,
-                                                                     unsigned long long* out_n) {
-    __shared__ unsigned int wcnt[kScanThreads / 64];
-    __shared__ unsigned long long bbase;
-    for (int64_t c0 = (int64_t)blockIdx.x * kScanThreads; c0 < n; c0 += (int64_t)gridDim.x * kScanThreads) {
-        const int64_t j = c0 + threadIdx.x;
-        const bool c = j < n && chosen[j];
-        const unsigned long long o = block_compact(c, out_n, wcnt, &bbase);
-        if (!c) continue;
-        out_keys[o] = keys[j];
-        out_k[o] = ks[j];
-        for (int s = 0; s < S; ++s) out_masks[o * S + s] = masks[j * S + s];
-    }
 }
 
 unsigned grid_of(int64_t n, int b) { return (unsigned)std::max<int64_t>(1, (n + b - 1) / b); }
@@ -787,6 +682,103 @@ __global__ void cand_mark_kernel(int64_t n, const uint32_t* lang_sorted, const u
     if (i >= n) return;
     const uint32_t l = lang_sorted[i];
     if (i - seg_start[l] < (int64_t)need[l]) chosen[cand_idx[perm[i]]] = 1;
+}
+
+// ---- top-K over the sparse table's pairs
+__global__ __launch_bounds__(kScanThreads) void gram_rows_kernel(const CountParams p, uint64_t cap, uint64_t* out_keys,
+                                                                 int32_t* out_k, uint32_t* rowof,
+                                                                 unsigned long long* out_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < cap; c0 += (uint64_t)gridDim.x * kScanThreads) {
+        const uint64_t i = c0 + threadIdx.x;
+        const bool occ = i < cap && p.keys[i] != kEmpty;
+        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
+        if (!occ) continue;
+        out_keys[o] = p.keys[i];
+        out_k[o] = (int32_t)p.kcnt[i];
+        rowof[i] = (uint32_t)o;
+    }
+}
+
+__device__ __forceinline__ uint32_t pair_lang(uint64_t pk) { return (uint32_t)(pk & ((1ull << kPairLangBits) - 1ull)); }
+__device__ __forceinline__ uint64_t pair_slot(uint64_t pk) { return (pk >> kPairLangBits) - 1ull; }
+
+// (language, k) histogram: in LDS for L <= 88 (L (L + 1) counters), flushed
+// once per block
+__global__ __launch_bounds__(256) void pair_hist_kernel(const CountParams p, uint64_t pcap, const uint32_t* rowof,
+                                                        const int32_t* ks, int L, unsigned int* hist) {
+    extern __shared__ unsigned int lh[];
+    const bool lds = L <= 88;
+    if (lds) {
+        for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x) lh[i] = 0u;
+        __syncthreads();
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pcap; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t pk = p.pkeys[i];
+        if (pk == kEmpty) continue;
+        const uint32_t l = pair_lang(pk);
+        const int k = ks[rowof[pair_slot(pk)]];
+        if (lds) atomicAdd(&lh[l * (L + 1) + k], 1u);
+        else atomicAdd(&hist[l * (L + 1) + k], 1u);
+    }
+    if (lds) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x)
+            if (lh[i]) atomicAdd(&hist[i], lh[i]);
+    }
+}
+
+__global__ void pair_select_kernel(const CountParams p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
+                                   const int32_t* ks, const int32_t* kstar, const int32_t* need, uint8_t* chosen,
+                                   int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= pcap) return;
+    const uint64_t pk = p.pkeys[i];
+    if (pk == kEmpty) return;
+    const uint32_t l = pair_lang(pk);
+    const uint32_t j = rowof[pair_slot(pk)];
+    const int k = ks[j];
+    if (k < kstar[l]) {
+        chosen[j] = 1;
+    } else if (k == kstar[l] && need[l] > 0) {
+        const unsigned int at = atomicAdd(cand_n, 1u);
+        cand_lang[at] = (int32_t)l;
+        cand_key[at] = sort_key(keys[j]);
+        cand_idx[at] = j;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void gather_rows_kernel(int64_t n, const uint8_t* chosen,
+                                                                   const uint64_t* keys, const int32_t* ks,
+                                                                   uint64_t* out_keys, int32_t* out_k,
+                                                                   uint32_t* outrow, unsigned long long* out_n,
+                                                                   int64_t out_cap) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (int64_t c0 = (int64_t)blockIdx.x * kScanThreads; c0 < n; c0 += (int64_t)gridDim.x * kScanThreads) {
+        const int64_t j = c0 + threadIdx.x;
+        const bool c = j < n && chosen[j];
+        const unsigned long long o = block_compact(c, out_n, wcnt, &bbase);
+        if (j >= n) continue;
+        outrow[j] = c && (int64_t)o < out_cap ? (uint32_t)o : 0xffffffffu;
+        if (!c || (int64_t)o >= out_cap) continue;  // more than out_cap: the caller fails
+        out_keys[o] = keys[j];
+        out_k[o] = ks[j];
+    }
+}
+
+__global__ void pair_masks_kernel(const CountParams p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow,
+                                  int S, uint64_t* masks) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= pcap) return;
+    const uint64_t pk = p.pkeys[i];
+    if (pk == kEmpty) return;
+    const uint32_t l = pair_lang(pk);
+    uint32_t r = rowof[pair_slot(pk)];
+    if (outrow) r = outrow[r];
+    if (r == 0xffffffffu) return;
+    atomicOr(reinterpret_cast<unsigned long long*>(&masks[(size_t)r * S + (l >> 6)]), 1ull << (l & 63));
 }
 
 // ---- multi-GPU merge: owner partition of the table (ldgpu_counts_merge)
@@ -880,6 +872,48 @@ __global__ void gather_u64_kernel(int64_t n, const uint32_t* idx, const uint64_t
 
 }  // namespace
 
+hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint32_t* rowof,
+                            unsigned long long* out_n, hipStream_t stream) {
+    hipLaunchKernelGGL(gram_rows_kernel, dim3(scan_grid(cap)), dim3(kScanThreads), 0, stream, p, cap, out_keys, out_k,
+                       rowof, out_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const int32_t* ks, int L,
+                            unsigned int* hist, hipStream_t stream) {
+    const size_t lds = L <= 88 ? (size_t)L * (L + 1) * 4 : 0;
+    const unsigned g = (unsigned)std::min<uint64_t>(4096, (pcap + 255) / 256);
+    hipLaunchKernelGGL(pair_hist_kernel, dim3(g), dim3(256), lds, stream, p, pcap, rowof, ks, L, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
+                              const int32_t* ks, const int32_t* kstar, const int32_t* need, uint8_t* chosen,
+                              int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n,
+                              hipStream_t stream) {
+    if (pcap == 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_select_kernel, dim3(grid_of((int64_t)pcap, 256)), dim3(256), 0, stream, p, pcap, rowof,
+                       keys, ks, kstar, need, chosen, cand_lang, cand_key, cand_idx, cand_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(int64_t n, const uint8_t* chosen, const uint64_t* keys, const int32_t* ks,
+                              uint64_t* out_keys, int32_t* out_k, uint32_t* outrow, unsigned long long* out_n,
+                              int64_t out_cap, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(scan_grid((uint64_t)n)), dim3(kScanThreads), 0, stream, n, chosen, keys,
+                       ks, out_keys, out_k, outrow, out_n, out_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow, int S,
+                             uint64_t* masks, hipStream_t stream) {
+    if (pcap == 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_masks_kernel, dim3(grid_of((int64_t)pcap, 256)), dim3(256), 0, stream, p, pcap, rowof,
+                       outrow, S, masks);
+    return hipGetLastError();
+}
+
 hipError_t launch_owner_count(const CountParams& p, uint64_t cap, uint32_t world, unsigned long long* n_of,
                               hipStream_t stream) {
     hipLaunchKernelGGL(owner_count_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap, world, n_of);
@@ -918,23 +952,6 @@ hipError_t launch_mark_threshold(int64_t n, const int32_t* cand_lang, const uint
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(mark_threshold_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, cand_lang, cand_key,
                        cand_idx, thr, chosen);
-    return hipGetLastError();
-}
-
-hipError_t launch_presence(const CountParams& p, uint64_t cap, int S, uint64_t* out_keys, uint64_t* out_masks,
-                           int32_t* out_k, unsigned long long* out_n, unsigned int* hist, hipStream_t stream) {
-    const size_t lds = p.L <= 88 ? (size_t)p.L * (p.L + 1) * 4 : 0;
-    hipLaunchKernelGGL(presence_kernel, dim3(scan_grid(cap)), dim3(kScanThreads), lds, stream, p, cap, S, out_keys, out_masks,
-                       out_k, out_n, hist);
-    return hipGetLastError();
-}
-
-hipError_t launch_select(int64_t n, int L, int S, const uint64_t* keys, const uint64_t* masks, const int32_t* ks,
-                         const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
-                         uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(select_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, L, S, keys, masks, ks, kstar,
-                       need, chosen, cand_lang, cand_key, cand_idx, cand_n);
     return hipGetLastError();
 }
 
@@ -998,15 +1015,6 @@ hipError_t launch_topk_candidates(int64_t cn, int L, const int32_t* cand_lang, c
 hipError_t launch_mark(const uint32_t* idx, int64_t n, uint8_t* chosen, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(mark_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, idx, n, chosen);
-    return hipGetLastError();
-}
-
-hipError_t launch_gather_chosen(int64_t n, int S, const uint8_t* chosen, const uint64_t* keys, const uint64_t* masks,
-                                const int32_t* ks, uint64_t* out_keys, uint64_t* out_masks, int32_t* out_k,
-                                unsigned long long* out_n, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_chosen_kernel, dim3(scan_grid((uint64_t)n)), dim3(kScanThreads), 0, stream, n, S, chosen,
-                       keys, masks, ks, out_keys, out_masks, out_k, out_n);
     return hipGetLastError();
 }
 
@@ -2095,10 +2103,16 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
 }
 
 // the same for a two-word pair table T1 (K = 2 records: a wide table with
-// one counter, lo = the window's packed key, hi = lang + 1 | kDerived)
+// one counter, lo = the window's packed key, hi = lang + 1 | kDerived).
+// Split (nx.khi set): the level's prefixes and the entries shorter than the
+// level go to nx, a fresh table for the levels below, so T1 never holds more
+// than two levels' entries at once (a 1 GB fit at L = 200 holds ~1.5G pairs
+// per level).
 __global__ __launch_bounds__(256) void derive_pairs2_level_kernel(const WideCountParams t1w, uint64_t s0, uint64_t s1,
                                                                   int lev, uint32_t mt, const CountParams to,
-                                                                  int ablate) {
+                                                                  const WideCountParams nx, int ablate) {
+    const bool split = nx.khi != nullptr;
+    const WideCountParams& dst = split ? nx : t1w;
     uint64_t n_to = 0;
     unsigned int n_t1 = 0;
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
@@ -2107,17 +2121,20 @@ __global__ __launch_bounds__(256) void derive_pairs2_level_kernel(const WideCoun
         if (hi == kEmpty) continue;
         const uint64_t key = t1w.klo[s];
         const int klen = (int)(key >> 56);
-        if (klen != lev) continue;
+        if (klen != lev) {
+            if (split && klen < lev) n_t1 += wide_add_q(nx, key, hi, 0, t1w.counts[s]);
+            continue;
+        }
         const unsigned long long c = t1w.counts[s];
         const int lang = (int)((hi & ~kDerived) - 1ull);
         if (mt && !(LDGPU_DIAG && (ablate & 1))) n_to += t_add_q(to, key, lang, c * mt);
         const int n = lev - 1;
         if (n >= 1 && !(LDGPU_DIAG && (ablate & 2)))
-            n_t1 += wide_add_q(t1w, (key & byte_mask(n)) | ((uint64_t)n << 56), ((uint64_t)lang + 1ull) | kDerived, 0,
+            n_t1 += wide_add_q(dst, (key & byte_mask(n)) | ((uint64_t)n << 56), ((uint64_t)lang + 1ull) | kDerived, 0,
                                c);
     }
     t_flush(to, n_to);
-    flush_new_keys(t1w.size, n_t1);
+    flush_new_keys(dst.size, n_t1);
 }
 
 // occupied T1 slots per key length (one-word and wide tables)
@@ -2250,10 +2267,12 @@ hipError_t launch_len_hist(const CountParams& t1, const WideCountParams& t1w, in
 }
 
 hipError_t launch_derive_pairs2_level(const WideCountParams& t1w, uint64_t s0, uint64_t s1, int lev, uint32_t mt,
-                                      const CountParams& to, int ablate, hipStream_t stream) {
+                                      const CountParams& to, const WideCountParams& nx, int ablate,
+                                      hipStream_t stream) {
     if (s1 <= s0) return hipSuccess;
     const unsigned g = (unsigned)std::min<uint64_t>(16384, (s1 - s0 + 255) / 256);
-    hipLaunchKernelGGL(derive_pairs2_level_kernel, dim3(g), dim3(256), 0, stream, t1w, s0, s1, lev, mt, to, ablate);
+    hipLaunchKernelGGL(derive_pairs2_level_kernel, dim3(g), dim3(256), 0, stream, t1w, s0, s1, lev, mt, to, nx,
+                       ablate);
     return hipGetLastError();
 }
 

@@ -11,8 +11,8 @@
 // claims the slot (CAS on the hash word, then the bytes, then the meta word
 // with release order); a reader that meets the slot's hash waits for the meta
 // word, then compares length and bytes.  Counts go to a pair table keyed
-// (slot + 1) << 12 | lang with one u64 counter, and a new pair sets its
-// presence bit in the slot's mask words (as the sparse T of ldgpu_fit.hip).
+// (slot + 1) << 12 | lang with one u64 counter (as the sparse T of
+// ldgpu_fit.hip).
 // Integer adds are order-free: the counts are bit-exact in any schedule.
 // The host sizes the slots, the pair table and the arena for a launch's
 // windows before it runs, so an insert always finds room.
@@ -88,9 +88,6 @@ __device__ bool long_pair_add(const LongCountParams& p, int64_t g, int lang, uns
         }
         if (hit) {
             atomicAdd(&p.pcounts[s], c);
-            if (fresh)
-                atomicOr(reinterpret_cast<unsigned long long*>(&p.masks[(size_t)g * p.S + (lang >> 6)]),
-                         1ull << (lang & 63));
             return fresh;
         }
         s = (s + 1) & p.pmask;
@@ -171,7 +168,6 @@ __global__ void long_rehash_kernel(const LongCountParams from, const LongCountPa
     while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.slots[s].h), 0ull, (unsigned long long)e.h) != 0ull)
         s = (s + 1) & to.mask;
     to.slots[s].meta = e.meta;
-    for (int w = 0; w < from.S; ++w) to.masks[s * to.S + w] = from.masks[i * from.S + w];
     remap[i] = s;
 }
 

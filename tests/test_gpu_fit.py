@@ -267,6 +267,7 @@ def test_config3_shape_counts_and_table():
     ("product", {}),                                         # FIT v4, the table's own record form: one batch
     ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v4: many small batches
     ("diag", {"LDGPU_FIT_K": "2"}),                          # two-word records (any L, grams <= 7 bytes)
+    ("diag", {"LDGPU_FIT_K": "2", "LDGPU_FIT_DERIVE_INPLACE": "1"}),  # ... one T1 for every derive level
     ("diag", {"LDGPU_FIT_K": "3", "LDGPU_FIT_BATCH_WINDOWS": "50000"}),  # three-word records, several batches
     ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "700"}),            # batches of one document (most are longer)
     ("diag", {"LDGPU_FIT_LEGACY": "1"}),                     # round-1 single-pass atomic kernels (A/B only)
