@@ -1119,7 +1119,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
             filter[b0 >> 5] |= 1u << (b0 & 31);
         } else if (kl == 2) {
             const uint32_t b01 = (uint32_t)(kw & 0xffff);
-            filter[kBmp1Words + (b01 >> 5)] |= 1u << (b01 & 31);
+            filter[kBmp1Words + bmp2_word(b01)] |= 1u << (b01 & 31);
         } else {
             const uint32_t lo = (uint32_t)kw;
             const uint32_t hi = (uint32_t)(kw >> 32) & ((1u << (8 * std::min(3, std::max(0, kl - 4)))) - 1u);
@@ -1206,7 +1206,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
             for (uint32_t wd = 0; wd < 2048; ++wd) {
                 base2[wd] = (uint16_t)lang2.size();
                 for (uint32_t b = 0; b < 32; ++b)
-                    if ((filter[kBmp1Words + wd] >> b) & 1u) lang2.push_back(lang2of[wd * 32 + b]);
+                    if ((filter[kBmp1Words + wd] >> b) & 1u) lang2.push_back(lang2of[bmp2_unword(wd) * 32 + b]);
             }
             const uint32_t dwords = 64u + 1024u + (uint32_t)((lang2.size() + 16) / 16) * 4u;  // uint4-padded
             if (score_lds_bytes(S, 3, image_words + dwords) * 2 <= 163840) {
@@ -2471,18 +2471,31 @@ int derive_pending(ldgpu_counts* c) {
         }
     }
     // two-word pair T1 (K = 2): each level writes its prefixes and the shorter
-    // entries into a fresh table (derive_pairs2_level_kernel's split), sized
-    // for all of them, and T1 is freed after the level: a level's scan reads
-    // only the entries still to derive, and T1 never holds the grown table
-    // next to the old one (diagnostics: LDGPU_FIT_DERIVE_INPLACE keeps one T1)
+    // entries into another table (derive_pairs2_level_kernel's split), sized
+    // for all of them: a level's scan reads only the entries still to derive,
+    // and T1 never holds a grown table next to the old one.  The two tables
+    // alternate (the one read by a level is cleared and written by the next,
+    // when it holds them: no allocation per level -- 51 GB at L = 200 on 1 GB
+    // of corpus).  Diagnostics: LDGPU_FIT_DERIVE_INPLACE keeps one T1.
     const bool split = pairs == 2 && !diag_env("LDGPU_FIT_DERIVE_INPLACE");
     struct Owned {
         ldgpu_counts* p = nullptr;
         ~Owned() {
             if (p) counts_free(p);
         }
+        void reset(ldgpu_counts* q) {
+            if (p) counts_free(p);
+            p = q;
+        }
+    };
+    Owned spare;  // the table the previous level read
+    const bool trace = diag_env("LDGPU_FIT_TRACE") != nullptr;
+    auto now_ms = [] {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
     for (int lev = maxg; lev >= 1; --lev) {
+        const double t_lev = trace ? now_ms() : 0.0;
+        int chunks = 0;
         const uint32_t mt = mult[lev];
         const int n = lev - 1;
         if (!cnt[lev] || (!mt && n < 1)) continue;
@@ -2493,8 +2506,21 @@ int derive_pending(ldgpu_counts* c) {
         if (n >= 1 && split) {
             uint64_t keep = cnt[lev];
             for (int j = 1; j < lev; ++j) keep += cnt[j];
-            if (int rc = counts_new(c->ctx, 1, c->G, c->nG, 1 << 12, &nx.p)) return rc;
-            if (int rc = wide_ensure(nx.p, keep)) return rc;
+            ldgpu_counts* sp = spare.p;
+            if (sp && sp->wcap && (double)keep <= load_limit(sp->wcap, 16ull + 8ull * (uint64_t)sp->L) * (double)sp->wcap) {
+                // the spare, emptied (a key word of 0 is an empty slot; the
+                // low words are written before a slot is published)
+                HIP_TRY(hipMemsetAsync(sp->d_whi, 0, sp->wcap * sizeof(uint64_t), st));
+                HIP_TRY(hipMemsetAsync(sp->d_wcounts, 0, sp->wcap * (size_t)sp->L * sizeof(unsigned long long), st));
+                HIP_TRY(hipMemsetAsync(sp->d_wsize, 0, sizeof(unsigned long long), st));
+                sp->wsize = 0;
+                nx.p = sp;
+                spare.p = nullptr;
+            } else {
+                spare.reset(nullptr);
+                if (int rc = counts_new(c->ctx, 1, c->G, c->nG, 1 << 12, &nx.p)) return rc;
+                if (int rc = wide_ensure(nx.p, keep)) return rc;
+            }
             cnt[n] += cnt[lev];
         } else if (n >= 1) {
             if (n <= kMaxGram && pairs != 2) {
@@ -2554,11 +2580,18 @@ int derive_pending(ldgpu_counts* c) {
             if (int rc = after_batch(c)) return rc;
             if (int rc = after_batch(t, false)) return rc;
             s0 += slots;
+            ++chunks;
         }
-        if (nx.p) {  // the next level's T1
-            counts_free(t);
+        if (nx.p) {  // the next level's T1; this one the spare
+            spare.reset(t);
             c->pend = t = nx.p;
             nx.p = nullptr;
+        }
+        if (trace) {
+            HIP_TRY(hipStreamSynchronize(st));
+            fprintf(stderr, "fit derive level %d: %llu entries, %d chunks, %.3f ms (T %llu grams / %llu slots, %llu pairs / %llu)\n",
+                    lev, cnt[lev], chunks, now_ms() - t_lev, (unsigned long long)c->size, (unsigned long long)c->cap,
+                    (unsigned long long)c->psize, (unsigned long long)c->pcap);
         }
     }
     return LDGPU_OK;
@@ -2922,8 +2955,8 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     }
     // every gram length from the call's maximal windows; T1 back to the
     // context's block cache (the next call starts an empty one, sized by this)
+    c->pend_hint = (int64_t)(c->pend->size + c->pend->wsize);  // (before the derive's levels replace T1)
     const int rc = derive_pending(c);
-    c->pend_hint = (int64_t)(c->pend->size + c->pend->wsize);
     counts_free(c->pend);
     c->pend = nullptr;
     if (rc) return rc;
@@ -4534,6 +4567,44 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
     HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
     HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, d_outrow, S, d_om, st));
+    std::vector<double> w(L + 1, 0.0);
+    for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
+    if (!cm || cm->world == 1) {
+        // one rank: the rows sorted by (length, bytes) on the device (radix
+        // sort of the sort keys, then a gather), copied back in table order
+        uint64_t *d_sk, *d_ok2, *d_om2;
+        unsigned long long* d_idx;
+        int32_t* d_okk2;
+        const size_t mm = std::max<unsigned long long>(m, 1);
+        HIP_TRY(db.alloc(&d_sk, mm));
+        HIP_TRY(db.alloc(&d_idx, mm));
+        HIP_TRY(db.alloc(&d_ok2, mm));
+        HIP_TRY(db.alloc(&d_okk2, mm));
+        HIP_TRY(db.alloc(&d_om2, mm * S));
+        HIP_TRY(launch_sort_keys_of((int64_t)m, d_ok, d_sk, d_idx, st));
+        HIP_TRY(sort_pairs_u64((int64_t)m, d_sk, d_idx, 64, st));
+        HIP_TRY(launch_rows_permute((int64_t)m, S, d_idx, d_ok, d_okk, d_om, d_ok2, d_okk2, d_om2, st));
+        std::vector<uint64_t> out_keys(m);
+        std::vector<int32_t> okk(m);
+        c->tbl_masks.resize((size_t)m * S);
+        if (m) {
+            HIP_TRY(hipMemcpyAsync(out_keys.data(), d_ok2, sizeof(uint64_t) * m, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(c->tbl_masks.data(), d_om2, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(okk.data(), d_okk2, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        c->tbl_vals.resize((size_t)m);
+        for (uint64_t r = 0; r < m; ++r) c->tbl_vals[r] = w[okk[r]];
+        int64_t nb = 0;
+        for (uint64_t k : out_keys) nb += key_len(k);
+        c->tbl_bytes.assign((size_t)std::max<int64_t>(nb, 1), 0);
+        c->tbl_off.assign(out_keys.size() + 1, 0);
+        write_keys(c, out_keys, c->tbl_bytes.data(), c->tbl_off.data());
+        c->tbl_valid = true;
+        if (n_rows) *n_rows = (int64_t)m;
+        if (key_bytes) *key_bytes = nb;
+        return LDGPU_OK;
+    }
     std::vector<uint64_t> ok(m), om((size_t)m * S);
     std::vector<int32_t> okk(m);
     if (m) {
@@ -4542,7 +4613,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         HIP_TRY(hipMemcpyAsync(okk.data(), d_okk, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
-    if (cm && cm->world > 1) {  // every rank's chosen rows
+    {  // every rank's chosen rows
         std::vector<uint8_t> blob;
         put(blob, ok.data(), ok.size());
         put(blob, om.data(), om.size());
@@ -4563,8 +4634,6 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         }
         m = ok.size();
     }
-    std::vector<double> w(L + 1, 0.0);
-    for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
     std::vector<std::pair<uint64_t, uint64_t>> order(m);
     for (uint64_t i = 0; i < m; ++i) order[i] = {sort_key(ok[i]), i};
     std::sort(order.begin(), order.end());

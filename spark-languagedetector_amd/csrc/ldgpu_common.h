@@ -138,6 +138,23 @@ constexpr uint32_t kBmp1Words = 8;
 constexpr uint32_t kBmp2Words = 2048;
 constexpr uint32_t kBloomBase = kBmp1Words + kBmp2Words;
 
+// The 2-byte bitmap's word of key b0 | b1 << 8 (its bit: b0 & 31).  Word
+// b01 >> 5 puts a wave's consecutive letter pairs on 4 LDS banks (bank = b1
+// mod 4 and b0 >> 5); LDGPU_BMP2_SWZ XORs its low 3 bits with bits 2..4 of b1,
+// so the lanes of an LDS read group spread over all 32 banks by their second
+// byte, while lanes of one (b0 >> 5, b1) still read one word (broadcast).
+#ifndef LDGPU_BMP2_SWZ
+#define LDGPU_BMP2_SWZ 0
+#endif
+__host__ __device__ __forceinline__ uint32_t bmp2_word(uint32_t b01) {
+    const uint32_t w = (b01 >> 5) & 2047u;
+    return LDGPU_BMP2_SWZ ? w ^ ((b01 >> 10) & 7u) : w;
+}
+// the inverse: the keys of physical word wd are (bmp2_unword(wd) << 5) | bit
+__host__ __device__ __forceinline__ uint32_t bmp2_unword(uint32_t wd) {
+    return LDGPU_BMP2_SWZ ? wd ^ ((wd >> 5) & 7u) : wd;
+}
+
 // Candidate queue entry: klen in the top 4 bits, window position below.
 constexpr uint32_t kPosBits = 28;
 constexpr int64_t kMaxDocBytes = (int64_t)1 << kPosBits;

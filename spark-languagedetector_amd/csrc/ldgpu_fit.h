@@ -299,6 +299,13 @@ hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_
 hipError_t launch_gather_rows(int64_t n, const uint8_t* chosen, const uint64_t* keys, const int32_t* ks,
                               uint64_t* out_keys, int32_t* out_k, uint32_t* outrow, unsigned long long* out_n,
                               int64_t out_cap, hipStream_t stream);
+// the chosen rows in (length, bytes) order: sk[i] = sort_key(keys[i]), idx[i]
+// = i (then sort_pairs_u64), and rows r of the permutation gathered
+hipError_t launch_sort_keys_of(int64_t n, const uint64_t* keys, uint64_t* sk, unsigned long long* idx,
+                               hipStream_t stream);
+hipError_t launch_rows_permute(int64_t n, int S, const unsigned long long* idx, const uint64_t* keys, const int32_t* ks,
+                               const uint64_t* masks, uint64_t* out_keys, int32_t* out_k, uint64_t* out_masks,
+                               hipStream_t stream);
 // presence masks: masks[row][l / 64] |= bit l for every pair, row = outrow[rowof[g]]
 // (outrow null: rowof[g]); masks zeroed by the caller
 hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow, int S,

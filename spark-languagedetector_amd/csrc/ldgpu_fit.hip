@@ -739,14 +739,20 @@ __global__ void pair_select_kernel(const CountParams p, uint64_t pcap, const uin
     const uint32_t l = pair_lang(pk);
     const uint32_t j = rowof[pair_slot(pk)];
     const int k = ks[j];
-    if (k < kstar[l]) {
-        chosen[j] = 1;
-    } else if (k == kstar[l] && need[l] > 0) {
-        const unsigned int at = atomicAdd(cand_n, 1u);
-        cand_lang[at] = (int32_t)l;
-        cand_key[at] = sort_key(keys[j]);
-        cand_idx[at] = j;
-    }
+    if (k < kstar[l]) chosen[j] = 1;
+    const bool cand = k == kstar[l] && need[l] > 0;
+    // one counter add per wave (the threshold class can hold most pairs)
+    const uint64_t m = __ballot(cand);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned int base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(cand_n, (unsigned int)__popcll(m));
+    base = __shfl(base, __builtin_ctzll(m));
+    if (!cand) return;
+    const unsigned int at = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
+    cand_lang[at] = (int32_t)l;
+    cand_key[at] = sort_key(keys[j]);
+    cand_idx[at] = j;
 }
 
 __global__ __launch_bounds__(kScanThreads) void gather_rows_kernel(int64_t n, const uint8_t* chosen,
@@ -779,6 +785,24 @@ __global__ void pair_masks_kernel(const CountParams p, uint64_t pcap, const uint
     if (outrow) r = outrow[r];
     if (r == 0xffffffffu) return;
     atomicOr(reinterpret_cast<unsigned long long*>(&masks[(size_t)r * S + (l >> 6)]), 1ull << (l & 63));
+}
+
+__global__ void sort_keys_of_kernel(int64_t n, const uint64_t* keys, uint64_t* sk, unsigned long long* idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    sk[i] = sort_key(keys[i]);
+    idx[i] = (unsigned long long)i;
+}
+
+__global__ void rows_permute_kernel(int64_t n, int S, const unsigned long long* idx, const uint64_t* keys,
+                                    const int32_t* ks, const uint64_t* masks, uint64_t* out_keys, int32_t* out_k,
+                                    uint64_t* out_masks) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t i = idx[r];
+    out_keys[r] = keys[i];
+    out_k[r] = ks[i];
+    for (int s = 0; s < S; ++s) out_masks[(size_t)r * S + s] = masks[i * S + s];
 }
 
 // ---- multi-GPU merge: owner partition of the table (ldgpu_counts_merge)
@@ -903,6 +927,22 @@ hipError_t launch_gather_rows(int64_t n, const uint8_t* chosen, const uint64_t* 
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(gather_rows_kernel, dim3(scan_grid((uint64_t)n)), dim3(kScanThreads), 0, stream, n, chosen, keys,
                        ks, out_keys, out_k, outrow, out_n, out_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_keys_of(int64_t n, const uint64_t* keys, uint64_t* sk, unsigned long long* idx,
+                               hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sort_keys_of_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, keys, sk, idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_permute(int64_t n, int S, const unsigned long long* idx, const uint64_t* keys, const int32_t* ks,
+                               const uint64_t* masks, uint64_t* out_keys, int32_t* out_k, uint64_t* out_masks,
+                               hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rows_permute_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, S, idx, keys, ks, masks,
+                       out_keys, out_k, out_masks);
     return hipGetLastError();
 }
 

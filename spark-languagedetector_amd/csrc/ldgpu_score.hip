@@ -653,7 +653,7 @@ __device__ __forceinline__ void filter_word(const uint32_t* img, uint32_t sh, ui
         w = img[(x.lo[k] >> 5) & 7u];
         bit = bit2 = x.lo[k];
     } else if constexpr (KIND == 2) {
-        w = img[kBmp1Words + ((x.lo[k] >> 5) & 2047u)];
+        w = img[kBmp1Words + bmp2_word(x.lo[k])];
         bit = bit2 = x.lo[k];
     } else if constexpr (KIND == 3) {
         w = f.w3[k];
@@ -834,7 +834,7 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
     } else {
         uint32_t w[kSub];
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) w[k] = img[kBmp1Words + __builtin_amdgcn_ubfe(x.lo[k], 5, 11)];
+        for (int k = 0; k < kSub; ++k) w[k] = img[kBmp1Words + bmp2_word(x.lo[k])];
 #pragma unroll
         for (int k = 0; k < kSub; ++k) {
             // bit (lo & 31) of the word; the offset / width operands of v_bfe
@@ -844,7 +844,7 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
             // hits only (a missing window costs one LDS read, not three)
             lang[k] = 0;
             if (hit[k])
-                lang[k] = l2[b2[__builtin_amdgcn_ubfe(x.lo[k], 5, 11)] +
+                lang[k] = l2[b2[bmp2_word(x.lo[k])] +
                              __builtin_popcount(__builtin_amdgcn_ubfe(w[k], 0, x.lo[k]))];
         }
     }
