@@ -2956,13 +2956,14 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     // every gram length from the call's maximal windows; T1 back to the
     // context's block cache (the next call starts an empty one, sized by this)
     c->pend_hint = (int64_t)(c->pend->size + c->pend->wsize);  // (before the derive's levels replace T1)
+    // the cached top-K table and sparse export describe the table before this
+    // call: invalid from here on, even if the derive fails part way through
+    c->tbl_valid = false;
+    c->sp_valid = false;
     const int rc = derive_pending(c);
     counts_free(c->pend);
     c->pend = nullptr;
-    if (rc) return rc;
-    c->tbl_valid = false;
-    c->sp_valid = false;
-    return LDGPU_OK;
+    return rc;
 }
 
 // Count documents [0, n_docs) of d_offsets / d_lang (h_off / h_lang: the
@@ -3139,6 +3140,8 @@ extern "C" int ldgpu_count_device(ldgpu_counts* c, const uint8_t* d_bytes, int64
     HIP_TRY(hipSetDevice(c->ctx->device));
     hipStream_t st = (hipStream_t)stream;
     if (n_docs == 0) return ok();
+    c->tbl_valid = false;  // a count changes the table, whatever happens below
+    c->sp_valid = false;
     std::vector<int64_t> h_off(n_docs + 1);
     std::vector<int32_t> h_lang(n_docs);
     HIP_TRY(hipMemcpyAsync(h_off.data(), d_offsets, sizeof(int64_t) * (n_docs + 1), hipMemcpyDeviceToHost, st));
@@ -3160,6 +3163,8 @@ extern "C" int ldgpu_count(ldgpu_counts* c, const uint8_t* bytes, const int64_t*
     ldgpu_ctx* x = c->ctx;
     std::lock_guard<std::mutex> lock(x->mu);
     HIP_TRY(hipSetDevice(x->device));
+    c->tbl_valid = false;  // a count changes the table, whatever happens below
+    c->sp_valid = false;
     const int64_t kChunkBytes = 64ll << 20, kChunkDocs = 4ll << 20;
     std::vector<int64_t> off;
     int64_t d0 = 0;
