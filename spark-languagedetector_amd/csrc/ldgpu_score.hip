@@ -1516,7 +1516,14 @@ hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const do
     return hipGetLastError();
 }
 
+// LDGPU_NARROW_VARIANT (tuning builds only, tools/build_variant.sh): just the
+// count-mode, LDS-bloom, one-slice kernels (config 2's), compiled in seconds
+// instead of minutes
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream) {
+#ifdef LDGPU_NARROW_VARIANT
+    if (mode != 3 || !lds_bloom || slices != 1) return hipErrorInvalidValue;
+    return launch_t<1, 3, 0>(p, grid, stream);
+#else
     switch (mode) {
         case 0: return launch_m<0>(p, slices, lds_bloom, grid, stream);
         case 1: return launch_m<1>(p, slices, lds_bloom, grid, stream);
@@ -1524,9 +1531,14 @@ hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_blo
         case 3: return launch_m<3>(p, slices, lds_bloom, grid, stream);
         default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu) {
+#ifdef LDGPU_NARROW_VARIANT
+    if (mode != 3 || !lds_bloom || slices != 1) return hipErrorInvalidValue;
+    return prepare_t<1, 3, 0>(lds_bytes, blocks_per_cu);
+#else
     switch (mode) {
         case 0: return prepare_m<0>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
         case 1: return prepare_m<1>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
@@ -1534,6 +1546,7 @@ hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size
         case 3: return prepare_m<3>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
         default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 }  // namespace ldgpu
