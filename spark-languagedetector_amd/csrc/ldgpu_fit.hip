@@ -49,7 +49,8 @@ unsigned scan_grid(uint64_t n) {
     return (unsigned)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + kScanThreads - 1) / kScanThreads));
 }
 
-__device__ __forceinline__ unsigned long long block_compact(bool occ, unsigned long long* out_n, unsigned int* wcnt,
+template <typename C = unsigned long long>
+__device__ __forceinline__ unsigned long long block_compact(bool occ, C* out_n, unsigned int* wcnt,
                                                             unsigned long long* bbase) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t m = __ballot(occ);
@@ -62,7 +63,7 @@ __device__ __forceinline__ unsigned long long block_compact(bool occ, unsigned l
             wcnt[w] = acc;
             acc += c;
         }
-        *bbase = acc ? atomicAdd(out_n, (unsigned long long)acc) : 0ull;
+        *bbase = acc ? (unsigned long long)atomicAdd(out_n, (C)acc) : 0ull;
     }
     __syncthreads();
     const unsigned long long o = *bbase + wcnt[wave] +
@@ -729,30 +730,37 @@ __global__ __launch_bounds__(256) void pair_hist_kernel(const CountParams p, uin
     }
 }
 
-__global__ void pair_select_kernel(const CountParams p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
-                                   const int32_t* ks, const int32_t* kstar, const int32_t* need, uint8_t* chosen,
-                                   int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= pcap) return;
-    const uint64_t pk = p.pkeys[i];
-    if (pk == kEmpty) return;
-    const uint32_t l = pair_lang(pk);
-    const uint32_t j = rowof[pair_slot(pk)];
-    const int k = ks[j];
-    if (k < kstar[l]) chosen[j] = 1;
-    const bool cand = k == kstar[l] && need[l] > 0;
-    // one counter add per wave (the threshold class can hold most pairs)
-    const uint64_t m = __ballot(cand);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    unsigned int base = 0;
-    if (lane == __builtin_ctzll(m)) base = atomicAdd(cand_n, (unsigned int)__popcll(m));
-    base = __shfl(base, __builtin_ctzll(m));
-    if (!cand) return;
-    const unsigned int at = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
-    cand_lang[at] = (int32_t)l;
-    cand_key[at] = sort_key(keys[j]);
-    cand_idx[at] = j;
+// grid-stride with block-level compaction of the candidates: the threshold
+// class can hold most pairs (config 3: nearly every gram is in one language),
+// and one counter add per wave serialised ~1M atomics on cand_n (47 ms of a
+// 72M-pair table)
+__global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountParams p, uint64_t pcap,
+                                                                   const uint32_t* rowof, const uint64_t* keys,
+                                                                   const int32_t* ks, const int32_t* kstar,
+                                                                   const int32_t* need, uint8_t* chosen,
+                                                                   int32_t* cand_lang, uint64_t* cand_key,
+                                                                   uint32_t* cand_idx, unsigned int* cand_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < pcap; c0 += (uint64_t)gridDim.x * kScanThreads) {
+        const uint64_t i = c0 + threadIdx.x;
+        const uint64_t pk = i < pcap ? p.pkeys[i] : kEmpty;
+        bool cand = false;
+        uint32_t l = 0, j = 0;
+        if (pk != kEmpty) {
+            l = pair_lang(pk);
+            j = rowof[pair_slot(pk)];
+            const int k = ks[j];
+            const int ksl = kstar[l];
+            if (k < ksl) chosen[j] = 1;
+            cand = k == ksl && need[l] > 0;
+        }
+        const unsigned long long at = block_compact<unsigned int>(cand, cand_n, wcnt, &bbase);
+        if (!cand) continue;
+        cand_lang[at] = (int32_t)l;
+        cand_key[at] = sort_key(keys[j]);
+        cand_idx[at] = j;
+    }
 }
 
 __global__ __launch_bounds__(kScanThreads) void gather_rows_kernel(int64_t n, const uint8_t* chosen,
@@ -916,7 +924,7 @@ hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_
                               int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n,
                               hipStream_t stream) {
     if (pcap == 0) return hipSuccess;
-    hipLaunchKernelGGL(pair_select_kernel, dim3(grid_of((int64_t)pcap, 256)), dim3(256), 0, stream, p, pcap, rowof,
+    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid(pcap)), dim3(kScanThreads), 0, stream, p, pcap, rowof,
                        keys, ks, kstar, need, chosen, cand_lang, cand_key, cand_idx, cand_n);
     return hipGetLastError();
 }
@@ -1756,17 +1764,33 @@ __global__ __launch_bounds__(kEmitWaves * 64) void part2_kernel(const PartParams
             if (done) break;
             continue;
         }
-        // gather: record i of the round from its run
-        for (uint32_t i = tid; i < T; i += NT) {
-            int lo = 0;
+        // gather: record i of the round from its run.  A thread's records of
+        // the round (CAP / NT of them) are located first and their loads all
+        // issued before any is used: one memory round trip per round, not one
+        // per record.
+        constexpr int PER = CAP / NT;
+        static_assert(CAP % NT == 0 && PER >= 1, "part2 gather");
+        Rec<K> r[PER];
 #pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (S.roff[lo + step] <= i) lo += step;
-            const Rec<K> r = load_rec<K>(p.rec, S.rstart[lo] + (int64_t)(i - S.roff[lo]));
-            const uint32_t q2 = (uint32_t)(rec_hash<K>(r, p.cb) >> (64 - 2 * kQBits)) & (kQ - 1);
-            store_rec<K>(S.in, i, r);
-            S.q2in[i] = (uint8_t)q2;
-            __hip_atomic_fetch_add(&S.hist[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = (uint32_t)tid + (uint32_t)(u * NT);
+            if (i < T) {
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (S.roff[lo + step] <= i) lo += step;
+                r[u] = load_rec<K>(p.rec, S.rstart[lo] + (int64_t)(i - S.roff[lo]));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = (uint32_t)tid + (uint32_t)(u * NT);
+            if (i < T) {
+                const uint32_t q2 = (uint32_t)(rec_hash<K>(r[u], p.cb) >> (64 - 2 * kQBits)) & (kQ - 1);
+                store_rec<K>(S.in, i, r[u]);
+                S.q2in[i] = (uint8_t)q2;
+                __hip_atomic_fetch_add(&S.hist[q2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
         __syncthreads();
         if (tid < 64) {
