@@ -83,11 +83,16 @@ __device__ __forceinline__ uint64_t kl_key(uint64_t kl, uint32_t lb) {
     return (sent ^ (1ull << (8 * klen))) | ((uint64_t)klen << 56);
 }
 
-// find-or-insert; returns the slot or -1 when the probe limit is reached
-__device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key, bool& new_key) {
-    uint64_t s = mix64(key) >> p.shift;
+// find-or-insert; returns the slot or -1 when the probe limit is reached.
+// PRE: k0 is keys[s] already loaded by the caller (the first probes of a
+// thread's several inserts issued together: one memory round trip for all of
+// them).  A stale k0 is harmless: keys are never removed, an empty one is
+// claimed by CAS (whose result decides), and another key stays there.
+template <bool PRE = false>
+__device__ __forceinline__ int64_t find_or_insert_at(const CountParams& p, uint64_t key, uint64_t s, uint64_t k0,
+                                                     bool& new_key) {
     for (uint32_t probe = 0; probe < p.max_probe; ++probe) {
-        uint64_t k = __hip_atomic_load(&p.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t k = (PRE && probe == 0) ? k0 : __hip_atomic_load(&p.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == key) return (int64_t)s;
         if (k == kEmpty) {
             const unsigned long long old =
@@ -101,6 +106,10 @@ __device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t
         s = (s + 1) & p.mask;
     }
     return -1;
+}
+
+__device__ __forceinline__ int64_t find_or_insert(const CountParams& p, uint64_t key, bool& new_key) {
+    return find_or_insert_at<false>(p, key, fit_hash(key) >> p.shift, 0ull, new_key);
 }
 
 // the table's distinct-key counter: one atomic per ballot of the lanes calling
@@ -131,10 +140,11 @@ __device__ __forceinline__ void flush_new_keys(unsigned long long* size, unsigne
 
 // Sparse table T (CountParams::pkeys): find-or-insert of a pair key in the
 // pair table; the slot or -1 at the probe limit
-__device__ __forceinline__ int64_t pair_find_or_insert(const CountParams& p, uint64_t pk, bool& new_pair) {
-    uint64_t s = mix64(pk) >> p.pshift;
+template <bool PRE = false>
+__device__ __forceinline__ int64_t pair_find_or_insert_at(const CountParams& p, uint64_t pk, uint64_t s, uint64_t k0,
+                                                          bool& new_pair) {
     for (uint32_t probe = 0; probe < p.max_probe; ++probe) {
-        uint64_t k = __hip_atomic_load(&p.pkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t k = (PRE && probe == 0) ? k0 : __hip_atomic_load(&p.pkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == pk) return (int64_t)s;
         if (k == kEmpty) {
             const unsigned long long old =
@@ -148,6 +158,10 @@ __device__ __forceinline__ int64_t pair_find_or_insert(const CountParams& p, uin
         s = (s + 1) & p.pmask;
     }
     return -1;
+}
+
+__device__ __forceinline__ int64_t pair_find_or_insert(const CountParams& p, uint64_t pk, bool& new_pair) {
+    return pair_find_or_insert_at<false>(p, pk, fit_hash(pk) >> p.pshift, 0ull, new_pair);
 }
 
 // c of (key, lang) into the sparse table: the gram's slot (its language
@@ -176,6 +190,22 @@ __device__ __forceinline__ uint64_t sparse_add_q(const CountParams& p, uint64_t 
         }
     }
     return (uint64_t)new_gram | ((uint64_t)new_pair << 32);
+}
+
+// c into (slot sl, lang) of a count table, or (sl < 0: probe limit) into the
+// overflow list
+__device__ __forceinline__ void count_add_slot(const CountParams& p, int64_t sl, uint64_t key, int lang,
+                                               unsigned long long c) {
+    if (sl >= 0) {
+        atomicAdd(&p.counts[(size_t)sl * p.L + lang], c);
+        return;
+    }
+    const unsigned int at = atomicAdd(p.ovf_n, 1u);
+    if (at < p.ovf_cap) {
+        p.ovf_keys[at] = key;
+        p.ovf_lang[at] = lang;
+        p.ovf_cnt[at] = c;
+    }
 }
 
 // add_count without the counter update: returns whether the key is new
@@ -414,7 +444,7 @@ __global__ void rehash_kernel(const CountParams from, const CountParams to, uint
     if (i >= from_cap) return;
     const uint64_t key = from.keys[i];
     if (key == kEmpty) return;
-    uint64_t s = mix64(key) >> to.shift;
+    uint64_t s = fit_hash(key) >> to.shift;
     for (;;) {
         const unsigned long long old =
             atomicCAS(reinterpret_cast<unsigned long long*>(&to.keys[s]), 0ull, (unsigned long long)key);
@@ -445,7 +475,7 @@ __global__ void sparse_rehash_kernel(const CountParams from, const CountParams t
     if (i >= from_cap) return;
     const uint64_t key = from.keys[i];
     if (key == kEmpty) return;
-    uint64_t s = mix64(key) >> to.shift;
+    uint64_t s = fit_hash(key) >> to.shift;
     while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.keys[s]), 0ull, (unsigned long long)key) != 0ull)
         s = (s + 1) & to.mask;
     to.kcnt[s] = from.kcnt[i];
@@ -462,7 +492,7 @@ __global__ void pair_rehash_kernel(const CountParams from, const CountParams to,
         const uint64_t g = (pk >> kPairLangBits) - 1ull;
         pk = ((remap[g] + 1ull) << kPairLangBits) | (pk & ((1ull << kPairLangBits) - 1ull));
     }
-    uint64_t s = mix64(pk) >> to.pshift;
+    uint64_t s = fit_hash(pk) >> to.pshift;
     while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.pkeys[s]), 0ull, (unsigned long long)pk) != 0ull)
         s = (s + 1) & to.pmask;
     to.pcounts[s] = from.pcounts[i];
@@ -1351,11 +1381,11 @@ __device__ __forceinline__ uint32_t rec_lang(const Rec<K>& r, uint32_t lb, uint3
 }
 
 // route hash of the record's (gram, language) pair; K = 1: the T1 pair
-// table's slot hash of the entry (mix64(kl)), so a bucket of records maps to
+// table's slot hash of the entry (fit_hash(kl)), so a bucket of records maps to
 // one contiguous slice of T1 (the merge's inserts stay local)
 template <int K>
 __device__ __forceinline__ uint64_t rec_hash(const Rec<K>& r, uint32_t cb) {
-    if constexpr (K == 1) return mix64(r.w[0] >> cb);
+    if constexpr (K == 1) return fit_hash(r.w[0] >> cb);
     else if constexpr (K == 2) return mix64(r.w[0] + (r.w[1] >> kCntBits) * kGolden);
     else return mix64(r.w[0] ^ mix64(r.w[1] + (r.w[2] >> kCntBits) * kGolden));
 }
@@ -1887,6 +1917,16 @@ constexpr uint32_t kBusy = 1u;
 
 constexpr int kRedRounds = 8;  // reduce: LDS probe rounds per record
 
+// K = 1 reduce probes without divergent branches: every lane issues the round's
+// LDS read, CAS and counter add, a lane with nothing to claim or add aiming
+// them at a dummy word of its own (kRedDummy u64 words after the table) -- the
+// exec-mask save / restore of each divergent branch cost ~1 SALU instruction
+// per record on the CU's one scalar unit
+#ifndef LDGPU_RED_BRANCHLESS
+#define LDGPU_RED_BRANCHLESS 1
+#endif
+constexpr int kRedDummy = kEmitWaves * 64;
+
 template <int K>
 __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartParams p) {
     constexpr int N = agg_slots<K>();
@@ -1898,6 +1938,8 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
     uint32_t* tag = lg + (K == 1 ? 0 : N);
     uint32_t* cnt = tag + (K == 1 ? 0 : N);
     uint32_t* n_out = cnt + N;
+    // K = 1, branch-light probes: a dummy u64 per thread (16-B aligned after n_out)
+    uint64_t* dummy = reinterpret_cast<uint64_t*>(red_smem + (((size_t)N * 12 + 4 + 15) & ~(size_t)15));
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -1933,14 +1975,47 @@ __global__ __launch_bounds__(kEmitWaves * 64, 1) void reduce_kernel(const PartPa
             pend[u] = i < end;
             c[u] = (uint32_t)rec_count<K>(r[u], p.cb);
             const uint64_t h = rec_hash<K>(r[u], p.cb);
-            slot[u] = (uint32_t)(((uint64_t)(uint32_t)h * (uint64_t)N) >> 32);
+            // (K = 1: bits 20..51 of fit_hash -- its low bits see only the
+            // key's low bits)
+            slot[u] = (uint32_t)(((uint64_t)(uint32_t)(K == 1 && LDGPU_FIT_FIB ? h >> 20 : h) * (uint64_t)N) >> 32);
             tg[u] = (uint32_t)(h >> 32) | 2u;  // never 0 (empty) or kBusy
         }
         // a bounded number of probe rounds: the wave waits for its slowest
         // lane, and a record still unplaced goes out as it is
         for (int t = 0; t < kRedRounds; ++t) {
             bool any = false;
-            if constexpr (K == 1) {
+            if constexpr (K == 1 && LDGPU_RED_BRANCHLESS) {
+                const uint4* KW2 = reinterpret_cast<const uint4*>(kw);
+                uint4 cur[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) cur[u] = KW2[slot[u] >> 1];
+                uint64_t* const dk = &dummy[tid];
+                uint32_t* const dc = reinterpret_cast<uint32_t*>(dk);
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const uint64_t kl = r[u].w[0] >> p.cb;  // never 0 for a record: the sentinel bit
+                    const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                    const uint64_t k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                    const uint32_t pr = slot[u] & ~1u;
+                    const bool h0 = k0 == kl, h1 = k1 == kl, e0 = k0 == 0ull, e1 = k1 == 0ull;
+                    const bool hit = pend[u] && (h0 || h1);
+                    const bool claim = pend[u] && !h0 && !h1 && (e0 || e1);
+                    const uint32_t ca = pr + (e0 ? 0u : 1u);
+                    const unsigned long long old = atomicCAS(
+                        reinterpret_cast<unsigned long long*>(claim ? &kw[ca] : dk), 0ull, (unsigned long long)kl);
+                    const bool won = claim && (old == 0ull || old == kl);
+                    const bool add = hit || won;
+                    const uint32_t at = hit ? pr + (h0 ? 0u : 1u) : ca;
+                    __hip_atomic_fetch_add(add ? &cnt[at] : dc, add ? c[u] : 0u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    // a full pair without the key: the next pair; a lost claim:
+                    // this pair again
+                    const bool full = pend[u] && !h0 && !h1 && !e0 && !e1;
+                    slot[u] = full ? (pr + 2u == (uint32_t)N ? 0u : pr + 2u) : slot[u];
+                    pend[u] = pend[u] && !add;
+                    any = any || pend[u];
+                }
+            } else if constexpr (K == 1) {
                 // slot pairs: one ds_read_b128 reads both keys of a pair
                 // (filled in slot order, never emptied)
                 const uint4* KW2 = reinterpret_cast<const uint4*>(kw);
@@ -2053,12 +2128,48 @@ __global__ __launch_bounds__(1024) void merge_kernel(const PartParams p, const C
     const int64_t n = p.nout[b];
     const int64_t base = (int64_t)p.boff[b];
     unsigned int nn = 0, nw = 0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if constexpr (K == 1) {
+        // kMU entries per thread at a time: their loads, then their tables'
+        // first probes, all issued before any is resolved (the merge waited
+        // ~80 % of its cycles on one dependent chain per entry)
+        constexpr int kMU = 4;
+        for (int64_t i0 = threadIdx.x; i0 < n; i0 += kMU * (int64_t)blockDim.x) {
+            uint64_t key[kMU], cn[kMU], sl[kMU], k0[kMU];
+            int lg[kMU];
+#pragma unroll
+            for (int u = 0; u < kMU; ++u) {
+                const int64_t i = i0 + (int64_t)u * blockDim.x;
+                key[u] = kEmpty;
+                cn[u] = 0;
+                if (i < n) {
+                    key[u] = p.out[2 * (base + i)];
+                    cn[u] = p.out[2 * (base + i) + 1];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kMU; ++u) {
+                lg[u] = 0;
+                if (key[u] != kEmpty && !pairs) {
+                    lg[u] = (int)(key[u] & ((1ull << p.lb) - 1ull));
+                    key[u] = kl_key(key[u], p.lb);
+                }
+                sl[u] = fit_hash(key[u]) >> c.shift;
+                k0[u] = key[u] != kEmpty ? __hip_atomic_load(&c.keys[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < kMU; ++u) {
+                if (key[u] == kEmpty) continue;
+                bool nk = false;
+                const int64_t at = find_or_insert_at<true>(c, key[u], sl[u], k0[u], nk);
+                nn += nk ? 1u : 0u;
+                count_add_slot(c, at, key[u], lg[u], cn[u]);
+            }
+        }
+    }
+    for (int64_t i = threadIdx.x; i < (K == 1 ? 0 : n); i += blockDim.x) {
         const int64_t at = base + i;
         if constexpr (K == 1) {
-            const uint64_t kl = p.out[2 * at];
-            if (pairs) nn += add_count_q(c, kl, 0, p.out[2 * at + 1]);
-            else nn += add_count_q(c, kl_key(kl, p.lb), (int)(kl & ((1ull << p.lb) - 1ull)), p.out[2 * at + 1]);
         } else {
             const Rec<K> r = load_rec<K>(p.out, at);
             const int lang = (int)(r.w[K - 1] >> kCntBits);
@@ -2145,6 +2256,99 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
     const uint64_t lmask = (1ull << lb) - 1ull;
     uint64_t n_to = 0;
     unsigned int n_t1 = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int n = lev - 1;
+    const bool to_t = mt && !(LDGPU_DIAG && (ablate & 1));
+    const bool to_t1 = n >= 1 && !(LDGPU_DIAG && (ablate & 2));
+    if (to.pkeys) {
+        // sparse T: kDU slots per thread at a time -- their T1 entries, then
+        // the first probes of their gram (T) and prefix (T1) inserts, then
+        // those of their pairs, each batch issued before any is resolved
+        constexpr int kDU = 4;
+        for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1; s += kDU * stride) {
+            uint64_t e[kDU];
+#pragma unroll
+            for (int u = 0; u < kDU; ++u) {
+                const uint64_t su = s + u * stride;
+                e[u] = su < s1 ? t1.keys[su] : kEmpty;
+            }
+            uint64_t gk[kDU], pk[kDU], gs[kDU], g0[kDU], ps[kDU], p0[kDU];
+            unsigned long long c[kDU];
+            int lang[kDU];
+            bool v[kDU];
+#pragma unroll
+            for (int u = 0; u < kDU; ++u) {
+                const uint64_t kl = e[u] & ~kDerived;
+                v[u] = e[u] != kEmpty && kl_len(kl, lb) == lev;
+                c[u] = v[u] ? t1.counts[s + u * stride] : 0ull;
+                lang[u] = (int)(kl & lmask);
+                const uint64_t bytes = (kl >> lb) ^ (1ull << (8 * lev));
+                gk[u] = bytes | ((uint64_t)lev << 56);
+                const uint64_t sent = (1ull << (8 * (n > 0 ? n : 0))) | (bytes & byte_mask(n > 0 ? n : 0));
+                pk[u] = ((sent << lb) | (uint64_t)lang[u]) | kDerived;
+                gs[u] = fit_hash(gk[u]) >> to.shift;
+                ps[u] = fit_hash(pk[u]) >> t1.shift;
+                g0[u] = v[u] && to_t ? __hip_atomic_load(&to.keys[gs[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                p0[u] = v[u] && to_t1 ? __hip_atomic_load(&t1.keys[ps[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0ull;
+            }
+            if (to_t) {
+                int64_t g[kDU];
+                bool ng[kDU];
+#pragma unroll
+                for (int u = 0; u < kDU; ++u) {
+                    ng[u] = false;
+                    // (a zero count adds nothing, as sparse_add_q: never the case
+                    // for a T1 entry, whose counts are sums of records)
+                    g[u] = v[u] && c[u] ? find_or_insert_at<true>(to, gk[u], gs[u], g0[u], ng[u]) : -1;
+                }
+                uint64_t pp[kDU], pa[kDU], pv[kDU];
+#pragma unroll
+                for (int u = 0; u < kDU; ++u) {
+                    pp[u] = ((uint64_t)(g[u] + 1) << kPairLangBits) | (uint64_t)lang[u];
+                    pa[u] = fit_hash(pp[u]) >> to.pshift;
+                    pv[u] = g[u] >= 0 ? __hip_atomic_load(&to.pkeys[pa[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < kDU; ++u) {
+                    if (!v[u] || !c[u]) continue;
+                    const unsigned long long cm = c[u] * mt;
+                    bool np = false;
+                    int64_t sp = -1;
+                    if (g[u] >= 0) {
+                        sp = pair_find_or_insert_at<true>(to, pp[u], pa[u], pv[u], np);
+                        if (sp >= 0) {
+                            atomicAdd(&to.pcounts[sp], cm);
+                            if (np) atomicAdd(&to.kcnt[g[u]], 1u);
+                        }
+                    }
+                    if (sp < 0) {  // a probe limit: (key, lang, c) to the overflow list (sparse_add_q)
+                        const unsigned int at = atomicAdd(to.ovf_n, 1u);
+                        if (at < to.ovf_cap) {
+                            to.ovf_keys[at] = gk[u];
+                            to.ovf_lang[at] = lang[u];
+                            to.ovf_cnt[at] = cm;
+                        }
+                    }
+                    n_to += (uint64_t)ng[u] | ((uint64_t)np << 32);
+                }
+            }
+            if (to_t1) {
+#pragma unroll
+                for (int u = 0; u < kDU; ++u) {
+                    if (!v[u]) continue;
+                    bool nk = false;
+                    const int64_t at = find_or_insert_at<true>(t1, pk[u], ps[u], p0[u], nk);
+                    n_t1 += nk ? 1u : 0u;
+                    count_add_slot(t1, at, pk[u], 0, c[u]);
+                }
+            }
+        }
+        t_flush(to, n_to);
+        flush_new_keys(t1.size, n_t1);
+        return;
+    }
     for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < s1;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t key = t1.keys[s];
@@ -2259,7 +2463,8 @@ size_t emit_lds_bytes(int K) {
 
 size_t reduce_lds_bytes(int K) {
     const size_t N = K == 1 ? agg_slots<1>() : (K == 2 ? agg_slots<2>() : agg_slots<3>());
-    return K == 1 ? N * (8 + 4) + 16 : N * (8 * (size_t)(K - 1) + 12) + 16;
+    return K == 1 ? ((N * (8 + 4) + 4 + 15) & ~(size_t)15) + (LDGPU_RED_BRANCHLESS ? 8 * (size_t)kRedDummy : 16)
+                  : N * (8 * (size_t)(K - 1) + 12) + 16;
 }
 
 hipError_t fit3_prepare(int K) {

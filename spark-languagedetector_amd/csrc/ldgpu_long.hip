@@ -76,7 +76,7 @@ __device__ int64_t long_find_or_insert(const LongCountParams& p, const uint8_t* 
 // c of (gram slot g, lang) into the pair table; returns whether the pair is new
 __device__ bool long_pair_add(const LongCountParams& p, int64_t g, int lang, unsigned long long c) {
     const uint64_t pk = ((uint64_t)(g + 1) << kPairLangBits) | (uint64_t)lang;
-    uint64_t s = mix64(pk) >> p.pshift;
+    uint64_t s = fit_hash(pk) >> p.pshift;  // (launch_pair_rehash grows this table)
     for (uint64_t probe = 0; probe <= p.pmask; ++probe) {
         const uint64_t k = __hip_atomic_load(&p.pkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool hit = k == pk, fresh = false;
