@@ -204,6 +204,11 @@ struct ldgpu_ctx {
     std::mutex cache_mu;
     std::vector<std::pair<size_t, void*>> cache;
     size_t cache_bytes = 0;
+    // FIT: T1 keys per corpus byte of the last count call on this context --
+    // sizes the next call's T1 (of any count table: an executor fits
+    // partition after partition of like text), so it is not grown by
+    // doubling from a small start, rehashing ~its final size each time
+    double t1_keys_per_byte = 0.0;
 };
 
 namespace {
@@ -2651,11 +2656,16 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     // gram lengths beyond 15 bytes: their own table (ldgpu_long.hip)
     if (int rc = long_count_launch(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
     if (c->nG == 0) return LDGPU_OK;  // no gram length of <= 15 bytes: no maximal windows
+    // T1's expected keys: this table's last call, or this context's last
+    // call scaled to this call's bytes
+    const int64_t call_bytes = h_off[n_docs] - h_off[0];
+    const int64_t t1_hint = std::max<int64_t>(
+        c->pend_hint, (int64_t)std::min(1.1 * x->t1_keys_per_byte * (double)call_bytes, (double)(1ll << 32)));
     if (!c->pend) {
         // one- and two-word records: T1 keyed by (window, language) pairs, one
         // counter each (K = 2: in its wide table, key (packed key, lang + 1));
         // a dense row of L counters per window otherwise
-        if (int rc = counts_new(x, K <= 2 ? 1 : c->L, c->G, c->nG, std::max<int64_t>(1 << 16, c->pend_hint), &c->pend))
+        if (int rc = counts_new(x, K <= 2 ? 1 : c->L, c->G, c->nG, std::max<int64_t>(1 << 16, t1_hint), &c->pend))
             return rc;
     }
     ldgpu_counts* t1 = c->pend;
@@ -2894,7 +2904,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
         // T1's wide table: windows of 8..15 bytes, or every pair (K = 2)
         const bool wide = (K == 3 && maxg > kMaxGram) || K == 2;
         if (wide) {
-            if (int rc = wide_ensure(t1, K == 2 ? (uint64_t)std::max<int64_t>(c->pend_hint, 1) : 1)) return rc;
+            if (int rc = wide_ensure(t1, K == 2 ? (uint64_t)std::max<int64_t>(t1_hint, 1) : 1)) return rc;
         }
         // Projected growth: the batch adds about E x (the last batch's new
         // keys per entry) keys.  A table short of that grows once, here --
@@ -2956,6 +2966,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     // every gram length from the call's maximal windows; T1 back to the
     // context's block cache (the next call starts an empty one, sized by this)
     c->pend_hint = (int64_t)(c->pend->size + c->pend->wsize);  // (before the derive's levels replace T1)
+    if (call_bytes > 0) x->t1_keys_per_byte = (double)c->pend_hint / (double)call_bytes;
     // the cached top-K table and sparse export describe the table before this
     // call: invalid from here on, even if the derive fails part way through
     c->tbl_valid = false;

@@ -51,6 +51,27 @@ constexpr int kSub = 4;  // 64-position sub-blocks per superblock
 #define LDGPU_SPLIT_VERIFY 1
 #endif
 
+
+// The launch's parameter block through an opaque pointer to the kernarg
+// segment, for fields used off the hot path (long documents, score outputs,
+// error flags): their loads stay at their use (s_load from the scalar cache)
+// instead of being hoisted to the kernel start and held in SGPRs across the
+// persistent loop (LDGPU_COLD_PARAMS; the score kernels spill ~30 SGPRs).
+#ifndef LDGPU_COLD_PARAMS
+#define LDGPU_COLD_PARAMS 1
+#endif
+typedef const __attribute__((address_space(4))) ScoreParams* ColdParams;
+__device__ __forceinline__ ColdParams cold_params() {
+    ColdParams q = (ColdParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return q;
+}
+#if LDGPU_COLD_PARAMS
+#define LDGPU_COLD(p) (*cold_params())
+#else
+#define LDGPU_COLD(p) (p)
+#endif
+
 // timing ablations exist only in the diagnostics build (LDGPU_DIAG)
 __device__ __forceinline__ bool ablated(const ScoreParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
 
@@ -320,7 +341,7 @@ __device__ __forceinline__ void verify_complete(const ScoreParams& p, const Wave
     const bool hit = row != 0xffffffffu;
     const bool bad = hit && (row & kBadRow);
     if (__ballot(bad)) {
-        if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1);
+        if ((threadIdx.x & 63) == 0) atomicOr(LDGPU_COLD(p).err, 1);
     }
     const bool good = hit && !bad;
 #ifdef LDGPU_STATS
@@ -339,7 +360,7 @@ __device__ __forceinline__ void verify_complete(const ScoreParams& p, const Wave
     } else if (good) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            uint64_t mm = p.masks[(size_t)row * S + s];
+            uint64_t mm = LDGPU_COLD(p).masks[(size_t)row * S + s];
             while (mm) {
                 const int l = __builtin_ctzll(mm);
                 mm &= mm - 1;
@@ -438,7 +459,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         const bool hit = row != 0xffffffffu;
         const bool bad = hit && (row & kBadRow);
         if (__ballot(bad)) {
-            if (lane == 0) atomicOr(p.err, 1);
+            if (lane == 0) atomicOr(LDGPU_COLD(p).err, 1);
         }
         const bool good = hit && !bad;
 #ifdef LDGPU_STATS
@@ -462,7 +483,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     // (a multi-language row: its mask words from the row arrays)
-                    uint64_t mm = p.masks[(size_t)row * S + s];
+                    uint64_t mm = LDGPU_COLD(p).masks[(size_t)row * S + s];
                     while (mm) {
                         const int l = __builtin_ctzll(mm);
                         mm &= mm - 1;
@@ -550,8 +571,9 @@ __device__ __forceinline__ void count_scores(const ScoreParams& p, const WaveLds
             cnt[l] = 0;
             double v = 0.0;
             if (c) {
-                v = p.fold[c < p.fold_max ? c : p.fold_max];
-                for (uint32_t i = p.fold_max; i < c; ++i) v = v + p.fold[1];
+                const auto& q = LDGPU_COLD(p);
+                v = q.fold[c < q.fold_max ? c : q.fold_max];
+                for (uint32_t i = q.fold_max; i < c; ++i) v = v + q.fold[1];
             }
             acc[s] = v;
         }
@@ -1164,13 +1186,14 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     }
     if (!general) {
     } else if (len >= kMaxDocBytes) {
-        if (lane == 0) atomicOr(p.err, 2);
+        if (lane == 0) atomicOr(LDGPU_COLD(p).err, 2);
     } else {
         // general path: partial windows (len < n) and long documents; n outer
         // (reference order), superblocks inner
-        for (int gi = 0; gi < p.nG; ++gi) {
-            const GramCtx g = gram_ctx(len, p.G[gi]);
-            if (!((p.len_mask >> g.klen) & 1u) || ablated(p, 2)) continue;
+        const auto& q = LDGPU_COLD(p);
+        for (int gi = 0; gi < q.nG; ++gi) {
+            const GramCtx g = gram_ctx(len, q.G[gi]);
+            if (!((q.len_mask >> g.klen) & 1u) || ablated(p, 2)) continue;
             for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
                 Windows x;
                 load_windows<STAGED>(p, src, p0, lane, x);
@@ -1190,7 +1213,10 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
         if (ablated(p, 32)) return 0;
-        if (!p.scores && !p.best && len <= p.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
+        {
+            const auto& q = LDGPU_COLD(p);
+            if (!q.scores && !q.best && len <= q.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
+        }
         count_scores<S>(p, wl, acc, lane);
     }
 
@@ -1217,11 +1243,12 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     // breeze keeps index 0 when the first score is NaN (NaN never compares
     // greater); in a language block other than the first, a NaN is just
     // never the maximum
-    const bool nan_first = p.block == 0 && __builtin_isnan(rdlaned(acc[0], 0));
+    const auto& q = LDGPU_COLD(p);
+    const bool nan_first = q.block == 0 && __builtin_isnan(rdlaned(acc[0], 0));
     if (nan_first) label = 0;
-    if (p.best && lane == 0) p.best[doc] = nan_first ? __builtin_inf() : M;
-    if (p.scores) {
-        double* out = p.scores + doc * (p.score_stride ? p.score_stride : (int64_t)p.L);
+    if (q.best && lane == 0) q.best[doc] = nan_first ? __builtin_inf() : M;
+    if (q.scores) {
+        double* out = q.scores + doc * (q.score_stride ? q.score_stride : (int64_t)p.L);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int l = s * 64 + lane;
@@ -1517,12 +1544,12 @@ hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const do
 }
 
 // LDGPU_NARROW_VARIANT (tuning builds only, tools/build_variant.sh): just the
-// count-mode, LDS-bloom, one-slice kernels (config 2's), compiled in seconds
-// instead of minutes
+// LDS-bloom, one-slice kernels of count mode and of the finite-value replay
+// (config 2's table on either path), compiled in seconds instead of minutes
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream) {
 #ifdef LDGPU_NARROW_VARIANT
-    if (mode != 3 || !lds_bloom || slices != 1) return hipErrorInvalidValue;
-    return launch_t<1, 3, 0>(p, grid, stream);
+    if ((mode != 3 && mode != 1) || !lds_bloom || slices != 1) return hipErrorInvalidValue;
+    return mode == 3 ? launch_t<1, 3, 0>(p, grid, stream) : launch_t<1, 1, 0>(p, grid, stream);
 #else
     switch (mode) {
         case 0: return launch_m<0>(p, slices, lds_bloom, grid, stream);
@@ -1536,8 +1563,8 @@ hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_blo
 
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu) {
 #ifdef LDGPU_NARROW_VARIANT
-    if (mode != 3 || !lds_bloom || slices != 1) return hipErrorInvalidValue;
-    return prepare_t<1, 3, 0>(lds_bytes, blocks_per_cu);
+    if ((mode != 3 && mode != 1) || !lds_bloom || slices != 1) return hipErrorInvalidValue;
+    return mode == 3 ? prepare_t<1, 3, 0>(lds_bytes, blocks_per_cu) : prepare_t<1, 1, 0>(lds_bytes, blocks_per_cu);
 #else
     switch (mode) {
         case 0: return prepare_m<0>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);

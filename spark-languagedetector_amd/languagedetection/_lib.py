@@ -20,7 +20,7 @@ _LIB_OVERRIDE = os.environ.get("LDGPU_LIB")
 # diagnostics build (make -C spark-languagedetector_amd diag): the only one that
 # reads the LDGPU_* path / ablation switches from the environment; tests load
 # it explicitly (variant="diag") to cover the alternative kernel paths
-DIAG_LIB_PATH = os.path.join(PKG_ROOT, "lib", "libldgpu_diag.so")
+DIAG_LIB_PATH = os.environ.get("LDGPU_DIAG_LIB") or os.path.join(PKG_ROOT, "lib", "libldgpu_diag.so")  # (override: A/B tools only)
 
 LDGPU_OK = 0
 LDGPU_EINVAL = 1
