@@ -209,6 +209,7 @@ struct ldgpu_ctx {
     // partition after partition of like text), so it is not grown by
     // doubling from a small start, rehashing ~its final size each time
     double t1_keys_per_byte = 0.0;
+    int64_t t1_keys = 0;  // (and its keys: a hint is capped at twice them)
 };
 
 namespace {
@@ -2660,7 +2661,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     // call scaled to this call's bytes
     const int64_t call_bytes = h_off[n_docs] - h_off[0];
     const int64_t t1_hint = std::max<int64_t>(
-        c->pend_hint, (int64_t)std::min(1.1 * x->t1_keys_per_byte * (double)call_bytes, (double)(1ll << 32)));
+        c->pend_hint, (int64_t)std::min(1.1 * x->t1_keys_per_byte * (double)call_bytes, 2.0 * (double)x->t1_keys));
     if (!c->pend) {
         // one- and two-word records: T1 keyed by (window, language) pairs, one
         // counter each (K = 2: in its wide table, key (packed key, lang + 1));
@@ -2966,7 +2967,10 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     // every gram length from the call's maximal windows; T1 back to the
     // context's block cache (the next call starts an empty one, sized by this)
     c->pend_hint = (int64_t)(c->pend->size + c->pend->wsize);  // (before the derive's levels replace T1)
-    if (call_bytes > 0) x->t1_keys_per_byte = (double)c->pend_hint / (double)call_bytes;
+    if (call_bytes > 0) {
+        x->t1_keys_per_byte = (double)c->pend_hint / (double)call_bytes;
+        x->t1_keys = c->pend_hint;
+    }
     // the cached top-K table and sparse export describe the table before this
     // call: invalid from here on, even if the derive fails part way through
     c->tbl_valid = false;
