@@ -2657,11 +2657,17 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     // gram lengths beyond 15 bytes: their own table (ldgpu_long.hip)
     if (int rc = long_count_launch(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
     if (c->nG == 0) return LDGPU_OK;  // no gram length of <= 15 bytes: no maximal windows
-    // T1's expected keys: this table's last call, or this context's last
-    // call scaled to this call's bytes
+    // T1's expected keys: this table's last call, or (K = 1 pair tables of up
+    // to 2^28 keys) this context's last call scaled to this call's bytes --
+    // larger T1s keep growing from the table's own hint, under the load
+    // limits of a device-filling fit (a hint of ~1G two-word pairs from a
+    // high-entropy fit would claim its table at load 1/2 at once: 100 GB)
     const int64_t call_bytes = h_off[n_docs] - h_off[0];
-    const int64_t t1_hint = std::max<int64_t>(
-        c->pend_hint, (int64_t)std::min(1.1 * x->t1_keys_per_byte * (double)call_bytes, 2.0 * (double)x->t1_keys));
+    int64_t t1_hint = c->pend_hint;
+    if (K == 1) {
+        const double h = std::min(1.1 * x->t1_keys_per_byte * (double)call_bytes, 2.0 * (double)x->t1_keys);
+        if (h <= (double)(1ll << 28)) t1_hint = std::max<int64_t>(t1_hint, (int64_t)h);
+    }
     if (!c->pend) {
         // one- and two-word records: T1 keyed by (window, language) pairs, one
         // counter each (K = 2: in its wide table, key (packed key, lang + 1));

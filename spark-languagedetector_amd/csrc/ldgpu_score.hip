@@ -66,11 +66,14 @@ __device__ __forceinline__ ColdParams cold_params() {
     asm volatile("" : "+s"(q));
     return q;
 }
-#if LDGPU_COLD_PARAMS
-#define LDGPU_COLD(p) (*cold_params())
-#else
-#define LDGPU_COLD(p) (p)
-#endif
+// f(params): with the cold pointer in the LDS-bloom kernels (KEYED == 0:
+// config 2's table on either path), with p itself in the keyed-bloom ones
+// (config 4's packs ran 5 % slower with it: same-box A/B)
+template <int KEYED, typename F>
+__device__ __forceinline__ auto with_cold(const ScoreParams& p, F&& f) {
+    if constexpr (LDGPU_COLD_PARAMS && KEYED == 0) return f(*cold_params());
+    else return f(p);
+}
 
 // timing ablations exist only in the diagnostics build (LDGPU_DIAG)
 __device__ __forceinline__ bool ablated(const ScoreParams& p, int bit) { return LDGPU_DIAG && (p.ablate & bit); }
@@ -341,7 +344,7 @@ __device__ __forceinline__ void verify_complete(const ScoreParams& p, const Wave
     const bool hit = row != 0xffffffffu;
     const bool bad = hit && (row & kBadRow);
     if (__ballot(bad)) {
-        if ((threadIdx.x & 63) == 0) atomicOr(LDGPU_COLD(p).err, 1);
+        if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1);
     }
     const bool good = hit && !bad;
 #ifdef LDGPU_STATS
@@ -360,7 +363,7 @@ __device__ __forceinline__ void verify_complete(const ScoreParams& p, const Wave
     } else if (good) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            uint64_t mm = LDGPU_COLD(p).masks[(size_t)row * S + s];
+            uint64_t mm = p.masks[(size_t)row * S + s];
             while (mm) {
                 const int l = __builtin_ctzll(mm);
                 mm &= mm - 1;
@@ -459,7 +462,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         const bool hit = row != 0xffffffffu;
         const bool bad = hit && (row & kBadRow);
         if (__ballot(bad)) {
-            if (lane == 0) atomicOr(LDGPU_COLD(p).err, 1);
+            if (lane == 0) with_cold<KEYED>(p, [](const auto& q) { atomicOr(q.err, 1); });
         }
         const bool good = hit && !bad;
 #ifdef LDGPU_STATS
@@ -483,7 +486,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     // (a multi-language row: its mask words from the row arrays)
-                    uint64_t mm = LDGPU_COLD(p).masks[(size_t)row * S + s];
+                    uint64_t mm = with_cold<KEYED>(p, [&](const auto& q) { return q.masks[(size_t)row * S + s]; });
                     while (mm) {
                         const int l = __builtin_ctzll(mm);
                         mm &= mm - 1;
@@ -571,9 +574,8 @@ __device__ __forceinline__ void count_scores(const ScoreParams& p, const WaveLds
             cnt[l] = 0;
             double v = 0.0;
             if (c) {
-                const auto& q = LDGPU_COLD(p);
-                v = q.fold[c < q.fold_max ? c : q.fold_max];
-                for (uint32_t i = q.fold_max; i < c; ++i) v = v + q.fold[1];
+                v = p.fold[c < p.fold_max ? c : p.fold_max];
+                for (uint32_t i = p.fold_max; i < c; ++i) v = v + p.fold[1];
             }
             acc[s] = v;
         }
@@ -1186,14 +1188,16 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     }
     if (!general) {
     } else if (len >= kMaxDocBytes) {
-        if (lane == 0) atomicOr(LDGPU_COLD(p).err, 2);
+        if (lane == 0) with_cold<KEYED>(p, [](const auto& q) { atomicOr(q.err, 2); });
     } else {
         // general path: partial windows (len < n) and long documents; n outer
         // (reference order), superblocks inner
-        const auto& q = LDGPU_COLD(p);
-        for (int gi = 0; gi < q.nG; ++gi) {
-            const GramCtx g = gram_ctx(len, q.G[gi]);
-            if (!((q.len_mask >> g.klen) & 1u) || ablated(p, 2)) continue;
+        const int nG = with_cold<KEYED>(p, [](const auto& q) { return q.nG; });
+        for (int gi = 0; gi < nG; ++gi) {
+            const int n = with_cold<KEYED>(p, [&](const auto& q) { return q.G[gi]; });
+            const uint32_t lm = with_cold<KEYED>(p, [](const auto& q) { return q.len_mask; });
+            const GramCtx g = gram_ctx(len, n);
+            if (!((lm >> g.klen) & 1u) || ablated(p, 2)) continue;
             for (int32_t p0 = 0; p0 < g.nwin; p0 += 64 * kSub) {
                 Windows x;
                 load_windows<STAGED>(p, src, p0, lane, x);
@@ -1213,10 +1217,8 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
     if constexpr (MODE == 3) {
         if (ablated(p, 32)) return 0;
-        {
-            const auto& q = LDGPU_COLD(p);
-            if (!q.scores && !q.best && len <= q.count_argmax_len) return count_argmax<S>(p, count_area(wl), lane);
-        }
+        if (with_cold<KEYED>(p, [&](const auto& q) { return !q.scores && !q.best && len <= q.count_argmax_len; }))
+            return count_argmax<S>(p, count_area(wl), lane);
         count_scores<S>(p, wl, acc, lane);
     }
 
@@ -1243,12 +1245,15 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     // breeze keeps index 0 when the first score is NaN (NaN never compares
     // greater); in a language block other than the first, a NaN is just
     // never the maximum
-    const auto& q = LDGPU_COLD(p);
-    const bool nan_first = q.block == 0 && __builtin_isnan(rdlaned(acc[0], 0));
+    const bool nan_first = with_cold<KEYED>(p, [](const auto& q) { return q.block == 0; }) &&
+                           __builtin_isnan(rdlaned(acc[0], 0));
     if (nan_first) label = 0;
-    if (q.best && lane == 0) q.best[doc] = nan_first ? __builtin_inf() : M;
-    if (q.scores) {
-        double* out = q.scores + doc * (q.score_stride ? q.score_stride : (int64_t)p.L);
+    double* const best = with_cold<KEYED>(p, [](const auto& q) { return q.best; });
+    if (best && lane == 0) best[doc] = nan_first ? __builtin_inf() : M;
+    double* const scores = with_cold<KEYED>(p, [](const auto& q) { return q.scores; });
+    if (scores) {
+        const int64_t stride = with_cold<KEYED>(p, [](const auto& q) { return q.score_stride; });
+        double* out = scores + doc * (stride ? stride : (int64_t)p.L);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int l = s * 64 + lane;
