@@ -31,7 +31,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spark-languagedetector_amd"))
 
-from languagedetection import synth  # noqa: E402
+from languagedetection import _lib, synth  # noqa: E402
 from languagedetection.runtime import DeviceCounts, DeviceModel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -469,6 +469,7 @@ def fit_main(args, world, rank, local, dev, backend):
         line["counts_match_oracle"] = bool(ok)
         line["oracle_check"] = {"docs_checked": int(n_s), "grams_checked": int(len(expect[1]) - 1),
                                 "pairs_checked": int(len(expect[3]))}
+    line["build"] = _lib.provenance()  # the loaded library's source hash against this tree's
     if rank == 0:
         print(json.dumps(line), flush=True)
         if args.json_out:
@@ -665,6 +666,8 @@ def main():
     }
     if line_note:
         line["note"] = line_note
+    # build provenance: the loaded library's source hash against this tree's
+    line["build"] = _lib.provenance()
     model.close()
     if rank == 0:
         s = json.dumps(line)

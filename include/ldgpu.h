@@ -63,6 +63,9 @@ enum ldgpu_status {
 #define LDGPU_MAX_GRAM_LENGTHS 32
 
 const char* ldgpu_version(void);
+/* build provenance: sha256 (first 16 hex digits) of the sources this library
+ * was compiled from (spark-languagedetector_amd/Makefile, PROV) */
+const char* ldgpu_build_id(void);
 const char* ldgpu_last_error(void);          /* thread-local, never NULL */
 int ldgpu_device_count(int32_t* out_count);
 

@@ -301,6 +301,10 @@ void pipe_release(ldgpu_ctx* c, ScorePipe* pp) {
 }  // namespace
 
 extern "C" const char* ldgpu_version(void) { return "ldgpu 0.1.0 (gfx950)"; }
+#ifndef LDGPU_SRC_HASH
+#define LDGPU_SRC_HASH "unknown"
+#endif
+extern "C" const char* ldgpu_build_id(void) { return LDGPU_SRC_HASH; }
 extern "C" const char* ldgpu_last_error(void) { return g_err.c_str(); }
 
 extern "C" int ldgpu_device_count(int32_t* out) {

@@ -47,6 +47,7 @@ _pi64 = ctypes.POINTER(ctypes.c_int64)
 # (name, restype, argtypes) -- exactly the entry points of include/ldgpu.h
 SIGNATURES = [
     ("ldgpu_version", ctypes.c_char_p, []),
+    ("ldgpu_build_id", ctypes.c_char_p, []),
     ("ldgpu_last_error", ctypes.c_char_p, []),
     ("ldgpu_device_count", ctypes.c_int, [_pi32]),
     ("ldgpu_ctx_create", ctypes.c_int, [_i32, _pp]),
@@ -185,3 +186,28 @@ def device_count() -> int:
     n = ctypes.c_int32(0)
     check(load().ldgpu_device_count(ctypes.byref(n)))
     return n.value
+
+
+# the sources the library is built from, in the Makefile's PROV order
+_PROV = ["csrc/ldgpu_api.hip", "csrc/ldgpu_score.hip", "csrc/ldgpu_fit.hip", "csrc/ldgpu_general.hip",
+         "csrc/ldgpu_long.hip", "csrc/ldgpu_common.h", "csrc/ldgpu_internal.h", "csrc/ldgpu_fit.h",
+         "../include/ldgpu.h"]
+
+
+def tree_source_hash() -> str:
+    """sha256 (16 hex digits) of the library's sources in this tree."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in _PROV:
+        with open(os.path.join(PKG_ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def provenance(variant: str = "product") -> dict:
+    """The loaded library's build id against this tree's sources."""
+    lib = load(variant=variant)
+    built = lib.ldgpu_build_id().decode()
+    tree = tree_source_hash()
+    return {"library_source_hash": built, "tree_source_hash": tree, "match": built == tree}
+

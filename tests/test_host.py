@@ -31,6 +31,14 @@ def test_library_exports_every_header_symbol():
     assert lib.ldgpu_version().decode().startswith("ldgpu")
 
 
+def test_libraries_are_built_from_this_tree():
+    # build provenance: the hash of the sources compiled into each library
+    # (ldgpu_build_id) equals the hash of the sources in this tree
+    for variant in ("product", "diag"):
+        prov = _lib.provenance(variant)
+        assert prov["match"], (variant, prov)
+
+
 def test_library_is_gfx950_code_object():
     so = _lib.LIB_PATH
     blob = open(so, "rb").read()
