@@ -27,6 +27,44 @@ using namespace ldgpu;
 // (ldgpu_internal.h); the product library sees none of them.
 static const char* diag_env(const char* name) { return LDGPU_DIAG ? getenv(name) : nullptr; }
 
+// Diagnostics build: LDGPU_FIT_TRACE prints the FIT runtime's host-side phase
+// times to stderr (a scope's time, its stream drained at the end).
+namespace {
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// consecutive phases of one function: mark("x") prints the time since the last mark
+struct PhaseMarks {
+    hipStream_t st;
+    bool on;
+    double t;
+    explicit PhaseMarks(hipStream_t s) : st(s), on(diag_env("LDGPU_FIT_TRACE") != nullptr), t(on ? now_ms() : 0.0) {}
+    void operator()(const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        const double u = now_ms();
+        fprintf(stderr, "fit %s: %.3f ms\n", what, u - t);
+        t = u;
+    }
+};
+struct PhaseTrace {
+    const char* what;
+    unsigned long long a, b;
+    hipStream_t st;
+    double t0;
+    bool on;
+    PhaseTrace(const char* w, unsigned long long a_, unsigned long long b_, hipStream_t s)
+        : what(w), a(a_), b(b_), st(s), t0(0.0), on(diag_env("LDGPU_FIT_TRACE") != nullptr) {
+        if (on) t0 = now_ms();
+    }
+    ~PhaseTrace() {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        fprintf(stderr, "fit %s (%llu, %llu): %.3f ms\n", what, a, b, now_ms() - t0);
+    }
+};
+}  // namespace
+
 // ------------------------------------------------------------------- errors
 namespace {
 thread_local std::string g_err;
@@ -196,6 +234,7 @@ struct ldgpu_ctx {
     // context's count tables under `mu` and kept between fits: multi-GB
     // allocations per fit would cost more than the counting itself
     DevBuf f_rec, f_rec2, f_bstart, f_bhdr, f_nblk, f_cnt3, f_wg, f_p2, f_boff, f_okl, f_ocnt, f_on;
+    DevBuf f_stmp;                     // FIT v5: the radix sort's scratch
     HostBuf h_fwg;                     // pinned staging of a batch's plan (one async copy to f_wg)
     HostBuf h_fon;                     // pinned landing of a batch's nout / boff (an async copy back)
     // device blocks of destroyed / grown count tables and overflow lists,
@@ -346,7 +385,7 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
     c->scores.release();
     c->langs.release();
     for (DevBuf* b : {&c->f_rec, &c->f_rec2, &c->f_bstart, &c->f_bhdr, &c->f_nblk, &c->f_cnt3, &c->f_wg, &c->f_p2,
-                      &c->f_boff, &c->f_okl, &c->f_ocnt, &c->f_on})
+                      &c->f_boff, &c->f_okl, &c->f_ocnt, &c->f_on, &c->f_stmp})
         b->release();
     c->h_fwg.release();
     c->h_fon.release();
@@ -1657,6 +1696,9 @@ struct ldgpu_counts {
     ldgpu_counts* pend = nullptr; // FIT v4: T1, the table of maximal windows of a count call
     int64_t pend_hint = 0;      // T1's keys in the last call (sizes the next one)
     double new_per_entry = 1.0; // new keys per merged entry in the last batch (projected growth)
+    // FIT v5 (count_launch_sorted): new grams / pairs per run entry of the last
+    // insert into T (projected growth of the next)
+    double run_new_grams = 1.0, run_new_pairs = 1.0;
     ldgpu_comm* comm = nullptr; // set by ldgpu_counts_merge: the table is this rank's owned shard
     // grams of 8..15 bytes: a two-word-key table of their own (ldgpu_fit.hip)
     uint64_t wcap = 0, wsize = 0;
@@ -1831,6 +1873,7 @@ int rebuild_pairs(ldgpu_counts* c, uint64_t new_pcap, const uint64_t* remap) {
 // new slots)
 int grow(ldgpu_counts* c, uint64_t new_cap) {
     if (new_cap <= c->cap) return LDGPU_OK;
+    PhaseTrace tr("grow grams", c->cap, new_cap, c->ctx->stream);
     uint64_t* nk = nullptr;
     void* nr = nullptr;
     if (int rc = alloc_table(c, new_cap, &nk, &nr)) return rc;
@@ -1841,28 +1884,43 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
     tmp.cap = new_cap;
     tmp.d_keys = nk;
     if (c->sparse) {
+        // The new gram table, the slot remap and the new pair table are all
+        // allocated and filled before the old ones are released: a failed
+        // grow leaves the table as it was (callers may go on without it).
         tmp.d_kcnt = static_cast<uint32_t*>(nr);
+        tmp.pcap = c->pcap;
         uint64_t* remap = nullptr;
         hipError_t e = cache_alloc(c->ctx, (void**)&remap, c->cap * sizeof(uint64_t));
-        if (e == hipSuccess) e = launch_sparse_rehash(from, count_params(&tmp), c->cap, remap, c->ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->ctx->stream);
-        if (e != hipSuccess) {
+        int rc = e == hipSuccess ? alloc_pairs(c, c->pcap, &tmp.d_pkeys, &tmp.d_pcounts) : LDGPU_ENOMEM;
+        if (e == hipSuccess && !rc) e = launch_sparse_rehash(from, count_params(&tmp), c->cap, remap, c->ctx->stream);
+        if (e == hipSuccess && !rc)
+            e = launch_pair_rehash(from, count_params(&tmp), c->pcap, remap, c->ctx->stream);
+        if (e == hipSuccess && !rc) e = hipStreamSynchronize(c->ctx->stream);
+        if (e != hipSuccess || rc) {
+            (void)hipGetLastError();
             if (remap) cache_free(c->ctx, remap, c->cap * sizeof(uint64_t));
+            cache_free(c->ctx, tmp.d_pkeys, c->pcap * sizeof(uint64_t));
+            cache_free(c->ctx, tmp.d_pcounts, c->pcap * sizeof(unsigned long long));
             cache_free(c->ctx, nk, new_cap * sizeof(uint64_t));
             cache_free(c->ctx, nr, new_cap * sizeof(uint32_t));
-            return fail(LDGPU_ENOMEM, "count table grow: %s", hipGetErrorString(e));
+            tmp.d_pkeys = nullptr;
+            tmp.d_pcounts = nullptr;
+            return fail(LDGPU_ENOMEM, "count table grow to %llu slots: %s", (unsigned long long)new_cap,
+                        e != hipSuccess ? hipGetErrorString(e) : "pair table allocation failed");
         }
-        const uint64_t old_cap = c->cap;
-        uint64_t* old_keys = c->d_keys;
-        uint32_t* old_kcnt = c->d_kcnt;
+        cache_free(c->ctx, remap, c->cap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_kcnt, c->cap * sizeof(uint32_t));
+        cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
+        cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
         c->d_keys = nk;
         c->d_kcnt = tmp.d_kcnt;
+        c->d_pkeys = tmp.d_pkeys;
+        c->d_pcounts = tmp.d_pcounts;
         c->cap = new_cap;
-        cache_free(c->ctx, old_keys, old_cap * sizeof(uint64_t));
-        cache_free(c->ctx, old_kcnt, old_cap * sizeof(uint32_t));
-        const int rc = rebuild_pairs(c, c->pcap, remap);
-        cache_free(c->ctx, remap, old_cap * sizeof(uint64_t));
-        return rc;
+        tmp.d_pkeys = nullptr;
+        tmp.d_pcounts = nullptr;
+        return LDGPU_OK;
     }
     tmp.d_counts = static_cast<unsigned long long*>(nr);
     CountParams to = count_params(&tmp);
@@ -1879,6 +1937,7 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
 // the sparse table's pair table to new_pcap slots
 int pgrow(ldgpu_counts* c, uint64_t new_pcap) {
     if (!c->sparse || new_pcap <= c->pcap) return LDGPU_OK;
+    PhaseTrace tr("grow pairs", c->pcap, new_pcap, c->ctx->stream);
     return rebuild_pairs(c, new_pcap, nullptr);
 }
 
@@ -1893,7 +1952,7 @@ int pgrow(ldgpu_counts* c, uint64_t new_pcap) {
 // to the overflow list and is re-inserted by the host.)
 constexpr uint64_t kBigTableBytes = 48ull << 30;
 
-double load_limit(uint64_t cap, uint64_t slot_bytes) { return 2 * cap * slot_bytes > kBigTableBytes ? 0.8 : 0.5; }
+double load_limit(uint64_t cap, uint64_t slot_bytes) { return 2 * cap * slot_bytes >= kBigTableBytes ? 0.8 : 0.5; }
 
 double max_load(const ldgpu_counts* c) { return load_limit(c->cap, 8ull + row_bytes(c)); }
 
@@ -2180,46 +2239,49 @@ int long_reserve(ldgpu_counts* c, uint64_t grams, uint64_t pairs, uint64_t bytes
         HIP_TRY(hipMalloc((void**)&c->d_lctr, 4 * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(c->d_lctr, 0, 4 * sizeof(unsigned long long), st));
     }
-    uint64_t* remap = nullptr;
-    if (2 * (c->lsize + grams) > c->lcap) {
-        const uint64_t cap = next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->lsize + grams)));
+    // Every new table is allocated and filled before any old one is
+    // released: a failure leaves the table as it was (a grown slot table
+    // re-keys the pairs through its remap, so both move together).
+    const bool gslots = 2 * (c->lsize + grams) > c->lcap;
+    if (gslots || 2 * (c->lpsize + pairs) > c->lpcap) {
+        const uint64_t cap = gslots ? next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->lsize + grams))) : c->lcap;
+        const uint64_t pcap = std::max<uint64_t>(c->lpcap, next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->lpsize + pairs))));
         ldgpu_counts t;
         t.L = c->L;
         t.lcap = cap;
-        hipError_t e = hipMalloc((void**)&t.d_lslots, cap * sizeof(LongSlot));
-        if (e == hipSuccess) e = hipMemsetAsync(t.d_lslots, 0, cap * sizeof(LongSlot), st);
-        if (e == hipSuccess && c->lcap) e = hipMalloc((void**)&remap, c->lcap * sizeof(uint64_t));
-        if (e == hipSuccess && c->lcap) e = launch_long_rehash(long_params(c), long_params(&t), c->lcap, remap, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) {
-            for (void* q : {(void*)t.d_lslots, (void*)remap})
-                if (q) (void)hipFree(q);
-            return fail(LDGPU_ENOMEM, "long gram table of %llu slots: %s", (unsigned long long)cap,
-                        hipGetErrorString(e));
-        }
-        if (c->d_lslots) (void)hipFree(c->d_lslots);
-        c->d_lslots = t.d_lslots;
-        c->lcap = cap;
-    }
-    if (remap || 2 * (c->lpsize + pairs) > c->lpcap) {
-        const uint64_t pcap = std::max<uint64_t>(c->lpcap, next_pow2(std::max<uint64_t>(1 << 12, 4 * (c->lpsize + pairs))));
+        uint64_t* remap = nullptr;
         uint64_t* nk = nullptr;
         unsigned long long* nc = nullptr;
-        hipError_t e = hipMalloc((void**)&nk, pcap * sizeof(uint64_t));
+        hipError_t e = hipSuccess;
+        if (gslots) {
+            e = hipMalloc((void**)&t.d_lslots, cap * sizeof(LongSlot));
+            if (e == hipSuccess) e = hipMemsetAsync(t.d_lslots, 0, cap * sizeof(LongSlot), st);
+            if (e == hipSuccess && c->lcap) e = hipMalloc((void**)&remap, c->lcap * sizeof(uint64_t));
+        }
+        if (e == hipSuccess) e = hipMalloc((void**)&nk, pcap * sizeof(uint64_t));
         if (e == hipSuccess) e = hipMalloc((void**)&nc, pcap * sizeof(unsigned long long));
         if (e == hipSuccess) e = hipMemsetAsync(nk, 0, pcap * sizeof(uint64_t), st);
         if (e == hipSuccess) e = hipMemsetAsync(nc, 0, pcap * sizeof(unsigned long long), st);
+        if (e == hipSuccess && gslots && c->lcap)
+            e = launch_long_rehash(long_params(c), long_params(&t), c->lcap, remap, st);
         if (e == hipSuccess && c->lpcap)
             e = launch_pair_rehash(long_pair_view(c, c->d_lpkeys, c->d_lpcounts, c->lpcap),
                                    long_pair_view(c, nk, nc, pcap), c->lpcap, remap, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (remap) (void)hipFree(remap);
         if (e != hipSuccess) {
-            for (void* q : {(void*)nk, (void*)nc})
+            for (void* q : {(void*)t.d_lslots, (void*)nk, (void*)nc})
                 if (q) (void)hipFree(q);
-            return fail(LDGPU_ENOMEM, "long gram pair table of %llu slots: %s", (unsigned long long)pcap,
-                        hipGetErrorString(e));
+            t.d_lslots = nullptr;
+            return fail(LDGPU_ENOMEM, "long gram tables of %llu / %llu slots: %s", (unsigned long long)cap,
+                        (unsigned long long)pcap, hipGetErrorString(e));
         }
+        if (gslots) {
+            if (c->d_lslots) (void)hipFree(c->d_lslots);
+            c->d_lslots = t.d_lslots;
+            c->lcap = cap;
+        }
+        t.d_lslots = nullptr;
         for (void* q : {(void*)c->d_lpkeys, (void*)c->d_lpcounts})
             if (q) (void)hipFree(q);
         c->d_lpkeys = nk;
@@ -2641,6 +2703,186 @@ int count_partial(ldgpu_counts* c, const uint8_t* d_bytes, const int64_t* d_offs
     return after_batch(c);
 }
 
+// n (key, language, count) run entries into T (FIT v5).  T first grows to
+// its projected size (new grams / pairs per entry as in the table's last
+// insert; a failed grow leaves T as it was and the chunks grow it instead),
+// then the entries go in chunks small enough that T stays within 0.1 of its
+// load limits even if every entry were new and the overflow lists hold them
+// all, T doubling whenever it passes a limit.
+int insert_runs(ldgpu_counts* c, const uint64_t* d_k, const int32_t* d_l, const unsigned long long* d_c, int64_t n) {
+    if (n <= 0) return LDGPU_OK;
+    hipStream_t st = c->ctx->stream;
+    const double eg = (double)c->size + c->run_new_grams * (double)n;
+    if (eg > max_load(c) * (double)c->cap && grow(c, cap_for(eg, 8ull + row_bytes(c))) != LDGPU_OK) {
+        (void)hipGetLastError();
+        (void)ok();
+    }
+    const double ep = (double)c->psize + c->run_new_pairs * (double)n;
+    if (c->sparse && ep > pair_load(c) * (double)c->pcap && pgrow(c, cap_for(ep, 16ull)) != LDGPU_OK) {
+        (void)hipGetLastError();
+        (void)ok();
+    }
+    const uint64_t g0 = c->size, p0 = c->psize;
+    for (int64_t i0 = 0; i0 < n;) {
+        while ((double)c->size > max_load(c) * (double)c->cap) {
+            if (int rc = grow(c, 2 * c->cap)) return rc;
+        }
+        while (c->sparse && (double)c->psize > pair_load(c) * (double)c->pcap) {
+            if (int rc = pgrow(c, 2 * c->pcap)) return rc;
+        }
+        double room = (max_load(c) + 0.1) * (double)c->cap - (double)c->size;
+        if (c->sparse) room = std::min(room, (pair_load(c) + 0.1) * (double)c->pcap - (double)c->psize);
+        const int64_t m = std::min<int64_t>(std::min<int64_t>(n - i0, (int64_t)kOvfMax), std::max<int64_t>(1, (int64_t)room));
+        if (int rc = ensure_ovf(c, m)) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+        HIP_TRY(launch_runs_add(count_params(c), d_k + i0, d_l + i0, d_c + i0, m, c->ctx->cus, st));
+        if (int rc = after_batch(c)) return rc;
+        i0 += m;
+    }
+    c->run_new_grams = std::max(0.02, (double)(c->size - g0) / (double)n);
+    c->run_new_pairs = std::max(0.02, (double)(c->psize - p0) / (double)n);
+    return LDGPU_OK;
+}
+
+// FIT v5 applies to a sparse count table of two-word records (grams of <= 7
+// bytes whose one-word record has no room: many languages) whose sort key
+// (8 max(G) bits of window, ceil(log2(L + 1)) of language) fits 64 bits.
+// Diagnostics: LDGPU_FIT_NO_SORT keeps such tables on FIT v4 (A/B, tests).
+bool sort_path(const ldgpu_counts* c) {
+    if (!c->sparse || c->K != 2 || c->nG == 0 || diag_env("LDGPU_FIT_NO_SORT")) return false;
+    int maxg = 0;
+    for (int i = 0; i < c->nG; ++i) maxg = std::max(maxg, c->G[i]);
+    return maxg <= kMaxGram && 8 * maxg + log2u((uint64_t)c->L + 1) <= 64;
+}
+
+// byte positions per FIT v5 batch: the keys and the sort's second buffer take
+// 16 B each, the run entries of one gram length <= 20 B per position
+constexpr int64_t kSortBatch = 1ll << 30;
+
+// Count documents [0, n_docs) with FIT v5 (ldgpu_fit.h): per batch of
+// documents, every position's sort key (the tail positions' grams straight
+// into T), one radix sort, then per distinct gram length n one pass that
+// turns the runs of equal (language, n-byte prefix) into (n-gram, language,
+// count) entries, inserted into T.  Partial windows and grams longer than 15
+// bytes take their own kernels, as in FIT v4.
+int count_launch_sorted(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets,
+                        const int32_t* d_lang, int64_t n_docs, const int64_t* h_off, const int32_t* h_lang) {
+    ldgpu_ctx* x = c->ctx;
+    hipStream_t st = x->stream;
+    if (c->pend) {
+        counts_free(c->pend);
+        c->pend = nullptr;
+    }
+    if (int rc = count_partial(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
+    if (int rc = long_count_launch(c, d_bytes, d_offsets, d_lang, n_docs, h_off, h_lang)) return rc;
+    int N = 0;
+    uint32_t mult[kMaxGram + 1] = {};
+    for (int i = 0; i < c->nG; ++i) {
+        N = std::max(N, c->G[i]);
+        mult[c->G[i]]++;
+    }
+    const int bits = 8 * N + log2u((uint64_t)c->L + 1);
+    const DeriveParams d = derive_params(c);
+    // tail adds of a document of len bytes: for each of its last min(N - 1,
+    // len) positions (r bytes left), the gram lengths <= r
+    int64_t tails_of[kMaxGram + 1] = {};
+    for (int r = 1; r < N; ++r) {
+        int64_t k = 0;
+        for (int j = 0; j < d.n && d.len[j] <= r; ++j) ++k;
+        tails_of[r] = tails_of[r - 1] + k;
+    }
+    int64_t batch = kSortBatch;
+    if (const char* b = diag_env("LDGPU_FIT_SORT_BATCH")) batch = std::max(1ll, atoll(b));
+    const bool trace = diag_env("LDGPU_FIT_TRACE") != nullptr;
+    auto now_ms = [] {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    HIP_TRY(x->f_on.ensure(64));
+    unsigned long long* d_n = (unsigned long long*)x->f_on.p;
+    for (int64_t d0 = 0; d0 < n_docs;) {
+        const double t0 = trace ? now_ms() : 0.0;
+        int64_t d1 = d0, R = 0, tails = 0;
+        while (d1 < n_docs) {
+            const int64_t len = h_off[d1 + 1] - h_off[d1];
+            const bool ok_doc = len > 0 && h_lang[d1] >= 0 && h_lang[d1] < c->L;
+            const int64_t t = ok_doc ? tails_of[std::min<int64_t>(len, N - 1)] : 0;
+            if (d1 > d0 && (h_off[d1 + 1] - h_off[d0] > batch || tails + t > (int64_t)kOvfMax)) break;
+            if (ok_doc) R += std::max<int64_t>(0, len - N + 1);
+            tails += t;
+            ++d1;
+        }
+        const int64_t P = h_off[d1] - h_off[d0];
+        if (P > INT32_MAX)
+            return fail(LDGPU_EUNSUPPORTED, "FIT: a document of %lld bytes exceeds the sort batch", (long long)P);
+        if (P > 0) {
+            HIP_TRY(x->f_rec.ensure(sizeof(uint64_t) * (size_t)P));
+            HIP_TRY(x->f_rec2.ensure(sizeof(uint64_t) * (size_t)P));
+            uint64_t* keys = (uint64_t*)x->f_rec.p;
+            uint64_t* alt = (uint64_t*)x->f_rec2.p;
+            if (tails) {
+                if (int rc = ensure_ovf(c, tails)) return rc;
+                if (int rc = reserve(c, (uint64_t)tails, (uint64_t)tails)) return rc;
+            }
+            HIP_TRY(hipMemsetAsync(c->d_ovf_n, 0, sizeof(unsigned int), st));
+            SortFitParams sp{};
+            sp.bytes = d_bytes;
+            sp.last_dword = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;
+            sp.offsets = d_offsets + d0;
+            sp.doc_lang = d_lang + d0;
+            sp.n_docs = d1 - d0;
+            sp.base = h_off[d0];
+            sp.N = N;
+            sp.L = c->L;
+            sp.keys = keys;
+            sp.d = d;
+            HIP_TRY(launch_sort_emit(sp, count_params(c), st));
+            if (int rc = after_batch(c)) return rc;  // the tail adds (overflow entries re-inserted)
+            const double t1 = trace ? now_ms() : 0.0;
+            size_t tb = 0;
+            bool in_alt = false;
+            HIP_TRY(sort_keys_u64(P, keys, alt, bits, nullptr, &tb, nullptr, st));
+            HIP_TRY(x->f_stmp.ensure(tb + 16));
+            HIP_TRY(sort_keys_u64(P, keys, alt, bits, x->f_stmp.p, &tb, &in_alt, st));
+            const uint64_t* sorted = in_alt ? alt : keys;
+            if (trace) HIP_TRY(hipStreamSynchronize(st));
+            const double t2 = trace ? now_ms() : 0.0;
+            // one gram length's run entries: key, count, language (20 B)
+            const size_t cap = (size_t)std::max<int64_t>(R, 1);
+            HIP_TRY(x->f_okl.ensure(cap * (2 * sizeof(uint64_t) + sizeof(int32_t)) + 64));
+            uint64_t* rk = (uint64_t*)x->f_okl.p;
+            unsigned long long* rcnt = (unsigned long long*)(rk + cap);
+            int32_t* rl = (int32_t*)(rcnt + cap);
+            double t_runs = 0.0, t_ins = 0.0;
+            for (int n = N; n >= 1 && R > 0; --n) {
+                if (!mult[n]) continue;
+                const double ta = trace ? now_ms() : 0.0;
+                HIP_TRY(hipMemsetAsync(d_n, 0, sizeof(unsigned long long), st));
+                HIP_TRY(launch_sort_runs(sorted, R, N, n, mult[n], rk, rl, rcnt, d_n, st));
+                unsigned long long rn = 0;
+                HIP_TRY(hipMemcpyAsync(&rn, d_n, sizeof rn, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                if (rn > (unsigned long long)R)
+                    return fail(LDGPU_EDEVICE, "FIT runs: %llu entries from %lld keys", rn, (long long)R);
+                const double tb2 = trace ? now_ms() : 0.0;
+                if (int rc = insert_runs(c, rk, rl, rcnt, (int64_t)rn)) return rc;
+                if (trace) {
+                    t_runs += tb2 - ta;
+                    t_ins += now_ms() - tb2;
+                    fprintf(stderr, "fit v5 length %d: %llu runs\n", n, rn);
+                }
+            }
+            if (trace)
+                fprintf(stderr, "fit v5 batch: %lld positions, %lld keys, %lld tail adds: emit %.3f sort %.3f runs %.3f "
+                                "insert %.3f ms (T %llu grams / %llu slots, %llu pairs / %llu)\n",
+                        (long long)P, (long long)R, (long long)tails, t1 - t0, t2 - t1, t_runs, t_ins,
+                        (unsigned long long)c->size, (unsigned long long)c->cap, (unsigned long long)c->psize,
+                        (unsigned long long)c->pcap);
+        }
+        d0 = d1;
+    }
+    return LDGPU_OK;
+}
+
 // Count documents [0, n_docs) on the device with FIT v4 (ldgpu_fit.hip): per
 // batch, the documents in language order (h_lang: their languages on the
 // host), emit -> part2 -> reduce -> merge into T1 (c->pend, the per-call table
@@ -3005,6 +3247,7 @@ int count_launch(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, const
     // call, which may fail part-way through changing them
     c->tbl_valid = false;
     c->sp_valid = false;
+    if (c->v3 && sort_path(c)) return count_launch_sorted(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, h_lang);
     if (c->v3) return count_launch_v3(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, h_lang);
     if (c->nGn > 0) {
         if (int rc = count_launch_narrow(c, d_bytes, n_bytes, d_offsets, d_lang, n_docs, h_off, c->ctx->stream))
@@ -4378,10 +4621,14 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(db.alloc(&d_rowof, c->cap));
     HIP_TRY(db.alloc(&d_n, 2));
     HIP_TRY(db.alloc(&d_hist, (size_t)L * (L + 1)));
+    PhaseMarks mark(st);
+    mark("table: scratch");
     HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(unsigned int) * L * (L + 1), st));
     HIP_TRY(launch_gram_rows(cp, c->cap, d_keys, d_k, d_rowof, d_n, st));
+    mark("table: gram rows");
     HIP_TRY(launch_pair_hist(cp, c->pcap, d_rowof, d_k, L, d_hist, st));
+    mark("table: pair histogram");
     std::vector<unsigned int> hist((size_t)L * (L + 1));
     unsigned long long got = 0;
     HIP_TRY(hipMemcpyAsync(hist.data(), d_hist, sizeof(unsigned int) * hist.size(), hipMemcpyDeviceToHost, st));
@@ -4522,6 +4769,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     HIP_TRY(hipStreamSynchronize(st));
     if (cn != cand_cap) return fail(LDGPU_EDEVICE, "select: %u candidates, %llu expected", cn,
                                     (unsigned long long)cand_cap);
+    mark("table: select");
     // per language: the need[l] smallest (length, bytes) keys of its threshold
     // class (candidates of language l form segment l once sorted)
     std::vector<int64_t> seg(L + 1, 0);
@@ -4580,6 +4828,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         HIP_TRY(hipMemcpyAsync(d_thr, thr.data(), sizeof(uint64_t) * L, hipMemcpyHostToDevice, st));
         HIP_TRY(launch_mark_threshold((int64_t)cn, d_cl, d_ck, d_ci, d_thr, d_chosen, st));
     }
+    mark("table: threshold ties");
     const int64_t cap_out = std::min<int64_t>(n, (int64_t)L * std::max<int32_t>(K, 0));
     uint64_t *d_ok, *d_om;
     int32_t* d_okk;
@@ -4596,7 +4845,9 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
                                          (long long)cap_out);
     HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
     HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
+    mark("table: gather rows");
     HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, d_outrow, S, d_om, st));
+    mark("table: masks");
     std::vector<double> w(L + 1, 0.0);
     for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
     if (!cm || cm->world == 1) {
@@ -4614,6 +4865,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         HIP_TRY(launch_sort_keys_of((int64_t)m, d_ok, d_sk, d_idx, st));
         HIP_TRY(sort_pairs_u64((int64_t)m, d_sk, d_idx, 64, st));
         HIP_TRY(launch_rows_permute((int64_t)m, S, d_idx, d_ok, d_okk, d_om, d_ok2, d_okk2, d_om2, st));
+        mark("table: row sort");
         std::vector<uint64_t> out_keys(m);
         std::vector<int32_t> okk(m);
         c->tbl_masks.resize((size_t)m * S);
@@ -4633,6 +4885,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         c->tbl_valid = true;
         if (n_rows) *n_rows = (int64_t)m;
         if (key_bytes) *key_bytes = nb;
+        mark("table: copy back + host rows");
         return LDGPU_OK;
     }
     std::vector<uint64_t> ok(m), om((size_t)m * S);

@@ -239,6 +239,53 @@ hipError_t launch_partial(const uint8_t* bytes, const int64_t* offsets, const in
                           int64_t n_docs, const CountParams& to, const WideCountParams& tow, const DeriveParams& d,
                           hipStream_t stream);
 
+// ---- FIT v5 (ldgpu_fit.hip, count_launch_sorted in ldgpu_api.hip): tables
+// of two-word records (grams of <= 7 bytes with many languages: config 5's
+// fit, L = 200, grams 1-7) counted by SORTING instead of through T1.  Every
+// byte position whose maximal window is a full N-byte window (N = max(G))
+// makes one u64 sort key, lang << 8N | the window's bytes big-endian (first
+// byte most significant).  Sorted, the positions of one (language, n-byte
+// prefix) form one contiguous run for EVERY n <= N, so one pass per gram
+// length finds the batch's (n-gram, language) counts as run lengths
+// (LanguageDetector.scala:32-43 counts every window once per n; :57-65 sums
+// them per (gram, language)); they go into T as one add each.  The last N - 1
+// positions of a document (windows shorter than N) add their grams to T
+// directly in the emit.  Positions without a full window and documents of
+// unsupported languages hold kSortNone, which sorts after every key: language
+// codes stay below 2^lbs - 1, lbs = ceil(log2(L + 1)), 8 N + lbs <= 64.
+constexpr uint64_t kSortNone = ~0ull;
+
+struct SortFitParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    int64_t last_dword;
+    const int64_t* offsets;     // the batch's documents [0, n_docs]
+    const int32_t* doc_lang;
+    int64_t n_docs;
+    int64_t base;               // offsets[0]: key i belongs to byte position base + i
+    int32_t N;                  // max(G) <= 7
+    int32_t L;
+    uint64_t* keys;             // [offsets[n_docs] - base]
+    DeriveParams d;             // distinct gram lengths (ascending) and multiplicities: the tail adds
+};
+
+// keys of every position of the batch; the tail positions' grams into T
+hipError_t launch_sort_emit(const SortFitParams& p, const CountParams& to, hipStream_t stream);
+// radix sort of n u64 keys by bits [0, bits) (hipcub onesweep) between keys
+// and alt; tmp == nullptr: *tmp_bytes = the scratch it needs.  *in_alt: the
+// sorted keys are in alt
+hipError_t sort_keys_u64(int64_t n, uint64_t* keys, uint64_t* alt, int bits, void* tmp, size_t* tmp_bytes,
+                         bool* in_alt, hipStream_t stream);
+// the runs of gram length n in sorted keys[0, R): one entry per distinct
+// (language, n-byte prefix) -- packed key, language, run length x mult --
+// appended at out_n (block-level compaction)
+hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, int n, uint32_t mult, uint64_t* out_key,
+                            int32_t* out_lang, unsigned long long* out_cnt, unsigned long long* out_n,
+                            hipStream_t stream);
+// n (key, language, count) entries into T (sparse or dense), grid-stride:
+// one counter update per thread, not per wave and entry
+hipError_t launch_runs_add(const CountParams& p, const uint64_t* keys, const int32_t* lang, const unsigned long long* cnt,
+                           int64_t n, int cus, hipStream_t stream);
+
 // ---- FIT of gram lengths beyond kMaxWideGram (ldgpu_long.hip): keys of any
 // length in a table of their own -- a slot per gram holds the hash of its
 // bytes and length (gen_hash, ldgpu_common.h) and where its bytes sit in the

@@ -2455,7 +2455,130 @@ __global__ __launch_bounds__(256) void partial_kernel(const uint8_t* bytes, cons
     else wide_add(tow, lo, hi | ((uint64_t)len << 56), lang, c);
 }
 
+// ---- FIT v5: counting by sorting (ldgpu_fit.h SortFitParams).
+// Emit: one wave per document (grid-stride), a lane per byte position; lanes
+// read their window's 8 bytes from three dwords and store consecutive keys
+// (coalesced).  A tail position (fewer than N bytes left) adds each gram
+// length n <= its bytes left straight into T: about N^2 / 2 adds per
+// document, next to the document's len sort keys.
+__global__ __launch_bounds__(256) void sort_emit_kernel(const SortFitParams p, const CountParams to) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t* W = reinterpret_cast<const uint32_t*>(p.bytes);
+    const int N = p.N;
+    const int sh = 64 - 8 * N;
+    uint64_t n_new = 0;
+    for (int64_t doc = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; doc < p.n_docs; doc += nw) {
+        const int64_t b = p.offsets[doc];
+        const int64_t len = p.offsets[doc + 1] - b;
+        const int lang = p.doc_lang[doc];
+        const bool ok = lang >= 0 && lang < p.L;
+        const uint64_t lk = ok ? (uint64_t)lang << (8 * N) : 0ull;
+        uint64_t* out = p.keys + (b - p.base);
+        for (int64_t q = lane; q < len; q += 64) {
+            const int64_t a = b + q, i = a >> 2;
+            const uint64_t lo = (uint64_t)ld_dw(W, i, p.last_dword) | ((uint64_t)ld_dw(W, i + 1, p.last_dword) << 32);
+            const uint32_t s = (uint32_t)(a & 3) * 8u;
+            const uint64_t v = s ? (lo >> s) | ((uint64_t)ld_dw(W, i + 2, p.last_dword) << (64u - s)) : lo;
+            const int64_t rest = len - q;
+            out[q] = ok && rest >= N ? lk | (__builtin_bswap64(v) >> sh) : kSortNone;
+            if (ok && rest < N) {
+                for (int j = 0; j < p.d.n && p.d.len[j] <= rest; ++j) {
+                    const int n = p.d.len[j];
+                    n_new += t_add_q(to, (v & byte_mask(n)) | ((uint64_t)n << 56), lang, p.d.mult[j]);
+                }
+            }
+        }
+    }
+    t_flush(to, n_new);
+}
+
+// Runs of gram length n: position i starts one when its n-byte prefix (with
+// the language) differs from position i - 1's; its length is found by a
+// galloping search (1, 2, 4, ... positions ahead, then bisection), so the
+// long runs of short grams cost O(log run) loads and the ~1-position runs of
+// long grams one load of the next key.  Compaction: one global atomic per
+// block-chunk.
+__global__ __launch_bounds__(kScanThreads) void sort_runs_kernel(const uint64_t* keys, int64_t R, int N, int n,
+                                                                 uint32_t mult, uint64_t* out_key, int32_t* out_lang,
+                                                                 unsigned long long* out_cnt,
+                                                                 unsigned long long* out_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    const int shift = 8 * (N - n);
+    for (int64_t c0 = (int64_t)blockIdx.x * kScanThreads; c0 < R; c0 += (int64_t)gridDim.x * kScanThreads) {
+        const int64_t i = c0 + threadIdx.x;
+        uint64_t pk = 0;
+        bool start = false;
+        if (i < R) {
+            pk = keys[i] >> shift;
+            start = i == 0 || (keys[i - 1] >> shift) != pk;
+        }
+        const unsigned long long o = block_compact(start, out_n, wcnt, &bbase);
+        if (!start) continue;
+        int64_t lo = i, hi = R;
+        for (int64_t step = 1; lo + step < R; step <<= 1) {
+            if ((keys[lo + step] >> shift) != pk) {
+                hi = lo + step;
+                break;
+            }
+            lo += step;
+        }
+        while (hi - lo > 1) {
+            const int64_t mid = lo + ((hi - lo) >> 1);
+            if ((keys[mid] >> shift) == pk) lo = mid;
+            else hi = mid;
+        }
+        out_key[o] = __builtin_bswap64((pk & byte_mask(n)) << (64 - 8 * n)) | ((uint64_t)n << 56);
+        out_lang[o] = (int32_t)(pk >> (8 * n));
+        out_cnt[o] = (unsigned long long)(hi - i) * mult;
+    }
+}
+
+// (key, language, count) entries into T, grid-stride; the new-key counters
+// once per thread (t_flush)
+__global__ __launch_bounds__(256) void runs_add_kernel(const CountParams p, const uint64_t* keys, const int32_t* lang,
+                                                       const unsigned long long* cnt, int64_t n) {
+    uint64_t n_new = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        n_new += t_add_q(p, keys[i], lang[i], cnt[i]);
+    t_flush(p, n_new);
+}
+
 }  // namespace
+
+hipError_t launch_sort_emit(const SortFitParams& p, const CountParams& to, hipStream_t stream) {
+    if (p.n_docs <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>(65536, (p.n_docs + 3) / 4);
+    hipLaunchKernelGGL(sort_emit_kernel, dim3(g), dim3(256), 0, stream, p, to);
+    return hipGetLastError();
+}
+
+hipError_t sort_keys_u64(int64_t n, uint64_t* keys, uint64_t* alt, int bits, void* tmp, size_t* tmp_bytes,
+                         bool* in_alt, hipStream_t stream) {
+    hipcub::DoubleBuffer<uint64_t> kb(keys, alt);
+    if (n > INT32_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipcub::DeviceRadixSort::SortKeys(tmp, *tmp_bytes, kb, (int)n, 0, bits, stream);
+    if (in_alt) *in_alt = kb.Current() == alt;
+    return e;
+}
+
+hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, int n, uint32_t mult, uint64_t* out_key,
+                            int32_t* out_lang, unsigned long long* out_cnt, unsigned long long* out_n,
+                            hipStream_t stream) {
+    if (R <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sort_runs_kernel, dim3(scan_grid((uint64_t)R)), dim3(kScanThreads), 0, stream, keys, R, N, n,
+                       mult, out_key, out_lang, out_cnt, out_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_runs_add(const CountParams& p, const uint64_t* keys, const int32_t* lang, const unsigned long long* cnt,
+                           int64_t n, int cus, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>((int64_t)cus * 8, (n + 255) / 256);
+    hipLaunchKernelGGL(runs_add_kernel, dim3(g), dim3(256), 0, stream, p, keys, lang, cnt, n);
+    return hipGetLastError();
+}
 
 size_t emit_lds_bytes(int K) {
     return K == 1 ? sizeof(EmitLds<1>) : (K == 2 ? sizeof(EmitLds<2>) : sizeof(EmitLds<3>));

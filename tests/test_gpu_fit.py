@@ -266,8 +266,10 @@ def test_config3_shape_counts_and_table():
 @pytest.mark.parametrize("variant,env", [
     ("product", {}),                                         # FIT v4, the table's own record form: one batch
     ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "20000"}),          # FIT v4: many small batches
-    ("diag", {"LDGPU_FIT_K": "2"}),                          # two-word records (any L, grams <= 7 bytes)
-    ("diag", {"LDGPU_FIT_K": "2", "LDGPU_FIT_DERIVE_INPLACE": "1"}),  # ... one T1 for every derive level
+    ("diag", {"LDGPU_FIT_K": "2"}),                          # two-word records: FIT v5 (sort + runs)
+    ("diag", {"LDGPU_FIT_K": "2", "LDGPU_FIT_SORT_BATCH": "5000"}),  # ... many sort batches
+    ("diag", {"LDGPU_FIT_K": "2", "LDGPU_FIT_NO_SORT": "1"}),  # ... FIT v4: T1 of two-word pairs + derive
+    ("diag", {"LDGPU_FIT_K": "2", "LDGPU_FIT_NO_SORT": "1", "LDGPU_FIT_DERIVE_INPLACE": "1"}),  # ... one T1
     ("diag", {"LDGPU_FIT_K": "3", "LDGPU_FIT_BATCH_WINDOWS": "50000"}),  # three-word records, several batches
     ("diag", {"LDGPU_FIT_BATCH_WINDOWS": "700"}),            # batches of one document (most are longer)
     ("diag", {"LDGPU_FIT_LEGACY": "1"}),                     # round-1 single-pass atomic kernels (A/B only)
@@ -276,7 +278,9 @@ def test_config3_shape_counts_and_table():
                                      (200, [1, 2, 3, 4, 5, 6, 7]), (20, [7]), (5, [2, 9, 15]), (30, [8, 1])])
 def test_count_paths_match_oracle(L, grams, variant, env, monkeypatch):
     """Every counting path, bit-exact against the C restatement over two
-    calls: FIT v4 (documents grouped by language, one record per byte
+    calls: FIT v5 for two-word records (every full maximal window's sort key
+    lang << 8N | bytes big-endian, radix-sorted, one run pass per gram length;
+    tail positions added directly), in one and in many sort batches; FIT v4 (documents grouped by language, one record per byte
     position -- its maximal window of min(max(G), rest) bytes --, records
     bucketed twice and LDS-aggregated into the call's table of maximal
     windows, which derives every gram length as prefixes) in the table's own
@@ -315,6 +319,7 @@ def test_count_4096_languages(variant, monkeypatch):
     per language id spread over all 4096 (dense export rows stay small)."""
     if variant == "diag":
         monkeypatch.setenv("LDGPU_FIT_BATCH_WINDOWS", "3000")
+        monkeypatch.setenv("LDGPU_FIT_SORT_BATCH", "300")
     L, grams = 4096, [2, 6, 1]
     rng = np.random.default_rng(4096)
     alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
