@@ -85,6 +85,15 @@ static int need_offsets(JNIEnv* env, jobject offsets, int64_t n, const char* wha
     return LDGPU_OK;
 }
 
+/* LDGPU_OK when the caller's size equals the handle's own (the library sizes
+ * every buffer from the handle: a caller that assumed another language count
+ * or row count would read or write its rows with the wrong stride) */
+static int same(int64_t caller, int64_t own, const char* what) {
+    if (caller == own) return LDGPU_OK;
+    snprintf(jerr, sizeof jerr, "%s %lld does not match the handle's %lld", what, (long long)caller, (long long)own);
+    return LDGPU_EINVAL;
+}
+
 #define CHECK(expr)                      \
     do {                                 \
         const int rc_ = (expr);          \
@@ -191,12 +200,11 @@ JNIEXPORT jint JNICALL FN(modelDestroy)(JNIEnv* env, jobject self, jlong model) 
 }
 
 /* ldgpu_score: thread-safe; concurrent task threads run on their own streams.
- * n_langs (the caller's) is unused: the scores buffer is sized by the model's
- * own language count. */
+ * The scores buffer is sized by the model's own language count, which the
+ * caller's n_langs must equal. */
 JNIEXPORT jint JNICALL FN(score)(JNIEnv* env, jobject self, jlong model, jobject bytes, jobject offsets,
                                  jlong n_docs, jobject labels, jobject scores, jint n_langs) {
     (void)self;
-    (void)n_langs;
     jclear();
     if (n_docs < 0) return ldgpu_score((ldgpu_model*)(intptr_t)model, NULL, NULL, n_docs, NULL, NULL);
     int64_t nb = 0;
@@ -206,6 +214,7 @@ JNIEXPORT jint JNICALL FN(score)(JNIEnv* env, jobject self, jlong model, jobject
     if (scores) {
         int32_t L = 0;
         CHECK(ldgpu_model_langs((const ldgpu_model*)(intptr_t)model, &L));
+        CHECK(same(n_langs, L, "nLangs"));
         CHECK(need(env, scores, bytes_of(8, n_docs, L), "scores"));
     }
     return ldgpu_score((ldgpu_model*)(intptr_t)model, (const uint8_t*)addr(env, bytes),
@@ -257,15 +266,15 @@ JNIEXPORT jint JNICALL FN(countsSize)(JNIEnv* env, jobject self, jlong counts, j
     return rc;
 }
 
-/* sizes from the table itself (n_langs, the caller's, is unused) */
+/* sizes from the table itself (the caller's n_langs must equal its language count) */
 JNIEXPORT jint JNICALL FN(countsExport)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
                                         jobject key_offsets, jobject counts_out, jint n_langs) {
     (void)self;
-    (void)n_langs;
     jclear();
     int64_t n = 0, nb = 0;
     int32_t L = 0;
     CHECK(ldgpu_counts_langs((const ldgpu_counts*)(intptr_t)counts, &L));
+    CHECK(same(n_langs, L, "nLangs"));
     CHECK(ldgpu_counts_size((ldgpu_counts*)(intptr_t)counts, &n, &nb));
     CHECK(need(env, key_bytes, nb, "keyBytes"));
     CHECK(need(env, key_offsets, bytes_of(8, n + 1, 1), "keyOffsets"));
@@ -325,16 +334,16 @@ JNIEXPORT jint JNICALL FN(countsAddSparse)(JNIEnv* env, jobject self, jlong coun
                                    (const int64_t*)addr(env, pair_counts));
 }
 
-/* rows are n x the table's own language count (n_langs, the caller's, is unused) */
+/* rows are n x the table's own language count (the caller's n_langs must equal it) */
 JNIEXPORT jint JNICALL FN(countsAdd)(JNIEnv* env, jobject self, jlong counts, jlong n, jobject key_bytes,
                                      jobject key_offsets, jobject rows, jint n_langs) {
     (void)self;
-    (void)n_langs;
     jclear();
     if (n <= 0) return ldgpu_counts_add((ldgpu_counts*)(intptr_t)counts, n, NULL, NULL, NULL);
     int64_t nb = 0;
     int32_t L = 0;
     CHECK(ldgpu_counts_langs((const ldgpu_counts*)(intptr_t)counts, &L));
+    CHECK(same(n_langs, L, "nLangs"));
     CHECK(need_offsets(env, key_offsets, n, "keyOffsets", &nb));
     CHECK(need(env, key_bytes, nb, "keyBytes"));
     CHECK(need(env, rows, bytes_of(8, n, L), "rows"));
@@ -355,24 +364,25 @@ JNIEXPORT jint JNICALL FN(fitTableSize)(JNIEnv* env, jobject self, jlong counts,
 }
 
 /* The cached table's sizes come from the library (ldgpu_fit_table_info) and
- * the table's own language count; n_rows / key_bytes_n / n_langs, the
- * caller's, are unused. */
-static int table_sizes(jlong counts, int64_t* n_rows, int64_t* key_bytes, int32_t* L) {
+ * the table's own language count; the caller's n_rows / key_bytes_n /
+ * n_langs must equal them. */
+static int table_sizes(jlong counts, int64_t* n_rows, int64_t* key_bytes, int32_t* L, int64_t c_rows, int64_t c_bytes,
+                       int64_t c_langs) {
     CHECK(ldgpu_counts_langs((const ldgpu_counts*)(intptr_t)counts, L));
-    return ldgpu_fit_table_info((ldgpu_counts*)(intptr_t)counts, n_rows, key_bytes);
+    CHECK(ldgpu_fit_table_info((ldgpu_counts*)(intptr_t)counts, n_rows, key_bytes));
+    CHECK(same(c_langs, *L, "nLangs"));
+    CHECK(same(c_rows, *n_rows, "nRows"));
+    return same(c_bytes, *key_bytes, "keyBytesN");
 }
 
 JNIEXPORT jint JNICALL FN(fitTableExport)(JNIEnv* env, jobject self, jlong counts, jobject key_bytes,
                                           jobject key_offsets, jobject rows, jlong n_rows, jlong key_bytes_n,
                                           jint n_langs) {
     (void)self;
-    (void)n_rows;
-    (void)key_bytes_n;
-    (void)n_langs;
     jclear();
     int64_t nr = 0, nb = 0;
     int32_t L = 0;
-    CHECK(table_sizes(counts, &nr, &nb, &L));
+    CHECK(table_sizes(counts, &nr, &nb, &L, n_rows, key_bytes_n, n_langs));
     CHECK(need(env, key_bytes, nb, "keyBytes"));
     CHECK(need(env, key_offsets, bytes_of(8, nr + 1, 1), "keyOffsets"));
     CHECK(need(env, rows, bytes_of(8, nr, L), "rows"));
@@ -385,13 +395,10 @@ JNIEXPORT jint JNICALL FN(fitTableExportMasks)(JNIEnv* env, jobject self, jlong 
                                                jobject key_offsets, jobject masks, jobject vals, jlong n_rows,
                                                jlong key_bytes_n, jint n_langs) {
     (void)self;
-    (void)n_rows;
-    (void)key_bytes_n;
-    (void)n_langs;
     jclear();
     int64_t nr = 0, nb = 0;
     int32_t L = 0;
-    CHECK(table_sizes(counts, &nr, &nb, &L));
+    CHECK(table_sizes(counts, &nr, &nb, &L, n_rows, key_bytes_n, n_langs));
     CHECK(need(env, key_bytes, nb, "keyBytes"));
     CHECK(need(env, key_offsets, bytes_of(8, nr + 1, 1), "keyOffsets"));
     CHECK(need(env, masks, bytes_of(8, nr, ((int64_t)L + 63) / 64), "masks"));

@@ -153,123 +153,153 @@ object LanguageDetector extends Logging {
         }
         LdgpuNative.check(LdgpuNative.count(counts, batch.bytes, batch.offsets, batch.langs, batch.n.toLong))
       }
-      exportCounts(counts, range).iterator
+    } catch {
+      case e: Throwable =>
+        LdgpuNative.countsDestroy(counts)
+        throw e
     } finally {
       batch.close()
-      LdgpuNative.countsDestroy(counts)
     }
+    new CountsExport(counts, range)
   }
 
   /** (key bytes as an ISO-8859-1 string: one char per byte, a hashable
     * shuffle key; its sparse counts) of every distinct gram of a count table,
-    * exported in ranges of at most `range` grams (halved while a range's
-    * buffers would pass 1 GiB) */
-  private def exportCounts(counts: Long, range: Long): Array[(String, SparseCounts)] = {
-    val size = new Array[Long](2)
-    LdgpuNative.check(LdgpuNative.countsSize(counts, size))
-    val total = size(0)
-    val out = new java.util.ArrayList[(String, SparseCounts)](math.min(total, Int.MaxValue - 8).toInt)
-    var first = 0L
-    while (first < total) {
-      var n = math.min(range, total - first)
+    * streamed: one ranged export of at most `range` grams (halved while a
+    * range's buffers would pass 1 GiB) is held at a time, its rows built as
+    * the shuffle consumes them.  The table is destroyed when the iterator is
+    * exhausted or the task ends. */
+  private final class CountsExport(counts: Long, range: Long) extends Iterator[(String, SparseCounts)] {
+    private var open = true
+    private val total: Long = {
+      val size = new Array[Long](2)
+      LdgpuNative.check(LdgpuNative.countsSize(counts, size))
+      size(0)
+    }
+    private var first = 0L
+    private var n = 0L
+    private var i = 0L
+    private var kb, ko, po, pl, pc: java.nio.ByteBuffer = _
+    Option(org.apache.spark.TaskContext.get()).foreach(_.addTaskCompletionListener { _: org.apache.spark.TaskContext =>
+      close()
+    })
+
+    private def close(): Unit = if (open) {
+      open = false
+      LdgpuNative.countsDestroy(counts)
+    }
+
+    private def load(): Unit = {
+      n = math.min(range, total - first)
       val sz = new Array[Long](2)
       LdgpuNative.check(LdgpuNative.countsSparseSize(counts, first, n, sz))
       while (n > 1 && (sz(0) > (1L << 30) || 8L * sz(1) > (1L << 30) || 8L * (n + 1) > (1L << 30))) {
         n = n / 2
         LdgpuNative.check(LdgpuNative.countsSparseSize(counts, first, n, sz))
       }
-      val kb = LdgpuNative.direct(sz(0))
-      val ko = LdgpuNative.direct(8L * (n + 1))
-      val po = LdgpuNative.direct(8L * (n + 1))
-      val pl = LdgpuNative.direct(4L * sz(1))
-      val pc = LdgpuNative.direct(8L * sz(1))
+      kb = LdgpuNative.direct(sz(0))
+      ko = LdgpuNative.direct(8L * (n + 1))
+      po = LdgpuNative.direct(8L * (n + 1))
+      pl = LdgpuNative.direct(4L * sz(1))
+      pc = LdgpuNative.direct(8L * sz(1))
       LdgpuNative.check(LdgpuNative.countsExportSparse(counts, first, n, kb, ko, po, pl, pc))
-      var i = 0
-      while (i < n) {
-        val (a, b) = (ko.getLong(8 * i).toInt, ko.getLong(8 * (i + 1)).toInt)
-        val key = new Array[Byte](b - a)
-        kb.position(a)
-        kb.get(key)
-        val (p0, p1) = (po.getLong(8 * i).toInt, po.getLong(8 * (i + 1)).toInt)
-        val langs = new Array[Int](p1 - p0)
-        val cnts = new Array[Long](p1 - p0)
-        var j = 0
-        while (j < langs.length) {
-          langs(j) = pl.getInt(4 * (p0 + j))
-          cnts(j) = pc.getLong(8 * (p0 + j))
-          j += 1
-        }
-        out.add((new String(key, ISO_8859_1), SparseCounts(langs, cnts)))
-        i += 1
-      }
       first += n
+      i = 0
     }
-    out.toArray(new Array[(String, SparseCounts)](out.size))
+
+    override def hasNext: Boolean = {
+      if (i < n) return true
+      if (open && first < total) {
+        load()
+        return true
+      }
+      close()
+      false
+    }
+
+    override def next(): (String, SparseCounts) = {
+      if (!hasNext) throw new NoSuchElementException("count table exhausted")
+      val (a, b) = (ko.getLong(8 * i.toInt).toInt, ko.getLong(8 * (i.toInt + 1)).toInt)
+      val key = new Array[Byte](b - a)
+      kb.position(a)
+      kb.get(key)
+      val (p0, p1) = (po.getLong(8 * i.toInt).toInt, po.getLong(8 * (i.toInt + 1)).toInt)
+      val langs = new Array[Int](p1 - p0)
+      val cnts = new Array[Long](p1 - p0)
+      var j = 0
+      while (j < langs.length) {
+        langs(j) = pl.getInt(4 * (p0 + j))
+        cnts(j) = pc.getLong(8 * (p0 + j))
+        j += 1
+      }
+      i += 1
+      (new String(key, ISO_8859_1), SparseCounts(langs, cnts))
+    }
   }
 
-  /** the partition's global rows into a device table (ranged sparse imports),
-    * its top-K table out in mask form: (key, mask words, value) */
+  /** the partition's global rows into a device table -- streamed through
+    * fixed direct buffers (at most `range` rows, 64 MiB of key bytes and
+    * 2^24 pairs per ranged sparse import), never held whole -- and its top-K
+    * table out in mask form: (key, mask words, value) */
   private def partitionTopK(it: Iterator[(String, SparseCounts)], nLangs: Int, grams: Array[Int],
                             profileSize: Int, range: Long): Iterator[(Array[Byte], Array[Long], Double)] = {
-    val rows = it.toArray
-    if (rows.isEmpty) return Iterator.empty
+    if (!it.hasNext) return Iterator.empty
     val ctx = LdgpuNative.context()
     val out = new Array[Long](1)
-    LdgpuNative.check(LdgpuNative.countsCreate(ctx, nLangs, grams, rows.length.toLong, out))
+    LdgpuNative.check(LdgpuNative.countsCreate(ctx, nLangs, grams, 0L, out))
     val counts = out(0)
     try {
-      var first = 0
-      while (first < rows.length) {
-        // the next range: at most `range` rows, its buffers within 1 GiB each
-        var n = 0
-        var keyBytes = 0L
-        var pairs = 0L
-        def fits(r: Int): Boolean = n == 0 ||
-          (n < range && keyBytes + rows(r)._1.length <= (1L << 30) && 8L * (pairs + rows(r)._2.langs.length) <= (1L << 30))
-        while (first + n < rows.length && fits(first + n)) {
-          keyBytes += rows(first + n)._1.length
-          pairs += rows(first + n)._2.langs.length
-          n += 1
-        }
-        var i = 0
-        val kb = LdgpuNative.direct(keyBytes)
-        val ko = LdgpuNative.direct(8L * (n + 1))
-        val po = LdgpuNative.direct(8L * (n + 1))
-        val pl = LdgpuNative.direct(4L * pairs)
-        val pc = LdgpuNative.direct(8L * pairs)
-        var (ko_, po_) = (0L, 0L)
-        ko.putLong(0, 0L)
-        po.putLong(0, 0L)
-        i = 0
-        while (i < n) {
-          val (key, sc) = rows(first + i)
-          kb.put(key.getBytes(ISO_8859_1))
-          ko_ += key.length
-          ko.putLong(8 * (i + 1), ko_)
-          var j = 0
-          while (j < sc.langs.length) {
-            pl.putInt(4 * (po_ + j).toInt, sc.langs(j))
-            pc.putLong(8 * (po_ + j).toInt, sc.counts(j))
-            j += 1
-          }
-          po_ += sc.langs.length
-          po.putLong(8 * (i + 1), po_)
-          i += 1
-        }
-        kb.flip()
+      val maxRows = math.max(1L, math.min(range, 1L << 24)).toInt
+      val maxKeyBytes = 64 << 20
+      val maxPairs = 1 << 24
+      val kb = LdgpuNative.direct(maxKeyBytes.toLong)
+      val ko = LdgpuNative.direct(8L * (maxRows + 1))
+      val po = LdgpuNative.direct(8L * (maxRows + 1))
+      val pl = LdgpuNative.direct(4L * maxPairs)
+      val pc = LdgpuNative.direct(8L * maxPairs)
+      var n = 0
+      var keyBytes = 0
+      var pairs = 0
+      def flush(): Unit = if (n > 0) {
+        kb.position(0)
         LdgpuNative.check(LdgpuNative.countsAddSparse(counts, n.toLong, kb, ko, po, pl, pc))
-        first += n
+        n = 0
+        keyBytes = 0
+        pairs = 0
       }
+      ko.putLong(0, 0L)
+      po.putLong(0, 0L)
+      while (it.hasNext) {
+        val (key, sc) = it.next()
+        val kbytes = key.getBytes(ISO_8859_1)
+        if (kbytes.length > maxKeyBytes || sc.langs.length > maxPairs)
+          throw new IllegalArgumentException(s"gram of ${kbytes.length} bytes / ${sc.langs.length} languages")
+        if (n == maxRows || keyBytes + kbytes.length > maxKeyBytes || pairs + sc.langs.length > maxPairs) flush()
+        kb.position(keyBytes)
+        kb.put(kbytes)
+        keyBytes += kbytes.length
+        ko.putLong(8 * (n + 1), keyBytes.toLong)
+        var j = 0
+        while (j < sc.langs.length) {
+          pl.putInt(4 * (pairs + j), sc.langs(j))
+          pc.putLong(8 * (pairs + j), sc.counts(j))
+          j += 1
+        }
+        pairs += sc.langs.length
+        po.putLong(8 * (n + 1), pairs.toLong)
+        n += 1
+      }
+      flush()
       val size = new Array[Long](2)
       LdgpuNative.check(LdgpuNative.fitTableSize(counts, profileSize, size))
-      val (n, nb) = (size(0), size(1))
+      val (rows, nb) = (size(0), size(1))
       val s = (nLangs + 63) / 64
       val tkb = LdgpuNative.direct(nb)
-      val tko = LdgpuNative.direct(8L * (n + 1))
-      val tmk = LdgpuNative.direct(8L * n * s)
-      val tvl = LdgpuNative.direct(8L * n)
-      LdgpuNative.check(LdgpuNative.fitTableExportMasks(counts, tkb, tko, tmk, tvl, n, nb, nLangs))
-      Iterator.tabulate(n.toInt) { i =>
+      val tko = LdgpuNative.direct(8L * (rows + 1))
+      val tmk = LdgpuNative.direct(8L * rows * s)
+      val tvl = LdgpuNative.direct(8L * rows)
+      LdgpuNative.check(LdgpuNative.fitTableExportMasks(counts, tkb, tko, tmk, tvl, rows, nb, nLangs))
+      Iterator.tabulate(rows.toInt) { i =>
         val (a, b) = (tko.getLong(8 * i).toInt, tko.getLong(8 * (i + 1)).toInt)
         val key = new Array[Byte](b - a)
         var j = 0
@@ -301,20 +331,99 @@ object LanguageDetector extends Logging {
 
   /** filterTopGrams' final step over the partitions' candidates (mask form):
     * per language the K largest values (ties by key order), the union of the
-    * picks with their dense rows (the reference's table type) */
+    * picks with their dense rows (the reference's table type).
+    *
+    * A candidate's value is log(1 + 1/k), k = its language count (the mask's
+    * popcount), so a language's order is its presence classes k = 1, 2, ...
+    * then the absent candidates (value 0), each class in key order.  One sort
+    * by key, a (language, class) histogram, then one pass in key order that
+    * takes every candidate above its language's threshold class and the first
+    * need(l) of the threshold class (and of the zero-valued fill when a
+    * language has fewer than K present candidates): O(C log C + C L) instead
+    * of a full sort per language (the device's pair_hist / pair_select rule). */
   private def selectTopK(candidates: Array[(Array[Byte], Array[Long], Double)], nLangs: Int,
                          profileSize: Int): Map[Seq[Byte], Array[Double]] = {
+    val K = math.max(profileSize, 0)
+    if (K == 0 || candidates.isEmpty) return Map.empty
     val byKey = candidates.sortWith((a, b) => keyOrder.lt(a._1, b._1))
-    def v(i: Int, l: Int): Double = if (((byKey(i)._2(l / 64) >>> (l % 64)) & 1L) != 0L) byKey(i)._3 else 0.0
-    val chosen = new java.util.BitSet(byKey.length)
+    val C = byKey.length
+    val kOf = new Array[Int](C)
+    val hist = Array.ofDim[Int](nLangs, nLangs + 2)
+    var i = 0
+    while (i < C) {
+      val m = byKey(i)._2
+      var k = 0
+      var w = 0
+      while (w < m.length) { k += java.lang.Long.bitCount(m(w)); w += 1 }
+      kOf(i) = k
+      w = 0
+      while (w < m.length) {
+        var bits = m(w)
+        while (bits != 0L) {
+          val l = 64 * w + java.lang.Long.numberOfTrailingZeros(bits)
+          if (l < nLangs) hist(l)(k) += 1
+          bits &= bits - 1
+        }
+        w += 1
+      }
+      i += 1
+    }
+    // per language: threshold class kStar (nLangs + 1: the absent class) and
+    // how many of it to take
+    val kStar = Array.fill(nLangs)(nLangs + 2)
+    val need = new Array[Int](nLangs)
+    var fillLangs = List.empty[Int]
     var l = 0
     while (l < nLangs) {
-      val lang = l
-      val order = byKey.indices.sortBy(i => -v(i, lang))  // stable: key order among equal values
-      order.take(math.max(profileSize, 0)).foreach(i => chosen.set(i))
+      var acc = 0
+      var k = 1
+      while (k <= nLangs && kStar(l) == nLangs + 2) {
+        if (acc + hist(l)(k) >= K) {
+          kStar(l) = k
+          need(l) = K - acc
+        }
+        acc += hist(l)(k)
+        k += 1
+      }
+      if (kStar(l) == nLangs + 2 && K > 0) {  // fewer than K present: every present one, then the fill
+        kStar(l) = nLangs + 1
+        need(l) = K - acc
+        fillLangs = l :: fillLangs
+      }
       l += 1
     }
-    byKey.indices.filter(i => chosen.get(i))
+    val taken = new Array[Int](nLangs)
+    val chosen = new java.util.BitSet(C)
+    i = 0
+    while (i < C) {
+      val m = byKey(i)._2
+      val k = kOf(i)
+      var w = 0
+      while (w < m.length) {
+        var bits = m(w)
+        while (bits != 0L) {
+          val l = 64 * w + java.lang.Long.numberOfTrailingZeros(bits)
+          if (l < nLangs) {
+            if (k < kStar(l)) chosen.set(i)
+            else if (k == kStar(l) && taken(l) < need(l)) {
+              chosen.set(i)
+              taken(l) += 1
+            }
+          }
+          bits &= bits - 1
+        }
+        w += 1
+      }
+      for (fl <- fillLangs) {  // absent from fl: the zero-valued fill, in key order
+        if (((m(fl / 64) >>> (fl % 64)) & 1L) == 0L && taken(fl) < need(fl)) {
+          chosen.set(i)
+          taken(fl) += 1
+        }
+      }
+      i += 1
+    }
+    def v(i: Int, l: Int): Double = if (((byKey(i)._2(l / 64) >>> (l % 64)) & 1L) != 0L) byKey(i)._3 else 0.0
+    (0 until C).filter(i => chosen.get(i))
       .map(i => (byKey(i)._1.toSeq: Seq[Byte]) -> Array.tabulate(nLangs)(x => v(i, x))).toMap
   }
 

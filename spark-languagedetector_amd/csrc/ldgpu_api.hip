@@ -84,6 +84,14 @@ int ok() {
     return LDGPU_OK;
 }
 
+// Diagnostics build: LDGPU_FAIL_AT=<point> makes the named point of the
+// runtime fail (tests of the ranks' status agreement around collectives)
+int injected(const char* point) {
+    const char* f = diag_env("LDGPU_FAIL_AT");
+    if (f && strcmp(f, point) == 0) return fail(LDGPU_EDEVICE, "injected failure at %s", point);
+    return 0;
+}
+
 #define HIP_TRY(expr)                                                                              \
     do {                                                                                           \
         hipError_t e_ = (expr);                                                                    \
@@ -999,7 +1007,21 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // cache-resident tables keep the two independent slot loads (one dependent
     // step less) (such a table's bloom never fits LDS: the keyed kernels, which
     // alone read buckets)
-    const bool use_buckets = m->mode == 3 && nn > (1 << 20);
+    // Also every other count-mode table whose bloom is keyed (those kernels
+    // alone read buckets) once its cuckoo slots (2.5 per key, 32 B) would pass
+    // kBucketL2Bytes: config 4's 100k keys take 8 MiB of slots, which an XCD's
+    // 4 MiB L2 does not hold, against 1.5 MiB of buckets (one L2-resident line
+    // per verify).  Diagnostics: LDGPU_BUCKETS=0/1 forces either layout.
+    int64_t n_long = nw;
+    for (int64_t i = 0; i < nn; ++i) n_long += key_len(keys[i]) >= 3;
+    double kpw = 2.5;
+    if (const char* s = diag_env("LDGPU_BLOOM_KPW")) kpw = std::max(0.05, atof(s));  // tuning experiments only
+    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
+    bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
+    const bool keyed = bwords > (1ull << kMaxLdsBloomLog2);
+    constexpr double kBucketL2Bytes = 2.0 * (1 << 20);
+    bool use_buckets = m->mode == 3 && (nn > (1 << 20) || (keyed && 2.5 * 32.0 * (double)nn > kBucketL2Bytes));
+    if (const char* b = diag_env("LDGPU_BUCKETS")) use_buckets = m->mode == 3 && keyed && atoi(b) != 0;
     if (use_buckets && (uint64_t)nk >= (uint64_t)kPayLang) {
         // a bucket payload holds a multi-language row's index below kPayLang
         // (bit 30 marks a one-language payload, bit 31 a bad row)
@@ -1143,18 +1165,10 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // ~2 keys per 32-bit word (one bit each) keeps false positives at a few
     // percent: they only cost verification lanes (~1 VALU op each, batched 64
     // at a time), while LDS costs resident workgroups.
-    int64_t n_long = nw;
-    for (int64_t i = 0; i < nn; ++i) {
-        const int kl = key_len(keys[i]);
-        m->len_mask |= 1u << kl;
-        n_long += kl >= 3;
-    }
+    // (n_long and bwords: computed with the key table's layout above)
+    for (int64_t i = 0; i < nn; ++i) m->len_mask |= 1u << key_len(keys[i]);
     for (int64_t j = 0; j < nw; ++j) m->len_mask |= 1u << key_len(t.whi[j]);
-    double kpw = 2.5;
-    if (const char* s = diag_env("LDGPU_BLOOM_KPW")) kpw = std::max(0.05, atof(s));  // tuning experiments only
-    uint64_t bwords = next_pow2(std::max<uint64_t>(64, (uint64_t)((double)n_long / kpw) + 1));
-    bwords = std::min<uint64_t>(bwords, 1ull << kMaxBloomLog2);
-    m->lds_filter = bwords <= (1ull << kMaxLdsBloomLog2);
+    m->lds_filter = !keyed;
     m->kb_lines = !m->lds_filter && (4 * bwords > kKbLineBytes || diag_env("LDGPU_KB_LINES"));  // (tests: any keyed bloom)
     m->filter_log2 = log2u(bwords);
     const uint32_t bshift = 32u - (uint32_t)m->filter_log2;
@@ -1194,7 +1208,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     // 128)^2 over the chunks of the keys' distinct 3-byte prefixes (a window
     // whose prefix many keys share is mostly a key itself: weighting chunks
     // by key count overstates it ~6x on config 4's table).
-    if (!m->lds_filter && !m->kb_lines && m->mode == 3 && bwords >= 4) {
+    if (!m->lds_filter && !m->kb_lines && m->mode == 3 && bwords >= 8) {  // >= 2 chunks: cshift < 32
         const uint64_t chunks = bwords / 4;
         const uint32_t cshift = 32u - (uint32_t)log2u(chunks);
         std::vector<uint32_t> cf(bwords, 0u);
@@ -4485,7 +4499,7 @@ int merge_long(ldgpu_counts* c, ldgpu_comm* m) {
 // alone meets (an allocation, a count check) ends the merge on EVERY rank
 // instead of leaving the others waiting in the next exchange.  Returns the
 // local code (with its message) or LDGPU_EDEVICE naming the failed rank.
-int comm_agree(ldgpu_comm* m, int rc) {
+int comm_agree(ldgpu_comm* m, int rc, const char* what = "merge") {
     if (m->world == 1) return rc;
     const std::string mine = g_err;
     int32_t v = rc;
@@ -4496,7 +4510,7 @@ int comm_agree(ldgpu_comm* m, int rc) {
         return rc;
     }
     for (int r = 0; r < m->world; ++r)
-        if (all[r]) return fail(LDGPU_EDEVICE, "merge: rank %d failed (status %d)", r, all[r]);
+        if (all[r]) return fail(LDGPU_EDEVICE, "%s: rank %d failed (status %d)", what, r, all[r]);
     return LDGPU_OK;
 }
 }  // namespace
@@ -4609,32 +4623,42 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     hipStream_t st = c->ctx->stream;
     DevBufs db;
     db.ctx = c->ctx;
-    if (n > (int64_t)0xffffffffll) return fail(LDGPU_EUNSUPPORTED, "fit table: %lld grams", (long long)n);
     const CountParams cp = count_params(c);
-    uint64_t* d_keys;
-    uint32_t* d_rowof;
-    int32_t* d_k;
-    unsigned long long* d_n;
-    unsigned int* d_hist;
-    HIP_TRY(db.alloc(&d_keys, n));
-    HIP_TRY(db.alloc(&d_k, n));
-    HIP_TRY(db.alloc(&d_rowof, c->cap));
-    HIP_TRY(db.alloc(&d_n, 2));
-    HIP_TRY(db.alloc(&d_hist, (size_t)L * (L + 1)));
-    PhaseMarks mark(st);
-    mark("table: scratch");
-    HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(unsigned int) * L * (L + 1), st));
-    HIP_TRY(launch_gram_rows(cp, c->cap, d_keys, d_k, d_rowof, d_n, st));
-    mark("table: gram rows");
-    HIP_TRY(launch_pair_hist(cp, c->pcap, d_rowof, d_k, L, d_hist, st));
-    mark("table: pair histogram");
+    // A merged table's build is collective: every rank agrees its status
+    // before each collective (comm_agree), so a failure on one rank (an
+    // allocation, a count check) ends the build on every rank instead of
+    // leaving the others waiting in the next all-gather.
+    auto agree = [&](int rc) { return cm ? comm_agree(cm, rc, "fit table") : rc; };
+    uint64_t* d_keys = nullptr;
+    uint32_t* d_rowof = nullptr;
+    int32_t* d_k = nullptr;
+    unsigned long long* d_n = nullptr;
+    unsigned int* d_hist = nullptr;
     std::vector<unsigned int> hist((size_t)L * (L + 1));
-    unsigned long long got = 0;
-    HIP_TRY(hipMemcpyAsync(hist.data(), d_hist, sizeof(unsigned int) * hist.size(), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if ((int64_t)got != n) return fail(LDGPU_EDEVICE, "presence: %llu grams, %lld expected", got, (long long)n);
+    PhaseMarks mark(st);
+    auto hist_phase = [&]() -> int {
+        if (int rc = injected("table_hist")) return rc;
+        if (n > (int64_t)0xffffffffll) return fail(LDGPU_EUNSUPPORTED, "fit table: %lld grams", (long long)n);
+        HIP_TRY(db.alloc(&d_keys, n));
+        HIP_TRY(db.alloc(&d_k, n));
+        HIP_TRY(db.alloc(&d_rowof, c->cap));
+        HIP_TRY(db.alloc(&d_n, 2));
+        HIP_TRY(db.alloc(&d_hist, (size_t)L * (L + 1)));
+        mark("table: scratch");
+        HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
+        HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(unsigned int) * L * (L + 1), st));
+        HIP_TRY(launch_gram_rows(cp, c->cap, d_keys, d_k, d_rowof, d_n, st));
+        mark("table: gram rows");
+        HIP_TRY(launch_pair_hist(cp, c->pcap, L, d_hist, c->ctx->cus, st));
+        mark("table: pair histogram");
+        unsigned long long got = 0;
+        HIP_TRY(hipMemcpyAsync(hist.data(), d_hist, sizeof(unsigned int) * hist.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&got, d_n, sizeof got, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if ((int64_t)got != n) return fail(LDGPU_EDEVICE, "presence: %llu grams, %lld expected", got, (long long)n);
+        return LDGPU_OK;
+    };
+    if (int rc = agree(hist_phase())) return rc;
     std::vector<int64_t> ghist(hist.begin(), hist.end());  // global (summed over ranks)
     if (cm && cm->world > 1) {
         std::vector<int64_t> mine(ghist), allh(ghist.size() * cm->world);
@@ -4669,7 +4693,9 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         if (!cm) return LDGPU_OK;  // the host build from the count table
         // merged table: gather every rank's presence rows, select on the host
         std::vector<uint64_t> hk(n), hm((size_t)n * S);
-        if (n) {
+        auto rows_phase = [&]() -> int {
+            if (int rc = injected("table_fallback")) return rc;
+            if (!n) return LDGPU_OK;
             uint64_t* d_masks;
             HIP_TRY(db.alloc(&d_masks, (size_t)n * S));
             HIP_TRY(hipMemsetAsync(d_masks, 0, sizeof(uint64_t) * n * S, st));
@@ -4677,7 +4703,9 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
             HIP_TRY(hipMemcpyAsync(hk.data(), d_keys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(hm.data(), d_masks, sizeof(uint64_t) * n * S, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
-        }
+            return LDGPU_OK;
+        };
+        if (int rc = agree(rows_phase())) return rc;
         std::vector<uint8_t> blob;
         put(blob, hk.data(), hk.size());
         put(blob, hm.data(), hm.size());
@@ -4699,7 +4727,11 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         }
         if (c->merged_wide) {  // every rank's grams of 8 or more bytes after them, in (length, bytes) order
             Ext x;
-            if (int rc = ext_export(c, x, true)) return rc;
+            auto ext_phase = [&]() -> int {
+                if (int rc = injected("table_wide")) return rc;
+                return ext_export(c, x, true);
+            };
+            if (int rc = agree(ext_phase())) return rc;
             // blob: count, then per gram its length, bytes and S mask words
             std::vector<uint8_t> wblob;
             const uint64_t nx = x.keys.size();
@@ -4746,54 +4778,121 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         *fallback = false;
         return table_from_presence(c, keys, masks, K, n_rows, key_bytes);
     }
-    int32_t *d_kstar, *d_need, *d_cl;
-    uint8_t* d_chosen;
-    uint64_t* d_ck;
-    uint32_t* d_ci;
-    unsigned int* d_cn;
-    HIP_TRY(db.alloc(&d_kstar, L));
-    HIP_TRY(db.alloc(&d_need, L));
-    HIP_TRY(db.alloc(&d_chosen, n));
-    HIP_TRY(db.alloc(&d_cl, cand_cap));
-    HIP_TRY(db.alloc(&d_ck, cand_cap));
-    HIP_TRY(db.alloc(&d_ci, cand_cap));
-    HIP_TRY(db.alloc(&d_cn, 1));
-    HIP_TRY(hipMemcpyAsync(d_kstar, kstar.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_need, need.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(d_cn, 0, sizeof(unsigned int), st));
-    HIP_TRY(hipMemsetAsync(d_chosen, 0, (size_t)n, st));
-    HIP_TRY(launch_pair_select(cp, c->pcap, d_rowof, d_keys, d_k, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn,
-                               st));
+    const bool multi = cm && cm->world > 1;
+    int32_t *d_kstar = nullptr, *d_need = nullptr, *d_cl = nullptr;
+    uint8_t* d_chosen = nullptr;
+    uint64_t* d_ck = nullptr;
+    uint32_t* d_ci = nullptr;
+    unsigned int* d_cn = nullptr;
+    uint64_t* d_thr = nullptr;
     unsigned int cn = 0;
-    HIP_TRY(hipMemcpyAsync(&cn, d_cn, sizeof cn, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (cn != cand_cap) return fail(LDGPU_EDEVICE, "select: %u candidates, %llu expected", cn,
-                                    (unsigned long long)cand_cap);
-    mark("table: select");
-    // per language: the need[l] smallest (length, bytes) keys of its threshold
-    // class (candidates of language l form segment l once sorted)
     std::vector<int64_t> seg(L + 1, 0);
-    for (int l = 0; l < L; ++l)
-        seg[l + 1] = seg[l] + (need[l] > 0 && kstar[l] <= L ? (int64_t)hist[(size_t)l * (L + 1) + kstar[l]] : 0);
-    if (seg[L] != (int64_t)cn)
-        return fail(LDGPU_EDEVICE, "select: %u candidates, %lld by class", cn, (long long)seg[L]);
-    int64_t* d_seg;
-    HIP_TRY(db.alloc(&d_seg, L + 1));
-    HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), sizeof(int64_t) * (L + 1), hipMemcpyHostToDevice, st));
-    if (!cm || cm->world == 1) {
-        HIP_TRY(launch_topk_candidates((int64_t)cn, L, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, nullptr, st));
-    } else {
+    // multi-rank: this rank's need[l] smallest threshold-class candidates of
+    // each language (their sort keys), gathered from every rank
+    std::vector<int64_t> take(L, 0);
+    std::vector<uint64_t> pre;
+    int64_t tot = 0;
+    auto select_phase = [&]() -> int {
+        if (int rc = injected("table_select")) return rc;
+        HIP_TRY(db.alloc(&d_kstar, L));
+        HIP_TRY(db.alloc(&d_need, L));
+        HIP_TRY(db.alloc(&d_chosen, n));
+        HIP_TRY(db.alloc(&d_cl, cand_cap));
+        HIP_TRY(db.alloc(&d_ck, cand_cap));
+        HIP_TRY(db.alloc(&d_ci, cand_cap));
+        HIP_TRY(db.alloc(&d_cn, 2));
+        // one rank: the threshold class's candidates per (language, length)
+        // too (<= 512 languages: the counters in LDS)
+        const bool split = !multi && L <= 512 && cand_cap > 0;
+        unsigned int* d_lh = nullptr;
+        if (split) {
+            HIP_TRY(db.alloc(&d_lh, (size_t)16 * L));
+            HIP_TRY(hipMemsetAsync(d_lh, 0, sizeof(unsigned int) * 16 * L, st));
+        }
+        HIP_TRY(hipMemcpyAsync(d_kstar, kstar.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_need, need.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(d_cn, 0, 2 * sizeof(unsigned int), st));
+        HIP_TRY(hipMemsetAsync(d_chosen, 0, (size_t)n, st));
+        HIP_TRY(launch_pair_select(cp, c->pcap, d_rowof, d_keys, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn, L,
+                                   d_lh, st));
+        std::vector<unsigned int> lh(split ? (size_t)16 * L : 0);
+        HIP_TRY(hipMemcpyAsync(&cn, d_cn, sizeof cn, hipMemcpyDeviceToHost, st));
+        if (split) HIP_TRY(hipMemcpyAsync(lh.data(), d_lh, sizeof(unsigned int) * lh.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (cn != cand_cap)
+            return fail(LDGPU_EDEVICE, "select: %u candidates, %llu expected", cn, (unsigned long long)cand_cap);
+        mark("table: select");
+        // per language: the need[l] smallest (length, bytes) keys of its
+        // threshold class (candidates of language l form segment l once sorted)
+        for (int l = 0; l < L; ++l)
+            seg[l + 1] = seg[l] + (need[l] > 0 && kstar[l] <= L ? (int64_t)hist[(size_t)l * (L + 1) + kstar[l]] : 0);
+        if (seg[L] != (int64_t)cn)
+            return fail(LDGPU_EDEVICE, "select: %u candidates, %lld by class", cn, (long long)seg[L]);
+        if (split) {
+            // The tie order is (length, bytes): per language, every candidate
+            // shorter than the length at which the cumulative count reaches
+            // need[l] is chosen outright, and only candidates of exactly that
+            // length are ranked (config 5's fit: ~1G class pairs -> the few
+            // thousand of one length per language, instead of sorting them all)
+            std::vector<int32_t> thr(L, 0);
+            std::vector<int64_t> seg2(L + 1, 0);
+            for (int l = 0; l < L; ++l) {
+                int64_t cnt_l = seg[l + 1] - seg[l], acc = 0;
+                if (need[l] > 0 && cnt_l > 0) {
+                    for (int len = 0; len < 16; ++len) {
+                        const int64_t c_len = lh[(size_t)16 * l + len];
+                        if (acc + c_len >= need[l]) {
+                            thr[l] = len;
+                            need[l] -= (int32_t)acc;
+                            cnt_l = c_len;
+                            break;
+                        }
+                        acc += c_len;
+                    }
+                }
+                seg2[l + 1] = seg2[l] + cnt_l;
+            }
+            int32_t *d_thr_len, *d_cl2;
+            uint64_t* d_ck2;
+            uint32_t* d_ci2;
+            const size_t n2 = (size_t)std::max<int64_t>(seg2[L], 1);
+            HIP_TRY(db.alloc(&d_thr_len, L));
+            HIP_TRY(db.alloc(&d_cl2, n2));
+            HIP_TRY(db.alloc(&d_ck2, n2));
+            HIP_TRY(db.alloc(&d_ci2, n2));
+            HIP_TRY(hipMemcpyAsync(d_thr_len, thr.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(d_need, need.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_cand_filter((int64_t)cn, d_cl, d_ck, d_ci, d_thr_len, d_chosen, d_cl2, d_ck2, d_ci2, d_cn + 1,
+                                       st));
+            unsigned int cn2 = 0;
+            HIP_TRY(hipMemcpyAsync(&cn2, d_cn + 1, sizeof cn2, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if ((int64_t)cn2 != seg2[L])
+                return fail(LDGPU_EDEVICE, "select: %u candidates of the split lengths, %lld expected", cn2,
+                            (long long)seg2[L]);
+            d_cl = d_cl2;
+            d_ck = d_ck2;
+            d_ci = d_ci2;
+            cn = cn2;
+            seg = seg2;
+            mark("table: length split");
+        }
+        int64_t* d_seg;
+        HIP_TRY(db.alloc(&d_seg, L + 1));
+        HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), sizeof(int64_t) * (L + 1), hipMemcpyHostToDevice, st));
+        if (!multi) {
+            HIP_TRY(launch_topk_candidates((int64_t)cn, L, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, nullptr, st));
+            return LDGPU_OK;
+        }
         // each rank's need[l] smallest candidates can hold the global ones:
         // gather those prefixes, the need[l]-th smallest key of language l is
         // its threshold, and every rank takes its candidates at or below it
-        uint64_t *d_sk, *d_thr;
+        uint64_t* d_sk;
         HIP_TRY(db.alloc(&d_sk, cn));
         HIP_TRY(db.alloc(&d_thr, L));
         HIP_TRY(launch_topk_candidates((int64_t)cn, L, d_cl, d_ck, d_ci, d_seg, d_need, d_chosen, d_sk, st));
-        std::vector<int64_t> take(L, 0);
-        int64_t tot = 0;
         for (int l = 0; l < L; ++l) tot += take[l] = std::min<int64_t>(need[l], seg[l + 1] - seg[l]);
-        std::vector<uint64_t> pre((size_t)std::max<int64_t>(tot, 1));
+        pre.assign((size_t)std::max<int64_t>(tot, 1), 0);
         int64_t at = 0;
         for (int l = 0; l < L; ++l) {
             if (take[l])
@@ -4802,6 +4901,11 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
             at += take[l];
         }
         HIP_TRY(hipStreamSynchronize(st));
+        return LDGPU_OK;
+    };
+    if (int rc = agree(select_phase())) return rc;
+    std::vector<uint64_t> thr(L, 0);
+    if (multi) {
         std::vector<uint8_t> blob;
         put(blob, take.data(), take.size());
         put(blob, pre.data(), (size_t)tot);
@@ -4816,7 +4920,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
                 ks += tk[l];
             }
         }
-        std::vector<uint64_t> thr(L, 0);
+        // (from gathered data: every rank takes the same branch here)
         for (int l = 0; l < L; ++l) {
             if (need[l] <= 0) continue;
             if ((int64_t)per[l].size() < need[l])
@@ -4825,32 +4929,50 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
             std::nth_element(per[l].begin(), per[l].begin() + (need[l] - 1), per[l].end());
             thr[l] = per[l][need[l] - 1];
         }
-        HIP_TRY(hipMemcpyAsync(d_thr, thr.data(), sizeof(uint64_t) * L, hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_mark_threshold((int64_t)cn, d_cl, d_ck, d_ci, d_thr, d_chosen, st));
     }
     mark("table: threshold ties");
     const int64_t cap_out = std::min<int64_t>(n, (int64_t)L * std::max<int32_t>(K, 0));
-    uint64_t *d_ok, *d_om;
-    int32_t* d_okk;
-    uint32_t* d_outrow;
-    HIP_TRY(db.alloc(&d_ok, cap_out));
-    HIP_TRY(db.alloc(&d_okk, cap_out));
-    HIP_TRY(db.alloc(&d_outrow, n));
-    HIP_TRY(hipMemsetAsync(d_n + 1, 0, sizeof(unsigned long long), st));
-    HIP_TRY(launch_gather_rows(n, d_chosen, d_keys, d_k, d_ok, d_okk, d_outrow, d_n + 1, cap_out, st));
+    uint64_t *d_ok = nullptr, *d_om = nullptr;
+    int32_t* d_okk = nullptr;
+    uint32_t* d_outrow = nullptr;
     unsigned long long m = 0;
-    HIP_TRY(hipMemcpyAsync(&m, d_n + 1, sizeof m, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if ((int64_t)m > cap_out) return fail(LDGPU_EDEVICE, "top-K: %llu grams chosen, at most %lld expected", m,
-                                         (long long)cap_out);
-    HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
-    HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
-    mark("table: gather rows");
-    HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, d_outrow, S, d_om, st));
-    mark("table: masks");
+    std::vector<uint64_t> ok, om;  // multi-rank: this rank's chosen rows, gathered below
+    std::vector<int32_t> okk;
+    auto rows_phase = [&]() -> int {
+        if (int rc = injected("table_rows")) return rc;
+        if (multi) {
+            HIP_TRY(hipMemcpyAsync(d_thr, thr.data(), sizeof(uint64_t) * L, hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_mark_threshold((int64_t)cn, d_cl, d_ck, d_ci, d_thr, d_chosen, st));
+        }
+        HIP_TRY(db.alloc(&d_ok, cap_out));
+        HIP_TRY(db.alloc(&d_okk, cap_out));
+        HIP_TRY(db.alloc(&d_outrow, n));
+        HIP_TRY(hipMemsetAsync(d_n + 1, 0, sizeof(unsigned long long), st));
+        HIP_TRY(launch_gather_rows(n, d_chosen, d_keys, d_k, d_ok, d_okk, d_outrow, d_n + 1, cap_out, st));
+        HIP_TRY(hipMemcpyAsync(&m, d_n + 1, sizeof m, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if ((int64_t)m > cap_out)
+            return fail(LDGPU_EDEVICE, "top-K: %llu grams chosen, at most %lld expected", m, (long long)cap_out);
+        mark("table: gather rows");
+        HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
+        HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
+        HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, d_outrow, S, d_om, st));
+        mark("table: masks");
+        if (multi && m) {
+            ok.resize(m);
+            om.resize((size_t)m * S);
+            okk.resize(m);
+            HIP_TRY(hipMemcpyAsync(ok.data(), d_ok, sizeof(uint64_t) * m, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(om.data(), d_om, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(okk.data(), d_okk, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        return LDGPU_OK;
+    };
+    if (int rc = agree(rows_phase())) return rc;
     std::vector<double> w(L + 1, 0.0);
     for (int k = 1; k <= L; ++k) w[k] = std::log(1.0 + 1.0 / (double)k);
-    if (!cm || cm->world == 1) {
+    if (!multi) {
         // one rank: the rows sorted by (length, bytes) on the device (radix
         // sort of the sort keys, then a gather), copied back in table order
         uint64_t *d_sk, *d_ok2, *d_om2;
@@ -4887,14 +5009,6 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         if (key_bytes) *key_bytes = nb;
         mark("table: copy back + host rows");
         return LDGPU_OK;
-    }
-    std::vector<uint64_t> ok(m), om((size_t)m * S);
-    std::vector<int32_t> okk(m);
-    if (m) {
-        HIP_TRY(hipMemcpyAsync(ok.data(), d_ok, sizeof(uint64_t) * m, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(om.data(), d_om, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(okk.data(), d_okk, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
     }
     {  // every rank's chosen rows
         std::vector<uint8_t> blob;

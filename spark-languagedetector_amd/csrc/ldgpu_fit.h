@@ -333,14 +333,21 @@ hipError_t launch_long_rehash(const LongCountParams& from, const LongCountParams
 // the selection and the chosen rows' presence masks all from the pairs
 hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint32_t* rowof,
                             unsigned long long* out_n, hipStream_t stream);
-hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const int32_t* ks, int L,
-                            unsigned int* hist, hipStream_t stream);
+hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, unsigned int* hist, int cus,
+                            hipStream_t stream);
 // chosen[j] = 1 when the gram is below its language's threshold class; the
-// threshold-class pairs (need[l] > 0) appended as candidates (lang, sort key, j)
+// threshold-class pairs (need[l] > 0) appended as candidates (lang, sort key, j);
+// lenhist (nullable, [L][16]) += the candidates per (language, key length)
 hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
-                              const int32_t* ks, const int32_t* kstar, const int32_t* need, uint8_t* chosen,
-                              int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n,
-                              hipStream_t stream);
+                              const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
+                              uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, int L,
+                              unsigned int* lenhist, hipStream_t stream);
+// the length split of the threshold class: candidates shorter than
+// thr_len[l] chosen, those of thr_len[l] bytes compacted into out_*, longer
+// ones dropped (thr_len[l] = 0: all kept)
+hipError_t launch_cand_filter(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key, const uint32_t* cand_idx,
+                              const int32_t* thr_len, uint8_t* chosen, int32_t* out_lang, uint64_t* out_key,
+                              uint32_t* out_idx, unsigned int* out_n, hipStream_t stream);
 // the chosen rows: out_keys[r], out_k[r], outrow[j] = r (0xffffffff: not
 // chosen); rows from out_cap on are counted in out_n, not written
 hipError_t launch_gather_rows(int64_t n, const uint8_t* chosen, const uint64_t* keys, const int32_t* ks,

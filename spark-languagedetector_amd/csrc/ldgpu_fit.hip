@@ -735,28 +735,30 @@ __global__ __launch_bounds__(kScanThreads) void gram_rows_kernel(const CountPara
 __device__ __forceinline__ uint32_t pair_lang(uint64_t pk) { return (uint32_t)(pk & ((1ull << kPairLangBits) - 1ull)); }
 __device__ __forceinline__ uint64_t pair_slot(uint64_t pk) { return (pk >> kPairLangBits) - 1ull; }
 
-// (language, k) histogram: in LDS for L <= 88 (L (L + 1) counters), flushed
-// once per block
-__global__ __launch_bounds__(256) void pair_hist_kernel(const CountParams p, uint64_t pcap, const uint32_t* rowof,
-                                                        const int32_t* ks, int L, unsigned int* hist) {
+// (language, k) histogram of the pairs, k = the gram's language count (kcnt
+// at its slot: one random read per pair).  Classes k <= kl count in LDS
+// ([L][kl + 1], kl = L when it fits), the rest -- rare: most grams are in
+// few languages -- in global memory; each block flushes its nonzero LDS
+// counters once.  (Global atomics on the ~L hot counters of k = 1: 152 ms on
+// config 5's 1.39G pairs.)
+__global__ __launch_bounds__(kScanThreads) void pair_hist_kernel(const CountParams p, uint64_t pcap, int L, int kl,
+                                                                 unsigned int* hist) {
     extern __shared__ unsigned int lh[];
-    const bool lds = L <= 88;
-    if (lds) {
-        for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x) lh[i] = 0u;
-        __syncthreads();
-    }
+    const int kw = kl + 1;
+    for (int i = threadIdx.x; i < L * kw; i += blockDim.x) lh[i] = 0u;
+    __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pcap; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t pk = p.pkeys[i];
         if (pk == kEmpty) continue;
         const uint32_t l = pair_lang(pk);
-        const int k = ks[rowof[pair_slot(pk)]];
-        if (lds) atomicAdd(&lh[l * (L + 1) + k], 1u);
+        const int k = (int)p.kcnt[pair_slot(pk)];
+        if (k <= kl) atomicAdd(&lh[l * kw + k], 1u);
         else atomicAdd(&hist[l * (L + 1) + k], 1u);
     }
-    if (lds) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < L * (L + 1); i += blockDim.x)
-            if (lh[i]) atomicAdd(&hist[i], lh[i]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < L * kw; i += blockDim.x) {
+        const unsigned int v = lh[i];
+        if (v) atomicAdd(&hist[(i / kw) * (L + 1) + i % kw], v);
     }
 }
 
@@ -764,14 +766,21 @@ __global__ __launch_bounds__(256) void pair_hist_kernel(const CountParams p, uin
 // class can hold most pairs (config 3: nearly every gram is in one language),
 // and one counter add per wave serialised ~1M atomics on cand_n (47 ms of a
 // 72M-pair table)
+// lenhist (nullable): the candidates per (language, key length) ([L][16],
+// in LDS, flushed once per block) -- the threshold class's length split
 __global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountParams p, uint64_t pcap,
                                                                    const uint32_t* rowof, const uint64_t* keys,
-                                                                   const int32_t* ks, const int32_t* kstar,
-                                                                   const int32_t* need, uint8_t* chosen,
-                                                                   int32_t* cand_lang, uint64_t* cand_key,
-                                                                   uint32_t* cand_idx, unsigned int* cand_n) {
+                                                                   const int32_t* kstar, const int32_t* need,
+                                                                   uint8_t* chosen, int32_t* cand_lang,
+                                                                   uint64_t* cand_key, uint32_t* cand_idx,
+                                                                   unsigned int* cand_n, int L, unsigned int* lenhist) {
     __shared__ unsigned int wcnt[kScanThreads / 64];
     __shared__ unsigned long long bbase;
+    extern __shared__ unsigned int lh[];
+    if (lenhist) {
+        for (int i = threadIdx.x; i < 16 * L; i += blockDim.x) lh[i] = 0u;
+        __syncthreads();
+    }
     for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < pcap; c0 += (uint64_t)gridDim.x * kScanThreads) {
         const uint64_t i = c0 + threadIdx.x;
         const uint64_t pk = i < pcap ? p.pkeys[i] : kEmpty;
@@ -779,17 +788,59 @@ __global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountPa
         uint32_t l = 0, j = 0;
         if (pk != kEmpty) {
             l = pair_lang(pk);
-            j = rowof[pair_slot(pk)];
-            const int k = ks[j];
+            const uint64_t g = pair_slot(pk);
+            j = rowof[g];
+            const int k = (int)p.kcnt[g];
             const int ksl = kstar[l];
             if (k < ksl) chosen[j] = 1;
             cand = k == ksl && need[l] > 0;
         }
         const unsigned long long at = block_compact<unsigned int>(cand, cand_n, wcnt, &bbase);
         if (!cand) continue;
+        const uint64_t sk = sort_key(keys[j]);
         cand_lang[at] = (int32_t)l;
-        cand_key[at] = sort_key(keys[j]);
+        cand_key[at] = sk;
         cand_idx[at] = j;
+        if (lenhist) atomicAdd(&lh[16 * l + (int)(sk >> 56)], 1u);
+    }
+    if (lenhist) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 16 * L; i += blockDim.x) {
+            const unsigned int v = lh[i];
+            if (v) atomicAdd(&lenhist[i], v);
+        }
+    }
+}
+
+// the threshold class's length split (fit_table_device): a candidate of
+// language l shorter than thr_len[l] is chosen outright, one of exactly
+// thr_len[l] bytes stays a candidate (compacted into out_*), a longer one
+// drops out; thr_len[l] = 0 keeps every candidate of l
+__global__ __launch_bounds__(kScanThreads) void cand_filter_kernel(int64_t n, const int32_t* cand_lang,
+                                                                   const uint64_t* cand_key, const uint32_t* cand_idx,
+                                                                   const int32_t* thr_len, uint8_t* chosen,
+                                                                   int32_t* out_lang, uint64_t* out_key,
+                                                                   uint32_t* out_idx, unsigned int* out_n) {
+    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned long long bbase;
+    for (int64_t c0 = (int64_t)blockIdx.x * kScanThreads; c0 < n; c0 += (int64_t)gridDim.x * kScanThreads) {
+        const int64_t i = c0 + threadIdx.x;
+        bool keep = false;
+        int32_t l = 0;
+        uint64_t sk = 0;
+        if (i < n) {
+            l = cand_lang[i];
+            sk = cand_key[i];
+            const int t = thr_len[l];
+            const int len = (int)(sk >> 56);
+            keep = t == 0 || len == t;
+            if (t && len < t) chosen[cand_idx[i]] = 1;
+        }
+        const unsigned long long at = block_compact<unsigned int>(keep, out_n, wcnt, &bbase);
+        if (!keep) continue;
+        out_lang[at] = l;
+        out_key[at] = sk;
+        out_idx[at] = cand_idx[i];
     }
 }
 
@@ -941,21 +992,35 @@ hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_ke
     return hipGetLastError();
 }
 
-hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const int32_t* ks, int L,
-                            unsigned int* hist, hipStream_t stream) {
-    const size_t lds = L <= 88 ? (size_t)L * (L + 1) * 4 : 0;
-    const unsigned g = (unsigned)std::min<uint64_t>(4096, (pcap + 255) / 256);
-    hipLaunchKernelGGL(pair_hist_kernel, dim3(g), dim3(256), lds, stream, p, pcap, rowof, ks, L, hist);
+hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, unsigned int* hist, int cus,
+                            hipStream_t stream) {
+    if (pcap == 0) return hipSuccess;
+    // LDS classes: every k when L (L + 1) counters fit 48 KiB, else as many
+    // as fit (at least k = 1)
+    const int kl = std::max(1, std::min(L, (int)(12288 / L) - 1));
+    const size_t lds = (size_t)L * (kl + 1) * 4;
+    const unsigned g = (unsigned)std::min<uint64_t>((uint64_t)cus * 2, (pcap + kScanThreads - 1) / kScanThreads);
+    hipLaunchKernelGGL(pair_hist_kernel, dim3(std::max(1u, g)), dim3(kScanThreads), lds, stream, p, pcap, L, kl, hist);
     return hipGetLastError();
 }
 
 hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
-                              const int32_t* ks, const int32_t* kstar, const int32_t* need, uint8_t* chosen,
-                              int32_t* cand_lang, uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n,
-                              hipStream_t stream) {
+                              const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
+                              uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, int L,
+                              unsigned int* lenhist, hipStream_t stream) {
     if (pcap == 0) return hipSuccess;
-    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid(pcap)), dim3(kScanThreads), 0, stream, p, pcap, rowof,
-                       keys, ks, kstar, need, chosen, cand_lang, cand_key, cand_idx, cand_n);
+    const size_t lds = lenhist ? (size_t)16 * L * 4 : 0;
+    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid(pcap)), dim3(kScanThreads), lds, stream, p, pcap, rowof,
+                       keys, kstar, need, chosen, cand_lang, cand_key, cand_idx, cand_n, L, lenhist);
+    return hipGetLastError();
+}
+
+hipError_t launch_cand_filter(int64_t n, const int32_t* cand_lang, const uint64_t* cand_key, const uint32_t* cand_idx,
+                              const int32_t* thr_len, uint8_t* chosen, int32_t* out_lang, uint64_t* out_key,
+                              uint32_t* out_idx, unsigned int* out_n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cand_filter_kernel, dim3(scan_grid((uint64_t)n)), dim3(kScanThreads), 0, stream, n, cand_lang,
+                       cand_key, cand_idx, thr_len, chosen, out_lang, out_key, out_idx, out_n);
     return hipGetLastError();
 }
 

@@ -37,6 +37,8 @@
 // one superblock); in count mode consecutive short ones share a superblock
 // (packs).  Shorter documents (partial windows) and longer ones loop n outer,
 // superblocks inner.
+#include <type_traits>
+
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
@@ -1306,6 +1308,9 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
 // pack path's registers never burden the single-document kernels
 // BL: the bloom layout (KEYED of the device functions): 0 = prefix Bloom in
 // LDS, 1 = keyed bloom (words / lines), 2 = keyed chunks
+// INVARIANT (cold_params): ScoreParams is the kernel's first and only explicit
+// argument, so it sits at offset 0 of the kernarg segment; the static_assert
+// after the kernel checks the signature.
 template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false>
 __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
     constexpr bool FLDS = BL == 0;
@@ -1523,6 +1528,16 @@ hipError_t prepare_m(int slices, bool lds_bloom, bool chunks, size_t lds, int* b
 
 // first maximum across language blocks: block maxima compared with '>' in
 // block order, as breeze's argmax compares scores in language order
+// cold_params() reads the kernarg segment as a ScoreParams: any other
+// argument list for score_kernel must change cold_params first
+template <typename T>
+struct ParamsOnlyKernel : std::false_type {};
+template <>
+struct ParamsOnlyKernel<void (*)(ScoreParams)> : std::true_type {};
+static_assert(ParamsOnlyKernel<decltype(&score_kernel<1, 3, 0, false, false>)>::value &&
+                  ParamsOnlyKernel<decltype(&score_kernel<4, 1, 1, true, true>)>::value,
+              "score_kernel must take exactly one argument, ScoreParams (cold_params reads it at kernarg offset 0)");
+
 __global__ void combine_blocks_kernel(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

@@ -205,9 +205,16 @@ def tree_source_hash() -> str:
 
 
 def provenance(variant: str = "product") -> dict:
-    """The loaded library's build id against this tree's sources."""
+    """The loaded library's build id against this tree's sources.  The id is
+    the sources' hash, plus "+<flags hash>" for a library built with other
+    compile flags than the product's (diagnostics, sanitizer and tuning
+    builds; spark-languagedetector_amd/Makefile): `match` holds when the
+    sources are this tree's and -- for the product variant -- the flags are
+    the product's."""
     lib = load(variant=variant)
     built = lib.ldgpu_build_id().decode()
+    src, _, flags = built.partition("+")
     tree = tree_source_hash()
-    return {"library_source_hash": built, "tree_source_hash": tree, "match": built == tree}
+    return {"library_source_hash": src, "build_flags_tag": flags or None, "tree_source_hash": tree,
+            "match": src == tree and (variant != "product" or not flags)}
 

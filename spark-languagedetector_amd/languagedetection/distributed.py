@@ -89,11 +89,13 @@ class Communicator:
     all-gather / all-to-all served by the group (gloo); "auto": RCCL when the
     group's backend is nccl."""
 
-    def __init__(self, group=None, device: Optional[int] = None, transport: str = "auto"):
+    def __init__(self, group=None, device: Optional[int] = None, transport: str = "auto", variant: str = "product"):
+        """variant: the library of the count tables it merges (handles of the
+        diagnostics library need a communicator of the same library)."""
         import torch.distributed as dist
 
-        self.lib = _lib.load()
-        self.ctx = _lib.context(device)
+        self.lib = _lib.load(variant=variant)
+        self.ctx = _lib.context(device, variant)
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -171,7 +173,7 @@ def merge_counts_device(local, comm: Optional[Communicator] = None, group=None):
     afterwards it holds the global counts of the grams this rank owns, and its
     fit_table() is the global table (collective).  Returns `local`."""
     if comm is None:
-        comm = Communicator(group, device=local.device)
+        comm = Communicator(group, device=local.device, variant=getattr(local, "variant", "product"))
     local._check(local.lib.ldgpu_counts_merge(local.h, comm.h))
     local.comm = comm  # the merged table's fit_table() runs its collectives
     return local

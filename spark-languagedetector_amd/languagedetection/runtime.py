@@ -158,6 +158,7 @@ class DeviceCounts(_Owner):
         self.lib = _lib.load(variant=variant)
         self.ctx = _lib.context(device, variant)
         self.device = device
+        self.variant = variant
         self.L = int(n_langs)
         self.gram_lengths = list(gram_lengths)
         g = _grams(gram_lengths)

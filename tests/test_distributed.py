@@ -167,6 +167,60 @@ def test_fit_merge_rccl_transport_world1(tmp_path, grams):
     _check_fit(tmp_path, 1, 80, grams)
 
 
+def _fail_worker(rank, world, port, out_dir, K, grams, point):
+    """A merged table's top-K with rank 1 failing at `point` (diagnostics
+    library, LDGPU_FAIL_AT): every rank must return an error, none may wait."""
+    dist = _init(rank, world, port)
+    from languagedetection import synth
+    from languagedetection.distributed import Communicator, merge_counts_device, shard_range
+    from languagedetection.runtime import DeviceCounts
+    ls, (data, off, lang) = _corpus()
+    lo, hi = shard_range(len(off) - 1, rank, world)
+    local = DeviceCounts(6, grams, device=0, variant="diag")
+    local.count(data[off[lo]:off[hi]], off[lo:hi + 1] - off[lo], lang[lo:hi])
+    comm = Communicator(device=0, transport="host", variant="diag")
+    merge_counts_device(local, comm)
+    if rank == 1:
+        os.environ["LDGPU_FAIL_AT"] = point
+    try:
+        local.fit_table(K)
+        msg = "no error"
+    except Exception as e:  # noqa: BLE001 -- the test reads the message
+        msg = f"{type(e).__name__}: {e}"
+    os.environ.pop("LDGPU_FAIL_AT", None)
+    with open(os.path.join(out_dir, f"err{rank}.txt"), "w") as f:
+        f.write(msg)
+    local.close()
+    comm.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("point,K,grams", [("table_hist", 80, [1, 2, 3]), ("table_select", 80, [1, 2, 3]),
+                                           ("table_rows", 80, [1, 2, 3]), ("table_fallback", 5000, [2, 3]),
+                                           ("table_wide", 60, [2, 9])])
+def test_fit_table_rank_failure_ends_every_rank(tmp_path, point, K, grams):
+    """The distributed top-K (LanguageDetector.scala:107-130 across ranks)
+    agrees every rank's status before each of its collectives: rank 1 fails
+    inside ldgpu_fit_table_size (injected at each phase: histogram, select,
+    chosen rows; the zero-fill and wide-gram host selections), and both ranks
+    return an error -- rank 1 its own, rank 0 naming rank 1 -- with no hang
+    (a 120 s bound here; a rank left waiting in an all-gather would hold it)."""
+    import time
+    ctx = mp.spawn(_fail_worker, args=(2, free_port(), str(tmp_path), K, grams, point), nprocs=2, join=False)
+    deadline = time.time() + 120
+    while not ctx.join(timeout=5):
+        if time.time() > deadline:
+            for p in ctx.processes:
+                p.kill()
+            pytest.fail(f"ranks still running 120 s after a failure at {point}")
+    e0 = open(os.path.join(tmp_path, "err0.txt")).read()
+    e1 = open(os.path.join(tmp_path, "err1.txt")).read()
+    assert f"injected failure at {point}" in e1, e1
+    assert "fit table: rank 1 failed" in e0, e0
+
+
 def _score_worker(rank, world, port, out_dir):
     dist = _init(rank, world, port)
     from languagedetection import LanguageDetectorModel, synth

@@ -548,6 +548,7 @@ def test_config4_timed_kernel_labels_only_packs():
     info = m.info()
     assert info["mode"] == 2, info
     assert "keyed_bloom_chunks" in info["layout"] and "packs" in info["layout"], info
+    assert "buckets" in info["layout"], info  # 100k keys: one 64-B bucket line per verify (1.5 MiB)
     data, off, _ = synth.generate(ls, 60000, 32, 96, seed=synth.SEED_BASE + 4)
     t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals, L)
     ol, _ = t.score(grams, data, off, want_scores=False, nthreads=8)
@@ -761,20 +762,22 @@ def test_product_library_ignores_env_switches(monkeypatch):
     assert m.info()["mode"] == 2
 
 
-@pytest.mark.parametrize("chunks", ["1", "0"])
+@pytest.mark.parametrize("chunks,buckets", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
 @pytest.mark.parametrize("grams,doc_range", [
     ([1, 2, 3, 4, 5], (200, 256)),   # single documents, the fast path
     ([1, 2, 3, 4, 5], (20, 90)),     # packs of short documents
     ([3, 4, 3, 7], (0, 300)),        # partial windows, long documents, a repeated length
     ([2, 9, 12, 3], (0, 120)),       # wide keys in their chunks
 ])
-def test_keyed_bloom_chunk_layout(chunks, grams, doc_range, monkeypatch):
+def test_keyed_bloom_chunk_layout(chunks, buckets, grams, doc_range, monkeypatch):
     """The keyed bloom's chunk layout (count mode: every key of >= 3 bytes
     sets two bits of ONE 16-B chunk chosen by its position's first three
     bytes; config 4's 100k-key table takes it) and the word-per-key layout,
-    forced through the diagnostics library (LDGPU_KB_CHUNKS) on a 60k-key
-    count-mode table: labels and fp64 scores bit-identical to the oracle,
-    labels-only (packs) too."""
+    forced through the diagnostics library (LDGPU_KB_CHUNKS), each with the
+    key table in 5-slot buckets (one 64-B line per verify: the product
+    layout of a keyed count-mode table beyond 2 MiB of cuckoo slots) or in
+    cuckoo slots (LDGPU_BUCKETS), on a 60k-key count-mode table: labels and
+    fp64 scores bit-identical to the oracle, labels-only (packs) too."""
     rng = np.random.default_rng(sum(grams) + doc_range[1] + int(chunks))
     L = 40
     ls = synth.make_languages(L, seed=93)
@@ -792,10 +795,12 @@ def test_keyed_bloom_chunk_layout(chunks, grams, doc_range, monkeypatch):
         mask[int(rng.integers(0, L))] = True
         table[raw[off[d] + p: off[d] + p + n]] = [math.log(2.0) if b else 0.0 for b in mask]
     monkeypatch.setenv("LDGPU_KB_CHUNKS", chunks)
+    monkeypatch.setenv("LDGPU_BUCKETS", buckets)
     m = check_parity(table, L, grams, data, off, variant="diag")
     info = m.info()
     assert info["mode"] == 2 and info["filter_bits"] > 64 * 1024 * 8  # count mode, keyed (global) bloom
     assert ("keyed_bloom_chunks" in info["layout"]) == (chunks == "1"), info
+    assert ("buckets" in info["layout"]) == (buckets == "1"), info
     labels, _ = m.score(data, off, want_scores=False)
     ol, _ = oracle_c(table, L, grams, data, off, scores=False)
     assert np.array_equal(labels, ol)

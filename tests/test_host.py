@@ -37,6 +37,11 @@ def test_libraries_are_built_from_this_tree():
     for variant in ("product", "diag"):
         prov = _lib.provenance(variant)
         assert prov["match"], (variant, prov)
+    # ... and the compile flags: a diagnostics (or any non-product) build
+    # reports its own id, never the product's
+    prod = _lib.load().ldgpu_build_id().decode()
+    diag = _lib.load(variant="diag").ldgpu_build_id().decode()
+    assert "+" not in prod and diag.startswith(prod + "+") and diag != prod
 
 
 def test_library_is_gfx950_code_object():

@@ -124,8 +124,10 @@ def test_count_add_and_table_exports_need_handles(jh):
 @pytest.mark.gpu
 def test_shim_on_device_handles(jh):
     """Real handles: the scores buffer and count rows are sized by the
-    handle's language count whatever n_langs the caller passes, and the fit
-    table export by the library's cached table; right-sized buffers work."""
+    handle's language count and the fit table export by the library's cached
+    table; a caller whose n_langs / n_rows / key bytes differ from the
+    handle's is refused (its rows would take another stride), right-sized
+    calls work."""
     from languagedetection.runtime import DeviceCounts, DeviceModel
     s = Shim(jh)
     L = 5
@@ -134,10 +136,13 @@ def test_shim_on_device_handles(jh):
     data, off = docs(8)
     lab = np.zeros(8, np.int32)
     sc = np.zeros((8, L))
-    # the caller claims 4 languages and passes a buffer for 4: refused
-    assert s.call("score", m.h, s.buf(data), s.buf(off), 8, s.buf(lab), s.buf(sc, 8 * 8 * 4), 4) == EINVAL
+    # a scores buffer for 4 of the model's 5 languages: refused
+    assert s.call("score", m.h, s.buf(data), s.buf(off), 8, s.buf(lab), s.buf(sc, 8 * 8 * 4), L) == EINVAL
     assert "scores" in s.err()
-    assert s.call("score", m.h, s.buf(data), s.buf(off), 8, s.buf(lab), s.buf(sc), 4) == 0
+    # a big enough buffer but another language count: refused, not scrambled
+    assert s.call("score", m.h, s.buf(data), s.buf(off), 8, s.buf(lab), s.buf(sc), 4) == EINVAL
+    assert "nLangs" in s.err()
+    assert s.call("score", m.h, s.buf(data), s.buf(off), 8, s.buf(lab), s.buf(sc), L) == 0
     expect, escore = m.score(data, off, want_scores=True)
     assert np.array_equal(lab, expect) and np.array_equal(sc, escore)
 
@@ -149,7 +154,9 @@ def test_shim_on_device_handles(jh):
     ko = np.zeros(n + 1, np.int64)
     cnt = np.zeros((n, L), np.int64)
     assert s.call("countsExport", c.h, s.buf(kb), s.buf(ko), s.buf(cnt, 8 * n * 3), 3) == EINVAL
-    assert s.call("countsExport", c.h, s.buf(kb), s.buf(ko), s.buf(cnt), 3) == 0
+    assert s.call("countsExport", c.h, s.buf(kb), s.buf(ko), s.buf(cnt), 3) == EINVAL
+    assert "nLangs" in s.err()
+    assert s.call("countsExport", c.h, s.buf(kb), s.buf(ko), s.buf(cnt), L) == 0
     k2, c2 = c.export()
     assert np.array_equal(cnt, c2)
     out = np.zeros(2, np.int64)
@@ -158,9 +165,13 @@ def test_shim_on_device_handles(jh):
     tk = np.zeros(max(key_b, 1), np.uint8)
     tko = np.zeros(rows_n + 1, np.int64)
     rows = np.zeros((rows_n, L))
-    # the caller's row count and language count are ignored (too small here)
-    assert s.call("fitTableExport", c.h, s.buf(tk), s.buf(tko), s.buf(rows, 8 * rows_n * 2), 1, 1, 2) == EINVAL
-    assert s.call("fitTableExport", c.h, s.buf(tk), s.buf(tko), s.buf(rows), 1, 1, 2) == 0
+    # the caller's row count, key bytes and language count must be the table's
+    assert s.call("fitTableExport", c.h, s.buf(tk), s.buf(tko), s.buf(rows, 8 * rows_n * 2), rows_n, key_b,
+                  L) == EINVAL
+    assert s.call("fitTableExport", c.h, s.buf(tk), s.buf(tko), s.buf(rows), 1, key_b, L) == EINVAL
+    assert "nRows" in s.err()
+    assert s.call("fitTableExport", c.h, s.buf(tk), s.buf(tko), s.buf(rows), rows_n, key_b, 2) == EINVAL
+    assert s.call("fitTableExport", c.h, s.buf(tk), s.buf(tko), s.buf(rows), rows_n, key_b, L) == 0
     assert {bytes(tk[tko[i]:tko[i + 1]]): list(rows[i]) for i in range(rows_n)} == c.fit_table(10)
     m.close()
     c.close()
