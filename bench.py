@@ -69,6 +69,8 @@ def parse():
                     help="score = the headline metric (config 2); fit = config 3's count + table build")
     ap.add_argument("--fit-bytes", type=int, default=6_250_000_000,
                     help="fit mode: corpus bytes per GPU (default: config 3's 50 GB over 8 GPUs)")
+    ap.add_argument("--count-only", action="store_true",
+                    help="fit mode: time the count alone, no top-K table (PMC passes of the count kernels)")
     ap.add_argument("--check-merge", action="store_true",
                     help="fit mode, N > 1: check the merged table against the oracle over every rank's corpus")
     args = ap.parse_args()
@@ -280,7 +282,19 @@ def traffic_from_profiles(workload_key):
 COUNT_KERNELS = ("emit_kernel", "fit_offsets_kernel", "part2_kernel", "reduce_kernel", "merge_kernel",
                  "derive_level_kernel", "derive_pairs_level_kernel", "derive_pairs2_level_kernel", "len_hist_kernel",
                  "partial_kernel", "rehash_kernel", "wide_rehash_kernel", "sparse_rehash_kernel", "pair_rehash_kernel",
-                 "counts_add_kernel")
+                 "counts_add_kernel", "sort_emit_kernel", "sort_runs_kernel", "runs_add_kernel")
+
+
+def fit_count_kernels(L, grams):
+    """The count path the library takes for (L, grams) (ldgpu_api.hip
+    counts_new / sort_path): FIT v5 (sort) for two-word records whose sort key
+    fits 64 bits, FIT v4 otherwise."""
+    maxg = max([g for g in grams if g <= 15] or [0])
+    lb = max(1, (L - 1).bit_length())
+    two_word = maxg <= 7 and 64 - (8 * maxg + 1) - lb < 8
+    if two_word and 8 * maxg + L.bit_length() <= 64:
+        return "count (FIT v5: sort_emit + radix sort + sort_runs per length + runs_add into T)"
+    return "count (FIT v4: emit + part2 + reduce + merge + derive)"
 
 
 def count_traffic(prof):
@@ -296,7 +310,8 @@ def count_traffic(prof):
     tot = 0.0
     for k, v in pk.items():
         name = k.split("(")[0].split("<")[0]
-        if name in COUNT_KERNELS:
+        # (a count-only profile: its radix sorts are the count's, FIT v5)
+        if name in COUNT_KERNELS or (prof.get("count_only") and name.startswith("rocprim")):
             tot += rf * v.get("FETCH_SIZE", 0.0) + wf * v.get("WRITE_SIZE", 0.0)
     return int(round(tot))
 
@@ -365,7 +380,7 @@ def fit_main(args, world, rank, local, dev, backend):
             t["merge_s"] = time.perf_counter() - t0 - t["create_s"] - t["count_s"]
         distinct = c.size()
         t1 = time.perf_counter()
-        table = c.fit_table_masks(args.profile_size)   # packed mask form: no per-row Python objects
+        table = None if args.count_only else c.fit_table_masks(args.profile_size)  # packed mask form
         t["table_s"] = time.perf_counter() - t1
         t2 = time.perf_counter()
         c.close()
@@ -414,7 +429,7 @@ def fit_main(args, world, rank, local, dev, backend):
                                f"grams {args.grams}, profile size {args.profile_size}",
                    "docs_per_gpu": n_docs, "corpus_bytes_per_gpu": n_bytes, "windows_per_gpu": windows,
                    "distinct_grams": parts[-1][1], "distinct_gram_language_pairs": st["pairs"],
-                   "table_rows": len(parts[-1][2][1]) - 1,
+                   "table_rows": None if args.count_only else len(parts[-1][2][1]) - 1,
                    "parallelism": f"dp{world} (corpus sharded; owner-exchange merge + distributed top-K)"},
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
                      for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
@@ -425,7 +440,7 @@ def fit_main(args, world, rank, local, dev, backend):
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
                      "traffic": count_traffic(traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}")),
-                     "kernel": "count (emit + part2 + reduce + merge + derive)", "count_ms": round(count_s * 1e3, 3),
+                     "kernel": fit_count_kernels(args.langs, grams), "count_ms": round(count_s * 1e3, 3),
                      "algorithmic_bytes_per_count": int(algo)},
     }
     if line["roofline"]["traffic"]:  # the counters' view: calibrated HBM bytes per count over the count time

@@ -136,25 +136,77 @@ object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
 
   /**
     * detect(Array[Byte], ...) (LanguageDetectorModel.scala:131-156): one
-    * document through a transient device table.  For many documents use
-    * transform, which keeps the table on the GPU and scores in batches.
+    * document.  The reference's callers put detect in a UDF, calling it per
+    * row with the same map, so the device table of a map is kept: a Scala Map
+    * is immutable, so the same object (eq) is the same table.  The last
+    * `detectCacheSize` tables stay resident (reference-counted: an evicted
+    * table is destroyed once no call is scoring with it); each thread keeps
+    * its own direct buffers.  For many documents, transform scores in
+    * batches.
     */
   def detect(text: Array[Byte], probabilityMap: Map[Seq[Byte], Array[Double]], supportedLanguages: Seq[String],
              gramLengths: Seq[Int]): String = {
-    val ctx = LdgpuNative.context()
-    val model = PackedTable.of(probabilityMap, supportedLanguages.length).upload(ctx, gramLengths.toArray)
+    val e = detectAcquire(probabilityMap, supportedLanguages.length, gramLengths)
     try {
-      val bytes = LdgpuNative.direct(text.length.toLong + 16)
-      bytes.put(text).flip()
-      val offsets = LdgpuNative.direct(16)
-      offsets.putLong(0, 0L)
-      offsets.putLong(8, text.length.toLong)
-      val label = LdgpuNative.direct(4)
-      LdgpuNative.check(LdgpuNative.score(model, bytes, offsets, 1L, label, null, supportedLanguages.length))
-      supportedLanguages(label.getInt(0))
+      val b = detectBuffers.get().ensure(text.length)
+      b.bytes.clear()
+      b.bytes.put(text).flip()
+      b.offsets.putLong(0, 0L)
+      b.offsets.putLong(8, text.length.toLong)
+      LdgpuNative.check(LdgpuNative.score(e.model, b.bytes, b.offsets, 1L, b.label, null, supportedLanguages.length))
+      supportedLanguages(b.label.getInt(0))
     } finally {
-      LdgpuNative.modelDestroy(model)
+      detectRelease(e)
     }
+  }
+
+  var detectCacheSize: Int = 4
+
+  private final class DetectEntry(val map: AnyRef, val grams: Seq[Int], val nLangs: Int, val model: Long) {
+    var refs = 0
+    var evicted = false
+  }
+  private val detectCache = new java.util.ArrayDeque[DetectEntry]()
+
+  private def detectAcquire(map: Map[Seq[Byte], Array[Double]], nLangs: Int, grams: Seq[Int]): DetectEntry =
+    detectCache.synchronized {
+      val it = detectCache.iterator()
+      while (it.hasNext) {
+        val e = it.next()
+        if ((e.map eq map) && e.nLangs == nLangs && e.grams == grams) {
+          e.refs += 1
+          return e
+        }
+      }
+      val model = PackedTable.of(map, nLangs).upload(LdgpuNative.context(), grams.toArray)
+      val e = new DetectEntry(map, grams.toList, nLangs, model)
+      e.refs = 1
+      detectCache.addFirst(e)
+      while (detectCache.size > math.max(1, detectCacheSize)) {
+        val old = detectCache.removeLast()
+        old.evicted = true
+        if (old.refs == 0) LdgpuNative.modelDestroy(old.model)
+      }
+      e
+    }
+
+  private def detectRelease(e: DetectEntry): Unit = detectCache.synchronized {
+    e.refs -= 1
+    if (e.evicted && e.refs == 0) LdgpuNative.modelDestroy(e.model)
+  }
+
+  /** a thread's direct buffers of one document (grown as documents grow) */
+  private final class DetectBuffers {
+    var bytes: java.nio.ByteBuffer = LdgpuNative.direct(4096)
+    val offsets: java.nio.ByteBuffer = LdgpuNative.direct(16)
+    val label: java.nio.ByteBuffer = LdgpuNative.direct(4)
+    def ensure(n: Int): DetectBuffers = {
+      if (bytes.capacity < n + 16) bytes = LdgpuNative.direct(math.max(2L * bytes.capacity, n + 16L))
+      this
+    }
+  }
+  private val detectBuffers = new ThreadLocal[DetectBuffers] {
+    override def initialValue(): DetectBuffers = new DetectBuffers
   }
 
   /** detect(String, ...) (:158-165): the low byte of every UTF-16 unit */

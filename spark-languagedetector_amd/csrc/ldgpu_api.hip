@@ -2,6 +2,7 @@
 // include/ldgpu.h (contexts, device tables, H2D/D2H staging, count-table
 // growth, probability / top-K table build).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -184,6 +185,27 @@ void par_memcpy(void* dst, const void* src, size_t n) {
     for (auto& x : th) x.join();
 }
 
+// fn(i0, i1) over [0, n) split across up to 8 threads (host loops over a
+// fit table's ~10M rows)
+template <typename F>
+void par_for(int64_t n, F fn) {
+    const int64_t kMin = 1 << 16;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int64_t t = std::min<int64_t>(std::min<unsigned>(8u, hw), std::max<int64_t>(1, n / kMin));
+    if (t <= 1) {
+        fn((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t part = (n + t - 1) / t;
+    for (int64_t i = 1; i < t; ++i) {
+        const int64_t a = std::min(n, part * i), b = std::min(n, part * (i + 1));
+        if (a < b) th.emplace_back([=] { fn(a, b); });
+    }
+    fn((int64_t)0, std::min(n, part));
+    for (auto& x : th) x.join();
+}
+
 int check_grams(const int32_t* G, int32_t nG, int max_len = kMaxGram) {
     if (nG < 0 || nG > LDGPU_MAX_GRAM_LENGTHS)
         return fail(LDGPU_EINVAL, "number of gram lengths %d outside [0, %d]", nG, LDGPU_MAX_GRAM_LENGTHS);
@@ -245,6 +267,12 @@ struct ldgpu_ctx {
     DevBuf f_stmp;                     // FIT v5: the radix sort's scratch
     HostBuf h_fwg;                     // pinned staging of a batch's plan (one async copy to f_wg)
     HostBuf h_fon;                     // pinned landing of a batch's nout / boff (an async copy back)
+    // pinned landing of a single-rank device fit table (keys, masks, k per
+    // row: one DMA); it stays the table of h_tbl_owner until another count
+    // table's build needs it (tbl_materialize moves the owner's into its own
+    // vectors first)
+    HostBuf h_tbl;
+    struct ldgpu_counts* h_tbl_owner = nullptr;
     // device blocks of destroyed / grown count tables and overflow lists,
     // reused by exact size: a Spark executor fits partition after partition,
     // and freeing and re-mapping ~10 GB per fit stalls the allocator
@@ -397,6 +425,7 @@ extern "C" int ldgpu_ctx_destroy(ldgpu_ctx* c) {
         b->release();
     c->h_fwg.release();
     c->h_fon.release();
+    c->h_tbl.release();
     for (ScorePipe* pp : c->pipes) pipe_destroy(pp);
     for (auto& b : c->cache) (void)hipFree(b.second);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1022,6 +1051,9 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     constexpr double kBucketL2Bytes = 2.0 * (1 << 20);
     bool use_buckets = m->mode == 3 && (nn > (1 << 20) || (keyed && 2.5 * 32.0 * (double)nn > kBucketL2Bytes));
     if (const char* b = diag_env("LDGPU_BUCKETS")) use_buckets = m->mode == 3 && keyed && atoi(b) != 0;
+#ifdef LDGPU_BIG_BUCKETS_ONLY  // A/B builds (tools/build_variant.sh): round 4's rule
+    use_buckets = m->mode == 3 && nn > (1 << 20);
+#endif
     if (use_buckets && (uint64_t)nk >= (uint64_t)kPayLang) {
         // a bucket payload holds a multi-language row's index below kPayLang
         // (bit 30 marks a one-language payload, bit 31 a bad row)
@@ -1753,6 +1785,10 @@ struct ldgpu_counts {
     std::vector<int64_t> tbl_off;
     std::vector<uint64_t> tbl_masks;  // [rows][S] presence masks of the chosen grams
     std::vector<double> tbl_vals;     // [rows] log(1 + 1/k): the value of every nonzero entry
+    // single-rank device build: the table is in ctx->h_tbl (keys [rows],
+    // masks [rows][S], k [rows]) instead of the vectors above
+    bool tbl_pin = false;
+    int64_t tbl_rows = 0, tbl_kb = 0;
 };
 
 namespace {
@@ -1801,6 +1837,7 @@ CountParams pair_view(const ldgpu_counts* c) { return pair_view_of(c->d_pkeys, c
 
 void counts_free(ldgpu_counts* c) {
     if (!c) return;
+    if (c->ctx && c->ctx->h_tbl_owner == c) c->ctx->h_tbl_owner = nullptr;
     if (c->pend) counts_free(c->pend);
     for (void* p : {(void*)c->d_wlo, (void*)c->d_whi, (void*)c->d_wcounts, (void*)c->d_wsize, (void*)c->d_wfull,
                     (void*)c->d_lslots, (void*)c->d_larena, (void*)c->d_lpkeys,
@@ -3761,6 +3798,59 @@ void write_keys(const ldgpu_counts* c, const std::vector<uint64_t>& keys, uint8_
         key_offsets[i + 1] = o;
     }
 }
+
+// write_keys for one-word keys (<= 7 bytes, no wide stand-ins) from a plain
+// array: offsets by a serial prefix sum of the lengths, the bytes in parallel
+void write_short_keys(const uint64_t* keys, int64_t n, std::vector<uint8_t>& key_bytes, std::vector<int64_t>& key_offsets) {
+    key_offsets.resize((size_t)n + 1);
+    key_offsets[0] = 0;
+    for (int64_t i = 0; i < n; ++i) key_offsets[i + 1] = key_offsets[i] + key_len(keys[i]);
+    key_bytes.resize((size_t)std::max<int64_t>(key_offsets[n], 1));
+    uint8_t* kb = key_bytes.data();
+    const int64_t* ko = key_offsets.data();
+    par_for(n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            const uint64_t k = keys[i];
+            for (int64_t j = 0; j < ko[i + 1] - ko[i]; ++j) kb[ko[i] + j] = (uint8_t)(k >> (8 * j));
+        }
+    });
+}
+}  // namespace
+
+namespace {
+// the pinned table's arrays (tbl_pin: ctx->h_tbl, owned by c)
+struct PinnedTable {
+    const uint64_t* keys;
+    const uint64_t* masks;
+    const int32_t* k;
+};
+PinnedTable pinned_table(const ldgpu_counts* c) {
+    const int S = (c->L + 63) / 64;
+    const uint64_t* keys = (const uint64_t*)c->ctx->h_tbl.p;
+    const uint64_t* masks = keys + c->tbl_rows;
+    return {keys, masks, (const int32_t*)(masks + (size_t)c->tbl_rows * S)};
+}
+
+double row_value(int k) { return std::log(1.0 + 1.0 / (double)k); }
+
+// rows, key bytes of the cached table
+int64_t tbl_rows(const ldgpu_counts* c) { return c->tbl_pin ? c->tbl_rows : (int64_t)c->tbl_off.size() - 1; }
+int64_t tbl_key_bytes(const ldgpu_counts* c) { return c->tbl_pin ? c->tbl_kb : c->tbl_off.back(); }
+
+// the pinned table into c's own vectors (before another table's build
+// reuses the context's pinned buffer, or for the dense export)
+void tbl_materialize(ldgpu_counts* c) {
+    if (!c->tbl_pin) return;
+    const PinnedTable t = pinned_table(c);
+    const int64_t m = c->tbl_rows;
+    const int S = (c->L + 63) / 64;
+    c->tbl_masks.assign(t.masks, t.masks + (size_t)m * S);
+    c->tbl_vals.resize((size_t)m);
+    for (int64_t r = 0; r < m; ++r) c->tbl_vals[r] = row_value(t.k[r]);
+    write_short_keys(t.keys, m, c->tbl_bytes, c->tbl_off);
+    c->tbl_pin = false;
+    if (c->ctx->h_tbl_owner == c) c->ctx->h_tbl_owner = nullptr;
+}
 }  // namespace
 
 extern "C" int ldgpu_counts_size(ldgpu_counts* c, int64_t* n_grams, int64_t* key_bytes) {
@@ -4988,26 +5078,54 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         HIP_TRY(sort_pairs_u64((int64_t)m, d_sk, d_idx, 64, st));
         HIP_TRY(launch_rows_permute((int64_t)m, S, d_idx, d_ok, d_okk, d_om, d_ok2, d_okk2, d_om2, st));
         mark("table: row sort");
-        std::vector<uint64_t> out_keys(m);
-        std::vector<int32_t> okk(m);
-        c->tbl_masks.resize((size_t)m * S);
+        // the rows come back in one DMA into pinned memory (a copy into
+        // pageable vectors ran at a fraction of PCIe), then host threads
+        // fill the table cache from it
+        // The rows stay in the context's pinned buffer, landed by one DMA
+        // (pageable vectors took a copy at a fraction of PCIe plus page
+        // faults): the exports copy from it straight into the caller's
+        // buffers.  Another table's build first moves its owner's rows out.
+        ldgpu_ctx* x = c->ctx;
+        if (ldgpu_counts* o = x->h_tbl_owner; o && o != c) {
+            if (o->tbl_valid) {
+                tbl_materialize(o);
+            } else {  // (a stale table: nothing to keep)
+                o->tbl_pin = false;
+                x->h_tbl_owner = nullptr;
+            }
+        }
+        c->tbl_pin = false;
+        const size_t hb = (size_t)m * (8 + 8 * (size_t)S + 4);
+        HIP_TRY(x->h_tbl.ensure(hb + 16));
+        uint64_t* h_keys = (uint64_t*)x->h_tbl.p;
+        uint64_t* h_masks = h_keys + m;
+        int32_t* h_k = (int32_t*)(h_masks + (size_t)m * S);
         if (m) {
-            HIP_TRY(hipMemcpyAsync(out_keys.data(), d_ok2, sizeof(uint64_t) * m, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(c->tbl_masks.data(), d_om2, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(okk.data(), d_okk2, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(h_keys, d_ok2, sizeof(uint64_t) * m, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(h_masks, d_om2, sizeof(uint64_t) * m * S, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(h_k, d_okk2, sizeof(int32_t) * m, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
         }
-        c->tbl_vals.resize((size_t)m);
-        for (uint64_t r = 0; r < m; ++r) c->tbl_vals[r] = w[okk[r]];
-        int64_t nb = 0;
-        for (uint64_t k : out_keys) nb += key_len(k);
-        c->tbl_bytes.assign((size_t)std::max<int64_t>(nb, 1), 0);
-        c->tbl_off.assign(out_keys.size() + 1, 0);
-        write_keys(c, out_keys, c->tbl_bytes.data(), c->tbl_off.data());
+        mark("table: copy back");
+        std::atomic<int64_t> nb_acc{0};
+        par_for((int64_t)m, [&](int64_t a, int64_t b) {
+            int64_t t = 0;
+            for (int64_t r = a; r < b; ++r) t += key_len(h_keys[r]);
+            nb_acc += t;
+        });
+        const int64_t nb = nb_acc.load();
+        c->tbl_masks.clear();
+        c->tbl_vals.clear();
+        c->tbl_bytes.clear();
+        c->tbl_off.assign(1, 0);
+        c->tbl_rows = (int64_t)m;
+        c->tbl_kb = nb;
+        c->tbl_pin = true;
+        x->h_tbl_owner = c;
         c->tbl_valid = true;
         if (n_rows) *n_rows = (int64_t)m;
         if (key_bytes) *key_bytes = nb;
-        mark("table: copy back + host rows");
+        mark("table: host rows");
         return LDGPU_OK;
     }
     {  // every rank's chosen rows
@@ -5061,6 +5179,10 @@ extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows,
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
     std::lock_guard<std::mutex> lock(c->ctx->mu);
     HIP_TRY(hipSetDevice(c->ctx->device));
+    // the previous table (pinned or in the vectors) is replaced whatever path builds this one
+    c->tbl_valid = false;
+    c->tbl_pin = false;
+    if (c->ctx->h_tbl_owner == c) c->ctx->h_tbl_owner = nullptr;
     // a merged table takes the device path on every rank (its collectives
     // must match), even for K <= 0 or an empty shard
     // (tables holding grams of 8..15 bytes take the host top-K over the
@@ -5089,16 +5211,18 @@ extern "C" int ldgpu_fit_table_size(ldgpu_counts* c, int32_t K, int64_t* n_rows,
 
 extern "C" int ldgpu_fit_table_info(ldgpu_counts* c, int64_t* n_rows, int64_t* key_bytes) {
     if (!c) return fail(LDGPU_EINVAL, "counts is NULL");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
     if (!c->tbl_valid) return fail(LDGPU_EINVAL, "call ldgpu_fit_table_size first");
-    const size_t n = c->tbl_off.size() - 1;
-    if (n_rows) *n_rows = (int64_t)n;
-    if (key_bytes) *key_bytes = c->tbl_off[n];
+    if (n_rows) *n_rows = tbl_rows(c);
+    if (key_bytes) *key_bytes = tbl_key_bytes(c);
     return ok();
 }
 
 extern "C" int ldgpu_fit_table_export(ldgpu_counts* c, uint8_t* key_bytes, int64_t* key_offsets, double* rows) {
     if (!c || !key_offsets || !rows) return fail(LDGPU_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
     if (!c->tbl_valid) return fail(LDGPU_EINVAL, "call ldgpu_fit_table_size first");
+    tbl_materialize(c);  // (dense rows: from the vectors)
     const size_t n = c->tbl_off.size() - 1;
     if (c->tbl_off[n] && !key_bytes) return fail(LDGPU_EINVAL, "key_bytes is NULL");
     if (c->tbl_off[n]) memcpy(key_bytes, c->tbl_bytes.data(), (size_t)c->tbl_off[n]);
@@ -5113,14 +5237,33 @@ extern "C" int ldgpu_fit_table_export(ldgpu_counts* c, uint8_t* key_bytes, int64
 extern "C" int ldgpu_fit_table_export_masks(ldgpu_counts* c, uint8_t* key_bytes, int64_t* key_offsets,
                                             uint64_t* masks, double* vals) {
     if (!c || !key_offsets || !masks || !vals) return fail(LDGPU_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lock(c->ctx->mu);
     if (!c->tbl_valid) return fail(LDGPU_EINVAL, "call ldgpu_fit_table_size first");
+    if (c->tbl_pin) {  // straight from the pinned rows into the caller's buffers
+        const PinnedTable t = pinned_table(c);
+        const int64_t m = c->tbl_rows;
+        const int S = (c->L + 63) / 64;
+        if (c->tbl_kb && !key_bytes) return fail(LDGPU_EINVAL, "key_bytes is NULL");
+        key_offsets[0] = 0;
+        for (int64_t i = 0; i < m; ++i) key_offsets[i + 1] = key_offsets[i] + key_len(t.keys[i]);
+        par_for(m, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) {
+                const uint64_t k = t.keys[i];
+                for (int64_t j = 0; j < key_offsets[i + 1] - key_offsets[i]; ++j)
+                    key_bytes[key_offsets[i] + j] = (uint8_t)(k >> (8 * j));
+                vals[i] = row_value(t.k[i]);
+            }
+            memcpy(masks + (size_t)a * S, t.masks + (size_t)a * S, sizeof(uint64_t) * (size_t)(b - a) * S);
+        });
+        return ok();
+    }
     const size_t n = c->tbl_off.size() - 1;
     if (c->tbl_off[n] && !key_bytes) return fail(LDGPU_EINVAL, "key_bytes is NULL");
-    if (c->tbl_off[n]) memcpy(key_bytes, c->tbl_bytes.data(), (size_t)c->tbl_off[n]);
-    memcpy(key_offsets, c->tbl_off.data(), sizeof(int64_t) * (n + 1));
+    if (c->tbl_off[n]) par_memcpy(key_bytes, c->tbl_bytes.data(), (size_t)c->tbl_off[n]);
+    par_memcpy(key_offsets, c->tbl_off.data(), sizeof(int64_t) * (n + 1));
     if (n) {
-        memcpy(masks, c->tbl_masks.data(), sizeof(uint64_t) * c->tbl_masks.size());
-        memcpy(vals, c->tbl_vals.data(), sizeof(double) * n);
+        par_memcpy(masks, c->tbl_masks.data(), sizeof(uint64_t) * c->tbl_masks.size());
+        par_memcpy(vals, c->tbl_vals.data(), sizeof(double) * n);
     }
     return ok();
 }

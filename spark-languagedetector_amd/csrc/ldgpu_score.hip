@@ -71,9 +71,12 @@ __device__ __forceinline__ ColdParams cold_params() {
 // f(params): with the cold pointer in the LDS-bloom kernels (KEYED == 0:
 // config 2's table on either path), with p itself in the keyed-bloom ones
 // (config 4's packs ran 5 % slower with it: same-box A/B)
+#ifndef LDGPU_COLD_KEYED
+#define LDGPU_COLD_KEYED 0
+#endif
 template <int KEYED, typename F>
 __device__ __forceinline__ auto with_cold(const ScoreParams& p, F&& f) {
-    if constexpr (LDGPU_COLD_PARAMS && KEYED == 0) return f(*cold_params());
+    if constexpr (LDGPU_COLD_PARAMS && (KEYED == 0 || LDGPU_COLD_KEYED)) return f(*cold_params());
     else return f(p);
 }
 
@@ -913,15 +916,23 @@ __device__ __forceinline__ uint32_t keyed_hash(const Windows& x, int k) {
     return kb_hash(lo, hi, (uint32_t)N);
 }
 
-// keyed Bloom (global memory): the words of lengths 3..2+kPreN are loaded
-// before the first test, so a pack waits one L2 round trip, not one per
-// length; the tests recompute the bit position (VALU is cheap next to the
-// latency).  Longer lengths load at their test (registers).
-constexpr int kPreN = 3;
+// keyed Bloom (global memory): the words of lengths 3 .. 2 + PRE are loaded
+// before the first test, so a document (or pack) waits one memory round trip,
+// not one per length; the tests recompute the bit position (VALU is cheap
+// next to the latency).  Single documents preload every length 3..7 (config
+// 5: 145 -> 121 ms per 10M documents, despite 6 VGPRs spilled), packs 3..5
+// (their registers hold the pack's positions).  Longer lengths load at their
+// test.  (Diagnostics of the single-document preload: LDGPU_SINGLE_PRELOAD=0
+// builds.)
+#ifndef LDGPU_SINGLE_PRELOAD
+#define LDGPU_SINGLE_PRELOAD 1
+#endif
+constexpr int kPreN = 5;      // single documents
+constexpr int kPackPreN = 3;  // packs
 
-template <int N>
+template <int N, int PRE = kPreN>
 __device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x, uint32_t fm, uint32_t (&kw)[kPreN][kSub]) {
-    if constexpr (N - 3 < kPreN) {
+    if constexpr (N - 3 < PRE) {
         if ((fm >> N) & 1u) {
 #pragma unroll
             for (int k = 0; k < kSub; ++k)
@@ -934,10 +945,12 @@ __device__ __forceinline__ void keyed_preload(const FWords& f, const Windows& x,
 // probe_count_all)
 constexpr int kFmDirect = 16;
 
+// kw: the keyed bloom words of lengths 3 .. 2 + kPreN, preloaded together
+// (keyed_preload; KEYED == 1 with LDGPU_SINGLE_PRELOAD)
 template <int N, bool FULL, int S, bool STAGED, int KEYED, bool WIDE>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
-                                            const DocSrc& src, uint32_t fm) {
+                                            const DocSrc& src, uint32_t fm, const uint32_t (&kw)[kPreN][kSub]) {
     if (!((fm >> N) & 1u)) return;
     if (ablated(p, N <= 2 ? 8 : 16)) return;
     if constexpr (N <= 2) {
@@ -949,7 +962,16 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
     constexpr int KIND = N < 3 ? N : kind_of(KEYED);
     constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
     uint64_t m[kSub];
-    if constexpr (FULL) {
+    if constexpr (KIND == 4 && N - 3 < kPreN && LDGPU_SINGLE_PRELOAD) {
+        // preloaded word: the bit position recomputed (VALU is cheap next to
+        // the latency the preload hides)
+        const int32_t nw = len - N + 1;
+#pragma unroll
+        for (int k = 0; k < kSub; ++k) {
+            const uint32_t bit = keyed_hash<N>(x, k) >> kb_sbit(N, f.lines, f.gshift);
+            m[k] = __builtin_amdgcn_ballot_w64(filter_hit(kw[N - 3][k], bit, bit) && 64 * k + lane < nw);
+        }
+    } else if constexpr (FULL) {
         test_len<KIND, 4>(img, sh, mul, f, x, len - N + 1, m);
     } else {
         test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
@@ -975,15 +997,26 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
     // issued, and the direct counts run while those loads are in flight
     // (LDGPU_SPLIT_VERIFY; one-word keys in cuckoo slots only)
     const bool split = LDGPU_SPLIT_VERIFY && !WIDE && !(KEYED && p.buckets) && ((fm >> kFmDirect) & 1u);
-    if (!split) {
-        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
-        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    // keyed bloom (config 5): the words of lengths 3 .. 2 + kPreN loaded
+    // together before the first test -- one memory round trip instead of one
+    // per length (the 1-/2-byte tests run while they are in flight)
+    uint32_t kw[kPreN][kSub];
+    if constexpr (KEYED == 1 && LDGPU_SINGLE_PRELOAD) {
+        keyed_preload<3>(f, x, fm, kw);
+        keyed_preload<4>(f, x, fm, kw);
+        keyed_preload<5>(f, x, fm, kw);
+        keyed_preload<6>(f, x, fm, kw);
+        keyed_preload<7>(f, x, fm, kw);
     }
-    probe_count<3, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
-    probe_count<4, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
-    probe_count<5, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
-    probe_count<6, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
-    probe_count<7, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+    if (!split) {
+        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    }
+    probe_count<3, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<4, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<5, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<6, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<7, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
     // wide gram lengths 8..15: one loop, the length a scalar (their filter
     // bits use the first seven bytes: the same two tests as length 7)
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {
@@ -1005,8 +1038,8 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
         VerifyIssue v;
         const bool pending = qn > 0 && !ablated(p, 1);
         if (pending) verify_issue<STAGED>(p, wl, qn, src, lane, v);
-        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
-        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm);
+        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
         if (pending) {
             verify_complete<S>(p, wl, v);
             if (qn > 64) {
@@ -1046,7 +1079,7 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
     uint32_t w[kSub], bit[kSub], bit2[kSub];
 #pragma unroll
     for (int k = 0; k < kSub; ++k) {
-        if constexpr (KIND == 4 && N - 3 < kPreN) {
+        if constexpr (KIND == 4 && N - 3 < kPackPreN) {
             w[k] = kw[N - 3][k];
             bit[k] = bit2[k] = keyed_hash<N>(x, k) >> kb_sbit(N, f.lines, f.gshift);
         } else {
@@ -1090,9 +1123,9 @@ __device__ __forceinline__ void score_pack(const ScoreParams& p, const WaveLds& 
     const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
     uint32_t kw[kPreN][kSub];
     if constexpr (KEYED == 1) {
-        keyed_preload<3>(f, x, fm, kw);
-        keyed_preload<4>(f, x, fm, kw);
-        keyed_preload<5>(f, x, fm, kw);
+        keyed_preload<3, kPackPreN>(f, x, fm, kw);
+        keyed_preload<4, kPackPreN>(f, x, fm, kw);
+        keyed_preload<5, kPackPreN>(f, x, fm, kw);
     }
     probe_pack<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
     probe_pack<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
@@ -1526,8 +1559,6 @@ hipError_t prepare_m(int slices, bool lds_bloom, bool chunks, size_t lds, int* b
     return prepare_s<MODE, 1>(slices, lds, blocks);
 }
 
-// first maximum across language blocks: block maxima compared with '>' in
-// block order, as breeze's argmax compares scores in language order
 // cold_params() reads the kernarg segment as a ScoreParams: any other
 // argument list for score_kernel must change cold_params first
 template <typename T>
@@ -1538,6 +1569,8 @@ static_assert(ParamsOnlyKernel<decltype(&score_kernel<1, 3, 0, false, false>)>::
                   ParamsOnlyKernel<decltype(&score_kernel<4, 1, 1, true, true>)>::value,
               "score_kernel must take exactly one argument, ScoreParams (cold_params reads it at kernarg offset 0)");
 
+// first maximum across language blocks: block maxima compared with '>' in
+// block order, as breeze's argmax compares scores in language order
 __global__ void combine_blocks_kernel(int64_t n, int nb, const int32_t* lab, const double* best, int32_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1564,10 +1597,22 @@ hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const do
 }
 
 // LDGPU_NARROW_VARIANT (tuning builds only, tools/build_variant.sh): just the
-// LDS-bloom, one-slice kernels of count mode and of the finite-value replay
-// (config 2's table on either path), compiled in seconds instead of minutes
+// kernels of one bench configuration, compiled in a minute instead of ten:
+//   1: config 2 -- LDS bloom, one slice, count mode and the finite-value replay
+//   4: config 4 -- keyed bloom in chunks, two slices (L = 100), count mode
+//   5: config 5 -- keyed bloom in lines, four slices (L = 200), count mode
+#if defined(LDGPU_NARROW_VARIANT) && LDGPU_NARROW_VARIANT == 4
+#define LDGPU_NARROW_OK(mode, lds, chunks, slices) ((mode) == 3 && !(lds) && (chunks) && (slices) == 2)
+#define LDGPU_NARROW_T 2, 3, 2
+#elif defined(LDGPU_NARROW_VARIANT) && LDGPU_NARROW_VARIANT == 5
+#define LDGPU_NARROW_OK(mode, lds, chunks, slices) ((mode) == 3 && !(lds) && !(chunks) && (slices) == 4)
+#define LDGPU_NARROW_T 4, 3, 1
+#endif
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream) {
-#ifdef LDGPU_NARROW_VARIANT
+#if defined(LDGPU_NARROW_T)
+    if (!LDGPU_NARROW_OK(mode, lds_bloom, p.kb_chunks, slices)) return hipErrorInvalidValue;
+    return launch_t<LDGPU_NARROW_T>(p, grid, stream);
+#elif defined(LDGPU_NARROW_VARIANT)
     if ((mode != 3 && mode != 1) || !lds_bloom || slices != 1) return hipErrorInvalidValue;
     return mode == 3 ? launch_t<1, 3, 0>(p, grid, stream) : launch_t<1, 1, 0>(p, grid, stream);
 #else
@@ -1582,7 +1627,10 @@ hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_blo
 }
 
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu) {
-#ifdef LDGPU_NARROW_VARIANT
+#if defined(LDGPU_NARROW_T)
+    if (!LDGPU_NARROW_OK(mode, lds_bloom, chunks, slices)) return hipErrorInvalidValue;
+    return prepare_t<LDGPU_NARROW_T>(lds_bytes, blocks_per_cu);
+#elif defined(LDGPU_NARROW_VARIANT)
     if ((mode != 3 && mode != 1) || !lds_bloom || slices != 1) return hipErrorInvalidValue;
     return mode == 3 ? prepare_t<1, 3, 0>(lds_bytes, blocks_per_cu) : prepare_t<1, 1, 0>(lds_bytes, blocks_per_cu);
 #else

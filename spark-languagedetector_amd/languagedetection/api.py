@@ -18,6 +18,7 @@ there is no CPU fallback.
 """
 from __future__ import annotations
 
+import threading
 import uuid
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -156,12 +157,39 @@ class LanguageDetectorModel(_Params):
         if text is None:
             raise NullPointerException("text is null")
         raw = text if isinstance(text, (bytes, bytearray)) else encoding.score_bytes(text)
-        m = DeviceModel({encoding.gram_key(k): v for k, v in probabilityMap.items()}, len(supportedLanguages),
-                        gramLengths)
+        m = _detect_model(probabilityMap, len(supportedLanguages), gramLengths)
         data, offsets = encoding.pack([bytes(raw)])
         labels, _ = m.score(data, offsets)
-        m.close()
         return supportedLanguages[int(labels[0])]
+
+
+# The device tables of recent detect() calls (the Scala drop-in's
+# detectAcquire): callers score row after row with the same map, so its
+# table is kept, keyed by the map object.  Scala's Map is immutable; a Python
+# dict is not, so an entry also records the dict's length and the identity of
+# its first row's value list (a caller that rebuilds the map gets a new
+# object, hence a new table).
+_DETECT_CACHE: list = []
+_DETECT_CACHE_SIZE = 4
+
+
+_DETECT_LOCK = threading.Lock()
+
+
+def _detect_model(probabilityMap, n_langs: int, gramLengths):
+    first = next(iter(probabilityMap.values()), None)
+    key = (id(probabilityMap), len(probabilityMap), id(first), n_langs, tuple(gramLengths))
+    with _DETECT_LOCK:
+        for i, (k, ref, m) in enumerate(_DETECT_CACHE):
+            if k == key and ref is probabilityMap:
+                _DETECT_CACHE.insert(0, _DETECT_CACHE.pop(i))
+                return m
+    m = DeviceModel({encoding.gram_key(k): v for k, v in probabilityMap.items()}, n_langs, gramLengths)
+    with _DETECT_LOCK:
+        _DETECT_CACHE.insert(0, (key, probabilityMap, m))
+        # (an evicted table is released when its last caller drops it)
+        del _DETECT_CACHE[_DETECT_CACHE_SIZE:]
+    return m
 
 
 class LanguageDetectorModelWriter:

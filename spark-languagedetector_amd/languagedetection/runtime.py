@@ -296,6 +296,21 @@ class DeviceCounts(_Owner):
         b = kb.tobytes()
         return {b[ko[i]:ko[i + 1]]: rows[i].tolist() for i in range(n.value)}
 
+    def cached_table_masks(self):
+        """The table of the last fit_table / fit_table_masks call, exported
+        again (ldgpu_fit_table_info + ldgpu_fit_table_export_masks): the same
+        arrays as fit_table_masks returned, without a rebuild."""
+        n = ctypes.c_int64()
+        nb = ctypes.c_int64()
+        self._check(self.lib.ldgpu_fit_table_info(self.h, ctypes.byref(n), ctypes.byref(nb)))
+        S = (self.L + 63) // 64
+        kb = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        ko = np.zeros(n.value + 1, dtype=np.int64)
+        masks = np.zeros((max(n.value, 1), S), dtype=np.uint64)
+        vals = np.zeros(max(n.value, 1), dtype=np.float64)
+        self._check(self.lib.ldgpu_fit_table_export_masks(self.h, _ptr(kb), _ptr(ko), _ptr(masks), _ptr(vals)))
+        return kb, ko, masks[:n.value], vals[:n.value]
+
     def fit_table_masks(self, profile_size: int):
         """The fit table in mask form, as packed arrays: (key_bytes uint8,
         key_offsets int64 [n+1], masks uint64 [n, S], vals fp64 [n]) -- what

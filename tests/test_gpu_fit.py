@@ -188,6 +188,33 @@ def test_fit_table_mask_form_and_model_from_masks(L, grams, K):
     assert np.array_equal(l1, l2) and np.array_equal(s1.view(np.uint64), s2.view(np.uint64))
 
 
+def test_fit_tables_of_two_count_tables_on_one_context():
+    """A single-rank device top-K leaves its rows in the context's pinned
+    buffer until exported; a second table's build on the same context first
+    moves them into the first table's own storage: both tables export what
+    they built, in mask and dense form, in any order."""
+    L, grams = 12, [1, 2, 3]
+    ls = synth.make_languages(L, seed=41)
+    d1, o1, l1 = synth.generate(ls, 800, 50, 400, seed=42)
+    d2, o2, l2 = synth.generate(ls, 800, 50, 400, seed=43)
+    a = DeviceCounts(L, grams)
+    a.count(d1, o1, l1)
+    b = DeviceCounts(L, grams)
+    b.count(d2, o2, l2)
+    ta = a.fit_table_masks(150)
+    tb = b.fit_table_masks(150)          # a's rows leave the pinned buffer first
+    ta2 = a.cached_table_masks()
+    tb2 = b.cached_table_masks()
+    for x, y in ((ta, ta2), (tb, tb2)):
+        assert all(np.array_equal(u, v) for u, v in zip(x, y))
+    dense_a = a.fit_table(150)           # rebuilt: pinned again, b's moved out
+    assert dense_a == _topk_table_from_counts(*OC.count(d1, o1, l1, L, grams), L, 150)
+    assert all(np.array_equal(u, v) for u, v in zip(tb, b.cached_table_masks()))
+    a.close()
+    assert all(np.array_equal(u, v) for u, v in zip(tb, b.cached_table_masks()))
+    b.close()
+
+
 def _topk_table_from_counts(keys, cnt, L, K):
     """filterTopGrams (LanguageDetector.scala:100-132) over oracle counts,
     vectorised: v_l = log(1 + [l] / k); per language the K largest v_l, ties

@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
-"""profiles/pmc_traffic_fit.json from tools/fit_pmc.sh: raw FETCH_SIZE /
-WRITE_SIZE (KB) summed per kernel over the run's two counts, calibrated on
-part2 (reads and writes each record once: K u64 words per corpus byte), per
-count and per window.   python tools/fit_pmc.py OUTDIR"""
+"""pmc_traffic_fit*.json from tools/fit_pmc.sh: raw FETCH_SIZE / WRITE_SIZE
+(KB) summed per kernel over the run's two counts, calibrated on kernels of
+known bytes, per count and per window:
+  FIT v4: part2 reads and writes each record once (8 B per corpus byte, K = 1);
+  FIT v5: sort_emit writes one 8-B sort key per corpus byte (write factor),
+          sort_runs reads the sorted keys once per gram length (8 B per full
+          window; its galloping reads stay within the lines it reads).
+    python tools/fit_pmc.py OUTDIR [OUTNAME]"""
 import json
 import os
 import re
@@ -17,9 +21,22 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
     for ln in open(os.path.join(out, ctr + ".sum")):
         k, n, v = ln.rstrip("\n").split("\t")
         raw.setdefault(k, {})[ctr] = float(v) * 1024 / counts
-rec_bytes = 8 * cfg["corpus_bytes_per_gpu"]  # K = 1 records, one per byte position
-p2 = next(v for k, v in raw.items() if k.startswith("part2_kernel"))
-rf, wf = rec_bytes / p2["FETCH_SIZE"], rec_bytes / p2["WRITE_SIZE"]
+rec_bytes = 8 * cfg["corpus_bytes_per_gpu"]  # K = 1 records / FIT v5 keys: one per byte position
+p2 = next((v for k, v in raw.items() if k.startswith("part2_kernel")), None)
+if p2:
+    rf, wf = rec_bytes / p2["FETCH_SIZE"], rec_bytes / p2["WRITE_SIZE"]
+    calibration = "part2 reads and writes every record once (8 B per corpus byte): factors = those bytes / its raw FETCH_SIZE, WRITE_SIZE; applied to every kernel (random probes of merge / derive: approximate)"
+else:
+    grams = [int(g) for g in re.search(r"grams ([\d,]+),", cfg["workload"]).group(1).split(",")]
+    n_len = len({g for g in grams if g <= 7})
+    em = next(v for k, v in raw.items() if k.startswith("sort_emit_kernel"))
+    rn = next(v for k, v in raw.items() if k.startswith("sort_runs_kernel"))
+    keys_read = 8 * cfg["windows_per_gpu"] / max(1, len(grams)) * n_len  # ~8 B per full window per length pass
+    wf = rec_bytes / em["WRITE_SIZE"]
+    rf = keys_read / rn["FETCH_SIZE"]
+    calibration = ("FIT v5: write factor = sort_emit's 8 B per corpus byte / its raw WRITE_SIZE; read factor = "
+                   "sort_runs' 8 B per key per gram-length pass / its raw FETCH_SIZE; applied to every kernel "
+                   "(the random probes of runs_add into T and the radix sort's scatter: approximate)")
 fetch = sum(v.get("FETCH_SIZE", 0.0) for v in raw.values())
 write = sum(v.get("WRITE_SIZE", 0.0) for v in raw.values())
 traffic = fetch * rf + write * wf
@@ -28,13 +45,13 @@ m = re.search(r"(\d+) languages, grams ([\d,]+), profile", cfg["workload"])
 d = {"workload_key": f"fit:bytes={cfg['corpus_bytes_per_gpu']}:L={m.group(1)}:G={m.group(2)}",
      "per_kernel_raw_bytes_per_count": raw,
      "read_factor": round(rf, 4), "write_factor": round(wf, 4),
-     "calibration": "part2 reads and writes every record once (8 B per corpus byte): factors = those bytes / its raw FETCH_SIZE, WRITE_SIZE; applied to every kernel (random probes of merge / derive: approximate)",
+     "calibration": calibration, "count_only": True,
      "traffic_bytes_per_launch": round(traffic), "traffic_raw_bytes_per_count": round(fetch + write),
      "windows_per_count": windows, "bytes_per_window_corrected": round(traffic / windows, 2),
      "bytes_per_window_raw": round((fetch + write) / windows, 2),
      "count_ms": line["roofline"]["count_ms"],
      "memory_side_GBps": round(traffic / (line["roofline"]["count_ms"] * 1e-3) / 1e9, 1)}
-json.dump(d, open(os.path.join(out, "pmc_traffic_fit.json"), "w"), indent=1)
+json.dump(d, open(os.path.join(out, sys.argv[2] if len(sys.argv) > 2 else "pmc_traffic_fit.json"), "w"), indent=1)
 print(json.dumps({k: d[k] for k in d if k != "per_kernel_raw_bytes_per_count"}, indent=1))
 for k, v in sorted(raw.items(), key=lambda kv: -sum(kv[1].values())):
     print(f"  {k:32s} fetch {v.get('FETCH_SIZE', 0) / 1e9:8.2f} GB  write {v.get('WRITE_SIZE', 0) / 1e9:8.2f} GB (raw)")
