@@ -220,35 +220,73 @@ def host_path(model, data, off, acc_labels):
 
 
 def mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs, d_lab, stream):
-    """The same table forced onto the ordered mask-replay path (the general
-    path of any table whose rows do not share one value: verified hits replayed
-    in reference order, s_l = s_l + v per hit) through the diagnostics library
-    (LDGPU_NO_COUNT_MODE): its kernel time and whether its labels equal the
-    count-mode launch's.  Reported beside `value`, never as it."""
-    os.environ["LDGPU_NO_COUNT_MODE"] = "1"
-    try:
-        alt = DeviceModel.from_masks(*packed, args.langs, grams, device=local, variant="diag")
-    finally:
-        del os.environ["LDGPU_NO_COUNT_MODE"]
+    """Config 2's documents on the paths a table whose rows do NOT share one
+    value takes (every mixed-presence-class fit table, every user mask
+    table), each timed like `value` and reported beside it, never as it:
+      - kernel_ms: the same table forced off count mode (diagnostics library,
+        LDGPU_NO_COUNT_MODE): its labels-only call takes class mode (per-
+        (value, language) hit counts + a rounding bound, ambiguous documents
+        replayed in order); labels must equal count mode's;
+      - ordered_kernel_ms: also LDGPU_NO_CLASS_MODE: the full ordered fp64
+        replay of every verified hit (LanguageDetectorModel.scala:139-154);
+      - two_values: the product library on the same table with every second
+        row's value halved (two presence classes): class mode, its ambiguous
+        share, labels against the C oracle on a sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     d_alt = torch.empty_like(d_lab)
 
-    def step():
-        alt.score_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), n_docs, d_alt.data_ptr(), 0, stream.cuda_stream)
-    for _ in range(max(1, args.warmup)):
-        step()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for s_, e_ in ev:
-        s_.record(stream)
-        step()
-        e_.record(stream)
-    torch.cuda.synchronize()
-    ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev]))
-    mode = alt.info()["mode"]
+    def timed(model):
+        def step():
+            model.score_device(d_bytes.data_ptr(), n_bytes, d_off.data_ptr(), n_docs, d_alt.data_ptr(), 0,
+                               stream.cuda_stream)
+        for _ in range(max(1, args.warmup)):
+            step()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for s_, e_ in ev:
+            s_.record(stream)
+            step()
+            e_.record(stream)
+        torch.cuda.synchronize()
+        return float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev]))
+
+    def diag_model(env):
+        os.environ.update(env)
+        try:
+            return DeviceModel.from_masks(*packed, args.langs, grams, device=local, variant="diag")
+        finally:
+            for k in env:
+                del os.environ[k]
+
+    res = {"library": "libldgpu_diag.so (LDGPU_NO_COUNT_MODE=1)"}
+    alt = diag_model({"LDGPU_NO_COUNT_MODE": "1"})
+    ms = timed(alt)
+    res.update(table_mode={0: "mask", 1: "mask, finite values (fma replay)", 2: "dense"}.get(alt.info()["mode"]),
+               layout=alt.info()["layout"], kernel_ms=round(ms, 4), docs_per_s=round(n_docs / (ms * 1e-3), 1),
+               labels_match_count_mode=bool(torch.equal(d_alt, d_lab)))
     alt.close()
-    return {"table_mode": {0: "mask", 1: "mask, finite values (fma replay)", 2: "dense"}.get(mode, str(mode)),
-            "kernel_ms": round(ms, 4), "docs_per_s": round(n_docs / (ms * 1e-3), 1),
-            "labels_match_count_mode": bool(torch.equal(d_alt, d_lab)),
-            "library": "libldgpu_diag.so (LDGPU_NO_COUNT_MODE=1)"}
+    alt = diag_model({"LDGPU_NO_COUNT_MODE": "1", "LDGPU_NO_CLASS_MODE": "1"})
+    ms = timed(alt)
+    res.update(ordered_kernel_ms=round(ms, 4), ordered_labels_match_count_mode=bool(torch.equal(d_alt, d_lab)))
+    alt.close()
+    # two presence classes on the product library
+    import ldoracle_c as OC
+    kb, ko, masks, vals = packed
+    vals2 = np.array(vals, dtype=np.float64, copy=True)
+    vals2[1::2] *= 0.5
+    two = DeviceModel.from_masks(kb, ko, masks, vals2, args.langs, grams, device=local)
+    ms = timed(two)
+    sample = min(n_docs, 200_000)
+    lab = d_alt[:sample].cpu().numpy()
+    off_h = d_off[:sample + 1].cpu().numpy()
+    data_h = d_bytes[:int(off_h[-1])].cpu().numpy()
+    t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals2, args.langs)
+    ol, _ = t.score(grams, data_h, off_h, nthreads=host_cores())
+    res["two_values"] = {"layout": two.info()["layout"], "kernel_ms": round(ms, 4),
+                         "docs_per_s": round(n_docs / (ms * 1e-3), 1),
+                         "labels_match_oracle": bool(np.array_equal(lab, ol)), "docs_checked": sample,
+                         "note": "every second row's value halved: two distinct values, product library"}
+    two.close()
+    return res
 
 
 def traffic_from_profiles(workload_key):

@@ -130,6 +130,10 @@ int ldgpu_model_info(const ldgpu_model* model, int32_t* mode, int64_t* n_keys,
 #define LDGPU_LAYOUT_LANG_BLOCKS        0x80
 #define LDGPU_LAYOUT_GENERAL_KEYS       0x100  /* keys of any length (a gram length > 15) */
 #define LDGPU_LAYOUT_KEYED_BLOOM_CHUNKS 0x200  /* count mode: one 16-B bloom chunk per window position */
+#define LDGPU_LAYOUT_CLASSES            0x400  /* labels-only calls on a mask table of at most 4 distinct
+                                                  finite values: per-(value, language) hit counts and a
+                                                  rounding bound; documents the bound cannot separate
+                                                  replayed in reference order */
 int ldgpu_model_layout(const ldgpu_model* model, int32_t* flags);
 /* The model's language count (a caller sizing score buffers, e.g. the JNI
  * shim, takes it from the model rather than trusting its own). */

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -492,6 +493,10 @@ struct ldgpu_model {
     uint32_t direct_off = 0, direct_words = 0;  // mode 3: direct tables in the image (ScoreParams)
     bool count_int_argmax = false;  // mode 3: label = first max of the counts (monotone fold)
     bool pack_ok = false;           // mode 3: short documents may be scored in packs (score_pack)
+    // mode 1 with at most class_max(slices) distinct row values: labels-only
+    // calls take class mode (kernel mode 4) with these values (unused: NaN)
+    int n_cls = 0;
+    double cls[4] = {};
     int32_t* d_err = nullptr;
     unsigned long long* d_stats = nullptr;  // LDGPU_STATS diagnostics (printed at destroy)
     // general keys (a gram length beyond kMaxWideGram: ldgpu_general.hip):
@@ -1020,7 +1025,37 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
             m->count_sign = v > 0.0 ? 1 : (v < 0.0 ? -1 : 0);
             m->count_int_argmax = std::fabs(v) < 1e300;
         }
+        // a few distinct values (e.g. a fit table's presence classes):
+        // labels-only calls count hits per (value, language) and replay only
+        // the documents a rounding bound cannot separate (class_label)
+        if (m->mode == 1 && !diag_env("LDGPU_NO_CLASS_MODE")) {
+            int nc = 0;
+            bool fits = true;
+            for (int64_t i = 0; i < nk && fits; ++i) {
+                bool any = false;
+                for (int s = 0; s < S; ++s) any |= masks[(size_t)i * S + s] != 0;
+                if (!any) continue;
+                int q = 0;
+                while (q < nc && !(m->cls[q] == vals[i])) ++q;  // == : 0.0 and -0.0 add alike
+                if (q < nc) continue;
+                if (nc == std::min(4, class_max(S))) fits = false;
+                else m->cls[nc++] = vals[i];
+            }
+            if (fits && nc > 0) {
+                m->n_cls = nc;
+                for (int q = nc; q < 4; ++q) m->cls[q] = std::numeric_limits<double>::quiet_NaN();
+            }
+        }
     }
+
+    // class mode: a one-language row's slot names its counter, class q and
+    // language l -> q 64 S + l (class_label's layout); other modes: l
+    auto lang_slot = [&](int64_t i, uint32_t l) -> uint32_t {
+        if (!m->n_cls || l == 0xffffffffu) return l;
+        uint32_t q = 0;
+        while ((int)q + 1 < m->n_cls && !(m->cls[q] == vals[i])) ++q;
+        return q * 64u * (uint32_t)S + l;
+    };
 
     // key -> row slots (mask form: the row's value and first mask word inline),
     // 2-choice cuckoo hashing: a key sits in slot h >> (64 - log2 cap) or
@@ -1111,6 +1146,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                     bits += __builtin_popcountll(w);
                 }
                 if (bits != 1) cur.pad = 0xffffffffu;
+                cur.pad = lang_slot(i, cur.pad);
             }
             if (t.bad[i]) {
                 cur.row |= kBadRow;
@@ -1167,6 +1203,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                         bits += __builtin_popcountll(w);
                     }
                     if (bits != 1) cur.lang1 = 0xffffffffu;
+                    cur.lang1 = lang_slot(i, cur.lang1);
                 }
                 if (t.bad[i]) {
                     cur.row |= kBadRow;
@@ -1277,9 +1314,12 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
 
     // count mode with every 1-/2-byte key naming ONE language (fit tables of
     // grams unique to a language): direct tables after the image (see
-    // ScoreParams::direct_*), so those keys are counted from LDS unverified
+    // ScoreParams::direct_*), so those keys are counted from LDS unverified.
+    // Class mode too, for L <= 63 (one slice): an entry is the counter,
+    // language | class << 6 (lang_slot; never 0xff)
     uint32_t image_words = kBloomBase + (m->lds_filter ? (uint32_t)bwords : 0u);
-    if (m->mode == 3 && m->lds_filter && n_langs <= 255 && !diag_env("LDGPU_NO_DIRECT")) {
+    const bool direct_mode = m->mode == 3 ? n_langs <= 255 : (m->n_cls > 0 && n_langs <= 63);
+    if (direct_mode && m->lds_filter && !diag_env("LDGPU_NO_DIRECT")) {
         std::vector<uint8_t> lang1(256, 0xff), lang2of(65536, 0xff);
         bool ok = true;
         for (int64_t i = 0; i < nn && ok; ++i) {
@@ -1292,8 +1332,9 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                 bits += __builtin_popcountll(w);
             }
             ok = bits == 1 && !t.bad[i];
-            if (kl == 1) lang1[keys[i] & 0xff] = (uint8_t)lang;
-            else lang2of[keys[i] & 0xffff] = (uint8_t)lang;
+            const uint8_t e = (uint8_t)lang_slot(i, (uint32_t)lang);
+            if (kl == 1) lang1[keys[i] & 0xff] = e;
+            else lang2of[keys[i] & 0xffff] = e;
         }
         if (ok) {
             std::vector<uint16_t> base2(2048);
@@ -1304,7 +1345,7 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                     if ((filter[kBmp1Words + wd] >> b) & 1u) lang2.push_back(lang2of[bmp2_unword(wd) * 32 + b]);
             }
             const uint32_t dwords = 64u + 1024u + (uint32_t)((lang2.size() + 16) / 16) * 4u;  // uint4-padded
-            if (score_lds_bytes(S, 3, image_words + dwords) * 2 <= 163840) {
+            if (score_lds_bytes(S, m->mode == 3 ? 3 : 4, image_words + dwords) * 2 <= 163840) {
                 m->direct_off = image_words;
                 m->direct_words = dwords;
                 filter.resize(image_words + dwords, 0u);
@@ -1340,6 +1381,11 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     }
     int resident = 0;
     if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->kb_chunks, m->lds_bytes, &resident);
+    if (e == hipSuccess && m->n_cls) {  // class mode shares the grid: the smaller occupancy
+        int r4 = 0;
+        e = score_prepare(S, 4, m->lds_filter, m->kb_chunks, m->lds_bytes, &r4);
+        if (r4 > 0) resident = resident > 0 ? std::min(resident, r4) : r4;
+    }
     // persistent grid = what is resident; never more workgroups than the LDS admits
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
     if (const char* ov = diag_env("LDGPU_WG_PER_CU")) m->wg_per_cu = std::max(1, atoi(ov));
@@ -1350,9 +1396,9 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
     }
     if (diag_env("LDGPU_DEBUG"))
         fprintf(stderr, "[ldgpu] model: keys=%lld mode=%d direct=%u slices=%d bloom_words=%llu lds_bloom=%d lds=%zu B "
-                        "resident_api=%d wg_per_cu=%d pack=%d\n",
+                        "resident_api=%d wg_per_cu=%d pack=%d classes=%d\n",
                 (long long)nk, m->mode, m->direct_words, S, (unsigned long long)bwords, (int)m->lds_filter, m->lds_bytes, resident,
-                m->wg_per_cu, (int)m->pack_ok);
+                m->wg_per_cu, (int)m->pack_ok, m->n_cls);
     if (e != hipSuccess) {
         model_free(m);
         return fail(e == hipErrorOutOfMemory ? LDGPU_ENOMEM : LDGPU_EDEVICE, "model upload: %s",
@@ -1398,6 +1444,7 @@ extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
     if (b->d_wslots) f |= LDGPU_LAYOUT_WIDE_KEYS;
     if (b->direct_words) f |= LDGPU_LAYOUT_DIRECT;
     if (b->pack_ok) f |= LDGPU_LAYOUT_PACKS;
+    if (b->n_cls && m->blocks.empty()) f |= LDGPU_LAYOUT_CLASSES;
     if (!m->blocks.empty()) f |= LDGPU_LAYOUT_LANG_BLOCKS;
     if (m->general) f = LDGPU_LAYOUT_GENERAL_KEYS;
     *flags = f;
@@ -1405,6 +1452,86 @@ extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
 }
 
 namespace {
+// the gram lengths the kernel scans: maxg, fast_mask, gpack / n_fast; order-
+// free modes (3, 4) scan a repeated length once (mult = its multiplicity)
+void gram_lists(const ldgpu_model* m, ScoreParams& p, int mode) {
+    p.maxg = 0;
+    p.n_fast = 0;
+    p.fast_mask = 0;
+    for (auto& g : p.gpack) g = 0;
+    for (auto& c : p.mult) c = 0;
+    for (int i = 0; i < m->nG; ++i) {
+        p.maxg = std::max(p.maxg, m->G[i]);
+        if (!((m->len_mask >> m->G[i]) & 1u)) continue;  // no key of that length: never a hit
+        p.fast_mask |= 1u << m->G[i];
+        if ((mode == 3 || mode == 4) && p.mult[m->G[i]]++) continue;
+        p.gpack[p.n_fast >> 4] |= (uint64_t)m->G[i] << (4 * (p.n_fast & 15));
+        ++p.n_fast;
+    }
+}
+
+// persistent grid: one wave per kScoreWaves documents, at most what is resident
+int score_grid(const ldgpu_model* m, int64_t n_docs) {
+    const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
+}
+
+// class mode's second step: the documents class_label left ambiguous (-1)
+// gathered into a packed sub-corpus, scored by the ordered replay (mode 1,
+// the reference's fold bit for bit) and their labels put back.  Reads back
+// two counts (ambiguous documents, their bytes): the sub-corpus is sized by
+// them, not by the batch.
+int class_replay(ldgpu_model* m, const ScoreParams& p4, hipStream_t st) {
+    const int64_t n = p4.n_docs;
+    int64_t* idx = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&idx, sizeof(int64_t) * (size_t)(n + 1), st));
+    unsigned long long* d_k = (unsigned long long*)(idx + n);
+    int64_t *sub_off = nullptr, *len_tmp = nullptr;
+    void* scan_tmp = nullptr;
+    uint8_t* sub = nullptr;
+    int32_t* sub_lab = nullptr;
+    unsigned long long k = 0;
+    int64_t total = 0;
+    size_t scan_bytes = 0;
+    hipError_t e = hipMemsetAsync(d_k, 0, sizeof *d_k, st);
+    if (e == hipSuccess) e = launch_amb_compact(p4.labels, n, idx, d_k, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&k, d_k, sizeof k, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && k > 0) {
+        const int64_t kk = (int64_t)k;
+        e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, nullptr, nullptr, nullptr, &scan_bytes, nullptr, st);
+        if (e == hipSuccess) e = hipMallocAsync((void**)&sub_off, sizeof(int64_t) * (size_t)(2 * kk + 2), st);
+        if (e == hipSuccess) e = hipMallocAsync(&scan_tmp, std::max<size_t>(scan_bytes, 16), st);
+        len_tmp = sub_off + kk + 1;
+        if (e == hipSuccess)
+            e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, sub_off, len_tmp, scan_tmp, &scan_bytes, nullptr, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&total, sub_off + kk, sizeof total, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = hipMallocAsync((void**)&sub, (size_t)total + 16, st);
+        if (e == hipSuccess) e = hipMallocAsync((void**)&sub_lab, sizeof(int32_t) * (size_t)kk, st);
+        if (e == hipSuccess)
+            e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, sub_off, len_tmp, scan_tmp, &scan_bytes, sub, st);
+        if (e == hipSuccess) {
+            ScoreParams p1 = p4;
+            p1.bytes = sub;
+            p1.n_bytes = total;
+            p1.last_dword = total > 0 ? (total - 1) >> 2 : 0;
+            p1.offsets = sub_off;
+            p1.n_docs = kk;
+            p1.labels = sub_lab;
+            p1.n_cls = 0;
+            p1.direct_words = 0;
+            gram_lists(m, p1, 1);
+            e = launch_score(p1, m->slices, 1, m->lds_filter, score_grid(m, kk), st);
+        }
+        if (e == hipSuccess) e = launch_amb_scatter(idx, kk, sub_lab, p4.labels, st);
+    }
+    for (void* q : {(void*)sub_lab, (void*)sub, scan_tmp, (void*)sub_off, (void*)idx})
+        if (q) (void)hipFreeAsync(q, st);
+    HIP_TRY(e);
+    return LDGPU_OK;
+}
+
 int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
                  int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st, double* d_best = nullptr,
                  int block = 0, int64_t score_stride = 0) {
@@ -1491,7 +1618,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.fold = m->d_fold;
     p.fold_max = kFoldMax;
     p.direct_off = m->direct_off;
-    p.direct_words = m->direct_words;
+    p.direct_words = m->direct_words;  // (order-free modes only: set below)
     p.count_sign = m->count_sign;
     // counts stay below 2^24: c <= windows of a document <= len * n_grams
     p.count_argmax_len = m->count_int_argmax ? ((1 << 24) - 1) / std::max(1, m->nG) : -1;
@@ -1504,20 +1631,17 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.ablate = m->ablate;
     p.nG = m->nG;
     for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
-    p.maxg = 0;
-    p.n_fast = 0;
-    for (int i = 0; i < m->nG; ++i) {
-        p.maxg = std::max(p.maxg, m->G[i]);
-        if (!((m->len_mask >> m->G[i]) & 1u)) continue;  // no key of that length: never a hit
-        // count mode: hit order is free, a repeated length is scanned once
-        p.fast_mask |= 1u << m->G[i];
-        if (m->mode == 3 && p.mult[m->G[i]]++) continue;
-        p.gpack[p.n_fast >> 4] |= (uint64_t)m->G[i] << (4 * (p.n_fast & 15));
-        ++p.n_fast;
+    // class mode: labels only, on a table of at most class_max(S) values
+    const bool classes = m->n_cls > 0 && !d_scores && !d_best && m->mode == 1;
+    const int mode = classes ? 4 : m->mode;
+    if (classes) {
+        for (int q = 0; q < 4; ++q) p.cls[q] = m->cls[q];
+        p.n_cls = m->n_cls;
     }
-    const int64_t want = (n_docs + kScoreWaves - 1) / kScoreWaves;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * m->wg_per_cu));
-    HIP_TRY(launch_score(p, m->slices, m->mode, m->lds_filter, grid, st));
+    gram_lists(m, p, mode);
+    if (mode != 3 && mode != 4) p.direct_words = 0;  // the ordered replay reads no direct tables
+    HIP_TRY(launch_score(p, m->slices, mode, m->lds_filter, score_grid(m, n_docs), st));
+    if (classes) return class_replay(m, p, st);
     return LDGPU_OK;
 }
 

@@ -44,6 +44,11 @@ struct ScoreParams {
     uint32_t fold_max;
     int32_t count_sign;         // count mode: sign of the value (fold[c] strictly monotone)
     int64_t count_argmax_len;   // count mode: documents up to this length take count_argmax (-1: none)
+    // class mode (4, labels only): the table's distinct row values; counters
+    // per (class, language); a document whose top two languages are not
+    // separated by the rounding bound gets label -1 (exact replay after)
+    double cls[4];
+    int32_t n_cls;
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     unsigned long long* stats;  // diagnostics build (-DLDGPU_STATS, env LDGPU_STATS): [0] candidates verified, [1] hits
     int32_t L;
@@ -117,6 +122,10 @@ constexpr uint32_t hit_area_words(int slices, int mode, bool pack = false) {
                      : 64u * 4u * (((uint32_t)slices + 2u) / 2u);
 }
 
+// class mode (4): at most this many distinct row values, so that its
+// (class, language) counters fit the ordered modes' hit area (same LDS)
+constexpr int class_max(int slices) { return (int)(4u * (((uint32_t)slices + 2u) / 2u) / (uint32_t)slices); }
+
 // bytes of dynamic LDS the score kernel needs; image_words = the filter image
 // staged in LDS (bitmaps, the bloom when it fits, direct tables)
 inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool pack = false) {
@@ -126,8 +135,22 @@ inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool p
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values
 // (fma accumulate), 2 = dense fp64 rows, 3 = mask rows sharing one finite
-// value (per-language hit counts); lds_bloom = bloom staged in LDS
+// value (per-language hit counts), 4 = mask rows of at most class_max(S)
+// finite values, labels only (per-(class, language) hit counts and a rounding
+// bound; ambiguous documents labelled -1); lds_bloom = bloom staged in LDS
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream);
+// class mode's ambiguous documents (ldgpu_replay.hip): idx[0 .. *n_out) = the
+// documents labelled -1; the sub-corpus of idx[0 .. k) (offsets sub_off[0 ..
+// k], bytes packed into sub; scan_tmp == nullptr: *scan_bytes = the scan's
+// scratch, nothing launched; sub == nullptr: the offsets only); the sub-corpus
+// labels back to labels[idx[i]]
+hipError_t launch_amb_compact(const int32_t* labels, int64_t n, int64_t* idx, unsigned long long* n_out,
+                              hipStream_t stream);
+hipError_t amb_sub_corpus(const int64_t* idx, int64_t k, const int64_t* offsets, const uint8_t* bytes, int64_t* sub_off,
+                          int64_t* len_tmp, void* scan_tmp, size_t* scan_bytes, uint8_t* sub, hipStream_t stream);
+hipError_t launch_amb_scatter(const int64_t* idx, int64_t k, const int32_t* sub_labels, int32_t* labels,
+                              hipStream_t stream);
+
 // General-key scoring (ldgpu_general.hip): models with a gram length beyond
 // kMaxWideGram -- keys of any length in one table (GenSlot), compared byte for
 // byte against the key arena on a hash match.  One wave per document; the

@@ -335,7 +335,7 @@ __device__ __forceinline__ void verify_issue(const ScoreParams& p, const WaveLds
     }
 }
 
-template <int S>
+template <int S, int MODE = 3>
 __device__ __forceinline__ void verify_complete(const ScoreParams& p, const WaveLds& w, const VerifyIssue& v) {
     uint32_t row = 0xffffffffu, lang1 = 0xffffffffu;
     if (v.valid) {
@@ -366,6 +366,10 @@ __device__ __forceinline__ void verify_complete(const ScoreParams& p, const Wave
     if (good && lang1 != 0xffffffffu) {
         count_inc<false>(cnt, lang1, v.inc);
     } else if (good) {
+        if constexpr (MODE == 4) {  // class mode: the row's class from its value
+            const double x = p.vals[row];
+            cnt += (x == p.cls[1] ? 1u : (x == p.cls[2] ? 2u : (x == p.cls[3] ? 3u : 0u))) * 64u * S;
+        }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             uint64_t mm = p.masks[(size_t)row * S + s];
@@ -398,7 +402,7 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
         if (j < qn) {
             const uint32_t e = w.queue[j];
             const int klen = (int)(e >> kPosBits);
-            if (MODE == 3 && weighted) inc = p.mult[klen];
+            if ((MODE == 3 || MODE == 4) && weighted) inc = p.mult[klen];
             if (PACK) coff = ((e >> 8) & (kPackDocs - 1u)) * 64u * S;
             const int64_t pos = (int64_t)(e & (PACK ? 255u : (1u << kPosBits) - 1u));
             if (WIDE && klen > kMaxGram) {  // (WIDE kernels: tables holding wide keys)
@@ -479,6 +483,32 @@ __device__ __forceinline__ void flush(const ScoreParams& p, const WaveLds& w, in
             }
         }
 #endif
+        if constexpr (MODE == 4) {
+            // class mode: order-free per-(class, language) hit counts.  A
+            // one-language row's slot holds its counter directly (class q,
+            // language l: q 64 S + l, the host's encoding of class-mode
+            // tables); another row's class is the index of its value among
+            // p.cls (exact: the host took p.cls from the rows' values; unused
+            // entries are NaN)
+            if (good) {
+                if (lang1 != 0xffffffffu) {
+                    count_inc<false>(count_area(w), lang1, inc);
+                } else {
+                    const uint32_t q = v == p.cls[1] ? 1u : (v == p.cls[2] ? 2u : (v == p.cls[3] ? 3u : 0u));
+                    uint32_t* cnt = count_area(w) + q * 64u * S;
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        uint64_t mm = s == 0 ? m0 : p.masks[(size_t)row * S + s];
+                        while (mm) {
+                            const int l = __builtin_ctzll(mm);
+                            mm &= mm - 1;
+                            count_inc<false>(cnt, 64 * s + l, inc);
+                        }
+                    }
+                }
+            }
+            continue;
+        }
         if constexpr (MODE == 3) {
             // uniform-value table: order-free per-language hit counts (the
             // score is the fold of that many adds of the one value, applied
@@ -606,6 +636,80 @@ __device__ __forceinline__ int count_argmax(const ScoreParams& p, C* cnt, int la
         }
     }
     return 255 - (int)(wave_max_u32(best) & 255u);
+}
+
+// MODE 4 label (labels only, at most 4 distinct row values v_q): per
+// language l (lane l of slice s) the hit counts c_ql of each class give
+// a_l = sum_q c_ql v_q and T_l = sum_q c_ql |v_q|; the reference's score f_l
+// is the ordered left fold of those n_l = sum_q c_ql adds
+// (LanguageDetectorModel.scala:139-154; adds of 0.0 are exact), and
+// |f_l - a_l| <= (gamma(n_l - 1) + gamma(4)) T_l, gamma(k) = k u / (1 - k u),
+// u = 2^-53; e_l = (n_l + 6) 2^-52 T_l bounds it with a margin that also
+// covers the roundings of a_l, T_l, e_l and of the comparisons below.  The
+// first maximum j of a is the reference's label when a_j - e_j > a_l + e_l for
+// every other l (then f_j > f_l: no tie, breeze's argmax is j); otherwise the
+// document is ambiguous: label -1, replayed exactly afterwards.  One class:
+// f_l = fold(n_l) is the same fold for every l, so n_l == n_j is an exact tie
+// and l > j loses it (j is the first maximum).  No hit at all: every f_l = 0.0,
+// label 0.  Clears the counters.
+template <int S>
+__device__ __forceinline__ int class_label(const ScoreParams& p, uint32_t* cnt, int lane) {
+    double a[S], e[S];
+    uint32_t nn[S];
+    uint32_t any = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int l = 64 * s + lane;
+        a[s] = -__builtin_inf();
+        e[s] = 0.0;
+        nn[s] = 0;
+        if (l < p.L) {
+            double acc = 0.0, t = 0.0;
+            uint32_t n = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q < p.n_cls) {
+                    const uint32_t c = cnt[q * 64 * S + 64 * s + lane];
+                    cnt[q * 64 * S + 64 * s + lane] = 0;
+                    acc = acc + (double)c * p.cls[q];
+                    t = t + (double)c * __builtin_fabs(p.cls[q]);
+                    n += c;
+                }
+            }
+            a[s] = acc;
+            e[s] = (double)(n + 6u) * 0x1p-52 * t;
+            nn[s] = n;
+            any |= n;
+        }
+    }
+    if (!__ballot(any != 0u)) return 0;
+    double lv = -__builtin_inf();
+#pragma unroll
+    for (int s = 0; s < S; ++s) lv = a[s] > lv ? a[s] : lv;
+    const double M = wave_max_f64(lv);
+    int j = -1;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const uint64_t b = __ballot(64 * s + lane < p.L && a[s] == M);
+        if (j < 0 && b) j = 64 * s + __builtin_ctzll(b);
+    }
+    double ej = 0.0;
+    uint32_t nj = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (j >> 6 == s) {
+            ej = rdlaned(e[s], j & 63);
+            nj = rdlane(nn[s], j & 63);
+        }
+    const double lo = M - ej;
+    const bool one = p.n_cls == 1;
+    bool clash = !__builtin_isfinite(lo);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int l = 64 * s + lane;
+        if (l < p.L && l != j && !(a[s] + e[s] < lo) && !(one && nn[s] == nj)) clash = true;
+    }
+    return __ballot(clash) ? -1 : j;
 }
 
 // The prefix-Bloom words the positions of one superblock need (chosen by
@@ -901,11 +1005,11 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
 // Count-mode verify of a full queue in the middle of a document's probe
 // (hit-dense tables: config 5's 10M keys); counts are order-free, so the
 // probe just continues.
-template <int S, bool STAGED, int KEYED, bool WIDE>
+template <int S, bool STAGED, int KEYED, bool WIDE, int MODE = 3>
 __device__ __forceinline__ void flush_count(const ScoreParams& p, const WaveLds& wl, int qn, const DocSrc& src,
                                             int lane) {
-    double acc[S];  // unused in count mode
-    if (!ablated(p, 1)) flush<S, 3, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, true);
+    double acc[S];  // unused in count / class mode
+    if (!ablated(p, 1)) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, true);
 }
 
 // keyed Bloom hash of sub-block k's N-byte window (filter_word, KIND 4)
@@ -947,7 +1051,7 @@ constexpr int kFmDirect = 16;
 
 // kw: the keyed bloom words of lengths 3 .. 2 + kPreN, preloaded together
 // (keyed_preload; KEYED == 1 with LDGPU_SINGLE_PRELOAD)
-template <int N, bool FULL, int S, bool STAGED, int KEYED, bool WIDE>
+template <int N, bool FULL, int S, bool STAGED, int KEYED, bool WIDE, int MODE = 3>
 __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                             const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                             const DocSrc& src, uint32_t fm, const uint32_t (&kw)[kPreN][kSub]) {
@@ -977,13 +1081,13 @@ __device__ __forceinline__ void probe_count(const ScoreParams& p, const WaveLds&
         test_nsb<KIND>(img, sh, mul, f, x, len - N + 1, m);
     }
     if (qn + count_sb(m) > kQueueCap) {
-        flush_count<S, STAGED, KEYED, WIDE>(p, wl, qn, src, lane);
+        flush_count<S, STAGED, KEYED, WIDE, MODE>(p, wl, qn, src, lane);
         qn = 0;
     }
     append_sb(wl.queue, qn, m, N, 0, lane);
 }
 
-template <bool FULL, int S, bool STAGED, int KEYED, bool WIDE>
+template <bool FULL, int S, bool STAGED, int KEYED, bool WIDE, int MODE = 3>
 __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                                 const FWords& f, const Windows& x, int32_t len, int lane, int& qn,
                                                 const DocSrc& src) {
@@ -1009,14 +1113,14 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
         keyed_preload<7>(f, x, fm, kw);
     }
     if (!split) {
-        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
-        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+        probe_count<1, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+        probe_count<2, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
     }
-    probe_count<3, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
-    probe_count<4, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
-    probe_count<5, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
-    probe_count<6, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
-    probe_count<7, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<3, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<4, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<5, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<6, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+    probe_count<7, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
     // wide gram lengths 8..15: one loop, the length a scalar (their filter
     // bits use the first seven bytes: the same two tests as length 7)
     for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {
@@ -1029,7 +1133,7 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
         else
             test_nsb<K3>(img, sh, mul, f, x, len - n + 1, m);
         if (qn + count_sb(m) > kQueueCap) {
-            flush_count<S, STAGED, KEYED, WIDE>(p, wl, qn, src, lane);
+            flush_count<S, STAGED, KEYED, WIDE, MODE>(p, wl, qn, src, lane);
             qn = 0;
         }
         append_sb(wl.queue, qn, m, n, 0, lane);
@@ -1038,13 +1142,13 @@ __device__ __forceinline__ void probe_count_all(const ScoreParams& p, const Wave
         VerifyIssue v;
         const bool pending = qn > 0 && !ablated(p, 1);
         if (pending) verify_issue<STAGED>(p, wl, qn, src, lane, v);
-        probe_count<1, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
-        probe_count<2, FULL, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+        probe_count<1, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
+        probe_count<2, FULL, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, len, lane, qn, src, fm, kw);
         if (pending) {
-            verify_complete<S>(p, wl, v);
+            verify_complete<S, MODE>(p, wl, v);
             if (qn > 64) {
                 double acc[S];  // unused in count mode
-                flush<S, 3, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, true, 64);
+                flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, true, 64);
             }
         }
         qn = 0;
@@ -1185,14 +1289,14 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             load_windows<STAGED>(p, src, 0, lane, x);
             FWords f;
             load_fwords<KEYED>(p, bloom, x, f);
-            if constexpr (MODE == 3) {
+            if constexpr (MODE == 3 || MODE == 4) {
                 if (len >= 192 + p.maxg)
-                    probe_count_all<true, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src);
+                    probe_count_all<true, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, (int32_t)len, lane, qn, src);
                 else
-                    probe_count_all<false, S, STAGED, KEYED, WIDE>(p, wl, img, f, x, (int32_t)len, lane, qn, src);
+                    probe_count_all<false, S, STAGED, KEYED, WIDE, MODE>(p, wl, img, f, x, (int32_t)len, lane, qn, src);
             }
             uint64_t gq = p.gpack[0];
-            for (int gi = 0; gi < (MODE == 3 ? 0 : p.n_fast); ++gi) {
+            for (int gi = 0; gi < (MODE == 3 || MODE == 4 ? 0 : p.n_fast); ++gi) {
                 const int n = (int)(gq & 15u);
                 gq = (gi & 15) == 15 ? p.gpack[1] : gq >> 4;
                 // pin the tests inside this loop: hoisted out of it (they are
@@ -1216,7 +1320,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
             }
             if (!general) {
                 if (ablated(p, 1)) qn = 0;
-                if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, MODE == 3);
+                if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane, MODE == 3 || MODE == 4);
             }
             qn = 0;
         }
@@ -1250,6 +1354,7 @@ __device__ __forceinline__ int score_doc(const ScoreParams& p, const WaveLds& wl
     }
     if (ablated(p, 1)) qn = 0;
     if (qn) flush<S, MODE, STAGED, KEYED, false, WIDE>(p, wl, qn, src, acc, lane);
+    if constexpr (MODE == 4) return ablated(p, 32) ? 0 : class_label<S>(p, count_area(wl), lane);
     if constexpr (MODE == 3) {
         if (ablated(p, 32)) return 0;
         if (with_cold<KEYED>(p, [&](const auto& q) { return !q.scores && !q.best && len <= q.count_argmax_len; }))
@@ -1371,6 +1476,11 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
         uint32_t* cnt = count_area(wl);
 #pragma unroll
         for (int s = 0; s < S * (PACK ? (int)kPackDocs / 2 : 1); ++s) cnt[64 * s + lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (MODE == 4) {  // (class, language) counters: the whole hit area
+        uint32_t* cnt = count_area(wl);
+        for (uint32_t i = (uint32_t)lane; i < kHitW; i += 64) cnt[i] = 0;
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -1621,6 +1731,7 @@ hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_blo
         case 1: return launch_m<1>(p, slices, lds_bloom, grid, stream);
         case 2: return launch_m<2>(p, slices, lds_bloom, grid, stream);
         case 3: return launch_m<3>(p, slices, lds_bloom, grid, stream);
+        case 4: return launch_m<4>(p, slices, lds_bloom, grid, stream);
         default: return hipErrorInvalidValue;
     }
 #endif
@@ -1639,6 +1750,7 @@ hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size
         case 1: return prepare_m<1>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
         case 2: return prepare_m<2>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
         case 3: return prepare_m<3>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
+        case 4: return prepare_m<4>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
         default: return hipErrorInvalidValue;
     }
 #endif

@@ -35,7 +35,7 @@ MAX_LANGS = 4096
 # ldgpu_model_layout flags
 LAYOUT_FLAGS = {"lds_bloom": 0x01, "keyed_bloom": 0x02, "keyed_bloom_lines": 0x04, "buckets": 0x08,
                 "wide_keys": 0x10, "direct": 0x20, "packs": 0x40, "lang_blocks": 0x80,
-                "general_keys": 0x100, "keyed_bloom_chunks": 0x200}
+                "general_keys": 0x100, "keyed_bloom_chunks": 0x200, "classes": 0x400}
 
 _p = ctypes.c_void_p
 _pp = ctypes.POINTER(ctypes.c_void_p)
@@ -190,8 +190,8 @@ def device_count() -> int:
 
 # the sources the library is built from, in the Makefile's PROV order
 _PROV = ["csrc/ldgpu_api.hip", "csrc/ldgpu_score.hip", "csrc/ldgpu_fit.hip", "csrc/ldgpu_general.hip",
-         "csrc/ldgpu_long.hip", "csrc/ldgpu_common.h", "csrc/ldgpu_internal.h", "csrc/ldgpu_fit.h",
-         "../include/ldgpu.h"]
+         "csrc/ldgpu_long.hip", "csrc/ldgpu_replay.hip", "csrc/ldgpu_common.h", "csrc/ldgpu_internal.h",
+         "csrc/ldgpu_fit.h", "../include/ldgpu.h"]
 
 
 def tree_source_hash() -> str:

@@ -1,0 +1,143 @@
+"""GPU parity of class mode: labels-only SCORE calls on a mask table whose rows
+hold at most a few distinct finite values (a fit table's presence classes,
+LanguageDetector.scala:98-105).  The kernel counts hits per (value, language),
+labels a document from the counts when a rounding bound separates its top
+language from every other, and replays the rest in reference order
+(LanguageDetectorModel.scala:139-154).  Labels must equal the oracle's exactly,
+ties and near ties included; scores calls keep the ordered replay."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import ldoracle_c as OC
+from languagedetection import encoding
+from languagedetection.runtime import DeviceModel
+
+pytestmark = pytest.mark.gpu
+
+ALPHABET = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+
+
+def class_table(rng, L, n_keys, grams, values):
+    """Each row: one of `values` at a random subset of the languages."""
+    table = {}
+    for _ in range(n_keys):
+        k = bytes(rng.choice(ALPHABET, size=int(rng.choice(grams))))
+        m = rng.random(L) < rng.uniform(0.02, 0.5)
+        if not m.any():
+            m[int(rng.integers(0, L))] = True
+        v = float(values[int(rng.integers(0, len(values)))])
+        table[k] = [v if b else 0.0 for b in m]
+    return table
+
+
+def oracle_labels(table, L, grams, data, off):
+    return OC.Table(table, L).score(grams, data, off, want_scores=False, nthreads=8)[0]
+
+
+def docs_of(rng, n, hi):
+    lens = rng.integers(0, hi, size=n)
+    lens[:6] = [0, 1, 2, 3, 7, 64]
+    return encoding.pack([bytes(rng.choice(ALPHABET, size=int(x))) for x in lens])
+
+
+# presence-class values: log(1 + 1/k), the shape of a fit table's probabilities
+PRESENCE = [math.log(1.0 + 1.0 / k) for k in (1, 2, 3, 5)]
+
+
+@pytest.mark.parametrize("L,grams,n_cls", [
+    (3, [1, 2, 3], 2), (20, [1, 2, 3, 4, 5], 4), (20, [1, 2, 3, 4, 5], 1), (64, [2, 3], 3),
+    (65, [3, 1], 4), (130, [1, 2, 3, 4, 5, 6, 7], 2), (200, [5, 5, 2], 3), (256, [4, 2], 2),
+])
+def test_class_mode_labels_match_oracle(L, grams, n_cls, monkeypatch):
+    """n_cls = 1: a one-value table takes count mode in the product library;
+    the diagnostics library's LDGPU_NO_COUNT_MODE sends it to class mode with
+    one class (exact ties decided by the counts)."""
+    rng = np.random.default_rng(L * 13 + n_cls)
+    values = PRESENCE[:n_cls] if n_cls > 1 else [-0.25]
+    table = class_table(rng, L, 400, grams, values)
+    data, off = docs_of(rng, 800, 200)
+    variant = "product"
+    if n_cls == 1:
+        monkeypatch.setenv("LDGPU_NO_COUNT_MODE", "1")
+        variant = "diag"
+    m = DeviceModel(table, L, grams, variant=variant)
+    assert "classes" in m.info()["layout"], m.info()
+    labels, _ = m.score(data, off)
+    assert np.array_equal(labels, oracle_labels(table, L, grams, data, off))
+    # a scores call keeps the ordered replay: same labels, scores bit-exact
+    lab2, sc = m.score(data, off, want_scores=True)
+    ol, os_ = OC.Table(table, L).score(grams, data, off, want_scores=True, nthreads=8)
+    assert np.array_equal(lab2, ol)
+    assert np.array_equal(np.ascontiguousarray(sc).view(np.uint64), np.ascontiguousarray(os_).view(np.uint64))
+
+
+def test_class_mode_order_dependent_ties():
+    """Two languages with the same (value, count) multiset in a different hit
+    order: the folds differ in the last bit (ln2, ln1.5, ln1.5 against ln1.5,
+    ln1.5, ln2), so neither the counts nor a first-maximum rule can decide --
+    only the ordered replay of those documents gives the reference's label."""
+    v1, v2 = math.log(2.0), math.log(1.5)
+    assert (0.0 + v1 + v2) + v2 != (0.0 + v2 + v2) + v1
+    table = {b"a": [v1, 0.0, 0.0], b"b": [v2, 0.0, 0.0], b"c": [0.0, v2, 0.0], b"d": [0.0, v1, 0.0],
+             b"e": [0.0, 0.0, v1], b"ab": [v2, v2, 0.0]}
+    rng = np.random.default_rng(5)
+    docs = [b"abbccd", b"ccdabb", b"abb", b"ccd", b"dcc", b"bba", b"", b"zzz", b"e"]
+    docs += [bytes(rng.choice(np.frombuffer(b"abcde", dtype=np.uint8), size=int(n)))
+             for n in rng.integers(1, 12, size=3000)]
+    data, off = encoding.pack(docs)
+    m = DeviceModel(table, 3, [1, 2])
+    assert "classes" in m.info()["layout"]
+    labels, _ = m.score(data, off)
+    ol = oracle_labels(table, 3, [1, 2], data, off)
+    assert np.array_equal(labels, ol), np.nonzero(labels != ol)[0][:10]
+    # the hand-made pair really is decided by order: labels differ between them
+    assert ol[0] != ol[2] or ol[0] == ol[1]
+
+
+def test_class_mode_device_api_and_all_ambiguous():
+    """ldgpu_score_device (device pointers, the stream the caller names): a
+    corpus where every document is an exact multi-class tie -- all of it goes
+    through the replay step."""
+    v1, v2 = math.log(2.0), math.log(1.5)
+    table = {b"a": [v1, v1], b"b": [v2, v2]}
+    docs = [b"ab" * int(n) for n in range(1, 400)] + [b"ba" * 3, b"aab", b"bba"]
+    data, off = encoding.pack(docs)
+    m = DeviceModel(table, 2, [1])
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_lab = torch.full((len(docs),), 7, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    m.score_device(d_bytes.data_ptr(), len(data), d_off.data_ptr(), len(docs), d_lab.data_ptr(), 0, st.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_lab.cpu().numpy(), oracle_labels(table, 2, [1], data, off))
+
+
+def test_too_many_values_keep_the_ordered_replay():
+    """More distinct values than the counters hold: no class mode, labels from
+    the ordered replay, still exact."""
+    rng = np.random.default_rng(9)
+    table = class_table(rng, 20, 300, [1, 2, 3], [math.log(1.0 + 1.0 / k) for k in range(1, 9)])
+    data, off = docs_of(rng, 500, 150)
+    m = DeviceModel(table, 20, [1, 2, 3])
+    assert "classes" not in m.info()["layout"]
+    labels, _ = m.score(data, off)
+    assert np.array_equal(labels, oracle_labels(table, 20, [1, 2, 3], data, off))
+
+
+def test_class_mode_switched_off_in_diag_library(monkeypatch):
+    """LDGPU_NO_CLASS_MODE (diagnostics library) forces the ordered replay on
+    the same table: the two paths agree."""
+    rng = np.random.default_rng(21)
+    table = class_table(rng, 20, 400, [1, 2, 3, 4, 5], PRESENCE)
+    data, off = docs_of(rng, 600, 200)
+    a = DeviceModel(table, 20, [1, 2, 3, 4, 5])
+    monkeypatch.setenv("LDGPU_NO_CLASS_MODE", "1")
+    b = DeviceModel(table, 20, [1, 2, 3, 4, 5], variant="diag")
+    assert "classes" in a.info()["layout"] and "classes" not in b.info()["layout"]
+    la, _ = a.score(data, off)
+    lb, _ = b.score(data, off)
+    assert np.array_equal(la, lb)
