@@ -289,6 +289,56 @@ def mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs
     return res
 
 
+def general_key_path(args, table, grams, local, d_bytes, d_off, n_docs, d_lab, stream):
+    """The general-key SCORE path (a gram length beyond 15 bytes moves every
+    key into the general table, ldgpu_general.hip) on config 2's table plus
+    one 16-byte key that valid UTF-8 never holds (0xff bytes), gram lengths
+    + [16], over the first 1M documents: its kernel time and whether its
+    labels equal the count-mode launch's.  Reported beside `value`."""
+    from languagedetection import LanguageDetectorModel
+    t2 = dict(table)
+    t2[b"\xff" * 16] = [next(iter(table.values()))[0] or 1.0] + [0.0] * (args.langs - 1)
+    m = DeviceModel(t2, args.langs, grams + [16], device=local)
+    n = min(n_docs, 1_000_000)
+    nb = int(d_off[n].item())
+    d_out = torch.empty(n, dtype=torch.int32, device=d_lab.device)
+
+    def step():
+        m.score_device(d_bytes.data_ptr(), nb, d_off.data_ptr(), n, d_out.data_ptr(), 0, stream.cuda_stream)
+    step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    for s_, e_ in ev:
+        s_.record(stream)
+        step()
+        e_.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev]))
+    res = {"layout": m.info()["layout"], "docs": n, "kernel_ms": round(ms, 4),
+           "docs_per_s": round(n / (ms * 1e-3), 1), "labels_match_count_mode": bool(torch.equal(d_out, d_lab[:n])),
+           "note": "config 2's table + one 16-byte key, gram lengths 1-5 and 16: every key in the general table"}
+    m.close()
+    # the static detect (LanguageDetectorModel.detect, one document per call,
+    # the table cached across calls with the same map)
+    lang_names = [f"l{i}" for i in range(args.langs)]
+    k = 2000
+    off_h = d_off[:k + 1].cpu().numpy()
+    raw = d_bytes[:int(off_h[-1])].cpu().numpy().tobytes()
+    docs = [raw[off_h[i]:off_h[i + 1]] for i in range(k)]
+    t0 = time.perf_counter()
+    first = LanguageDetectorModel.detect(docs[0], table, lang_names, grams)
+    t_first = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    got = [LanguageDetectorModel.detect(d, table, lang_names, grams) for d in docs]
+    dt = time.perf_counter() - t0
+    want = [lang_names[int(x)] for x in d_lab[:k].cpu().numpy()]
+    res["static_detect"] = {"calls": k, "calls_per_s": round(k / dt, 1), "first_call_s": round(t_first, 4),
+                            "labels_match_count_mode": got == want and first == want[0],
+                            "note": "LanguageDetectorModel.detect(bytes, map, languages, grams) per document; "
+                                    "the device table is built on the first call and cached"}
+    return res
+
+
 def traffic_from_profiles(workload_key):
     """HBM bytes per launch (per count, for FIT) from the committed rocprofv3
     PMC passes (profiles/pmc_traffic*.json), if they were collected for this
@@ -674,6 +724,9 @@ def main():
     alt = None
     if rank == 0 and world == 1 and args.config == 2 and not args.no_alt_paths and not args.empty_table:
         alt = mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs, d_lab, stream)
+    general = None
+    if rank == 0 and world == 1 and args.config == 2 and not args.no_alt_paths and table:
+        general = general_key_path(args, table, grams, local, d_bytes, d_off, n_docs, d_lab, stream)
     host = None
     if rank == 0 and world == 1 and not args.no_host_path and not args.empty_table:
         host = host_path(model, data, off, acc_labels=d_lab.cpu().numpy())
@@ -714,6 +767,7 @@ def main():
         "oracle_check": oracle_check,
         "host_path": host,
         "mask_replay_path": alt,
+        "general_keys_path": general,
         "fit_setup": fit_info,
         "label_accuracy_vs_generator": acc,
     }

@@ -520,3 +520,67 @@ def test_bench_fit_two_ranks_merged_table_matches_oracle():
     assert line["n_gpus"] == 2
     assert line["merged_table_matches_oracle"] is True, line.get("merge_check")
     assert line["windows_counted_exactly_once"] is True
+
+
+def _sparse_topk_masks(expect, L, K):
+    """filterTopGrams over the oracle's sparse counts (kb, ko, po, pl, pc in
+    (length, bytes, language) order): every gram in some language's top K by
+    (v_l desc, index asc), as (keys, mask words [n][ceil(L/64)], values)."""
+    kb, ko, po, pl, pc = expect
+    n = len(ko) - 1
+    k = np.diff(po)
+    w = np.zeros(n)
+    w[k > 0] = np.log(1.0 + 1.0 / k[k > 0])
+    g = np.repeat(np.arange(n), k)
+    order = np.lexsort((g, -w[g], pl))
+    sl = pl[order]
+    chosen = np.zeros(n, dtype=bool)
+    starts = np.searchsorted(sl, np.arange(L + 1))
+    for l in range(L):
+        chosen[g[order[starts[l]:min(starts[l + 1], starts[l] + K)]]] = True
+    idx = np.nonzero(chosen)[0]
+    b = kb.tobytes()
+    keys = [b[ko[i]:ko[i + 1]] for i in idx]
+    words = (L + 63) // 64
+    masks = np.zeros((len(idx), words), dtype=np.uint64)
+    for j, i in enumerate(idx):
+        for l in pl[po[i]:po[i + 1]]:
+            masks[j, l // 64] |= np.uint64(1) << np.uint64(l % 64)
+    return keys, masks, w[idx]
+
+
+def test_config5_shape_fit_counts_table_and_scores():
+    """Config 5's fit shape at test size -- L = 200, grams 1-7 (two-word
+    records: the radix-sort + run-pass count), a ~10 MB corpus of 1-5 KB
+    documents, K = 2000 -- through the product library: the sparse counts equal
+    the C restatement's pair for pair, the mask-form top-K table equals the
+    rule over those counts, and the model built from it labels (labels-only:
+    class or replay mode) and scores (fp64 bits) like the oracle."""
+    from languagedetection.runtime import DeviceModel
+    L, grams, K = 200, [1, 2, 3, 4, 5, 6, 7], 2000
+    ls = synth.make_languages(L)
+    data, off, lang = synth.generate(ls, 3400, 1024, 5120, seed=synth.SEED_BASE + 5)
+    counts = DeviceCounts(L, grams)
+    counts.count(data, off, lang)
+    got = counts.export_sparse()
+    expect = OC.count_sparse(data, off, lang, L, grams, nthreads=8)
+    assert len(got) == len(expect) and all(np.array_equal(a, b) for a, b in zip(got, expect))
+    kb, ko, masks, vals = counts.fit_table_masks(K)
+    counts.close()
+    b = kb.tobytes()
+    gkeys = [b[ko[i]:ko[i + 1]] for i in range(len(ko) - 1)]
+    order = sorted(range(len(gkeys)), key=lambda i: (len(gkeys[i]), gkeys[i]))
+    ekeys, emasks, evals = _sparse_topk_masks(expect, L, K)
+    assert [gkeys[i] for i in order] == ekeys
+    assert np.array_equal(masks[order], emasks)
+    assert np.array_equal(np.asarray(vals)[order], evals)
+    sdata, soff, _ = synth.generate(ls, 20000, 0, 300, seed=synth.SEED_BASE + 6)
+    m = DeviceModel.from_masks(kb, ko, masks, vals, L, grams)
+    t = OC.Table.from_masks(kb[:max(int(ko[-1]), 1)], ko, masks, vals, L)
+    labels, _ = m.score(sdata, soff)
+    ol, _ = t.score(grams, sdata, soff, nthreads=8)
+    assert np.array_equal(labels, ol)
+    n2 = 2000
+    lab2, sc2 = m.score(sdata[:int(soff[n2])], soff[:n2 + 1], want_scores=True)
+    ol2, os2 = t.score(grams, sdata[:int(soff[n2])], soff[:n2 + 1], want_scores=True, nthreads=8)
+    assert np.array_equal(lab2, ol2) and np.array_equal(sc2.view(np.uint64), os2.view(np.uint64))
