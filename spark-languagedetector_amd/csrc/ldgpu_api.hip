@@ -1345,7 +1345,8 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
                     if ((filter[kBmp1Words + wd] >> b) & 1u) lang2.push_back(lang2of[bmp2_unword(wd) * 32 + b]);
             }
             const uint32_t dwords = 64u + 1024u + (uint32_t)((lang2.size() + 16) / 16) * 4u;  // uint4-padded
-            if (score_lds_bytes(S, m->mode == 3 ? 3 : 4, image_words + dwords) * 2 <= 163840) {
+            const uint32_t hw4 = m->mode == 3 ? 0u : 64u * (uint32_t)S * (uint32_t)m->n_cls;
+            if (score_lds_bytes(S, m->mode == 3 ? 3 : 4, image_words + dwords, false, hw4) * 2 <= 163840) {
                 m->direct_off = image_words;
                 m->direct_words = dwords;
                 filter.resize(image_words + dwords, 0u);
@@ -1380,11 +1381,18 @@ int model_build(ldgpu_ctx* ctx, int32_t n_langs, const int32_t* gram_lengths, in
         }
     }
     int resident = 0;
-    if (e == hipSuccess) e = score_prepare(S, m->mode, m->lds_filter, m->kb_chunks, m->lds_bytes, &resident);
-    if (e == hipSuccess && m->n_cls) {  // class mode shares the grid: the smaller occupancy
-        int r4 = 0;
-        e = score_prepare(S, 4, m->lds_filter, m->kb_chunks, m->lds_bytes, &r4);
+    if (m->n_cls) {
+        // the ordered replay reads no direct tables; class mode's hit area
+        // holds its classes' counters: the larger of the two launches
+        const size_t l1 = score_lds_bytes(S, 1, image_words - m->direct_words);
+        const size_t l4 = score_lds_bytes(S, 4, image_words, false, 64u * (uint32_t)S * (uint32_t)m->n_cls);
+        m->lds_bytes = std::max(l1, l4);
+        if (e == hipSuccess) e = score_prepare(S, 1, m->lds_filter, m->kb_chunks, l1, &resident);
+        int r4 = 0;  // class mode shares the grid: the smaller occupancy
+        if (e == hipSuccess) e = score_prepare(S, 4, m->lds_filter, m->kb_chunks, l4, &r4);
         if (r4 > 0) resident = resident > 0 ? std::min(resident, r4) : r4;
+    } else if (e == hipSuccess) {
+        e = score_prepare(S, m->mode, m->lds_filter, m->kb_chunks, m->lds_bytes, &resident);
     }
     // persistent grid = what is resident; never more workgroups than the LDS admits
     m->wg_per_cu = std::max<int>(1, std::min<int>(resident > 0 ? resident : 1, (int)(163840 / m->lds_bytes)));
@@ -1520,6 +1528,7 @@ int class_replay(ldgpu_model* m, const ScoreParams& p4, hipStream_t st) {
             p1.n_docs = kk;
             p1.labels = sub_lab;
             p1.n_cls = 0;
+            p1.hit_words = 0;
             p1.direct_words = 0;
             gram_lists(m, p1, 1);
             e = launch_score(p1, m->slices, 1, m->lds_filter, score_grid(m, kk), st);
@@ -1637,6 +1646,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     if (classes) {
         for (int q = 0; q < 4; ++q) p.cls[q] = m->cls[q];
         p.n_cls = m->n_cls;
+        p.hit_words = 64u * (uint32_t)m->slices * (uint32_t)m->n_cls;
     }
     gram_lists(m, p, mode);
     if (mode != 3 && mode != 4) p.direct_words = 0;  // the ordered replay reads no direct tables

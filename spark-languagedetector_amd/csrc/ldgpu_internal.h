@@ -49,6 +49,7 @@ struct ScoreParams {
     // separated by the rounding bound gets label -1 (exact replay after)
     double cls[4];
     int32_t n_cls;
+    uint32_t hit_words;         // class mode: the hit area per wave (64 S n_cls words), sized by the table
     int32_t* err;               // bit 0: a window hit a wrong-length row; bit 1: doc too long
     unsigned long long* stats;  // diagnostics build (-DLDGPU_STATS, env LDGPU_STATS): [0] candidates verified, [1] hits
     int32_t L;
@@ -128,9 +129,10 @@ constexpr int class_max(int slices) { return (int)(4u * (((uint32_t)slices + 2u)
 
 // bytes of dynamic LDS the score kernel needs; image_words = the filter image
 // staged in LDS (bitmaps, the bloom when it fits, direct tables)
-inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool pack = false) {
-    return (size_t)image_words * 4u + (size_t)kScoreWaves * (kQueueCap * 4u + hit_area_words(slices, mode, pack) * 4u +
-                                                              2u * kBufWords * 4u + 64u * 4u);
+// (hit_words: class mode's area, 64 S counters per class; 0 = the mode's)
+inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool pack = false, uint32_t hit_words = 0) {
+    const uint32_t hw = hit_words ? hit_words : hit_area_words(slices, mode, pack);
+    return (size_t)image_words * 4u + (size_t)kScoreWaves * (kQueueCap * 4u + hw * 4u + 2u * kBufWords * 4u + 64u * 4u);
 }
 
 // slices = ceil(L / 64); mode 0 = mask rows, 1 = mask rows with finite values

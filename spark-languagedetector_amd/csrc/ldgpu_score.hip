@@ -1466,7 +1466,8 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
     const uint32_t* bloom = FLDS ? lds + kBloomBase : p.filter + kBloomBase;
     WaveLds wl;
     wl.queue = lds + img_words + wave * kQueueCap;
-    constexpr uint32_t kHitW = hit_area_words(S, MODE, PACK);
+    // class mode: the hit area holds the table's classes' counters only
+    const uint32_t kHitW = MODE == 4 ? __builtin_amdgcn_readfirstlane(p.hit_words) : hit_area_words(S, MODE, PACK);
     wl.hits = reinterpret_cast<uint64_t*>(lds + img_words + kScoreWaves * kQueueCap + wave * kHitW);
     wl.buf = lds + img_words + kScoreWaves * (kQueueCap + kHitW) + wave * 2 * kBufWords;
     wl.labels = lds + img_words + kScoreWaves * (kQueueCap + kHitW + 2 * kBufWords) + wave * 64;
@@ -1585,7 +1586,8 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
 template <int S, int MODE, int BL, bool WIDE>
 hipError_t launch_w(const ScoreParams& p, int grid, hipStream_t stream) {
     const bool pack = MODE == 3 && p.pack;
-    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (BL == 0 ? p.bloom_words : 0u) + p.direct_words, pack);
+    const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (BL == 0 ? p.bloom_words : 0u) + p.direct_words, pack,
+                                       MODE == 4 ? p.hit_words : 0u);
     if constexpr (MODE == 3) {
         if (pack) {
             hipLaunchKernelGGL((score_kernel<S, MODE, BL, true, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds,

@@ -141,3 +141,41 @@ def test_class_mode_switched_off_in_diag_library(monkeypatch):
     la, _ = a.score(data, off)
     lb, _ = b.score(data, off)
     assert np.array_equal(la, lb)
+
+
+@pytest.mark.parametrize("L,n_cls", [(20, 2), (63, 1), (40, 3)])
+def test_class_mode_direct_tables(L, n_cls, monkeypatch):
+    """Every 1-/2-byte key names one language (a fit table's unique grams),
+    L <= 63: class mode counts those windows from the LDS direct tables (an
+    entry = language | class << 6) and the longer keys through the split
+    verify; labels equal to the oracle's."""
+    rng = np.random.default_rng(L * 3 + n_cls)
+    values = PRESENCE[:n_cls] if n_cls > 1 else [0.375]
+    table = {}
+    for _ in range(600):
+        n = int(rng.choice([1, 2, 3, 4, 5]))
+        k = bytes(rng.choice(ALPHABET, size=n))
+        v = float(values[int(rng.integers(0, len(values)))])
+        if n <= 2:
+            row = [0.0] * L
+            row[int(rng.integers(0, L))] = v
+        else:
+            m = rng.random(L) < rng.uniform(0.02, 0.4)
+            if not m.any():
+                m[0] = True
+            row = [v if b else 0.0 for b in m]
+        table[k] = row
+    data, off = docs_of(rng, 3000, 300)
+    variant = "product"
+    if n_cls == 1:
+        monkeypatch.setenv("LDGPU_NO_COUNT_MODE", "1")
+        variant = "diag"
+    m = DeviceModel(table, L, [1, 2, 3, 4, 5], variant=variant)
+    lay = m.info()["layout"]
+    assert "classes" in lay and "direct" in lay, lay
+    labels, _ = m.score(data, off)
+    assert np.array_equal(labels, oracle_labels(table, L, [1, 2, 3, 4, 5], data, off))
+    lab2, sc = m.score(data[:int(off[500])], off[:501], want_scores=True)
+    ol, os_ = OC.Table(table, L).score([1, 2, 3, 4, 5], data[:int(off[500])], off[:501], want_scores=True, nthreads=8)
+    assert np.array_equal(lab2, ol)
+    assert np.array_equal(np.ascontiguousarray(sc).view(np.uint64), np.ascontiguousarray(os_).view(np.uint64))
