@@ -3226,6 +3226,21 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
     };
     BatchPlan cur, nxt;
     make_plan(0, cur);
+    // The last merge of a batch is not waited for: its table size and
+    // overflow count are read back after the next batch's reduce (the host
+    // waits there anyway), so the next batch's emit follows the merge on the
+    // stream without a host round trip.  (Tables with a wide part check it
+    // after every merge.)
+    bool t1_pending = false;
+    uint64_t pend_size0 = 0;
+    unsigned long long pend_E = 0;
+    auto settle_t1 = [&]() -> int {
+        if (!t1_pending) return LDGPU_OK;
+        t1_pending = false;
+        if (int rc = after_batch(t1)) return rc;
+        if (pend_E) t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - pend_size0) / (double)pend_E);
+        return LDGPU_OK;
+    };
     // diagnostics build: host-side phase times per batch (LDGPU_FIT_TRACE)
     const bool trace = diag_env("LDGPU_FIT_TRACE") != nullptr;
     auto now_ms = [] {
@@ -3323,6 +3338,7 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             memcpy(nout.data(), x->h_fon.p, sizeof(uint32_t) * nout.size());
             memcpy(boff.data(), (uint8_t*)x->h_fon.p + sizeof(uint32_t) * nout.size(), sizeof(uint64_t) * boff.size());
         }
+        if (int rc = settle_t1()) return rc;  // the previous batch's last merge
         const int64_t R = (int64_t)boff[(size_t)kQ * kQ];
         if (R > acc) return fail(LDGPU_EDEVICE, "fit emit: %lld records from %lld positions", (long long)R, (long long)acc);
         unsigned long long E = 0;
@@ -3389,10 +3405,19 @@ int count_launch_v3(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes, co
             if (wide) {
                 if (int rc = wide_after(t1)) return rc;
             }
-            if (int rc = after_batch(t1)) return rc;
+            if (!wide && more && b1 == kQ * kQ) {
+                t1_pending = true;  // settled after the next batch's reduce
+            } else if (int rc = after_batch(t1)) {
+                return rc;
+            }
             b0 = b1;
         }
-        if (E) t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - size0) / (double)E);
+        if (t1_pending) {
+            pend_size0 = size0;
+            pend_E = E;
+        } else if (E) {
+            t1->new_per_entry = std::max(0.02, (double)(t1->size + t1->wsize - size0) / (double)E);
+        }
         if (trace) {
             tt[5] = now_ms();
             fprintf(stderr, "fit batch: upload+launch %.3f plan %.3f gpu-wait %.3f pre-merge %.3f merge %.3f ms\n",
