@@ -845,3 +845,25 @@ def test_keyed_bloom_line_layout(form, grams, doc_range, monkeypatch):
     monkeypatch.delenv("LDGPU_KB_LINES")
     plain, _ = DeviceModel(table, L, grams).score(data, off, want_scores=False)
     assert np.array_equal(plain, ol)
+
+
+def test_models_of_one_kernel_with_different_lds_sizes():
+    """Two models on the same kernel instantiation (LDS bloom, count mode, one
+    slice) whose dynamic LDS differs (a 64 KiB bloom against a tiny one): the
+    larger model still launches after the smaller one was built, and both
+    score like the oracle."""
+    rng = np.random.default_rng(31)
+    alphabet = np.arange(256, dtype=np.uint8)
+    big = _random_table(rng, 20, 30000, [3, 4, 5], alphabet, True, uniform=0.5)
+    small = _random_table(rng, 20, 50, [3, 4, 5], alphabet, True, uniform=0.5)
+    data, off = encoding.pack([bytes(rng.integers(0, 256, size=int(n), dtype=np.uint8))
+                               for n in rng.integers(0, 300, size=2000)])
+    a = DeviceModel(big, 20, [3, 4, 5])
+    la1, _ = a.score(data, off)
+    b = DeviceModel(small, 20, [3, 4, 5])
+    lb, _ = b.score(data, off)
+    la2, _ = a.score(data, off)
+    assert a.info()["mode"] == b.info()["mode"] == 2
+    assert "lds_bloom" in a.info()["layout"] and "lds_bloom" in b.info()["layout"]
+    assert np.array_equal(la1, la2) and np.array_equal(la1, oracle_c(big, 20, [3, 4, 5], data, off, scores=False)[0])
+    assert np.array_equal(lb, oracle_c(small, 20, [3, 4, 5], data, off, scores=False)[0])
