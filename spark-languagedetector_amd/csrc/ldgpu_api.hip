@@ -1953,21 +1953,26 @@ CountParams count_params(const ldgpu_counts* c) {
         p.pshift = (uint32_t)(64 - log2u(c->pcap));
         p.pmask = c->pcap - 1;
         p.psize = c->d_psize;
+        p.pinter = 1;  // alloc_pairs: keys and counts interleaved
     }
     return p;
 }
 
-// the sparse table's pairs seen as a dense table of one counter per slot
-// (stats_kernel: occupied pairs and the sum of their counts)
-CountParams pair_view_of(uint64_t* pkeys, unsigned long long* pcounts) {
+// a pair table for stats_kernel (occupied pairs and the sum of their counts);
+// inter: keys and counts interleaved (T) or separate (the long-gram table)
+CountParams pair_view_of(uint64_t* pkeys, unsigned long long* pcounts, uint32_t inter) {
     CountParams p{};
-    p.keys = pkeys;
-    p.counts = pcounts;
+    p.pkeys = pkeys;
+    p.pcounts = pcounts;
+    p.pinter = inter;
     p.L = 1;
     return p;
 }
 
-CountParams pair_view(const ldgpu_counts* c) { return pair_view_of(c->d_pkeys, c->d_pcounts); }
+CountParams pair_view(const ldgpu_counts* c) { return pair_view_of(c->d_pkeys, c->d_pcounts, 1); }
+
+// T's pair table (alloc_pairs): one block of 16-B entries, pcounts = pkeys + 1
+void free_pairs(ldgpu_ctx* ctx, uint64_t* pkeys, uint64_t pcap) { cache_free(ctx, pkeys, pcap * 16u); }
 
 void counts_free(ldgpu_counts* c) {
     if (!c) return;
@@ -1985,14 +1990,13 @@ void counts_free(ldgpu_counts* c) {
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_counts, c->cap * (size_t)c->L * sizeof(unsigned long long));
         cache_free(c->ctx, c->d_kcnt, c->cap * sizeof(uint32_t));
-        cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
-        cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
+        free_pairs(c->ctx, c->d_pkeys, c->pcap);
         cache_free(c->ctx, c->d_ovf_keys, sizeof(uint64_t) * c->ovf_cap);
         cache_free(c->ctx, c->d_ovf_lang, sizeof(int32_t) * c->ovf_cap);
         cache_free(c->ctx, c->d_ovf_cnt, sizeof(unsigned long long) * c->ovf_cap);
     } else {
         for (void* p : {(void*)c->d_keys, (void*)c->d_counts, (void*)c->d_kcnt, (void*)c->d_pkeys,
-                        (void*)c->d_pcounts, (void*)c->d_ovf_keys, (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt})
+                        (void*)c->d_ovf_keys, (void*)c->d_ovf_lang, (void*)c->d_ovf_cnt})
             if (p) (void)hipFree(p);
     }
     for (void* p : {(void*)c->d_size, (void*)c->d_psize, (void*)c->d_ovf_n, (void*)c->d_ovf2_keys,
@@ -2017,17 +2021,18 @@ int alloc_table(ldgpu_counts* c, uint64_t cap, uint64_t** keys, void** rows) {
     return LDGPU_OK;
 }
 
-// the sparse table's pair table of pcap slots, zeroed
+// the sparse table's pair table of pcap slots, zeroed: 16-B entries {key,
+// count} (CountParams::pinter), so a pair insert claims its key and adds its
+// count in one 64-B line
 int alloc_pairs(ldgpu_counts* c, uint64_t pcap, uint64_t** pkeys, unsigned long long** pcounts) {
-    HIP_TRY(cache_alloc(c->ctx, (void**)pkeys, pcap * sizeof(uint64_t)));
-    hipError_t e = cache_alloc(c->ctx, (void**)pcounts, pcap * sizeof(unsigned long long));
+    hipError_t e = cache_alloc(c->ctx, (void**)pkeys, pcap * 16u);
     if (e != hipSuccess) {
-        cache_free(c->ctx, *pkeys, pcap * sizeof(uint64_t));
         *pkeys = nullptr;
+        *pcounts = nullptr;
         return fail(LDGPU_ENOMEM, "pair table of %llu slots: %s", (unsigned long long)pcap, hipGetErrorString(e));
     }
-    HIP_TRY(hipMemsetAsync(*pkeys, 0, pcap * sizeof(uint64_t), c->ctx->stream));
-    HIP_TRY(hipMemsetAsync(*pcounts, 0, pcap * sizeof(unsigned long long), c->ctx->stream));
+    *pcounts = reinterpret_cast<unsigned long long*>(*pkeys) + 1;
+    HIP_TRY(hipMemsetAsync(*pkeys, 0, pcap * 16u, c->ctx->stream));
     return LDGPU_OK;
 }
 
@@ -2045,8 +2050,7 @@ int rebuild_pairs(ldgpu_counts* c, uint64_t new_pcap, const uint64_t* remap) {
     tmp.d_pcounts = nc;
     HIP_TRY(launch_pair_rehash(count_params(c), count_params(&tmp), c->pcap, remap, c->ctx->stream));
     HIP_TRY(hipStreamSynchronize(c->ctx->stream));
-    cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
-    cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
+    free_pairs(c->ctx, c->d_pkeys, c->pcap);
     c->d_pkeys = nk;
     c->d_pcounts = nc;
     c->pcap = new_pcap;
@@ -2084,8 +2088,7 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
         if (e != hipSuccess || rc) {
             (void)hipGetLastError();
             if (remap) cache_free(c->ctx, remap, c->cap * sizeof(uint64_t));
-            cache_free(c->ctx, tmp.d_pkeys, c->pcap * sizeof(uint64_t));
-            cache_free(c->ctx, tmp.d_pcounts, c->pcap * sizeof(unsigned long long));
+            if (tmp.d_pkeys) free_pairs(c->ctx, tmp.d_pkeys, c->pcap);
             cache_free(c->ctx, nk, new_cap * sizeof(uint64_t));
             cache_free(c->ctx, nr, new_cap * sizeof(uint32_t));
             tmp.d_pkeys = nullptr;
@@ -2096,8 +2099,7 @@ int grow(ldgpu_counts* c, uint64_t new_cap) {
         cache_free(c->ctx, remap, c->cap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_kcnt, c->cap * sizeof(uint32_t));
-        cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
-        cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
+        free_pairs(c->ctx, c->d_pkeys, c->pcap);
         c->d_keys = nk;
         c->d_kcnt = tmp.d_kcnt;
         c->d_pkeys = tmp.d_pkeys;
@@ -4038,7 +4040,7 @@ extern "C" int ldgpu_counts_stats(ldgpu_counts* c, int64_t* n_grams, int64_t* n_
     // the sparse table's pairs (one counter each), the wide table's rows
     if (e == hipSuccess) e = launch_stats(pair_view(c), c->pcap, d, c->ctx->stream);
     if (e == hipSuccess && c->lpcap)  // the long grams' pairs
-        e = launch_stats(pair_view_of(c->d_lpkeys, c->d_lpcounts), c->lpcap, d, c->ctx->stream);
+        e = launch_stats(pair_view_of(c->d_lpkeys, c->d_lpcounts, 0), c->lpcap, d, c->ctx->stream);
     if (e == hipSuccess && c->wcap) {  // the wide table, through the same kernel (hi != 0: occupied)
         CountParams w{};
         w.keys = c->d_whi;
@@ -4826,8 +4828,7 @@ extern "C" int ldgpu_counts_merge(ldgpu_counts* c, ldgpu_comm* m) {
         HIP_TRY(hipStreamSynchronize(st));
         cache_free(c->ctx, c->d_keys, c->cap * sizeof(uint64_t));
         cache_free(c->ctx, c->d_kcnt, c->cap * sizeof(uint32_t));
-        cache_free(c->ctx, c->d_pkeys, c->pcap * sizeof(uint64_t));
-        cache_free(c->ctx, c->d_pcounts, c->pcap * sizeof(unsigned long long));
+        free_pairs(c->ctx, c->d_pkeys, c->pcap);
         c->d_keys = c->d_pkeys = nullptr;
         c->d_kcnt = nullptr;
         c->d_pcounts = nullptr;

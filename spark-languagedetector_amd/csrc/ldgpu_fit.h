@@ -42,7 +42,17 @@ struct CountParams {
     uint32_t pshift;            // pair slot = fit_hash(pair key) >> pshift
     uint64_t pmask;             // pcap - 1
     unsigned long long* psize;  // distinct pairs inserted
+    // pair entry i: key pkeys[i << pinter], count pcounts[i << pinter].  T's
+    // pair table interleaves them (pinter 1, pcounts = pkeys + 1: an insert's
+    // key claim and count add touch one 64-B line); 0 = separate arrays (the
+    // long-gram table's views)
+    uint32_t pinter;
 };
+
+__host__ __device__ __forceinline__ uint64_t* pkey_at(const CountParams& p, uint64_t i) { return p.pkeys + (i << p.pinter); }
+__host__ __device__ __forceinline__ unsigned long long* pcnt_at(const CountParams& p, uint64_t i) {
+    return p.pcounts + (i << p.pinter);
+}
 
 constexpr uint32_t kPairLangBits = 12;  // pair key: (gram slot + 1) << 12 | lang (L <= 4096)
 

@@ -144,11 +144,11 @@ template <bool PRE = false>
 __device__ __forceinline__ int64_t pair_find_or_insert_at(const CountParams& p, uint64_t pk, uint64_t s, uint64_t k0,
                                                           bool& new_pair) {
     for (uint32_t probe = 0; probe < p.max_probe; ++probe) {
-        uint64_t k = (PRE && probe == 0) ? k0 : __hip_atomic_load(&p.pkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t k = (PRE && probe == 0) ? k0 : __hip_atomic_load(pkey_at(p, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == pk) return (int64_t)s;
         if (k == kEmpty) {
             const unsigned long long old =
-                atomicCAS(reinterpret_cast<unsigned long long*>(&p.pkeys[s]), 0ull, (unsigned long long)pk);
+                atomicCAS(reinterpret_cast<unsigned long long*>(pkey_at(p, s)), 0ull, (unsigned long long)pk);
             if (old == 0ull) {
                 new_pair = true;
                 return (int64_t)s;
@@ -177,7 +177,7 @@ __device__ __forceinline__ uint64_t sparse_add_q(const CountParams& p, uint64_t 
     if (g >= 0) {
         s = pair_find_or_insert(p, ((uint64_t)(g + 1) << kPairLangBits) | (uint64_t)lang, new_pair);
         if (s >= 0) {
-            atomicAdd(&p.pcounts[s], c);
+            atomicAdd(pcnt_at(p, s), c);
             if (new_pair) atomicAdd(&p.kcnt[g], 1u);
         }
     }
@@ -412,6 +412,13 @@ __global__ __launch_bounds__(256) void stats_kernel(const CountParams p, uint64_
     __shared__ unsigned long long red[2][4];
     unsigned long long pairs = 0, total = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (p.pkeys) {  // a pair table
+            if (*pkey_at(p, i) == kEmpty) continue;
+            const unsigned long long c = *pcnt_at(p, i);
+            pairs += c != 0ull;
+            total += c;
+            continue;
+        }
         if (p.keys[i] == kEmpty) continue;
         for (int l = 0; l < p.L; ++l) {
             const unsigned long long c = p.counts[i * p.L + l];
@@ -486,16 +493,16 @@ __global__ void pair_rehash_kernel(const CountParams from, const CountParams to,
                                    const uint64_t* remap) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= from_pcap) return;
-    uint64_t pk = from.pkeys[i];
+    uint64_t pk = *pkey_at(from, i);
     if (pk == kEmpty) return;
     if (remap) {
         const uint64_t g = (pk >> kPairLangBits) - 1ull;
         pk = ((remap[g] + 1ull) << kPairLangBits) | (pk & ((1ull << kPairLangBits) - 1ull));
     }
     uint64_t s = fit_hash(pk) >> to.pshift;
-    while (atomicCAS(reinterpret_cast<unsigned long long*>(&to.pkeys[s]), 0ull, (unsigned long long)pk) != 0ull)
+    while (atomicCAS(reinterpret_cast<unsigned long long*>(pkey_at(to, s)), 0ull, (unsigned long long)pk) != 0ull)
         s = (s + 1) & to.pmask;
-    to.pcounts[s] = from.pcounts[i];
+    *pcnt_at(to, s) = *pcnt_at(from, i);
 }
 
 __global__ __launch_bounds__(kScanThreads) void gram_compact_kernel(const CountParams p, uint64_t cap,
@@ -526,13 +533,13 @@ __global__ __launch_bounds__(kScanThreads) void pair_compact_kernel(const CountP
     __shared__ unsigned long long bbase;
     for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < pcap; c0 += (uint64_t)gridDim.x * kScanThreads) {
         const uint64_t i = c0 + threadIdx.x;
-        const uint64_t pk = i < pcap ? p.pkeys[i] : kEmpty;
+        const uint64_t pk = i < pcap ? *pkey_at(p, i) : kEmpty;
         const bool occ = pk != kEmpty;
         const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
         if (!occ) continue;
         const uint64_t g = (pk >> kPairLangBits) - 1ull;
         out_pk[o] = ((uint64_t)rank_of[g] << kPairLangBits) | (pk & ((1ull << kPairLangBits) - 1ull));
-        out_cnt[o] = p.pcounts[i];
+        out_cnt[o] = *pcnt_at(p, i);
     }
 }
 
@@ -540,10 +547,10 @@ __global__ void pair_dense_kernel(const CountParams p, uint64_t pcap, const uint
                                   unsigned long long* rows) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= pcap) return;
-    const uint64_t pk = p.pkeys[i];
+    const uint64_t pk = *pkey_at(p, i);
     if (pk == kEmpty) return;
     const uint64_t g = (pk >> kPairLangBits) - 1ull;
-    rows[(uint64_t)rank_of[g] * p.L + (pk & ((1ull << kPairLangBits) - 1ull))] = p.pcounts[i];
+    rows[(uint64_t)rank_of[g] * p.L + (pk & ((1ull << kPairLangBits) - 1ull))] = *pcnt_at(p, i);
 }
 
 __global__ __launch_bounds__(256) void nnz_kernel(const unsigned long long* v, int64_t n, unsigned long long* out) {
@@ -748,7 +755,7 @@ __global__ __launch_bounds__(kScanThreads) void pair_hist_kernel(const CountPara
     for (int i = threadIdx.x; i < L * kw; i += blockDim.x) lh[i] = 0u;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pcap; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t pk = p.pkeys[i];
+        const uint64_t pk = *pkey_at(p, i);
         if (pk == kEmpty) continue;
         const uint32_t l = pair_lang(pk);
         const int k = (int)p.kcnt[pair_slot(pk)];
@@ -783,7 +790,7 @@ __global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountPa
     }
     for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < pcap; c0 += (uint64_t)gridDim.x * kScanThreads) {
         const uint64_t i = c0 + threadIdx.x;
-        const uint64_t pk = i < pcap ? p.pkeys[i] : kEmpty;
+        const uint64_t pk = i < pcap ? *pkey_at(p, i) : kEmpty;
         bool cand = false;
         uint32_t l = 0, j = 0;
         if (pk != kEmpty) {
@@ -867,7 +874,7 @@ __global__ void pair_masks_kernel(const CountParams p, uint64_t pcap, const uint
                                   int S, uint64_t* masks) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= pcap) return;
-    const uint64_t pk = p.pkeys[i];
+    const uint64_t pk = *pkey_at(p, i);
     if (pk == kEmpty) return;
     const uint32_t l = pair_lang(pk);
     uint32_t r = rowof[pair_slot(pk)];
@@ -926,7 +933,7 @@ __device__ __forceinline__ uint64_t pair_gram(const CountParams& p, uint64_t pk)
 __global__ void owner_pair_count_kernel(const CountParams p, uint64_t cap, uint32_t world, unsigned long long* n_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p.pkeys) {
-        if (i < cap && p.pkeys[i] != kEmpty) atomicAdd(&n_of[owner_of(pair_gram(p, p.pkeys[i]), world)], 1ull);
+        if (i < cap && *pkey_at(p, i) != kEmpty) atomicAdd(&n_of[owner_of(pair_gram(p, *pkey_at(p, i)), world)], 1ull);
         return;
     }
     if (i >= cap || p.keys[i] == kEmpty) return;
@@ -939,11 +946,11 @@ __global__ void owner_pair_scatter_kernel(const CountParams p, uint64_t cap, uin
                                           uint64_t* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p.pkeys) {
-        if (i >= cap || p.pkeys[i] == kEmpty) return;
-        const uint64_t pk = p.pkeys[i], key = pair_gram(p, pk);
+        if (i >= cap || *pkey_at(p, i) == kEmpty) return;
+        const uint64_t pk = *pkey_at(p, i), key = pair_gram(p, pk);
         const unsigned long long o = atomicAdd(&cursor[owner_of(key, world)], 1ull);
         out[2 * o] = key;
-        out[2 * o + 1] = ((pk & ((1ull << kPairLangBits) - 1ull)) << kPairCntBits) | p.pcounts[i];
+        out[2 * o + 1] = ((pk & ((1ull << kPairLangBits) - 1ull)) << kPairCntBits) | *pcnt_at(p, i);
         return;
     }
     if (i >= cap || p.keys[i] == kEmpty) return;
@@ -2372,7 +2379,7 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
                 for (int u = 0; u < kDU; ++u) {
                     pp[u] = ((uint64_t)(g[u] + 1) << kPairLangBits) | (uint64_t)lang[u];
                     pa[u] = fit_hash(pp[u]) >> to.pshift;
-                    pv[u] = g[u] >= 0 ? __hip_atomic_load(&to.pkeys[pa[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    pv[u] = g[u] >= 0 ? __hip_atomic_load(pkey_at(to, pa[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                       : 0ull;
                 }
 #pragma unroll
@@ -2384,7 +2391,7 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
                     if (g[u] >= 0) {
                         sp = pair_find_or_insert_at<true>(to, pp[u], pa[u], pv[u], np);
                         if (sp >= 0) {
-                            atomicAdd(&to.pcounts[sp], cm);
+                            atomicAdd(pcnt_at(to, sp), cm);
                             if (np) atomicAdd(&to.kcnt[g[u]], 1u);
                         }
                     }
