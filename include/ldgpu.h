@@ -144,7 +144,9 @@ int ldgpu_model_langs(const ldgpu_model* model, int32_t* n_langs);
  * languages of argmax(scores of d): first maximum, all-zero -> 0.  Chunks of
  * documents are pipelined over two streams (copy-in / score / copy-out of one
  * chunk overlap the host staging of the next); buffers from ldgpu_host_alloc
- * are copied from / to directly, pageable ones through pinned staging. */
+ * are copied from / to directly, pageable ones through pinned staging.  (This
+ * pipeline scores class-mode tables on the ordered replay path, which never
+ * waits for the GPU between chunks; see ldgpu_score_device.) */
 int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets,
                 int64_t n_docs, int32_t* out_labels, double* out_scores);
 

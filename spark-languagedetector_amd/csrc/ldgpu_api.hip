@@ -1543,7 +1543,7 @@ int class_replay(ldgpu_model* m, const ScoreParams& p4, hipStream_t st) {
 
 int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
                  int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st, double* d_best = nullptr,
-                 int block = 0, int64_t score_stride = 0) {
+                 int block = 0, int64_t score_stride = 0, bool allow_classes = true) {
     if (n_docs == 0) return LDGPU_OK;
     if (m->general) {
         GenScoreParams g{};
@@ -1641,7 +1641,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.nG = m->nG;
     for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
     // class mode: labels only, on a table of at most class_max(S) values
-    const bool classes = m->n_cls > 0 && !d_scores && !d_best && m->mode == 1;
+    const bool classes = allow_classes && m->n_cls > 0 && !d_scores && !d_best && m->mode == 1;
     const int mode = classes ? 4 : m->mode;
     if (classes) {
         for (int q = 0; q < 4; ++q) p.cls[q] = m->cls[q];
@@ -1761,9 +1761,13 @@ int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_
         }
         if (nb) HIP_TRY(hipMemcpyAsync(st.bytes.p, src, nb, hipMemcpyHostToDevice, st.stream));
         HIP_TRY(hipMemcpyAsync(st.offsets.p, ho, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, st.stream));
+        // (no class mode here: its replay step reads counts back from the
+        // stream, which would serialise this pipeline's host staging with the
+        // GPU; the ordered replay is asynchronous, and the host path is bound
+        // by PCIe and staging, not by the kernel)
         if (int r = score_launch(m, (const uint8_t*)st.bytes.p, nb, (const int64_t*)st.offsets.p, nd,
                                  (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, pp->d_err,
-                                 st.stream))
+                                 st.stream, nullptr, 0, 0, false))
             return r;
         int32_t* lab_dst = out_labels + d0;
         double* sc_dst = out_scores ? out_scores + d0 * m->L : nullptr;

@@ -4,7 +4,8 @@ LanguageDetector.scala:98-105).  The kernel counts hits per (value, language),
 labels a document from the counts when a rounding bound separates its top
 language from every other, and replays the rest in reference order
 (LanguageDetectorModel.scala:139-154).  Labels must equal the oracle's exactly,
-ties and near ties included; scores calls keep the ordered replay."""
+ties and near ties included; scores calls keep the ordered replay, and so
+does the host-buffer pipeline (ldgpu_score), which stays asynchronous."""
 import math
 
 import numpy as np
@@ -37,6 +38,21 @@ def oracle_labels(table, L, grams, data, off):
     return OC.Table(table, L).score(grams, data, off, want_scores=False, nthreads=8)[0]
 
 
+def labels_device(m, data, off):
+    """Labels-only scoring through ldgpu_score_device -- the path that takes
+    class mode (the host pipeline, ldgpu_score, keeps the asynchronous ordered
+    replay)."""
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
+    n = len(off) - 1
+    d_lab = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    m.score_device(d_bytes.data_ptr(), len(data), d_off.data_ptr(), n, d_lab.data_ptr(), 0,
+                   torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    return d_lab.cpu().numpy()
+
+
 def docs_of(rng, n, hi):
     lens = rng.integers(0, hi, size=n)
     lens[:6] = [0, 1, 2, 3, 7, 64]
@@ -65,8 +81,10 @@ def test_class_mode_labels_match_oracle(L, grams, n_cls, monkeypatch):
         variant = "diag"
     m = DeviceModel(table, L, grams, variant=variant)
     assert "classes" in m.info()["layout"], m.info()
-    labels, _ = m.score(data, off)
-    assert np.array_equal(labels, oracle_labels(table, L, grams, data, off))
+    ol = oracle_labels(table, L, grams, data, off)
+    assert np.array_equal(labels_device(m, data, off), ol)
+    labels, _ = m.score(data, off)  # the host pipeline (ordered replay)
+    assert np.array_equal(labels, ol)
     # a scores call keeps the ordered replay: same labels, scores bit-exact
     lab2, sc = m.score(data, off, want_scores=True)
     ol, os_ = OC.Table(table, L).score(grams, data, off, want_scores=True, nthreads=8)
@@ -90,7 +108,7 @@ def test_class_mode_order_dependent_ties():
     data, off = encoding.pack(docs)
     m = DeviceModel(table, 3, [1, 2])
     assert "classes" in m.info()["layout"]
-    labels, _ = m.score(data, off)
+    labels = labels_device(m, data, off)
     ol = oracle_labels(table, 3, [1, 2], data, off)
     assert np.array_equal(labels, ol), np.nonzero(labels != ol)[0][:10]
     # the hand-made pair really is decided by order: labels differ between them
@@ -124,8 +142,7 @@ def test_too_many_values_keep_the_ordered_replay():
     data, off = docs_of(rng, 500, 150)
     m = DeviceModel(table, 20, [1, 2, 3])
     assert "classes" not in m.info()["layout"]
-    labels, _ = m.score(data, off)
-    assert np.array_equal(labels, oracle_labels(table, 20, [1, 2, 3], data, off))
+    assert np.array_equal(labels_device(m, data, off), oracle_labels(table, 20, [1, 2, 3], data, off))
 
 
 def test_class_mode_switched_off_in_diag_library(monkeypatch):
@@ -138,9 +155,7 @@ def test_class_mode_switched_off_in_diag_library(monkeypatch):
     monkeypatch.setenv("LDGPU_NO_CLASS_MODE", "1")
     b = DeviceModel(table, 20, [1, 2, 3, 4, 5], variant="diag")
     assert "classes" in a.info()["layout"] and "classes" not in b.info()["layout"]
-    la, _ = a.score(data, off)
-    lb, _ = b.score(data, off)
-    assert np.array_equal(la, lb)
+    assert np.array_equal(labels_device(a, data, off), labels_device(b, data, off))
 
 
 @pytest.mark.parametrize("L,n_cls", [(20, 2), (63, 1), (40, 3)])
@@ -173,8 +188,7 @@ def test_class_mode_direct_tables(L, n_cls, monkeypatch):
     m = DeviceModel(table, L, [1, 2, 3, 4, 5], variant=variant)
     lay = m.info()["layout"]
     assert "classes" in lay and "direct" in lay, lay
-    labels, _ = m.score(data, off)
-    assert np.array_equal(labels, oracle_labels(table, L, [1, 2, 3, 4, 5], data, off))
+    assert np.array_equal(labels_device(m, data, off), oracle_labels(table, L, [1, 2, 3, 4, 5], data, off))
     lab2, sc = m.score(data[:int(off[500])], off[:501], want_scores=True)
     ol, os_ = OC.Table(table, L).score([1, 2, 3, 4, 5], data[:int(off[500])], off[:501], want_scores=True, nthreads=8)
     assert np.array_equal(lab2, ol)
