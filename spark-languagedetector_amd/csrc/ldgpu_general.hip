@@ -18,7 +18,10 @@
 // LDS.  A mask-form row adds v at its set languages (adding 0.0 elsewhere is
 // exact: a score is never -0.0).  This path favours generality over speed:
 // tables with every gram length <= 15 take the LDS-filtered kernels of
-// ldgpu_score.hip.
+// ldgpu_score.hip.  A document of up to kGenBuf bytes is first copied into the
+// wave's LDS buffer: a window's hash then reads its bytes from LDS -- up to 12
+// bytes as three byte-aligned words, the FNV steps unrolled in registers --
+// instead of one dependent global load per byte.
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
@@ -45,6 +48,45 @@ __device__ __forceinline__ int64_t gen_lookup(const GenScoreParams& p, const uin
     }
 }
 
+constexpr int kGenBuf = 4096;  // staged document bytes per wave (+ 64 B of read slack)
+
+__device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint32_t byte) { return (h ^ byte) * 1099511628211ull; }
+
+// gen_hash (ldgpu_common.h) of the klen-byte window at byte pos of the
+// wave's staged document
+__device__ __forceinline__ uint64_t gen_hash_staged(const uint8_t* buf, uint32_t pos, int64_t klen) {
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)klen;
+    if (klen <= 12) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(buf) + (pos >> 2);
+        const uint32_t sh = pos & 3u;
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+        const uint32_t x[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               __builtin_amdgcn_alignbyte(w3, w2, sh)};
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+            if (i < klen) h = fnv_step(h, (x[i >> 2] >> (8 * (i & 3))) & 0xffu);
+    } else {
+        for (int64_t i = 0; i < klen; ++i) h = fnv_step(h, buf[pos + i]);
+    }
+    return mix64(h);
+}
+
+// gen_lookup of a window of the staged document
+__device__ __forceinline__ int64_t gen_lookup_staged(const GenScoreParams& p, const uint8_t* buf, uint32_t pos,
+                                                     int64_t klen) {
+    const uint64_t h = gen_hash_staged(buf, pos, klen);
+    uint64_t s = h >> p.slot_shift;
+    for (;;) {
+        const GenSlot e = p.slots[s];
+        if (e.len == 0) return -1;
+        if (e.h == h && e.len == (uint32_t)klen) {
+            const uint32_t r = e.row & ~kBadRow;
+            if (key_equal(buf + pos, p.arena + p.koff[r], klen)) return (int64_t)e.row;
+        }
+        s = (s + 1) & p.slot_mask;
+    }
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -59,6 +101,7 @@ __global__ __launch_bounds__(kGenWaves * 64) void general_score_kernel(const Gen
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     double* acc = gen_acc + (size_t)wave * p.L;
+    uint8_t* const buf = reinterpret_cast<uint8_t*>(gen_acc + (size_t)kGenWaves * p.L) + wave * (kGenBuf + 64);
     const int S = (p.L + 63) / 64;
     const int64_t stride = (int64_t)gridDim.x * kGenWaves;
     for (int64_t doc = (int64_t)blockIdx.x * kGenWaves + wave; doc < p.n_docs; doc += stride) {
@@ -66,13 +109,21 @@ __global__ __launch_bounds__(kGenWaves * 64) void general_score_kernel(const Gen
         const int64_t b = p.offsets[doc];
         const int64_t len = p.offsets[doc + 1] - b;
         const uint8_t* d = p.bytes + b;
+        const bool staged = len <= kGenBuf;
+        if (staged) {  // the document into the wave's buffer (LDS ops of a wave complete in order)
+            __builtin_amdgcn_wave_barrier();
+            for (int64_t i = lane; i < len; i += 64) buf[i] = d[i];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
         for (int gi = 0; gi < p.nG; ++gi) {
             const int64_t n = p.G[gi];
             const int64_t nw = n_windows(len, (int)(n > 0x7fffffff ? 0x7fffffff : n));
             const int64_t klen = len < n ? len : n;
             for (int64_t p0 = 0; p0 < nw; p0 += 64) {
                 const int64_t pos = p0 + lane;
-                const int64_t row = pos < nw ? gen_lookup(p, d + pos, klen) : -1;
+                const int64_t row = pos >= nw ? -1
+                                    : (staged ? gen_lookup_staged(p, buf, (uint32_t)pos, klen) : gen_lookup(p, d + pos, klen));
                 uint64_t hits = __ballot(row >= 0);
                 while (hits) {  // in window order
                     const int j = __builtin_ctzll(hits);
@@ -119,12 +170,12 @@ __global__ __launch_bounds__(kGenWaves * 64) void general_score_kernel(const Gen
 }  // namespace
 
 hipError_t launch_general_score(const GenScoreParams& p, int grid, hipStream_t stream) {
-    const size_t lds = sizeof(double) * kGenWaves * p.L;  // <= 64 KiB (L <= 4096)
+    // scores (<= 64 KiB: L <= 4096) and the staged documents
+    const size_t lds = sizeof(double) * kGenWaves * p.L + (size_t)kGenWaves * (kGenBuf + 64);
     hipError_t e = hipFuncSetAttribute((const void*)&general_score_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(general_score_kernel, dim3(grid), dim3(kGenWaves * 64), sizeof(double) * kGenWaves * p.L,
-                       stream, p);
+    hipLaunchKernelGGL(general_score_kernel, dim3(grid), dim3(kGenWaves * 64), lds, stream, p);
     return hipGetLastError();
 }
 
