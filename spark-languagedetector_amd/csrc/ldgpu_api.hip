@@ -1505,6 +1505,10 @@ int class_replay(ldgpu_model* m, const ScoreParams& p4, hipStream_t st) {
     if (e == hipSuccess) e = launch_amb_compact(p4.labels, n, idx, d_k, st);
     if (e == hipSuccess) e = hipMemcpyAsync(&k, d_k, sizeof k, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && k >= (unsigned long long)std::numeric_limits<int>::max()) {
+        for (void* q : {(void*)idx}) (void)hipFreeAsync(q, st);
+        return fail(LDGPU_EUNSUPPORTED, "class mode: %llu ambiguous documents in one call (the scan takes < 2^31)", k);
+    }
     if (e == hipSuccess && k > 0) {
         const int64_t kk = (int64_t)k;
         e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, nullptr, nullptr, nullptr, &scan_bytes, nullptr, st);
