@@ -155,10 +155,9 @@ int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets
  * d_bytes must be 4-byte aligned and n_bytes >= d_offsets[n_docs].
  * d_scores is nullable.  Offsets are trusted (validate with the host API);
  * documents must be shorter than 2^28 bytes (the host API checks this).
- * Exception to the asynchrony: a labels-only call (d_scores NULL) on a model
- * in class mode (LDGPU_LAYOUT_CLASSES) reads two counts back from `stream`
- * (the documents its rounding bound left ambiguous, and their bytes) to size
- * their exact replay, so it returns once the stream has reached that point. */
+ * A labels-only call (d_scores NULL) on a model in class mode
+ * (LDGPU_LAYOUT_CLASSES) replays the documents its rounding bound left
+ * ambiguous on the same stream, sized on the device: it is asynchronous too. */
 int ldgpu_score_device(ldgpu_model* model, const uint8_t* d_bytes, int64_t n_bytes,
                        const int64_t* d_offsets, int64_t n_docs, int32_t* d_labels,
                        double* d_scores, void* stream);

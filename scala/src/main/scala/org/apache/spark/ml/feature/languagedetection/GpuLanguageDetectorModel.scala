@@ -137,8 +137,11 @@ object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
   /**
     * detect(Array[Byte], ...) (LanguageDetectorModel.scala:131-156): one
     * document.  The reference's callers put detect in a UDF, calling it per
-    * row with the same map, so the device table of a map is kept: a Scala Map
-    * is immutable, so the same object (eq) is the same table.  The last
+    * row with the same map, so the device table of a map is kept.  The
+    * reference reads the map on every call, and a Map's Array[Double] values
+    * can be edited in place, so a kept table serves a call only while the
+    * map is the same object (eq) AND its rows equal (bitwise) a copy taken
+    * when the table was built (unchanged: one Arrays.equals per row).  The last
     * `detectCacheSize` tables stay resident (reference-counted: an evicted
     * table is destroyed once no call is scoring with it); each thread keeps
     * its own direct buffers.  For many documents, transform scores in
@@ -162,7 +165,8 @@ object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
 
   var detectCacheSize: Int = 4
 
-  private final class DetectEntry(val map: AnyRef, val grams: Seq[Int], val nLangs: Int, val model: Long) {
+  private final class DetectEntry(val map: AnyRef, val snapshot: Map[Seq[Byte], Array[Double]], val grams: Seq[Int],
+                                   val nLangs: Int, val model: Long) {
     var refs = 0
     var evicted = false
   }
@@ -173,13 +177,13 @@ object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
       val it = detectCache.iterator()
       while (it.hasNext) {
         val e = it.next()
-        if ((e.map eq map) && e.nLangs == nLangs && e.grams == grams) {
+        if ((e.map eq map) && e.nLangs == nLangs && e.grams == grams && unchanged(map, e.snapshot)) {
           e.refs += 1
           return e
         }
       }
       val model = PackedTable.of(map, nLangs).upload(LdgpuNative.context(), grams.toArray)
-      val e = new DetectEntry(map, grams.toList, nLangs, model)
+      val e = new DetectEntry(map, map.map { case (k, v) => (k, v.clone()) }, grams.toList, nLangs, model)
       e.refs = 1
       detectCache.addFirst(e)
       while (detectCache.size > math.max(1, detectCacheSize)) {
@@ -188,6 +192,15 @@ object LanguageDetectorModel extends MLReadable[LanguageDetectorModel] {
         if (old.refs == 0) LdgpuNative.modelDestroy(old.model)
       }
       e
+    }
+
+  /** every row of map equals (bitwise, java.util.Arrays.equals) the snapshot's */
+  private def unchanged(map: Map[Seq[Byte], Array[Double]], snap: Map[Seq[Byte], Array[Double]]): Boolean =
+    map.size == snap.size && map.forall { case (k, v) =>
+      snap.get(k) match {
+        case Some(w) => java.util.Arrays.equals(v, w)
+        case None => false
+      }
     }
 
   private def detectRelease(e: DetectEntry): Unit = detectCache.synchronized {

@@ -506,6 +506,15 @@ struct ldgpu_model {
     uint64_t gslot_cap = 0;
     uint8_t* d_arena = nullptr;
     int64_t* d_koff = nullptr;
+    // mixed tables (general, and some gram length <= 15): the model of the
+    // keys of <= 15 bytes over those lengths (nullptr: every length is long),
+    // the long lengths and the long keys' prefilter bitmap (long_bits)
+    ldgpu_model* short_m = nullptr;
+    int n_long = 0;
+    int32_t Glong[kMaxGramLengths] = {};
+    int32_t max_long = 0;
+    uint32_t* d_lbits = nullptr;
+    uint32_t lbits_log2 = 0;
     // L > kBlockLangs: one sub-model per block of kBlockLangs languages
     // (model_build_blocked); this model then holds no table of its own
     std::vector<ldgpu_model*> blocks;
@@ -518,6 +527,7 @@ namespace {
 void model_free(ldgpu_model* m) {
     if (!m) return;
     for (ldgpu_model* b : m->blocks) model_free(b);
+    model_free(m->short_m);
     if (m->ctx) (void)hipSetDevice(m->ctx->device);
     if (m->d_stats) {
         unsigned long long st[2] = {0, 0};
@@ -526,7 +536,8 @@ void model_free(ldgpu_model* m) {
         (void)hipFree(m->d_stats);
     }
     for (void* p : {(void*)m->d_slots, (void*)m->d_wslots, (void*)m->d_buckets, (void*)m->d_filter, (void*)m->d_masks, (void*)m->d_vals, (void*)m->d_rows,
-                    (void*)m->d_fold, (void*)m->d_err, (void*)m->d_gslots, (void*)m->d_arena, (void*)m->d_koff})
+                    (void*)m->d_fold, (void*)m->d_err, (void*)m->d_gslots, (void*)m->d_arena, (void*)m->d_koff,
+                    (void*)m->d_lbits})
         if (p) (void)hipFree(p);
     delete m;
 }
@@ -680,6 +691,15 @@ bool bucket_place(const std::vector<uint64_t>& keys, const std::vector<uint64_t>
 }
 }  // namespace
 
+extern "C" int ldgpu_model_create(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                                  const int64_t* key_offsets, const double* rows, const uint8_t* row_ok,
+                                  int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                                  ldgpu_model** out);
+extern "C" int ldgpu_model_create_masks(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_bytes,
+                                        const int64_t* key_offsets, const uint64_t* masks, const double* vals,
+                                        int32_t n_langs, const int32_t* gram_lengths, int32_t n_grams,
+                                        ldgpu_model** out);
+
 namespace {
 // A model with a gram length beyond kMaxWideGram (ldgpu_general.hip): every
 // key of 1..max(G) bytes (longer keys can never be hit) in one GenSlot table
@@ -800,9 +820,53 @@ int model_create_general(ldgpu_ctx* ctx, int64_t n_rows, const uint8_t* key_byte
     if (e == hipSuccess && !dense) e = upload(&m->d_masks, mk, &m->device_bytes);
     if (e == hipSuccess && !dense) e = upload(&m->d_vals, vv, &m->device_bytes);
     if (e == hipSuccess) e = upload(&m->d_err, std::vector<int32_t>{0}, &m->device_bytes);
+    // mixed table: the long lengths (distinct), the prefilter bitmap of the
+    // keys a full window of one of them can equal (2 bits per key, ~32 bits
+    // per key: ~0.4 % of windows pass), and the short lengths' model
+    std::vector<int32_t> gshort;
+    for (int i = 0; i < n_grams; ++i) {
+        const int32_t n = gram_lengths[i];
+        if (n <= kMaxWideGram) {
+            gshort.push_back(n);
+            continue;
+        }
+        m->max_long = std::max(m->max_long, n);
+        if (std::find(m->Glong, m->Glong + m->n_long, n) == m->Glong + m->n_long) m->Glong[m->n_long++] = n;
+    }
+    if (e == hipSuccess) {
+        auto is_long = [&](int64_t len) { return std::find(m->Glong, m->Glong + m->n_long, (int32_t)len) != m->Glong + m->n_long; };
+        int64_t nl = 0;
+        for (int64_t i = 0; i < nk; ++i) nl += is_long(koff[i + 1] - koff[i]);
+        uint32_t lb = 12;
+        while (lb < 19 && ((uint64_t)1 << lb) < 32ull * (uint64_t)nl) ++lb;
+        m->lbits_log2 = lb;
+        std::vector<uint32_t> bits((size_t)1 << (lb - 5), 0u);
+        for (int64_t i = 0; i < nk; ++i) {
+            const int64_t len = koff[i + 1] - koff[i];
+            if (!is_long(len)) continue;
+            uint32_t w[2] = {0u, 0u};
+            memcpy(w, arena.data() + koff[i], 8);
+            uint32_t b1, b2;
+            long_bits(w[0], w[1], (uint32_t)len, lb, b1, b2);
+            bits[b1 >> 5] |= 1u << (b1 & 31);
+            bits[b2 >> 5] |= 1u << (b2 & 31);
+        }
+        e = upload(&m->d_lbits, bits, &m->device_bytes);
+    }
     if (e != hipSuccess) {
         model_free(m);
         return fail(LDGPU_ENOMEM, "model upload: %s", hipGetErrorString(e));
+    }
+    if (!gshort.empty()) {
+        const int rc = rows ? ldgpu_model_create(ctx, n_rows, key_bytes, key_offsets, rows, row_ok, n_langs,
+                                                 gshort.data(), (int32_t)gshort.size(), &m->short_m)
+                            : ldgpu_model_create_masks(ctx, n_rows, key_bytes, key_offsets, masks, vals, n_langs,
+                                                       gshort.data(), (int32_t)gshort.size(), &m->short_m);
+        if (rc) {
+            model_free(m);
+            return rc;
+        }
+        m->device_bytes += m->short_m->device_bytes;
     }
     *out = m;
     return ok();
@@ -1454,7 +1518,14 @@ extern "C" int ldgpu_model_layout(const ldgpu_model* m, int32_t* flags) {
     if (b->pack_ok) f |= LDGPU_LAYOUT_PACKS;
     if (b->n_cls && m->blocks.empty()) f |= LDGPU_LAYOUT_CLASSES;
     if (!m->blocks.empty()) f |= LDGPU_LAYOUT_LANG_BLOCKS;
-    if (m->general) f = LDGPU_LAYOUT_GENERAL_KEYS;
+    if (m->general) {  // (a mixed table: its short lengths' model's layout too)
+        f = LDGPU_LAYOUT_GENERAL_KEYS;
+        if (m->short_m) {
+            int32_t fs = 0;
+            if (int rc = ldgpu_model_layout(m->short_m, &fs)) return rc;
+            f |= fs;
+        }
+    }
     *flags = f;
     return ok();
 }
@@ -1485,72 +1556,77 @@ int score_grid(const ldgpu_model* m, int64_t n_docs) {
 }
 
 // class mode's second step: the documents class_label left ambiguous (-1)
-// gathered into a packed sub-corpus, scored by the ordered replay (mode 1,
-// the reference's fold bit for bit) and their labels put back.  Reads back
-// two counts (ambiguous documents, their bytes): the sub-corpus is sized by
-// them, not by the batch.
+// listed (amb_compact, their count written on the device) and scored in place
+// by an indirect launch of the ordered replay (mode 1, the reference's fold bit
+// for bit), which reads that count itself: nothing is read back, so the call
+// stays asynchronous on its stream.  The list is stream-ordered scratch of the
+// worst case (every document ambiguous).
 int class_replay(ldgpu_model* m, const ScoreParams& p4, hipStream_t st) {
     const int64_t n = p4.n_docs;
     int64_t* idx = nullptr;
     HIP_TRY(hipMallocAsync((void**)&idx, sizeof(int64_t) * (size_t)(n + 1), st));
     unsigned long long* d_k = (unsigned long long*)(idx + n);
-    int64_t *sub_off = nullptr, *len_tmp = nullptr;
-    void* scan_tmp = nullptr;
-    uint8_t* sub = nullptr;
-    int32_t* sub_lab = nullptr;
-    unsigned long long k = 0;
-    int64_t total = 0;
-    size_t scan_bytes = 0;
     hipError_t e = hipMemsetAsync(d_k, 0, sizeof *d_k, st);
     if (e == hipSuccess) e = launch_amb_compact(p4.labels, n, idx, d_k, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(&k, d_k, sizeof k, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e == hipSuccess && k >= (unsigned long long)std::numeric_limits<int>::max()) {
-        for (void* q : {(void*)idx}) (void)hipFreeAsync(q, st);
-        return fail(LDGPU_EUNSUPPORTED, "class mode: %llu ambiguous documents in one call (the scan takes < 2^31)", k);
+    if (e == hipSuccess) {
+        ScoreParams p1 = p4;
+        p1.doc_idx = idx;
+        p1.n_docs_dev = d_k;
+        p1.n_cls = 0;
+        p1.hit_words = 0;
+        p1.direct_words = 0;
+        gram_lists(m, p1, 1);
+        e = launch_score(p1, m->slices, 1, m->lds_filter, score_grid(m, n), st);
     }
-    if (e == hipSuccess && k > 0) {
-        const int64_t kk = (int64_t)k;
-        e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, nullptr, nullptr, nullptr, &scan_bytes, nullptr, st);
-        if (e == hipSuccess) e = hipMallocAsync((void**)&sub_off, sizeof(int64_t) * (size_t)(2 * kk + 2), st);
-        if (e == hipSuccess) e = hipMallocAsync(&scan_tmp, std::max<size_t>(scan_bytes, 16), st);
-        len_tmp = sub_off + kk + 1;
-        if (e == hipSuccess)
-            e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, sub_off, len_tmp, scan_tmp, &scan_bytes, nullptr, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(&total, sub_off + kk, sizeof total, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e == hipSuccess) e = hipMallocAsync((void**)&sub, (size_t)total + 16, st);
-        if (e == hipSuccess) e = hipMallocAsync((void**)&sub_lab, sizeof(int32_t) * (size_t)kk, st);
-        if (e == hipSuccess)
-            e = amb_sub_corpus(idx, kk, p4.offsets, p4.bytes, sub_off, len_tmp, scan_tmp, &scan_bytes, sub, st);
-        if (e == hipSuccess) {
-            ScoreParams p1 = p4;
-            p1.bytes = sub;
-            p1.n_bytes = total;
-            p1.last_dword = total > 0 ? (total - 1) >> 2 : 0;
-            p1.offsets = sub_off;
-            p1.n_docs = kk;
-            p1.labels = sub_lab;
-            p1.n_cls = 0;
-            p1.hit_words = 0;
-            p1.direct_words = 0;
-            gram_lists(m, p1, 1);
-            e = launch_score(p1, m->slices, 1, m->lds_filter, score_grid(m, kk), st);
-        }
-        if (e == hipSuccess) e = launch_amb_scatter(idx, kk, sub_lab, p4.labels, st);
-    }
-    for (void* q : {(void*)sub_lab, (void*)sub, scan_tmp, (void*)sub_off, (void*)idx})
-        if (q) (void)hipFreeAsync(q, st);
+    (void)hipFreeAsync(idx, st);
     HIP_TRY(e);
     return LDGPU_OK;
 }
 
 int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_offsets, int64_t n_docs,
                  int32_t* d_labels, double* d_scores, int32_t* d_err, hipStream_t st, double* d_best = nullptr,
-                 int block = 0, int64_t score_stride = 0, bool allow_classes = true) {
+                 int block = 0, int64_t score_stride = 0) {
     if (n_docs == 0) return LDGPU_OK;
     if (m->general) {
+        // mixed table: the short lengths on the LDS-filtered kernels (or, with
+        // none, label 0 and zero scores: the reference's result without a
+        // hit), then the documents a long length hits rescored exactly
+        int64_t* idx = nullptr;
+        if (m->n_long > 0) {
+            if (m->short_m) {
+                if (int rc = score_launch(m->short_m, d_bytes, n_bytes, d_offsets, n_docs, d_labels, d_scores, d_err, st))
+                    return rc;
+            } else {
+                HIP_TRY(hipMemsetAsync(d_labels, 0, sizeof(int32_t) * (size_t)n_docs, st));
+                if (d_scores) HIP_TRY(hipMemsetAsync(d_scores, 0, sizeof(double) * (size_t)n_docs * m->L, st));
+            }
+            HIP_TRY(hipMallocAsync((void**)&idx, sizeof(int64_t) * (size_t)(n_docs + 1), st));
+            LongFlagParams f{};
+            f.bytes = d_bytes;
+            f.offsets = d_offsets;
+            f.n_docs = n_docs;
+            f.bitmap = m->d_lbits;
+            f.lb = m->lbits_log2;
+            f.n_long = m->n_long;
+            for (int i = 0; i < m->n_long; ++i) f.Glong[i] = m->Glong[i];
+            f.max_long = m->max_long;
+            f.slots = m->d_gslots;
+            f.slot_mask = m->gslot_cap - 1;
+            f.slot_shift = (uint32_t)(64 - log2u(m->gslot_cap));
+            f.arena = m->d_arena;
+            f.koff = m->d_koff;
+            f.idx = idx;
+            f.n_out = (unsigned long long*)(idx + n_docs);
+            hipError_t e = hipMemsetAsync(f.n_out, 0, sizeof(unsigned long long), st);
+            if (e == hipSuccess) e = launch_long_flag(f, m->ctx->cus, st);
+            if (e != hipSuccess) {
+                (void)hipFreeAsync(idx, st);
+                HIP_TRY(e);
+            }
+        }
         GenScoreParams g{};
+        g.doc_idx = idx;
+        g.n_docs_dev = idx ? (const unsigned long long*)(idx + n_docs) : nullptr;
         g.bytes = d_bytes;
         g.offsets = d_offsets;
         g.n_docs = n_docs;
@@ -1570,7 +1646,9 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
         for (int i = 0; i < m->nG; ++i) g.G[i] = m->G[i];
         const int64_t want = (n_docs + kGenWaves - 1) / kGenWaves;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)m->ctx->cus * 8));
-        HIP_TRY(launch_general_score(g, grid, st));
+        const hipError_t e = launch_general_score(g, grid, st);
+        if (idx) (void)hipFreeAsync(idx, st);
+        HIP_TRY(e);
         return LDGPU_OK;
     }
     if (!m->blocks.empty()) {
@@ -1645,7 +1723,7 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     p.nG = m->nG;
     for (int i = 0; i < m->nG; ++i) p.G[i] = m->G[i];
     // class mode: labels only, on a table of at most class_max(S) values
-    const bool classes = allow_classes && m->n_cls > 0 && !d_scores && !d_best && m->mode == 1;
+    const bool classes = m->n_cls > 0 && !d_scores && !d_best && m->mode == 1;
     const int mode = classes ? 4 : m->mode;
     if (classes) {
         for (int q = 0; q < 4; ++q) p.cls[q] = m->cls[q];
@@ -1765,13 +1843,11 @@ int score_host(ldgpu_model* m, ScorePipe* pp, const uint8_t* bytes, const int64_
         }
         if (nb) HIP_TRY(hipMemcpyAsync(st.bytes.p, src, nb, hipMemcpyHostToDevice, st.stream));
         HIP_TRY(hipMemcpyAsync(st.offsets.p, ho, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, st.stream));
-        // (no class mode here: its replay step reads counts back from the
-        // stream, which would serialise this pipeline's host staging with the
-        // GPU; the ordered replay is asynchronous, and the host path is bound
-        // by PCIe and staging, not by the kernel)
+        // (class mode included: its replay of ambiguous documents reads no
+        // count back, so the staging of the next chunk still overlaps)
         if (int r = score_launch(m, (const uint8_t*)st.bytes.p, nb, (const int64_t*)st.offsets.p, nd,
                                  (int32_t*)st.labels.p, out_scores ? (double*)st.scores.p : nullptr, pp->d_err,
-                                 st.stream, nullptr, 0, 0, false))
+                                 st.stream))
             return r;
         int32_t* lab_dst = out_labels + d0;
         double* sc_dst = out_scores ? out_scores + d0 * m->L : nullptr;

@@ -203,6 +203,21 @@ __host__ __device__ __forceinline__ uint64_t gen_hash(const uint8_t* p, int64_t 
     return mix64(h);
 }
 
+// Long-gram prefilter of mixed tables (a gram length beyond kMaxWideGram next to
+// shorter ones): two bits per key of >= 16 bytes in a bitmap of 2^lb bits,
+// chosen by the key's first eight bytes (lo, hi: little-endian words) and its
+// length -- a window of n >= 16 bytes whose two bits are not both set is no
+// key.  32-bit arithmetic only (host and device alike).
+__host__ __device__ __forceinline__ void long_bits(uint32_t lo, uint32_t hi, uint32_t n, uint32_t lb, uint32_t& b1,
+                                                   uint32_t& b2) {
+    uint32_t h = lo * 0x9E3779B1u + ((hi * 0x85EBCA77u) << 13 | (hi * 0x85EBCA77u) >> 19) + n * 0xC2B2AE3Du;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 13;
+    b1 = h >> (32 - lb);
+    b2 = (h * 0x297A2D39u) >> (32 - lb);
+}
+
 // Slot of the general key table (open addressing, linear probes): the key's
 // hash, its length (0: empty slot) and its row (kBadRow: wrong length).
 struct alignas(16) GenSlot {

@@ -22,6 +22,12 @@
 // wave's LDS buffer: a window's hash then reads its bytes from LDS -- up to 12
 // bytes as three byte-aligned words, the FNV steps unrolled in registers --
 // instead of one dependent global load per byte.
+//
+// Mixed tables (long lengths next to lengths <= 15): the LDS-filtered kernels
+// score the short lengths over the short keys, long_flag_kernel lists the
+// documents a long length can hit, and this kernel rescores only those
+// (indirect launch, every length, every key): a document no long window hits
+// gets exactly the short lengths' adds, in the reference's order.
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
@@ -104,7 +110,9 @@ __global__ __launch_bounds__(kGenWaves * 64) void general_score_kernel(const Gen
     uint8_t* const buf = reinterpret_cast<uint8_t*>(gen_acc + (size_t)kGenWaves * p.L) + wave * (kGenBuf + 64);
     const int S = (p.L + 63) / 64;
     const int64_t stride = (int64_t)gridDim.x * kGenWaves;
-    for (int64_t doc = (int64_t)blockIdx.x * kGenWaves + wave; doc < p.n_docs; doc += stride) {
+    const int64_t n_docs = p.doc_idx ? (int64_t)*p.n_docs_dev : p.n_docs;
+    for (int64_t i = (int64_t)blockIdx.x * kGenWaves + wave; i < n_docs; i += stride) {
+        const int64_t doc = p.doc_idx ? p.doc_idx[i] : i;
         for (int l = lane; l < p.L; l += 64) acc[l] = 0.0;
         const int64_t b = p.offsets[doc];
         const int64_t len = p.offsets[doc + 1] - b;
@@ -167,7 +175,73 @@ __global__ __launch_bounds__(kGenWaves * 64) void general_score_kernel(const Gen
     }
 }
 
+// Mixed tables: list the documents a long gram length can hit (LongFlagParams).
+// One wave per document; lanes take 64 consecutive window positions of each
+// long length n, read the window's first eight bytes (three dword loads and a
+// byte align: n >= 16, so they lie inside the document) and test its two
+// prefilter bits in the workgroup's LDS copy of the bitmap; a window passing
+// both is looked up in the general table (hash of its n bytes, linear probes,
+// byte compare).  A document shorter than some long n is also looked up whole
+// (its one partial window, whatever its length).  The first hit lists the
+// document (one atomic per listed document) and ends its scan.
+constexpr int kFlagWaves = 4;
+
+__global__ __launch_bounds__(kFlagWaves * 64) void long_flag_kernel(const LongFlagParams p) {
+    extern __shared__ uint32_t bm[];
+    for (uint32_t i = threadIdx.x; i < (1u << p.lb) / 32u; i += blockDim.x) bm[i] = p.bitmap[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    GenScoreParams g{};
+    g.slots = p.slots;
+    g.slot_mask = p.slot_mask;
+    g.slot_shift = p.slot_shift;
+    g.arena = p.arena;
+    g.koff = p.koff;
+    const int64_t stride = (int64_t)gridDim.x * kFlagWaves;
+    for (int64_t doc = (int64_t)blockIdx.x * kFlagWaves + wave; doc < p.n_docs; doc += stride) {
+        const int64_t b = p.offsets[doc];
+        const int64_t len = p.offsets[doc + 1] - b;
+        const uint8_t* d = p.bytes + b;
+        bool hit = false;
+        if (len > 0 && len < p.max_long && lane == 0) hit = gen_lookup(g, d, len) >= 0;
+        uint64_t any = __ballot(hit);
+        for (int gi = 0; gi < p.n_long && !any; ++gi) {
+            const int64_t n = p.Glong[gi];
+            const int64_t nw = len - n + 1;  // full windows (n > len: none)
+            for (int64_t p0 = 0; p0 < nw && !any; p0 += 64) {
+                const int64_t pos = p0 + lane;
+                bool h = false;
+                if (pos < nw) {
+                    const uintptr_t a = (uintptr_t)(d + pos);
+                    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+                    const uint32_t sh = (uint32_t)(a & 3), w0 = w[0], w1 = w[1], w2 = w[2];
+                    uint32_t b1, b2;
+                    long_bits(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                              (uint32_t)n, p.lb, b1, b2);
+                    if (((bm[b1 >> 5] >> (b1 & 31)) & (bm[b2 >> 5] >> (b2 & 31)) & 1u) != 0u)
+                        h = gen_lookup(g, d + pos, n) >= 0;
+                }
+                any = __ballot(h);
+            }
+        }
+        if (any && lane == 0) p.idx[atomicAdd(p.n_out, 1ull)] = doc;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_long_flag(const LongFlagParams& p, int cus, hipStream_t stream) {
+    if (p.n_docs <= 0) return hipSuccess;
+    const size_t lds = (size_t)(1u << p.lb) / 8u;
+    hipError_t e = hipFuncSetAttribute((const void*)&long_flag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    const int64_t want = (p.n_docs + kFlagWaves - 1) / kFlagWaves;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)cus * 8));
+    hipLaunchKernelGGL(long_flag_kernel, dim3(grid), dim3(kFlagWaves * 64), lds, stream, p);
+    return hipGetLastError();
+}
 
 hipError_t launch_general_score(const GenScoreParams& p, int grid, hipStream_t stream) {
     // scores (<= 64 KiB: L <= 4096) and the staged documents

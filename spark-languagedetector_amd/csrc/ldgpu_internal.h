@@ -82,6 +82,11 @@ struct ScoreParams {
     double* best;
     int32_t block;
     int64_t score_stride;       // 0: L
+    // indirect launch (class mode's exact replay, mode 1): document i of the
+    // launch is document doc_idx[i] of the corpus, i < *n_docs_dev (a count
+    // the device wrote: no readback), its label stored to labels[doc_idx[i]]
+    const int64_t* doc_idx;     // nullptr: document i is document i
+    const unsigned long long* n_docs_dev;
 };
 
 // languages per block of a blocked model (L > kBlockLangs)
@@ -141,16 +146,20 @@ inline size_t score_lds_bytes(int slices, int mode, uint32_t image_words, bool p
 // finite values, labels only (per-(class, language) hit counts and a rounding
 // bound; ambiguous documents labelled -1); lds_bloom = bloom staged in LDS
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream);
+// the per-(mode, slices) entry points behind launch_score / score_prepare
+// (ldgpu_score.hip compiled once per pair: launch_score_<mode>_<slices>)
+#define LDGPU_SCORE_PAIR_DECL(m, s)                                                                              \
+    hipError_t launch_score_##m##_##s(const ScoreParams& p, bool lds_bloom, int grid, hipStream_t stream);        \
+    hipError_t prepare_score_##m##_##s(bool lds_bloom, bool chunks, size_t lds, int* blocks);
+LDGPU_SCORE_PAIR_DECL(0, 1) LDGPU_SCORE_PAIR_DECL(0, 2) LDGPU_SCORE_PAIR_DECL(0, 3) LDGPU_SCORE_PAIR_DECL(0, 4)
+LDGPU_SCORE_PAIR_DECL(1, 1) LDGPU_SCORE_PAIR_DECL(1, 2) LDGPU_SCORE_PAIR_DECL(1, 3) LDGPU_SCORE_PAIR_DECL(1, 4)
+LDGPU_SCORE_PAIR_DECL(2, 1) LDGPU_SCORE_PAIR_DECL(2, 2) LDGPU_SCORE_PAIR_DECL(2, 3) LDGPU_SCORE_PAIR_DECL(2, 4)
+LDGPU_SCORE_PAIR_DECL(3, 1) LDGPU_SCORE_PAIR_DECL(3, 2) LDGPU_SCORE_PAIR_DECL(3, 3) LDGPU_SCORE_PAIR_DECL(3, 4)
+LDGPU_SCORE_PAIR_DECL(4, 1) LDGPU_SCORE_PAIR_DECL(4, 2) LDGPU_SCORE_PAIR_DECL(4, 3) LDGPU_SCORE_PAIR_DECL(4, 4)
+#undef LDGPU_SCORE_PAIR_DECL
 // class mode's ambiguous documents (ldgpu_replay.hip): idx[0 .. *n_out) = the
-// documents labelled -1; the sub-corpus of idx[0 .. k) (offsets sub_off[0 ..
-// k], bytes packed into sub; scan_tmp == nullptr: *scan_bytes = the scan's
-// scratch, nothing launched; sub == nullptr: the offsets only); the sub-corpus
-// labels back to labels[idx[i]]
+// documents labelled -1 (then replayed by an indirect mode-1 launch)
 hipError_t launch_amb_compact(const int32_t* labels, int64_t n, int64_t* idx, unsigned long long* n_out,
-                              hipStream_t stream);
-hipError_t amb_sub_corpus(const int64_t* idx, int64_t k, const int64_t* offsets, const uint8_t* bytes, int64_t* sub_off,
-                          int64_t* len_tmp, void* scan_tmp, size_t* scan_bytes, uint8_t* sub, hipStream_t stream);
-hipError_t launch_amb_scatter(const int64_t* idx, int64_t k, const int32_t* sub_labels, int32_t* labels,
                               hipStream_t stream);
 
 // General-key scoring (ldgpu_general.hip): models with a gram length beyond
@@ -177,9 +186,39 @@ struct GenScoreParams {
     int32_t L;
     int32_t nG;
     int32_t G[kMaxGramLengths];
+    // indirect launch (mixed tables: the documents the long-gram pass listed):
+    // document i of the launch is doc_idx[i], i < *n_docs_dev
+    const int64_t* doc_idx;     // nullptr: document i is document i
+    const unsigned long long* n_docs_dev;
 };
 constexpr int kGenWaves = 2;    // waves per workgroup (LDS: 2 x L doubles)
 hipError_t launch_general_score(const GenScoreParams& p, int grid, hipStream_t stream);
+
+// Mixed tables (gram lengths beyond kMaxWideGram next to shorter ones): the
+// shorter lengths are scored by the LDS-filtered kernels over the keys of <=
+// 15 bytes; this pass lists the documents that the longer lengths can hit --
+// a window of a long length n whose bits of the long-key prefilter (long_bits)
+// are set and which is a key of the general table, or (a document shorter
+// than some long n: Scala's partial window) the whole document if it is a key
+// -- and those documents are then rescored exactly by the general kernel.
+struct LongFlagParams {
+    const uint8_t* bytes;       // 4-byte aligned
+    const int64_t* offsets;
+    int64_t n_docs;
+    const uint32_t* bitmap;     // 2^lb bits
+    uint32_t lb;
+    int32_t n_long;             // distinct long gram lengths
+    int32_t Glong[kMaxGramLengths];
+    int32_t max_long;
+    const GenSlot* slots;       // the general table (every key)
+    uint64_t slot_mask;
+    uint32_t slot_shift;
+    const uint8_t* arena;
+    const int64_t* koff;
+    int64_t* idx;               // out: listed documents
+    unsigned long long* n_out;  // out: their count (zeroed by the caller)
+};
+hipError_t launch_long_flag(const LongFlagParams& p, int cus, hipStream_t stream);
 
 // label[i] = the first block maximum over nb language blocks (block b's
 // labels / maxima at lab + b n, best + b n)

@@ -39,10 +39,17 @@
 // superblocks inner.
 #include <type_traits>
 
+//
+// Build: this file is compiled once per (mode, slices) pair with
+// -DLDGPU_SCORE_MODE=m -DLDGPU_SCORE_S=s (the Makefile's score_<m>_<s>
+// objects: twenty translation units that compile in parallel), each defining
+// that pair's launch / prepare entry points, and once without them for the
+// dispatch (launch_score, score_prepare) and the language-block combine.
 #include "ldgpu_internal.h"
 
 namespace ldgpu {
 
+#if defined(LDGPU_SCORE_MODE)
 namespace {
 
 constexpr int kSub = 4;  // 64-position sub-blocks per superblock
@@ -1449,13 +1456,22 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
 // INVARIANT (cold_params): ScoreParams is the kernel's first and only explicit
 // argument, so it sits at offset 0 of the kernarg segment; the static_assert
 // after the kernel checks the signature.
-template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false>
+// IND (mode 1 only): the indirect launch of class mode's exact replay -- wave w
+// scores documents p.doc_idx[i], i = w, w + waves, ... < *p.n_docs_dev (count
+// written by the device), each in place from global memory, its label stored
+// to labels[doc_idx[i]]; workgroups with no document exit before staging.
+template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false, bool IND = false>
 __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
     constexpr bool FLDS = BL == 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int64_t n_ind = 0;
+    if constexpr (IND) {
+        n_ind = (int64_t)*p.n_docs_dev;  // (uniform address: a scalar load)
+        if ((int64_t)blockIdx.x * kScoreWaves >= n_ind) return;
+    }
     const uint32_t img_words = kBloomBase + (FLDS ? p.bloom_words : 0u) + p.direct_words;
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.filter);
@@ -1483,6 +1499,17 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
         uint32_t* cnt = count_area(wl);
         for (uint32_t i = (uint32_t)lane; i < kHitW; i += 64) cnt[i] = 0;
         __builtin_amdgcn_wave_barrier();
+    }
+
+    if constexpr (IND) {
+        const int64_t nw = (int64_t)gridDim.x * kScoreWaves;
+        for (int64_t i = (int64_t)blockIdx.x * kScoreWaves + wave; i < n_ind; i += nw) {
+            const int64_t d = p.doc_idx[i];
+            const int64_t b = p.offsets[d], len = p.offsets[d + 1] - b;
+            const int lab = score_doc<S, MODE, false, BL, WIDE>(p, wl, lds, bloom, d, b, len, DocSrc{nullptr, b}, lane);
+            if (lane == 0) p.labels[d] = lab;
+        }
+        return;
     }
 
     // this wave's contiguous range of documents, walked in groups of p.group
@@ -1588,6 +1615,13 @@ hipError_t launch_w(const ScoreParams& p, int grid, hipStream_t stream) {
     const bool pack = MODE == 3 && p.pack;
     const size_t lds = score_lds_bytes(S, MODE, kBloomBase + (BL == 0 ? p.bloom_words : 0u) + p.direct_words, pack,
                                        MODE == 4 ? p.hit_words : 0u);
+    if constexpr (MODE == 1) {
+        if (p.doc_idx) {
+            hipLaunchKernelGGL((score_kernel<S, MODE, BL, false, WIDE, true>), dim3(grid), dim3(kScoreWaves * 64), lds,
+                               stream, p);
+            return hipGetLastError();
+        }
+    }
     if constexpr (MODE == 3) {
         if (pack) {
             hipLaunchKernelGGL((score_kernel<S, MODE, BL, true, WIDE>), dim3(grid), dim3(kScoreWaves * 64), lds,
@@ -1605,9 +1639,9 @@ hipError_t launch_t(const ScoreParams& p, int grid, hipStream_t stream) {
     return p.wslots ? launch_w<S, MODE, BL, true>(p, grid, stream) : launch_w<S, MODE, BL, false>(p, grid, stream);
 }
 
-template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false>
+template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false, bool IND = false>
 hipError_t prepare_k(size_t lds, int* blocks) {
-    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, BL, PACK, WIDE>);
+    const void* f = reinterpret_cast<const void*>(&score_kernel<S, MODE, BL, PACK, WIDE, IND>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, kScoreWaves * 64, lds);
@@ -1621,6 +1655,11 @@ hipError_t prepare_t(size_t lds, int* blocks) {
     int b2 = 0;
     if (e == hipSuccess) e = prepare_k<S, MODE, BL, false, true>(lds, &b2);
     if (e == hipSuccess) *blocks = std::min(*blocks, b2);
+    if constexpr (MODE == 1) {  // (the indirect replay: its LDS limit; it never sets the grid)
+        int b3 = 0;
+        if (e == hipSuccess) e = prepare_k<S, MODE, BL, false, false, true>(lds, &b3);
+        if (e == hipSuccess) e = prepare_k<S, MODE, BL, false, true, true>(lds, &b3);
+    }
     if constexpr (MODE == 3) {
         if (e == hipSuccess) e = prepare_k<S, MODE, BL, true>(lds, &b2);
         if (e == hipSuccess) *blocks = std::min(*blocks, b2);
@@ -1630,47 +1669,6 @@ hipError_t prepare_t(size_t lds, int* blocks) {
     return e;
 }
 
-template <int MODE, int BL>
-hipError_t launch_s(const ScoreParams& p, int slices, int grid, hipStream_t stream) {
-    switch (slices) {
-        case 1: return launch_t<1, MODE, BL>(p, grid, stream);
-        case 2: return launch_t<2, MODE, BL>(p, grid, stream);
-        case 3: return launch_t<3, MODE, BL>(p, grid, stream);
-        case 4: return launch_t<4, MODE, BL>(p, grid, stream);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-template <int MODE, int BL>
-hipError_t prepare_s(int slices, size_t lds, int* blocks) {
-    switch (slices) {
-        case 1: return prepare_t<1, MODE, BL>(lds, blocks);
-        case 2: return prepare_t<2, MODE, BL>(lds, blocks);
-        case 3: return prepare_t<3, MODE, BL>(lds, blocks);
-        case 4: return prepare_t<4, MODE, BL>(lds, blocks);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-// the chunk layout is built for count-mode tables only (MODE 3)
-template <int MODE>
-hipError_t launch_m(const ScoreParams& p, int slices, bool lds_bloom, int grid, hipStream_t stream) {
-    if (lds_bloom) return launch_s<MODE, 0>(p, slices, grid, stream);
-    if constexpr (MODE == 3) {
-        if (p.kb_chunks) return launch_s<MODE, 2>(p, slices, grid, stream);
-    }
-    return launch_s<MODE, 1>(p, slices, grid, stream);
-}
-
-template <int MODE>
-hipError_t prepare_m(int slices, bool lds_bloom, bool chunks, size_t lds, int* blocks) {
-    if (lds_bloom) return prepare_s<MODE, 0>(slices, lds, blocks);
-    if constexpr (MODE == 3) {
-        if (chunks) return prepare_s<MODE, 2>(slices, lds, blocks);
-    }
-    return prepare_s<MODE, 1>(slices, lds, blocks);
-}
-
 // cold_params() reads the kernarg segment as a ScoreParams: any other
 // argument list for score_kernel must change cold_params first
 template <typename T>
@@ -1678,8 +1676,82 @@ struct ParamsOnlyKernel : std::false_type {};
 template <>
 struct ParamsOnlyKernel<void (*)(ScoreParams)> : std::true_type {};
 static_assert(ParamsOnlyKernel<decltype(&score_kernel<1, 3, 0, false, false>)>::value &&
-                  ParamsOnlyKernel<decltype(&score_kernel<4, 1, 1, true, true>)>::value,
+                  ParamsOnlyKernel<decltype(&score_kernel<4, 1, 1, true, true>)>::value &&
+                  ParamsOnlyKernel<decltype(&score_kernel<2, 1, 0, false, true, true>)>::value,
               "score_kernel must take exactly one argument, ScoreParams (cold_params reads it at kernarg offset 0)");
+
+constexpr int kM = LDGPU_SCORE_MODE, kS = LDGPU_SCORE_S;
+
+// LDGPU_NARROW_VARIANT (tuning builds only, tools/build_variant.sh): just the
+// kernels of one bench configuration, compiled in a minute instead of ten:
+//   1: config 2 -- LDS bloom, one slice, count mode and the finite-value replay
+//   4: config 4 -- keyed bloom in chunks, two slices (L = 100), count mode
+//   5: config 5 -- keyed bloom in lines, four slices (L = 200), count mode
+// kNarrowBl: the one bloom layout built (-1: every layout, a product build)
+#if !defined(LDGPU_NARROW_VARIANT)
+constexpr bool kBuilt = true;
+constexpr int kNarrowBl = -1;
+#elif LDGPU_NARROW_VARIANT == 4
+constexpr bool kBuilt = kM == 3 && kS == 2;
+constexpr int kNarrowBl = 2;
+#elif LDGPU_NARROW_VARIANT == 5
+constexpr bool kBuilt = kM == 3 && kS == 4;
+constexpr int kNarrowBl = 1;
+#else
+constexpr bool kBuilt = (kM == 3 || kM == 1) && kS == 1;
+constexpr int kNarrowBl = 0;
+#endif
+
+// the bloom layout of a launch: 0 = prefix Bloom in LDS, 2 = keyed chunks
+// (built for count-mode tables only), 1 = keyed words / lines
+int bloom_layout(bool lds_bloom, bool chunks) { return lds_bloom ? 0 : (kM == 3 && chunks ? 2 : 1); }
+
+}  // namespace
+
+#define LDGPU_CAT4(a, b, c, d) a##b##c##d
+#define LDGPU_FN(pre, m, s) LDGPU_CAT4(pre, m, _, s)
+
+hipError_t LDGPU_FN(launch_score_, LDGPU_SCORE_MODE, LDGPU_SCORE_S)(const ScoreParams& p, bool lds_bloom, int grid,
+                                                                   hipStream_t stream) {
+    if constexpr (!kBuilt) {
+        return hipErrorInvalidValue;
+    } else {
+        const int bl = bloom_layout(lds_bloom, p.kb_chunks != 0);
+        if constexpr (kNarrowBl < 0 || kNarrowBl == 0) {
+            if (bl == 0) return launch_t<kS, kM, 0>(p, grid, stream);
+        }
+        if constexpr (kM == 3 && (kNarrowBl < 0 || kNarrowBl == 2)) {
+            if (bl == 2) return launch_t<kS, kM, 2>(p, grid, stream);
+        }
+        if constexpr (kNarrowBl < 0 || kNarrowBl == 1) {
+            if (bl == 1) return launch_t<kS, kM, 1>(p, grid, stream);
+        }
+        return hipErrorInvalidValue;
+    }
+}
+
+hipError_t LDGPU_FN(prepare_score_, LDGPU_SCORE_MODE, LDGPU_SCORE_S)(bool lds_bloom, bool chunks, size_t lds,
+                                                                    int* blocks) {
+    if constexpr (!kBuilt) {
+        return hipErrorInvalidValue;
+    } else {
+        const int bl = bloom_layout(lds_bloom, chunks);
+        if constexpr (kNarrowBl < 0 || kNarrowBl == 0) {
+            if (bl == 0) return prepare_t<kS, kM, 0>(lds, blocks);
+        }
+        if constexpr (kM == 3 && (kNarrowBl < 0 || kNarrowBl == 2)) {
+            if (bl == 2) return prepare_t<kS, kM, 2>(lds, blocks);
+        }
+        if constexpr (kNarrowBl < 0 || kNarrowBl == 1) {
+            if (bl == 1) return prepare_t<kS, kM, 1>(lds, blocks);
+        }
+        return hipErrorInvalidValue;
+    }
+}
+
+#else  // the dispatch translation unit
+
+namespace {
 
 // first maximum across language blocks: block maxima compared with '>' in
 // block order, as breeze's argmax compares scores in language order
@@ -1708,54 +1780,34 @@ hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const do
     return hipGetLastError();
 }
 
-// LDGPU_NARROW_VARIANT (tuning builds only, tools/build_variant.sh): just the
-// kernels of one bench configuration, compiled in a minute instead of ten:
-//   1: config 2 -- LDS bloom, one slice, count mode and the finite-value replay
-//   4: config 4 -- keyed bloom in chunks, two slices (L = 100), count mode
-//   5: config 5 -- keyed bloom in lines, four slices (L = 200), count mode
-#if defined(LDGPU_NARROW_VARIANT) && LDGPU_NARROW_VARIANT == 4
-#define LDGPU_NARROW_OK(mode, lds, chunks, slices) ((mode) == 3 && !(lds) && (chunks) && (slices) == 2)
-#define LDGPU_NARROW_T 2, 3, 2
-#elif defined(LDGPU_NARROW_VARIANT) && LDGPU_NARROW_VARIANT == 5
-#define LDGPU_NARROW_OK(mode, lds, chunks, slices) ((mode) == 3 && !(lds) && !(chunks) && (slices) == 4)
-#define LDGPU_NARROW_T 4, 3, 1
-#endif
+#define LDGPU_SCORE_CASE(m, s, ...)  \
+    case (m) * 8 + (s):                \
+        return launch_score_##m##_##s(__VA_ARGS__);
+#define LDGPU_PREPARE_CASE(m, s, ...)  \
+    case (m) * 8 + (s):                  \
+        return prepare_score_##m##_##s(__VA_ARGS__);
+#define LDGPU_FOR_PAIRS(X, ...)                                                                              \
+    X(0, 1, __VA_ARGS__) X(0, 2, __VA_ARGS__) X(0, 3, __VA_ARGS__) X(0, 4, __VA_ARGS__) X(1, 1, __VA_ARGS__) \
+    X(1, 2, __VA_ARGS__) X(1, 3, __VA_ARGS__) X(1, 4, __VA_ARGS__) X(2, 1, __VA_ARGS__) X(2, 2, __VA_ARGS__) \
+    X(2, 3, __VA_ARGS__) X(2, 4, __VA_ARGS__) X(3, 1, __VA_ARGS__) X(3, 2, __VA_ARGS__) X(3, 3, __VA_ARGS__) \
+    X(3, 4, __VA_ARGS__) X(4, 1, __VA_ARGS__) X(4, 2, __VA_ARGS__) X(4, 3, __VA_ARGS__) X(4, 4, __VA_ARGS__)
+
 hipError_t launch_score(const ScoreParams& p, int slices, int mode, bool lds_bloom, int grid, hipStream_t stream) {
-#if defined(LDGPU_NARROW_T)
-    if (!LDGPU_NARROW_OK(mode, lds_bloom, p.kb_chunks, slices)) return hipErrorInvalidValue;
-    return launch_t<LDGPU_NARROW_T>(p, grid, stream);
-#elif defined(LDGPU_NARROW_VARIANT)
-    if ((mode != 3 && mode != 1) || !lds_bloom || slices != 1) return hipErrorInvalidValue;
-    return mode == 3 ? launch_t<1, 3, 0>(p, grid, stream) : launch_t<1, 1, 0>(p, grid, stream);
-#else
-    switch (mode) {
-        case 0: return launch_m<0>(p, slices, lds_bloom, grid, stream);
-        case 1: return launch_m<1>(p, slices, lds_bloom, grid, stream);
-        case 2: return launch_m<2>(p, slices, lds_bloom, grid, stream);
-        case 3: return launch_m<3>(p, slices, lds_bloom, grid, stream);
-        case 4: return launch_m<4>(p, slices, lds_bloom, grid, stream);
+    if (slices < 1 || slices > 4) return hipErrorInvalidValue;
+    switch (mode * 8 + slices) {
+        LDGPU_FOR_PAIRS(LDGPU_SCORE_CASE, p, lds_bloom, grid, stream)
         default: return hipErrorInvalidValue;
     }
-#endif
 }
 
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu) {
-#if defined(LDGPU_NARROW_T)
-    if (!LDGPU_NARROW_OK(mode, lds_bloom, chunks, slices)) return hipErrorInvalidValue;
-    return prepare_t<LDGPU_NARROW_T>(lds_bytes, blocks_per_cu);
-#elif defined(LDGPU_NARROW_VARIANT)
-    if ((mode != 3 && mode != 1) || !lds_bloom || slices != 1) return hipErrorInvalidValue;
-    return mode == 3 ? prepare_t<1, 3, 0>(lds_bytes, blocks_per_cu) : prepare_t<1, 1, 0>(lds_bytes, blocks_per_cu);
-#else
-    switch (mode) {
-        case 0: return prepare_m<0>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
-        case 1: return prepare_m<1>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
-        case 2: return prepare_m<2>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
-        case 3: return prepare_m<3>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
-        case 4: return prepare_m<4>(slices, lds_bloom, chunks, lds_bytes, blocks_per_cu);
+    if (slices < 1 || slices > 4) return hipErrorInvalidValue;
+    switch (mode * 8 + slices) {
+        LDGPU_FOR_PAIRS(LDGPU_PREPARE_CASE, lds_bloom, chunks, lds_bytes, blocks_per_cu)
         default: return hipErrorInvalidValue;
     }
-#endif
 }
+
+#endif  // LDGPU_SCORE_MODE
 
 }  // namespace ldgpu

@@ -4,12 +4,12 @@ Mirrors org.apache.spark.ml.feature.languagedetection (LanguageDetector,
 LanguageDetectorModel) over pandas DataFrames; the FIT counting and SCORE
 kernels run on gfx950 through libldgpu.so (include/ldgpu.h).
 """
-from .api import (FitValidationError, LanguageDetector, LanguageDetectorModel, LanguageDetectorModelReader,
-                  LanguageDetectorModelWriter, NullPointerException, save_grams)
+from .api import (FitValidationError, FrozenTable, LanguageDetector, LanguageDetectorModel, LanguageDetectorModelReader,
+                  LanguageDetectorModelWriter, NullPointerException, freeze_table, save_grams)
 from .language import Language
 from .preprocessing import LowerCasePreprocessor, PatternSyntaxException, SpecialCharPreprocessor
 from .runtime import DeviceCounts, DeviceModel
 
 __all__ = ["LanguageDetector", "LanguageDetectorModel", "LanguageDetectorModelReader", "LanguageDetectorModelWriter",
-           "FitValidationError", "NullPointerException", "DeviceCounts", "DeviceModel", "save_grams",
+           "FitValidationError", "NullPointerException", "FrozenTable", "freeze_table", "DeviceCounts", "DeviceModel", "save_grams",
            "LowerCasePreprocessor", "SpecialCharPreprocessor", "PatternSyntaxException", "Language"]

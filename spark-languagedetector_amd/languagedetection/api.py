@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import threading
 import uuid
+from collections.abc import Mapping
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -163,12 +164,40 @@ class LanguageDetectorModel(_Params):
         return supportedLanguages[int(labels[0])]
 
 
+class FrozenTable(Mapping):
+    """An immutable gram -> probability-row map (keys bytes, rows tuples of
+    floats).  detect() reuses its device table by identity alone; any other
+    mapping is compared with a snapshot of its contents on every call."""
+
+    __slots__ = ("_d",)
+
+    def __init__(self, table):
+        self._d = {encoding.gram_key(k): tuple(float(x) for x in v) for k, v in table.items()}
+
+    def __getitem__(self, k):
+        return self._d[k]
+
+    def __iter__(self):
+        return iter(self._d)
+
+    def __len__(self):
+        return len(self._d)
+
+
+def freeze_table(table) -> FrozenTable:
+    """The table as a FrozenTable: detect() over it skips the content check."""
+    return table if isinstance(table, FrozenTable) else FrozenTable(table)
+
+
 # The device tables of recent detect() calls (the Scala drop-in's
 # detectAcquire): callers score row after row with the same map, so its
-# table is kept, keyed by the map object.  Scala's Map is immutable; a Python
-# dict is not, so an entry also records the dict's length and the identity of
-# its first row's value list (a caller that rebuilds the map gets a new
-# object, hence a new table).
+# table is kept.  The reference builds its lookups from the map on every
+# call, so a cached table may serve a call only if the map's contents are
+# those it was built from: a FrozenTable cannot change, and any other mapping
+# (a dict and its value lists can be edited in place) is compared with a copy
+# of its contents taken at build time (one C-level dict compare, ~0.7 ms for
+# 10k rows of 20 values); a mapping whose values cannot be compared that way
+# (e.g. numpy rows) is never cached.
 _DETECT_CACHE: list = []
 _DETECT_CACHE_SIZE = 4
 
@@ -176,19 +205,40 @@ _DETECT_CACHE_SIZE = 4
 _DETECT_LOCK = threading.Lock()
 
 
+def _snapshot(probabilityMap):
+    """A copy of the map's contents to compare later calls with, or None."""
+    if isinstance(probabilityMap, FrozenTable):
+        return probabilityMap
+    if not all(isinstance(v, (list, tuple)) for v in probabilityMap.values()):
+        return None
+    return {k: (list(v) if isinstance(v, list) else v) for k, v in probabilityMap.items()}
+
+
+def _unchanged(probabilityMap, snap) -> bool:
+    if isinstance(probabilityMap, FrozenTable):
+        return snap is probabilityMap
+    try:
+        return type(probabilityMap) is dict and probabilityMap == snap
+    except (TypeError, ValueError):
+        return False
+
+
 def _detect_model(probabilityMap, n_langs: int, gramLengths):
-    first = next(iter(probabilityMap.values()), None)
-    key = (id(probabilityMap), len(probabilityMap), id(first), n_langs, tuple(gramLengths))
+    key = (id(probabilityMap), n_langs, tuple(gramLengths))
     with _DETECT_LOCK:
-        for i, (k, ref, m) in enumerate(_DETECT_CACHE):
-            if k == key and ref is probabilityMap:
+        for i, (k, ref, snap, m) in enumerate(_DETECT_CACHE):
+            if k == key and ref is probabilityMap and _unchanged(probabilityMap, snap):
                 _DETECT_CACHE.insert(0, _DETECT_CACHE.pop(i))
                 return m
+    snap = _snapshot(probabilityMap)
     m = DeviceModel({encoding.gram_key(k): v for k, v in probabilityMap.items()}, n_langs, gramLengths)
-    with _DETECT_LOCK:
-        _DETECT_CACHE.insert(0, (key, probabilityMap, m))
-        # (an evicted table is released when its last caller drops it)
-        del _DETECT_CACHE[_DETECT_CACHE_SIZE:]
+    if snap is not None:
+        with _DETECT_LOCK:
+            # (a stale entry of the same map object is replaced; an evicted
+            # table is released when its last caller drops it)
+            _DETECT_CACHE[:] = [e for e in _DETECT_CACHE if e[0] != key]
+            _DETECT_CACHE.insert(0, (key, probabilityMap, snap, m))
+            del _DETECT_CACHE[_DETECT_CACHE_SIZE:]
     return m
 
 

@@ -4,8 +4,9 @@ LanguageDetector.scala:98-105).  The kernel counts hits per (value, language),
 labels a document from the counts when a rounding bound separates its top
 language from every other, and replays the rest in reference order
 (LanguageDetectorModel.scala:139-154).  Labels must equal the oracle's exactly,
-ties and near ties included; scores calls keep the ordered replay, and so
-does the host-buffer pipeline (ldgpu_score), which stays asynchronous."""
+ties and near ties included; scores calls keep the ordered replay.  Both the
+device-buffer call and the host-buffer pipeline (ldgpu_score) take class mode,
+and both stay asynchronous (the replay is sized on the device)."""
 import math
 
 import numpy as np
@@ -39,9 +40,7 @@ def oracle_labels(table, L, grams, data, off):
 
 
 def labels_device(m, data, off):
-    """Labels-only scoring through ldgpu_score_device -- the path that takes
-    class mode (the host pipeline, ldgpu_score, keeps the asynchronous ordered
-    replay)."""
+    """Labels-only scoring through ldgpu_score_device (HBM-resident buffers)."""
     dev = torch.device("cuda", 0)
     d_bytes = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
     d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
@@ -83,7 +82,7 @@ def test_class_mode_labels_match_oracle(L, grams, n_cls, monkeypatch):
     assert "classes" in m.info()["layout"], m.info()
     ol = oracle_labels(table, L, grams, data, off)
     assert np.array_equal(labels_device(m, data, off), ol)
-    labels, _ = m.score(data, off)  # the host pipeline (ordered replay)
+    labels, _ = m.score(data, off)  # the host pipeline (class mode too)
     assert np.array_equal(labels, ol)
     # a scores call keeps the ordered replay: same labels, scores bit-exact
     lab2, sc = m.score(data, off, want_scores=True)
@@ -193,3 +192,65 @@ def test_class_mode_direct_tables(L, n_cls, monkeypatch):
     ol, os_ = OC.Table(table, L).score([1, 2, 3, 4, 5], data[:int(off[500])], off[:501], want_scores=True, nthreads=8)
     assert np.array_equal(lab2, ol)
     assert np.array_equal(np.ascontiguousarray(sc).view(np.uint64), np.ascontiguousarray(os_).view(np.uint64))
+
+
+def _ulps(a, b):
+    """distance of two finite doubles of one sign in units in the last place"""
+    ia = np.asarray(a, dtype=np.float64).view(np.int64)
+    ib = np.asarray(b, dtype=np.float64).view(np.int64)
+    return np.abs(ia - ib)
+
+
+@pytest.mark.parametrize("L,tiny", [(2, False), (3, True), (20, True)])
+def test_class_mode_near_ties_at_many_hits(L, tiny):
+    """Near ties at 100-2,000 hits per document: the top two languages' folds
+    differ by 0-4 ulps.  Values 0.1 and 0.3 (and 2^-40 when `tiny`) make exact
+    sums that differ by far less than an ulp (a + 3b = c + 3d hits), so the
+    label is decided by the fold's roundings, i.e. by hit ORDER -- class_label's
+    rounding bound (ldgpu_score.hip) must send every such document to the
+    ordered replay, and a document it labels from counts must be one whose
+    fold agrees.  `tiny` adds one-off hits of 2^-40, which move the exact sums
+    apart by amounts around the bound itself (~1e-11 at these sizes).  Each
+    1-byte key names one (language, value): letters a/b -> language 0 with
+    0.1/0.3, c/d -> language 1, e/f -> 2^-40, g -> every language 0.1."""
+    v1, v3, vt = 0.1, 0.3, 2.0 ** -40
+    table = {b"a": [v1] + [0.0] * (L - 1), b"b": [v3] + [0.0] * (L - 1),
+             b"c": [0.0, v1] + [0.0] * (L - 2), b"d": [0.0, v3] + [0.0] * (L - 2),
+             b"g": [v1] * L}
+    if tiny:
+        table[b"e"] = [vt] + [0.0] * (L - 1)
+        table[b"f"] = [0.0, vt] + [0.0] * (L - 2)
+    if L > 2:  # a third language well behind
+        table[b"h"] = [0.0, 0.0, v3] + [0.0] * (L - 3)
+    rng = np.random.default_rng(L * 7 + tiny)
+    docs = []
+    for _ in range(3000):
+        n = int(rng.integers(100, 2001))
+        b = int(rng.integers(0, n // 4))
+        a = n - 3 * b if n - 3 * b > 0 else n
+        d = int(rng.integers(max(0, b - 30), b + 31))
+        c = a + 3 * (b - d)
+        if c < 0:
+            c, d = a, b
+        parts = [b"a"] * a + [b"b"] * b + [b"c"] * c + [b"d"] * d + [b"g"] * int(rng.integers(0, 40))
+        if tiny:  # equal tiny counts in half of the documents, else 1-2 apart
+            ne = int(rng.integers(0, 40))
+            nf = max(0, ne + (int(rng.integers(-2, 3)) if rng.random() < 0.5 else 0))
+            parts += [b"e"] * ne + [b"f"] * nf
+        if L > 2:
+            parts += [b"h"] * int(rng.integers(0, 20))
+        rng.shuffle(parts)
+        docs.append(b"".join(parts))
+    data, off = encoding.pack(docs)
+    m = DeviceModel(table, L, [1])
+    assert "classes" in m.info()["layout"], m.info()
+    ol, os_ = OC.Table(table, L).score([1], data, off, want_scores=True, nthreads=8)
+    # the corpus really is made of near ties: most documents' top two folds
+    # are within 4 ulps, and order decides many of them
+    top2 = np.sort(os_, axis=1)[:, -2:]
+    gap = _ulps(top2[:, 0], top2[:, 1])
+    assert (gap <= 4).mean() > 0.25, np.bincount(np.minimum(gap, 10))
+    assert ((gap >= 1) & (gap <= 4)).sum() >= 300
+    assert np.array_equal(labels_device(m, data, off), ol)
+    labels, _ = m.score(data, off)   # the host pipeline, class mode
+    assert np.array_equal(labels, ol)

@@ -77,6 +77,29 @@ def test_detect_static_string_and_bytes():
     assert LanguageDetectorModel.detect("", table, ["de", "en"], [3]) == "de"  # no hit -> index 0
 
 
+def test_detect_sees_in_place_edits_of_the_map():
+    """The reference builds its lookups from the map on every call
+    (LanguageDetectorModel.scala:131-156): an edit between two calls changes
+    the second call's label even though the cached device table is reused for
+    unchanged maps."""
+    from languagedetection import freeze_table
+    table = {"Die": [1.0, 0.0], "Thi": [0.0, 1.0]}
+    assert LanguageDetectorModel.detect("Dies", table, ["de", "en"], [3]) == "de"
+    table["Die"][0], table["Die"][1] = 0.0, 2.0          # edit a value list in place
+    assert LanguageDetectorModel.detect("Dies", table, ["de", "en"], [3]) == "en"
+    table["Thi"] = [3.0, 0.0]                           # replace a non-first entry, same length
+    assert LanguageDetectorModel.detect("This", table, ["de", "en"], [3]) == "de"
+    del table["Thi"]
+    table["Dat"] = [0.0, 1.0]                           # same length, other key
+    assert LanguageDetectorModel.detect("Dat", table, ["de", "en"], [3]) == "en"
+    assert LanguageDetectorModel.detect("This", table, ["de", "en"], [3]) == "de"  # no hit now
+    frozen = freeze_table(table)
+    assert LanguageDetectorModel.detect("Dies", frozen, ["de", "en"], [3]) == "en"
+    assert LanguageDetectorModel.detect("Dat", frozen, ["de", "en"], [3]) == "en"
+    with pytest.raises(TypeError):
+        frozen["Dat"] = [1.0, 0.0]
+
+
 def _random_table(rng, L, n_keys, grams, alphabet, mask_form, uniform=None):
     """uniform: one shared value for every row (the count-mode kernel)."""
     table = {}
@@ -323,9 +346,40 @@ def test_long_keys_general_table(grams, form):
     docs = [bytes(rng.choice(alphabet, size=int(n))) for n in lens]
     data, off = encoding.pack(docs)
     m = check_parity(table, L, grams, data, off)
-    assert m.info()["layout"] == ["general_keys"]
+    lay = m.info()["layout"]
+    assert "general_keys" in lay
+    # a mixed table (some length <= 15) scores those lengths on the
+    # LDS-filtered kernels: their layout is reported beside general_keys
+    assert (len(lay) > 1) == any(g <= 15 for g in grams), lay
     labels, _ = m.score(data, off, want_scores=False)
     ol, _ = oracle_c(table, L, grams, data, off, scores=False)
+    assert np.array_equal(labels, ol)
+
+
+@pytest.mark.parametrize("form", ["count", "mask", "dense"])
+def test_mixed_table_long_hits_and_partial_windows(form):
+    """A mixed table (grams 1-5 and 16): documents that no 16-byte window
+    hits keep the short lengths' result (count / class / replay kernels),
+    documents with a long hit are rescored whole by the general kernel, and a
+    document shorter than 16 bytes is its own partial window of n = 16 --
+    which can equal a SHORT key ("abcde" below) and then counts twice."""
+    L = 20
+    rng = np.random.default_rng(len(form) + 7)
+    alphabet = np.frombuffer(b"abcdefgh ", dtype=np.uint8)
+    uniform = math.log(2.0) if form == "count" else None
+    table = _random_table(rng, L, 400, [1, 2, 3, 4, 5], alphabet, form != "dense", uniform=uniform)
+    long_keys = [b"abcdefgh abcdefg", b"hhhhhhhhhhhhhhhh", b"a" * 16]
+    for k in long_keys:
+        table[k] = (_random_table(rng, L, 1, [16], alphabet, form != "dense", uniform=uniform).popitem()[1])
+    table[b"abcde"] = [uniform or 0.5] + [0.0] * (L - 1) if form != "dense" else rng.normal(size=L).tolist()
+    docs = [bytes(rng.choice(alphabet, size=int(n))) for n in rng.integers(0, 300, size=1500)]
+    docs += [b"abcde", b"abcd", b"xx" + long_keys[0] + b"yy", long_keys[1] * 3, b"a" * 40, b"", b"ab" * 100]
+    data, off = encoding.pack(docs)
+    m = check_parity(table, L, [1, 2, 3, 4, 5, 16], data, off)
+    lay = m.info()["layout"]
+    assert "general_keys" in lay and "lds_bloom" in lay, lay
+    labels, _ = m.score(data, off, want_scores=False)
+    ol, _ = oracle_c(table, L, [1, 2, 3, 4, 5, 16], data, off, scores=False)
     assert np.array_equal(labels, ol)
 
 

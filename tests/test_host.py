@@ -154,3 +154,22 @@ def test_bench_traffic_lookup_scales_profiled_launch():
     assert scaled["traffic_bytes_per_launch"] == round(5 * prof["traffic_bytes_per_launch"])
     assert "x5" in scaled["traffic_scaled_from"]
     assert bench.traffic_from_profiles(key.replace(":L=200:", ":L=201:")) is None
+
+
+def test_detect_cache_reuses_only_unchanged_maps():
+    """The detect() cache (api._detect_model) may reuse a device table only
+    while the map's contents equal the snapshot it was built from."""
+    from languagedetection.api import FrozenTable, _snapshot, _unchanged, freeze_table
+    t = {"ab": [1.0, 0.0], "cd": [0.0, 1.0]}
+    s = _snapshot(t)
+    assert _unchanged(t, s)
+    t["ab"][0] = 0.5                      # value list edited in place
+    assert not _unchanged(t, s)
+    t["ab"][0] = 1.0
+    assert _unchanged(t, s)
+    t["cd"] = [0.0, 2.0]                  # non-first entry replaced, same length
+    assert not _unchanged(t, s)
+    assert _snapshot({"ab": np.zeros(2)}) is None   # rows not comparable: never cached
+    f = freeze_table(t)
+    assert isinstance(f, FrozenTable) and freeze_table(f) is f
+    assert _unchanged(f, _snapshot(f)) and dict(f) == {b"ab": (1.0, 0.0), b"cd": (0.0, 2.0)}
