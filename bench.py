@@ -156,9 +156,15 @@ def cpu_baseline(args, table, grams, data, off, packed=None):
     t0 = time.perf_counter()
     labels, _ = t.score(grams, data, off[:n + 1], nthreads=threads)
     dt = time.perf_counter() - t0
+    # config 5's bytes model: the table hits per document (windows whose key
+    # is in the table), from the first documents of the sample
+    hits = None
+    if args.config == 5:
+        k = min(5000, len(off) - 1)
+        hits = {"docs": k, "hits_per_doc": t.hits(grams, data, off[:k + 1]) / max(k, 1)}
     return {"value": round(n / dt, 1), "unit": "docs/s", "cores": threads, "kind": "port",
             "sample": f"first {n} of the GPU's documents ({args.doc_min}-{args.doc_max} B), same table, "
-                      f"{threads} pthreads, {dt:.1f} s"}, labels
+                      f"{threads} pthreads, {dt:.1f} s"}, labels, hits
 
 
 def cpu_baseline_fit(args, grams, data, off, lang):
@@ -290,11 +296,13 @@ def mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs
 
 
 def general_key_path(args, table, grams, local, d_bytes, d_off, n_docs, d_lab, stream):
-    """The general-key SCORE path (a gram length beyond 15 bytes moves every
-    key into the general table, ldgpu_general.hip) on config 2's table plus
-    one 16-byte key that valid UTF-8 never holds (0xff bytes), gram lengths
-    + [16], over the first 1M documents: its kernel time and whether its
-    labels equal the count-mode launch's.  Reported beside `value`."""
+    """A mixed table (a gram length beyond 15 bytes next to shorter ones):
+    config 2's table plus one 16-byte key that valid UTF-8 never holds (0xff
+    bytes), gram lengths + [16], over the first 1M documents -- lengths 1-5 on
+    the count-mode kernel, the long-gram pass (ldgpu_general.hip) listing the
+    documents a 16-byte window hits, those rescored by the general kernel: its
+    time and whether its labels equal the count-mode launch's.  Reported
+    beside `value`."""
     from languagedetection import LanguageDetectorModel
     t2 = dict(table)
     t2[b"\xff" * 16] = [next(iter(table.values()))[0] or 1.0] + [0.0] * (args.langs - 1)
@@ -316,7 +324,8 @@ def general_key_path(args, table, grams, local, d_bytes, d_off, n_docs, d_lab, s
     ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev]))
     res = {"layout": m.info()["layout"], "docs": n, "kernel_ms": round(ms, 4),
            "docs_per_s": round(n / (ms * 1e-3), 1), "labels_match_count_mode": bool(torch.equal(d_out, d_lab[:n])),
-           "note": "config 2's table + one 16-byte key, gram lengths 1-5 and 16: every key in the general table"}
+           "note": "config 2's table + one 16-byte key, gram lengths 1-5 and 16: lengths 1-5 on the LDS kernels, "
+                   "the long-gram pass, documents with a long hit rescored on the general kernel"}
     m.close()
     # the static detect (LanguageDetectorModel.detect, one document per call,
     # the table cached across calls with the same map)
@@ -382,22 +391,33 @@ COUNT_KERNELS = ("emit_kernel", "fit_offsets_kernel", "part2_kernel", "reduce_ke
                  "counts_add_kernel", "sort_emit_kernel", "sort_runs_kernel", "runs_add_kernel")
 
 
-def fit_count_kernels(L, grams):
-    """The count path the library takes for (L, grams) (ldgpu_api.hip
-    counts_new / sort_path): FIT v5 (sort) for two-word records whose sort key
-    fits 64 bits, FIT v4 otherwise."""
+def fit_sort_path(L, grams):
+    """Whether the library counts (L, grams) by FIT v5 (ldgpu_api.hip
+    counts_new / sort_path: two-word records whose sort key fits 64 bits --
+    the radix sorts are then the count's own) or FIT v4 (no sort)."""
     maxg = max([g for g in grams if g <= 15] or [0])
     lb = max(1, (L - 1).bit_length())
     two_word = maxg <= 7 and 64 - (8 * maxg + 1) - lb < 8
-    if two_word and 8 * maxg + L.bit_length() <= 64:
+    return bool(two_word and 8 * maxg + L.bit_length() <= 64)
+
+
+def fit_count_kernels(L, grams):
+    if fit_sort_path(L, grams):
         return "count (FIT v5: sort_emit + radix sort + sort_runs per length + runs_add into T)"
     return "count (FIT v4: emit + part2 + reduce + merge + derive)"
 
 
-def count_traffic(prof):
-    """Calibrated HBM bytes per count from a FIT PMC profile, summed over the
-    count's own kernels only (the profile's run also holds the table phase:
-    presence, select, top-K, stats)."""
+def is_count_kernel(name, L, grams):
+    """A profiled kernel belongs to the count: one of COUNT_KERNELS, or a
+    radix sort when the count is FIT v5's (FIT v4 sorts nothing; any other
+    sort of a profiled run is an export's: sort_pairs_u64 in counts_pull)."""
+    base = name.split("(")[0].split("<")[0]
+    return base in COUNT_KERNELS or (base.startswith("rocprim") and fit_sort_path(L, grams))
+
+
+def count_traffic(prof, L, grams):
+    """Calibrated HBM bytes per count from a FIT PMC profile
+    (tools/fit_pmc.py), summed over the count's own kernels only."""
     if not prof:
         return None
     pk = prof.get("per_kernel_raw_bytes_per_count")
@@ -406,9 +426,7 @@ def count_traffic(prof):
     rf, wf = prof.get("read_factor", 1.0), prof.get("write_factor", 1.0)
     tot = 0.0
     for k, v in pk.items():
-        name = k.split("(")[0].split("<")[0]
-        # (a count-only profile: its radix sorts are the count's, FIT v5)
-        if name in COUNT_KERNELS or (prof.get("count_only") and name.startswith("rocprim")):
+        if is_count_kernel(k, L, grams):
             tot += rf * v.get("FETCH_SIZE", 0.0) + wf * v.get("WRITE_SIZE", 0.0)
     return int(round(tot))
 
@@ -536,7 +554,8 @@ def fit_main(args, world, rank, local, dev, backend):
         "windows_counted_exactly_once": windows_ok,
         "roofline": {"bound": "hbm", "achieved": round(algo / count_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / count_s / 1e9 / HBM_PEAK_GBS, 6),
-                     "traffic": count_traffic(traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}")),
+                     "traffic": count_traffic(traffic_from_profiles(f"fit:bytes={n_bytes}:L={args.langs}:G={args.grams}"),
+                                              args.langs, grams),
                      "kernel": fit_count_kernels(args.langs, grams), "count_ms": round(count_s * 1e3, 3),
                      "algorithmic_bytes_per_count": int(algo)},
     }
@@ -696,11 +715,42 @@ def main():
     info = model.info()
     doc_b = n_bytes / max(n_docs, 1)                      # mean document bytes
     windows = int(sum(synth_windows(off, n) for n in grams))
+
+    cpu = None
+    oracle_check = None
+    hits = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and (table or packed):
+        cpu, ol, hits = cpu_baseline(args, table, grams, data, off, packed)
+        # the timed kernel's own labels (the last step's) against the oracle's
+        # on the CPU sample: the exact code path the value measures
+        dl = d_lab[:len(ol)].cpu().numpy()
+        oracle_check = {"labels_match_oracle": bool(np.array_equal(dl, ol)), "docs_checked": int(len(ol)),
+                        "mismatches": int((dl != ol).sum())}
+
     algo_per_launch = n_bytes + 12 * n_docs               # bytes + int64 offset + int32 label
     algo_per_launch += info["device_bytes"]               # the table, read once per launch (amortised)
+    survey_algo = algo_per_launch + 64 * windows          # SURVEY §8d's notional 64-B sector per window probe
+    model_note = None
     if args.config == 5:
-        # table far beyond LDS / L2: SURVEY §8d charges one 64-B HBM sector per window probe
-        algo_per_launch += 64 * windows
+        # table far beyond LDS / L2: the bytes THIS design must move (keyed
+        # bloom, line layout: one 64-B line per window position for length 3's
+        # word and one for lengths 4..7 together; the 1-/2-byte tests are LDS
+        # bitmaps) plus one 64-B bucket line per table hit (a hit must be
+        # verified; false candidates are the filter's waste, not counted)
+        lens = set(grams)
+        lines = 0
+        if 3 in lens:
+            lines += synth_windows(off, 3)
+        g47 = [n for n in lens if 4 <= n <= 7]
+        if g47:
+            lines += synth_windows(off, min(g47))
+        algo_per_launch += 64 * int(lines)
+        if hits:
+            algo_per_launch += int(64 * hits["hits_per_doc"] * n_docs)
+        model_note = (f"algorithmic bytes: corpus + 12 B/doc + the table once + one 64-B bloom line per window "
+                      f"position per length group ({int(lines)} lines) + one 64-B bucket line per table hit "
+                      f"({'%.1f' % hits['hits_per_doc'] if hits else 'not measured'} per doc, C oracle on the first "
+                      f"{hits['docs'] if hits else 0} docs); survey_frac: SURVEY 8d's 64 B per window probe")
     achieved = algo_per_launch / (kernel_ms * 1e-3) / 1e9
     workload_key = (f"score:docs={n_docs}:bytes={args.doc_min}-{args.doc_max}:L={args.langs}:G={args.grams}"
                     f":K={args.profile_size}")
@@ -715,8 +765,10 @@ def main():
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "lookups_per_s": round(windows / (kernel_ms * 1e-3), 1)}
     if args.config == 5:
-        roofline["note"] = ("SURVEY 8d charges one 64-B HBM sector per window probe (ceiling ~7.0e7 docs/s); the keyed "
-                            "bloom skips most probes, so frac can pass 1: traffic_frac is the measured fraction")
+        roofline["note"] = model_note
+        roofline["survey_algorithmic_bytes_per_launch"] = int(survey_algo)
+        roofline["survey_frac"] = round(survey_algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        roofline["table_hits_per_doc"] = hits["hits_per_doc"] if hits else None
     # the counters' view beside SURVEY's algorithmic one: calibrated HBM bytes
     # per launch over the kernel time, as a fraction of the same peak
     if roofline["traffic"]:
@@ -724,15 +776,6 @@ def main():
         roofline["traffic_GBps"] = round(tgbs, 1)
         roofline["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
 
-    cpu = None
-    oracle_check = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and (table or packed):
-        cpu, ol = cpu_baseline(args, table, grams, data, off, packed)
-        # the timed kernel's own labels (the last step's) against the oracle's
-        # on the CPU sample: the exact code path the value measures
-        dl = d_lab[:len(ol)].cpu().numpy()
-        oracle_check = {"labels_match_oracle": bool(np.array_equal(dl, ol)), "docs_checked": int(len(ol)),
-                        "mismatches": int((dl != ol).sum())}
     alt = None
     if rank == 0 and world == 1 and args.config == 2 and not args.no_alt_paths and not args.empty_table:
         alt = mask_replay_path(args, packed, grams, local, d_bytes, n_bytes, d_off, n_docs, d_lab, stream)

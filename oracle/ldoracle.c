@@ -201,6 +201,24 @@ int ldo_score(const ldo_table* t, const int32_t* G, int32_t nG, const uint8_t* b
     return 0;
 }
 
+/* table hits (windows whose key is in the table) of the documents, summed
+ * (the reference's loop of score_one, LanguageDetectorModel.scala:139-149,
+ * without the adds): bench.py's bytes model of a table beyond the caches */
+int64_t ldo_hits(const ldo_table* t, const int32_t* G, int32_t nG, const uint8_t* bytes, const int64_t* offsets,
+                 int64_t n_docs) {
+    int64_t hits = 0;
+    for (int64_t d = 0; d < n_docs; ++d) {
+        const uint8_t* p = bytes + offsets[d];
+        const int64_t len = offsets[d + 1] - offsets[d];
+        for (int32_t gi = 0; gi < nG; ++gi) {
+            const int64_t n = G[gi];
+            const int64_t nw = len == 0 ? 0 : (len < n ? 1 : len - n + 1), wl = len < n ? len : n;
+            for (int64_t q = 0; q < nw; ++q) hits += hm_find(&t->m, p + q, wl, hbytes(p + q, wl)) >= 0;
+        }
+    }
+    return hits;
+}
+
 /* -------------------------------------------------------------------- count */
 /* reduceGrams keys its sums by (language, gram) (LanguageDetector.scala:57-65):
  * so does this table -- one slot per distinct (gram, language) pair holding

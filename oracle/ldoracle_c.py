@@ -40,6 +40,8 @@ def lib():
         L.ldo_table_destroy.argtypes = [_p]
         L.ldo_score.restype = ctypes.c_int
         L.ldo_score.argtypes = [_p, _p, _i32, _p, _p, _i64, _p, _p, _i32]
+        L.ldo_hits.restype = _i64
+        L.ldo_hits.argtypes = [_p, _p, _i32, _p, _p, _i64]
         L.ldo_count.restype = _p
         L.ldo_count.argtypes = [_p, _p, _p, _i64, _i32, _p, _i32]
         L.ldo_count_mt.restype = _p
@@ -113,6 +115,13 @@ class Table:
         if rc != 0:
             raise ValueError("ldo_score: invalid arguments")
         return labels, scores
+
+    def hits(self, gram_lengths: Sequence[int], data: np.ndarray, offsets: np.ndarray) -> int:
+        """windows (of every n in gram_lengths) whose key is in the table"""
+        g = np.asarray(gram_lengths, dtype=np.int32)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        return int(lib().ldo_hits(self._h, _ptr(g), len(g), _ptr(data), _ptr(offsets), len(offsets) - 1))
 
 
 def count(data: np.ndarray, offsets: np.ndarray, doc_lang: np.ndarray, n_langs: int,

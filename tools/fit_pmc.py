@@ -12,6 +12,9 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import count_traffic, is_count_kernel  # noqa: E402  (one attribution rule for both)
+
 out = sys.argv[1]
 line = json.load(open(os.path.join(out, "WRITE_SIZE.json")))
 cfg = line["config"]
@@ -37,16 +40,21 @@ else:
     calibration = ("FIT v5: write factor = sort_emit's 8 B per corpus byte / its raw WRITE_SIZE; read factor = "
                    "sort_runs' 8 B per key per gram-length pass / its raw FETCH_SIZE; applied to every kernel "
                    "(the random probes of runs_add into T and the radix sort's scatter: approximate)")
-fetch = sum(v.get("FETCH_SIZE", 0.0) for v in raw.values())
-write = sum(v.get("WRITE_SIZE", 0.0) for v in raw.values())
-traffic = fetch * rf + write * wf
-windows = cfg["windows_per_gpu"]
 m = re.search(r"(\d+) languages, grams ([\d,]+), profile", cfg["workload"])
-d = {"workload_key": f"fit:bytes={cfg['corpus_bytes_per_gpu']}:L={m.group(1)}:G={m.group(2)}",
+L, grams = int(m.group(1)), [int(g) for g in m.group(2).split(",")]
+# only the count's own kernels (bench.is_count_kernel): a FIT v4 count sorts
+# nothing, so a radix sort of its run belongs to an export or the table phase
+own = {k: v for k, v in raw.items() if is_count_kernel(k, L, grams)}
+fetch = sum(v.get("FETCH_SIZE", 0.0) for v in own.values())
+write = sum(v.get("WRITE_SIZE", 0.0) for v in own.values())
+windows = cfg["windows_per_gpu"]
+d = {"workload_key": f"fit:bytes={cfg['corpus_bytes_per_gpu']}:L={L}:G={m.group(2)}",
      "per_kernel_raw_bytes_per_count": raw,
+     "excluded_kernels": sorted(k for k in raw if k not in own),
      "read_factor": round(rf, 4), "write_factor": round(wf, 4),
-     "calibration": calibration, "count_only": True,
-     "traffic_bytes_per_launch": round(traffic), "traffic_raw_bytes_per_count": round(fetch + write),
+     "calibration": calibration, "count_only": True}
+traffic = count_traffic(d, L, grams)
+d.update({"traffic_bytes_per_launch": traffic, "traffic_raw_bytes_per_count": round(fetch + write),
      "windows_per_count": windows, "bytes_per_window_corrected": round(traffic / windows, 2),
      "bytes_per_window_raw": round((fetch + write) / windows, 2),
      "count_ms": line["roofline"]["count_ms"],
