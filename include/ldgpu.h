@@ -144,9 +144,9 @@ int ldgpu_model_langs(const ldgpu_model* model, int32_t* n_langs);
  * languages of argmax(scores of d): first maximum, all-zero -> 0.  Chunks of
  * documents are pipelined over two streams (copy-in / score / copy-out of one
  * chunk overlap the host staging of the next); buffers from ldgpu_host_alloc
- * are copied from / to directly, pageable ones through pinned staging.  (This
- * pipeline scores class-mode tables on the ordered replay path, which never
- * waits for the GPU between chunks; see ldgpu_score_device.) */
+ * are copied from / to directly, pageable ones through pinned staging.  (A
+ * class-mode table's replay of ambiguous documents is sized on the device, so
+ * the pipeline never waits for the GPU between chunks.) */
 int ldgpu_score(ldgpu_model* model, const uint8_t* bytes, const int64_t* offsets,
                 int64_t n_docs, int32_t* out_labels, double* out_scores);
 
@@ -296,6 +296,51 @@ int ldgpu_fit_table_info(ldgpu_counts* counts, int64_t* n_rows, int64_t* key_byt
  * takes (config-5 tables: 10M rows x 200 languages). */
 int ldgpu_fit_table_export_masks(ldgpu_counts* counts, uint8_t* key_bytes, int64_t* key_offsets,
                                  uint64_t* masks, double* vals);
+
+/* ----------------------------------------------------------- PREPROCESS */
+/* The caller-side preprocessors on the device, over Java strings (UTF-16 code
+ * units, offsets in units):
+ *   LDGPU_PRE_LOWER  LowerCasePreprocessor (LowerCasePreprocessor.scala:44-76):
+ *                    String.toLowerCase(Locale.forLanguageTag(label)) -- each
+ *                    unit through the host language's 1:1 mapping (`lower`,
+ *                    e.g. Character.toLowerCase), the 1:1 locale rules of
+ *                    tr / az (I -> U+0131, U+0130 -> i) applied on the device;
+ *   LDGPU_PRE_CLEAN  SpecialCharPreprocessor's documented intent
+ *                    (SpecialCharPreprocessor.scala:40-70): the symbols
+ *                    / _ [ ] * ( ) % ^ & @ $ # : | { } < > ~ ` " \ and every
+ *                    space removed (the reference's own pattern never
+ *                    compiles: the JVM throws PatternSyntaxException);
+ *   LDGPU_PRE_LOW_BYTES  the output is the SCORE encoding (the low byte of each
+ *                    unit, LanguageDetectorModel.scala:226) instead of units:
+ *                    ldgpu_score_device's input.
+ * A document whose lower-casing is not 1:1 or needs context -- a unit marked
+ * in `special` (U+0130 outside tr / az, capital sigma's Final_Sigma rule, the
+ * high surrogates of cased supplementary planes), tr / az "I" + U+0307, lt
+ * I / J / U+012E before a mark above, U+00CC / U+00CD / U+0128 -- is not
+ * processed: host[d] = 1 and its output is empty; the caller lower-cases it
+ * itself (the Java locale rules stay on the host). */
+#define LDGPU_PRE_LOWER      1
+#define LDGPU_PRE_CLEAN      2
+#define LDGPU_PRE_LOW_BYTES  4
+#define LDGPU_LOCALE_ROOT    0  /* per-document locale class of the label */
+#define LDGPU_LOCALE_TR_AZ   1  /* Locale.forLanguageTag(label).getLanguage() is tr or az */
+#define LDGPU_LOCALE_LT      2  /* ... lt */
+
+typedef struct ldgpu_casemap ldgpu_casemap;
+/* lower: [65536] the lower-case unit of each unit (1:1); special: [8192]
+ * bytes, bit u set = unit u sends its document to the host. */
+int ldgpu_casemap_create(ldgpu_ctx* ctx, const uint16_t* lower, const uint8_t* special, ldgpu_casemap** out);
+int ldgpu_casemap_destroy(ldgpu_casemap* map);
+/* Device buffers, asynchronous on `stream` (NULL: the default stream).
+ * d_out holds up to d_offsets[n_docs] - d_offsets[0] units (bytes with
+ * LDGPU_PRE_LOW_BYTES); d_out_offsets [n_docs + 1] receives the output's
+ * offsets (from 0); d_host [n_docs]; d_locale (nullable: root) [n_docs]. */
+int ldgpu_preprocess_device(ldgpu_casemap* map, const uint16_t* d_units, const int64_t* d_offsets,
+                            int64_t n_docs, const uint8_t* d_locale, int32_t flags, void* d_out,
+                            int64_t* d_out_offsets, uint8_t* d_host, void* stream);
+/* The same over host buffers (copied in and out; returns when done). */
+int ldgpu_preprocess(ldgpu_casemap* map, const uint16_t* units, const int64_t* offsets, int64_t n_docs,
+                     const uint8_t* locale, int32_t flags, void* out, int64_t* out_offsets, uint8_t* host);
 
 #ifdef __cplusplus
 }

@@ -459,6 +459,123 @@ extern "C" int ldgpu_host_free(ldgpu_ctx* c, void* p) {
     return ok();
 }
 
+// --------------------------------------------------------------- preprocess
+// The caller-side preprocessors (ldgpu_pre.hip; include/ldgpu.h PREPROCESS):
+// the host language's 1:1 lower-case mapping of UTF-16 units and the units
+// whose documents stay on the host, resident on the context's device.
+struct ldgpu_casemap {
+    ldgpu_ctx* ctx = nullptr;
+    uint16_t* d_map = nullptr;
+    uint32_t* d_special = nullptr;
+};
+
+extern "C" int ldgpu_casemap_create(ldgpu_ctx* ctx, const uint16_t* lower, const uint8_t* special, ldgpu_casemap** out) {
+    if (!ctx || !lower || !special || !out) return fail(LDGPU_EINVAL, "ctx/lower/special/out is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto* m = new ldgpu_casemap();
+    m->ctx = ctx;
+    hipError_t e = hipMalloc((void**)&m->d_map, 65536 * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&m->d_special, 8192);
+    if (e == hipSuccess) e = hipMemcpy(m->d_map, lower, 65536 * sizeof(uint16_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(m->d_special, special, 8192, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(m->d_map);
+        (void)hipFree(m->d_special);
+        delete m;
+        return fail(e == hipErrorOutOfMemory ? LDGPU_ENOMEM : LDGPU_EDEVICE, "casemap upload: %s", hipGetErrorString(e));
+    }
+    *out = m;
+    return ok();
+}
+
+extern "C" int ldgpu_casemap_destroy(ldgpu_casemap* m) {
+    if (!m) return ok();
+    (void)hipSetDevice(m->ctx->device);
+    (void)hipFree(m->d_map);
+    (void)hipFree(m->d_special);
+    delete m;
+    return ok();
+}
+
+extern "C" int ldgpu_preprocess_device(ldgpu_casemap* m, const uint16_t* d_units, const int64_t* d_offsets,
+                                       int64_t n_docs, const uint8_t* d_locale, int32_t flags, void* d_out,
+                                       int64_t* d_out_offsets, uint8_t* d_host, void* stream) {
+    if (!m) return fail(LDGPU_EINVAL, "casemap is NULL");
+    if (n_docs < 0) return fail(LDGPU_EINVAL, "n_docs < 0");
+    if (flags & ~(LDGPU_PRE_LOWER | LDGPU_PRE_CLEAN | LDGPU_PRE_LOW_BYTES))
+        return fail(LDGPU_EINVAL, "unknown preprocess flags 0x%x", flags);
+    if (!d_out_offsets || (n_docs > 0 && (!d_offsets || !d_host || !d_out)))
+        return fail(LDGPU_EINVAL, "device pointer is NULL");
+    if (n_docs >= (int64_t)std::numeric_limits<int>::max())
+        return fail(LDGPU_EUNSUPPORTED, "%lld documents in one call (the scan takes < 2^31)", (long long)n_docs);
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(m->ctx->device));
+    PreParams p{};
+    p.units = d_units;
+    p.offsets = d_offsets;
+    p.n_docs = n_docs;
+    p.locale = d_locale;
+    p.flags = flags;
+    p.map = m->d_map;
+    p.special = m->d_special;
+    p.out = d_out;
+    p.host = d_host;
+    size_t scan_bytes = 0;
+    HIP_TRY(launch_preprocess(p, nullptr, nullptr, nullptr, &scan_bytes, m->ctx->cus, st));
+    int64_t* len_tmp = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&len_tmp, sizeof(int64_t) * (size_t)(n_docs + 1) + scan_bytes + 16, st));
+    const hipError_t e = launch_preprocess(p, len_tmp, d_out_offsets, len_tmp + n_docs + 1, &scan_bytes, m->ctx->cus, st);
+    (void)hipFreeAsync(len_tmp, st);
+    HIP_TRY(e);
+    return ok();
+}
+
+extern "C" int ldgpu_preprocess(ldgpu_casemap* m, const uint16_t* units, const int64_t* offsets, int64_t n_docs,
+                                const uint8_t* locale, int32_t flags, void* out, int64_t* out_offsets, uint8_t* host) {
+    if (!m) return fail(LDGPU_EINVAL, "casemap is NULL");
+    if (int rc = check_offsets(offsets, n_docs)) return rc;
+    if (!out_offsets || (n_docs > 0 && (!host || !out))) return fail(LDGPU_EINVAL, "output pointer is NULL");
+    const int64_t b0 = n_docs > 0 ? offsets[0] : 0, nu = n_docs > 0 ? offsets[n_docs] - b0 : 0;
+    if (nu > 0 && !units) return fail(LDGPU_EINVAL, "units is NULL");
+    HIP_TRY(hipSetDevice(m->ctx->device));
+    const size_t ob = (flags & LDGPU_PRE_LOW_BYTES) ? 1 : 2;
+    std::vector<int64_t> off0((size_t)n_docs + 1);
+    for (int64_t i = 0; i <= n_docs; ++i) off0[(size_t)i] = n_docs > 0 ? offsets[i] - b0 : 0;
+    // one device block: units, offsets (in, out), locale, host flags, output
+    const size_t a_units = ((size_t)nu * 2 + 15) & ~(size_t)15, a_off = sizeof(int64_t) * ((size_t)n_docs + 1);
+    const size_t a_small = ((size_t)n_docs + 15) & ~(size_t)15, a_out = ((size_t)nu * ob + 15) & ~(size_t)15;
+    uint8_t* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, a_units + 2 * a_off + 2 * a_small + a_out + 16));
+    uint16_t* d_units = (uint16_t*)d;
+    int64_t* d_off = (int64_t*)(d + a_units);
+    int64_t* d_ooff = (int64_t*)(d + a_units + a_off);
+    uint8_t* d_loc = d + a_units + 2 * a_off;
+    uint8_t* d_host = d_loc + a_small;
+    void* d_out = d_host + a_small;
+    hipStream_t st = m->ctx->stream;
+    int rc = LDGPU_OK;
+    hipError_t e = hipSuccess;
+    {
+        std::lock_guard<std::mutex> lock(m->ctx->mu);  // the context's stream
+        if (nu) e = hipMemcpyAsync(d_units, units + b0, (size_t)nu * 2, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_off, off0.data(), a_off, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && locale && n_docs)
+            e = hipMemcpyAsync(d_loc, locale, (size_t)n_docs, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            rc = ldgpu_preprocess_device(m, d_units, d_off, n_docs, locale ? d_loc : nullptr, flags, d_out, d_ooff,
+                                         d_host, st);
+        if (e == hipSuccess && !rc) e = hipMemcpyAsync(out_offsets, d_ooff, a_off, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && !rc && n_docs) e = hipMemcpyAsync(host, d_host, (size_t)n_docs, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && !rc) e = hipStreamSynchronize(st);
+        if (e == hipSuccess && !rc && out_offsets[n_docs] > 0)
+            e = hipMemcpy(out, d_out, (size_t)out_offsets[n_docs] * ob, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d);
+    if (rc) return rc;
+    HIP_TRY(e);
+    return ok();
+}
+
 // -------------------------------------------------------------------- model
 struct ldgpu_model {
     ldgpu_ctx* ctx = nullptr;

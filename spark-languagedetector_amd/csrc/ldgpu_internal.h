@@ -228,4 +228,24 @@ hipError_t launch_combine_blocks(int64_t n, int nb, const int32_t* lab, const do
 // (chunks: a count-mode table's keyed bloom in the chunk layout)
 hipError_t score_prepare(int slices, int mode, bool lds_bloom, bool chunks, size_t lds_bytes, int* blocks_per_cu);
 
+// ------------------------------------------------------------- PREPROCESS
+// The caller-side preprocessors (ldgpu_pre.hip; flags and locale classes:
+// LDGPU_PRE_* / LDGPU_LOCALE_* of include/ldgpu.h)
+struct PreParams {
+    const uint16_t* units;      // UTF-16 code units
+    const int64_t* offsets;     // [n_docs + 1], in units
+    int64_t n_docs;
+    const uint8_t* locale;      // nullable [n_docs]
+    int32_t flags;
+    const uint16_t* map;        // [65536] 1:1 lower-case unit
+    const uint32_t* special;    // [2048] words: units whose document goes to the host
+    void* out;                  // units (u16) or, LDGPU_PRE_LOW_BYTES, bytes
+    uint8_t* host;              // [n_docs] 1 = redo on the host (empty output)
+};
+// pass 1 (kept units per document: len_tmp [n_docs + 1]), the scan into
+// out_off [n_docs + 1], pass 2 (the output); scan_tmp == nullptr: *scan_bytes =
+// the scan's scratch, nothing launched
+hipError_t launch_preprocess(const PreParams& p, int64_t* len_tmp, int64_t* out_off, void* scan_tmp, size_t* scan_bytes,
+                             int cus, hipStream_t stream);
+
 }  // namespace ldgpu

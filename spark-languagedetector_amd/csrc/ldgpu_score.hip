@@ -955,7 +955,7 @@ __device__ __forceinline__ void append_pack(uint32_t* queue, int& qn, const uint
     }
 }
 
-template <int N, bool FULL, int S = 1, bool PACK = false>
+template <int N, bool FULL, int S = 1, bool PACK = false, int NK = kSub>
 __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
                                              const Windows& x, int32_t nw, int lane, const PackPos* pk = nullptr) {
     const uint8_t* l1 = reinterpret_cast<const uint8_t*>(img + p.direct_off);
@@ -967,16 +967,16 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
     bool hit[kSub];
     if constexpr (N == 1) {
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) lang[k] = l1[x.lo[k] & 0xffu];
+        for (int k = 0; k < NK; ++k) lang[k] = l1[x.lo[k] & 0xffu];
         // (a zero-extended byte: 0xff is its only value >= 0xff)
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) hit[k] = lang[k] < 0xffu;
+        for (int k = 0; k < NK; ++k) hit[k] = lang[k] < 0xffu;
     } else {
         uint32_t w[kSub];
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) w[k] = img[kBmp1Words + bmp2_word(x.lo[k])];
+        for (int k = 0; k < NK; ++k) w[k] = img[kBmp1Words + bmp2_word(x.lo[k])];
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) {
+        for (int k = 0; k < NK; ++k) {
             // bit (lo & 31) of the word; the offset / width operands of v_bfe
             // take their low 5 bits, so no masking
             hit[k] = __builtin_amdgcn_ubfe(w[k], x.lo[k], 1) != 0u;
@@ -990,7 +990,7 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
     }
     if constexpr (PACK) {
 #pragma unroll
-        for (int k = 0; k < kSub; ++k) {
+        for (int k = 0; k < NK; ++k) {
             hit[k] = hit[k] && pk->rem[k] >= N;
             lang[k] += (pk->tb[k] >> 8) * 64u * S;
         }
@@ -1000,7 +1000,7 @@ __device__ __forceinline__ void direct_count(const ScoreParams& p, const WaveLds
         for (int k = FULL ? kSub - 1 : 0; k < kSub; ++k) hit[k] = hit[k] && 64 * k + lane < nw;
     }
 #pragma unroll
-    for (int k = 0; k < kSub; ++k)
+    for (int k = 0; k < NK; ++k)
         if (hit[k]) count_inc<PACK>(cnt, lang[k], inc);
 }
 
@@ -1025,6 +1025,14 @@ __device__ __forceinline__ uint32_t keyed_hash(const Windows& x, int k) {
     const uint32_t lo = N >= 4 ? x.lo[k] : x.lo[k] & ((1u << (8 * N)) - 1u);
     const uint32_t hi = N <= 4 ? 0u : x.hi[k] & ((1u << (8 * (N < 7 ? N - 4 : 3))) - 1u);
     return kb_hash(lo, hi, (uint32_t)N);
+}
+
+// keyed_hash of sub-block 0's window for a length n known only at run time
+// (n in 3..7, after unrolling a constant)
+__device__ __forceinline__ uint32_t kb_hash_n(const Windows& x, int n) {
+    const uint32_t lo = n >= 4 ? x.lo[0] : x.lo[0] & ((1u << (8 * n)) - 1u);
+    const uint32_t hi = n <= 4 ? 0u : x.hi[0] & ((1u << (8 * (n < 7 ? n - 4 : 3))) - 1u);
+    return kb_hash(lo, hi, (uint32_t)n);
 }
 
 // keyed Bloom (global memory): the words of lengths 3 .. 2 + PRE are loaded
@@ -1205,6 +1213,127 @@ __device__ __forceinline__ void probe_pack(const ScoreParams& p, const WaveLds& 
         qn = 0;
     }
     append_pack(wl.queue, qn, m, (uint32_t)N, pk, dummy_a);
+}
+
+#ifndef LDGPU_PACK_KOUTER
+#define LDGPU_PACK_KOUTER 1
+#endif
+
+// Packs, one sub-block at a time (LDGPU_PACK_KOUTER): count mode is order-
+// free, so the 64 positions of sub-block k are tested for every gram length
+// before sub-block k + 1 is loaded -- only one position's window bytes, bloom
+// chunk / word and pack position are live per lane (the pack kernel ran at
+// the 80-VGPR cap with 14 VGPRs spilled when all four sub-blocks' were: config
+// 4's scratch writes).  Sub-block k's tests of length N (x, f, pk hold the
+// lane's position 64 k + lane in their index 0).
+template <int N, int S, int KEYED, bool WIDE>
+__device__ __forceinline__ void probe_pack1(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                            const FWords& f, const Windows& x, const PackPos& pk, int lane, int& qn,
+                                            const DocSrc& src, uint32_t dummy_a, uint32_t fm,
+                                            const uint32_t (&kw)[kPreN][kSub]) {
+    if (!((fm >> N) & 1u)) return;
+    if (ablated(p, N <= 2 ? 8 : 16)) return;
+    if constexpr (N <= 2) {
+        if ((fm >> kFmDirect) & 1u) {
+            direct_count<N, false, S, true, 1>(p, wl, img, x, 0, lane, &pk);
+            return;
+        }
+    }
+    constexpr int KIND = N < 3 ? N : kind_of(KEYED);
+    constexpr uint32_t sh = N < 3 ? 0u : (KEYED ? (uint32_t)N : pf_shift(N)), mul = N < 3 ? 0u : pf_mult(N);
+    uint32_t w, bit, bit2;
+    if constexpr (KIND == 4 && N - 3 < kPackPreN) {
+        w = kw[N - 3][0];
+        bit = bit2 = keyed_hash<N>(x, 0) >> kb_sbit(N, f.lines, f.gshift);
+    } else {
+        filter_word<KIND>(img, sh, mul, f, x, 0, w, bit, bit2);
+    }
+    uint64_t m[kSub] = {__ballot(filter_hit(w, bit, bit2) && pk.rem[0] >= N), 0, 0, 0};
+    if (qn + __popcll(m[0]) > kQueueCap) {
+        double acc[S];  // unused in count mode
+        flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
+        qn = 0;
+    }
+    append_pack(wl.queue, qn, m, (uint32_t)N, pk, dummy_a);
+}
+
+template <int S, int KEYED, bool WIDE>
+__device__ __forceinline__ void score_pack_kouter(const ScoreParams& p, const WaveLds& wl, const uint32_t* img,
+                                                  const uint32_t* bloom, const DocSrc& src, int32_t e1, int32_t e2,
+                                                  int32_t e3, int32_t tot, int nd, int i, int lane) {
+    uint32_t fm = __builtin_amdgcn_readfirstlane(p.fast_mask | (p.direct_words ? 1u << kFmDirect : 0u));
+    asm volatile("" : "+s"(fm));
+    int qn = 0;
+    if (ablated(p, 2)) fm = 0;
+    const uint32_t dummy_a = (uint32_t)(uintptr_t)(reinterpret_cast<uint32_t*>(wl.hits) + lane);
+#pragma unroll 1
+    for (int k = 0; 64 * k < tot; ++k) {  // (uniform: tot <= 256)
+        Windows x;
+        {
+            const uint32_t a = (uint32_t)src.base + 64u * k + (uint32_t)lane;
+            const uint32_t sh = a & 3u;
+            const uint32_t* w = src.lds + (a >> 2);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            x.lo[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            x.hi[0] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        }
+        FWords f;
+        if constexpr (KEYED == 2) {
+            f.ck[0] = reinterpret_cast<const u32x4*>(bloom)[kb_chunk(x.lo[0]) >> p.bloom_shift];
+        } else if constexpr (KEYED) {
+            f.gb = bloom;
+            f.gshift = p.bloom_shift;
+            f.lines = p.kb_lines != 0;
+            f.w3[0] = f.lines ? kb_line16(x.lo[0], p.bloom_shift) : 0u;
+        } else {
+            f.w3[0] = bloom[pf_word(x.lo[0], p.bloom_shift)];
+        }
+        PackPos pk;
+        {
+            const int32_t j = 64 * k + lane;
+            const uint32_t d = (uint32_t)(j >= e1) + (uint32_t)(j >= e2) + (uint32_t)(j >= e3);
+            const int32_t end = j < e1 ? e1 : (j < e2 ? e2 : (j < e3 ? e3 : tot));
+            pk.rem[0] = end - j;
+            pk.tb[0] = (d << 8) | (uint32_t)j;
+        }
+        uint32_t kw[kPreN][kSub];
+        if constexpr (KEYED == 1) {
+#pragma unroll
+            for (int n = 3; n < 3 + kPackPreN; ++n)
+                if ((fm >> n) & 1u)
+                    kw[n - 3][0] = f.gb[(n >= 4 ? f.w3[0] : 0u) + (kb_hash_n(x, n) >> kb_sword(n, f.lines, f.gshift))];
+        }
+        probe_pack1<1, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        probe_pack1<2, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        probe_pack1<3, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        probe_pack1<4, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        probe_pack1<5, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        probe_pack1<6, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        probe_pack1<7, S, KEYED, WIDE>(p, wl, img, f, x, pk, lane, qn, src, dummy_a, fm, kw);
+        for (uint32_t wm = WIDE ? (fm >> 8) & 0xffu : 0u; wm; wm &= wm - 1u) {  // wide lengths 8..15
+            const int n = 8 + __builtin_ctz(wm);
+            constexpr int K3 = kind_of(KEYED);
+            const uint32_t sh = KEYED ? (uint32_t)n : pf_shift(n), mul = pf_mult(n);
+            uint32_t w, bit, bit2;
+            filter_word<K3>(img, sh, mul, f, x, 0, w, bit, bit2);
+            uint64_t m[kSub] = {__ballot(filter_hit(w, bit, bit2) && pk.rem[0] >= n), 0, 0, 0};
+            if (qn + __popcll(m[0]) > kQueueCap) {
+                double acc[S];
+                flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
+                qn = 0;
+            }
+            append_pack(wl.queue, qn, m, (uint32_t)n, pk, dummy_a);
+        }
+    }
+    if (ablated(p, 1)) qn = 0;
+    if (qn) {
+        double acc[S];
+        flush<S, 3, true, KEYED, true, WIDE>(p, wl, qn, src, acc, lane, true);
+    }
+    for (int q = 0; q < (ablated(p, 32) ? 0 : nd); ++q) {
+        const int lab = count_argmax<S>(p, reinterpret_cast<uint16_t*>(count_area(wl)) + q * 64 * S, lane);
+        if (lane == 0) wl.labels[i + q] = lab;
+    }
 }
 
 // One pack: documents [i, i + nd) of the staged group, ends e1 < e2 < e3 <=
@@ -1580,8 +1709,12 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
                         }
                         if (nd > 1) {
                             const int32_t tot = e[nd - 1];
-                            score_pack<S, BL, WIDE>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
-                                                 nd > 3 ? e[2] : tot, tot, nd, i, lane);
+                            if constexpr (LDGPU_PACK_KOUTER)
+                                score_pack_kouter<S, BL, WIDE>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
+                                                               nd > 3 ? e[2] : tot, tot, nd, i, lane);
+                            else
+                                score_pack<S, BL, WIDE>(p, wl, lds, bloom, src, e[0], nd > 2 ? e[1] : tot,
+                                                     nd > 3 ? e[2] : tot, tot, nd, i, lane);
                             i += nd;
                             continue;
                         }

@@ -87,7 +87,15 @@ SIGNATURES = [
     ("ldgpu_fit_table_info", ctypes.c_int, [_p, _pi64, _pi64]),
     ("ldgpu_fit_table_export", ctypes.c_int, [_p, _p, _p, _p]),
     ("ldgpu_fit_table_export_masks", ctypes.c_int, [_p, _p, _p, _p, _p]),
+    ("ldgpu_casemap_create", ctypes.c_int, [_p, _p, _p, _pp]),
+    ("ldgpu_casemap_destroy", ctypes.c_int, [_p]),
+    ("ldgpu_preprocess_device", ctypes.c_int, [_p, _p, _p, _i64, _p, _i32, _p, _p, _p, _p]),
+    ("ldgpu_preprocess", ctypes.c_int, [_p, _p, _p, _i64, _p, _i32, _p, _p, _p]),
 ]
+
+# include/ldgpu.h PREPROCESS
+PRE_LOWER, PRE_CLEAN, PRE_LOW_BYTES = 1, 2, 4
+LOCALE_ROOT, LOCALE_TR_AZ, LOCALE_LT = 0, 1, 2
 
 _libs = {}
 _lock = threading.RLock()
@@ -190,8 +198,8 @@ def device_count() -> int:
 
 # the sources the library is built from, in the Makefile's PROV order
 _PROV = ["csrc/ldgpu_api.hip", "csrc/ldgpu_score.hip", "csrc/ldgpu_fit.hip", "csrc/ldgpu_general.hip",
-         "csrc/ldgpu_long.hip", "csrc/ldgpu_replay.hip", "csrc/ldgpu_common.h", "csrc/ldgpu_internal.h",
-         "csrc/ldgpu_fit.h", "../include/ldgpu.h"]
+         "csrc/ldgpu_long.hip", "csrc/ldgpu_replay.hip", "csrc/ldgpu_pre.hip", "csrc/ldgpu_common.h",
+         "csrc/ldgpu_internal.h", "csrc/ldgpu_fit.h", "../include/ldgpu.h"]
 
 
 def tree_source_hash() -> str:

@@ -4,8 +4,15 @@ Reference (org.apache.spark.ml.feature.languagedetection.preprocessing):
   LowerCasePreprocessor    LowerCasePreprocessor.scala:19-76
   SpecialCharPreprocessor  SpecialCharPreprocessor.scala:19-70
 
-Both are plain host-side Transformers a user runs before ``fit``/``transform``;
-they are not on the GPU path.  Their behaviour is reproduced as written,
+Both are host-side Transformers a user runs before ``fit``/``transform``.
+Given ``device=``, LowerCasePreprocessor lower-cases on the GPU
+(ldgpu_preprocess, ``csrc/ldgpu_pre.hip``): each UTF-16 unit through the 1:1
+mapping of ``str.lower``, the tr/az rules that stay 1:1 on the device, and
+the documents whose lower-casing is not 1:1 or needs context (U+0130 outside
+tr/az, capital sigma, the lt rules, tr/az "I" + U+0307, cased supplementary
+characters) redone here by ``java_lower``.  ``preprocess_device`` also
+applies the documented SpecialChar cleanup and can emit the SCORE encoding
+packed for the scoring kernels.  Their behaviour is reproduced as written,
 including the reference's quirks:
 
 * ``setInputCol`` sets ``outputCol`` (LowerCase :32, SpecialChar :30): the
@@ -32,6 +39,8 @@ from __future__ import annotations
 
 import re
 from typing import Dict, Optional
+
+import numpy as np
 
 from .api import NullPointerException, _Params, _random_uid
 
@@ -116,13 +125,15 @@ def _require(df, *cols: str) -> None:
 
 
 class LowerCasePreprocessor(_Params):
-    """LowerCasePreprocessor (LowerCasePreprocessor.scala:19-76)."""
+    """LowerCasePreprocessor (LowerCasePreprocessor.scala:19-76); device: lower-
+    case on that GPU (preprocess_device), else on the host."""
 
     _defaults = {"outputCol": "fulltext", "labelCol": "lang"}
 
-    def __init__(self, uid: Optional[str] = None):
+    def __init__(self, uid: Optional[str] = None, device: Optional[int] = None):
         super().__init__()
         self.uid = uid or _random_uid("LowerCasePreprocessor")
+        self._device = device
 
     def setInputCol(self, value: str):  # sets outputCol, as in the reference (:32)
         return self._set("outputCol", value)
@@ -145,13 +156,16 @@ class LowerCasePreprocessor(_Params):
         df = _frame(dataset)
         col, label = self.getOutputCol(), self.getLabelCol()
         _require(df, col, label)
-        values = []
-        for text, lang in zip(df[col], df[label]):
+        texts, langs = list(df[col]), list(df[label])
+        for text, lang in zip(texts, langs):
             if lang is None:
                 raise NullPointerException("Locale.forLanguageTag(null)")
             if text is None:
                 raise NullPointerException("text is null")
-            values.append(java_lower(text, lang))
+        if self._device is not None:
+            values = preprocess_device(texts, langs, lower=True, device=self._device)
+        else:
+            values = [java_lower(t, lang) for t, lang in zip(texts, langs)]
         return _move_to_end(df, col, values)
 
 
@@ -196,3 +210,67 @@ def intended_special_char_clean(text: str) -> str:
         raise NullPointerException("text is null")
     text = re.sub("[" + re.escape(SPECIAL_CHAR_PATTERN) + "]", "", text)
     return re.sub("  *", "", text)
+
+
+_CASEMAPS: Dict[object, object] = {}
+
+
+def _casemap(device, variant="product"):
+    from .runtime import DeviceCaseMap
+    key = (device, variant)
+    if key not in _CASEMAPS:
+        _CASEMAPS[key] = DeviceCaseMap(device, variant=variant)
+    return _CASEMAPS[key]
+
+
+def _host_pre(text: str, lang, lower: bool, clean: bool) -> str:
+    if lower:
+        text = java_lower(text, lang)
+    return intended_special_char_clean(text) if clean else text
+
+
+def preprocess_device(texts, langs=None, lower: bool = True, clean: bool = False, device: int = 0,
+                      score_encoding: bool = False):
+    """LowerCasePreprocessor's lower-casing (labels `langs` as locales) and/or
+    the documented SpecialChar cleanup (``intended_special_char_clean``) on the
+    GPU (ldgpu_preprocess).  Returns the texts, or with ``score_encoding`` the
+    SCORE input packed as ``encoding.pack`` does (data, offsets): the low byte
+    of each UTF-16 unit, what ``LanguageDetectorModel.transform`` scores.  The
+    documents the device leaves to the host (not 1:1, or context-dependent)
+    are done by ``java_lower`` here."""
+    from . import _lib, encoding
+    from .runtime import DeviceCaseMap, locale_class
+    texts = list(texts)
+    for t in texts:
+        if t is None:
+            raise NullPointerException("text is null")
+    if lower:
+        if langs is None:
+            raise ValueError("lower-casing needs the labels (the locale of each row)")
+        langs = list(langs)
+        for lang in langs:
+            if lang is None:
+                raise NullPointerException("Locale.forLanguageTag(null)")
+        locale = np.fromiter((locale_class(lang) for lang in langs), dtype=np.uint8, count=len(texts))
+    else:
+        langs = [None] * len(texts)
+        locale = None
+    flags = (_lib.PRE_LOWER if lower else 0) | (_lib.PRE_CLEAN if clean else 0) | \
+        (_lib.PRE_LOW_BYTES if score_encoding else 0)
+    units, off = DeviceCaseMap.pack_units(texts)
+    out, out_off, host = _casemap(device).run(units, off, locale, flags)
+    redo = np.nonzero(host)[0]
+    if score_encoding:
+        if len(redo) == 0:
+            n = int(out_off[-1])
+            data = np.zeros(((n + 3) // 4) * 4 + 4, dtype=np.uint8)
+            data[:n] = out[:n]
+            return data, out_off
+        parts = [out[out_off[i]:out_off[i + 1]].tobytes() for i in range(len(texts))]
+        for i in redo:
+            parts[i] = encoding.score_bytes(_host_pre(texts[i], langs[i], lower, clean))
+        return encoding.pack(parts)
+    res = [out[out_off[i]:out_off[i + 1]].tobytes().decode("utf-16-le", "surrogatepass") for i in range(len(texts))]
+    for i in redo:
+        res[i] = _host_pre(texts[i], langs[i], lower, clean)
+    return res

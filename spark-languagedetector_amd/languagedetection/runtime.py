@@ -327,3 +327,90 @@ class DeviceCounts(_Owner):
         self._check(self.lib.ldgpu_fit_table_export_masks(self.h, _ptr(kb), _ptr(ko), _ptr(masks), _ptr(vals)))
         return kb, ko, masks[:n.value], vals[:n.value]
 
+
+
+def case_tables() -> Tuple[np.ndarray, np.ndarray]:
+    """The host language's 1:1 lower-case mapping of UTF-16 units (str.lower of
+    one character; Java: Character.toLowerCase) and the `special` bitmap of the
+    units whose String.toLowerCase is not that mapping or needs context
+    (include/ldgpu.h PREPROCESS): U+0130 (-> "i" + U+0307), capital sigma
+    (Final_Sigma), and the high surrogates of supplementary planes holding
+    cased letters."""
+    global _CASE_TABLES
+    if _CASE_TABLES is None:
+        lower = np.arange(65536, dtype=np.uint16)
+        special = np.zeros(65536, dtype=bool)
+        for c in range(65536):
+            if 0xD800 <= c <= 0xDFFF:
+                continue
+            low = chr(c).lower()
+            if len(low) == 1 and ord(low) < 0x10000:
+                lower[c] = ord(low)
+            else:
+                special[c] = True
+        special[0x3A3] = True
+        for c in range(0x10000, 0x110000):
+            if chr(c).lower() != chr(c):
+                special[0xD800 + ((c - 0x10000) >> 10)] = True
+        _CASE_TABLES = (lower, np.packbits(special, bitorder="little"))
+    return _CASE_TABLES
+
+
+_CASE_TABLES = None
+
+
+def locale_class(lang_tag) -> int:
+    """Locale.forLanguageTag(tag).getLanguage() -> the device's locale class."""
+    from .preprocessing import _language_of
+    lang = _language_of(lang_tag)
+    return _lib.LOCALE_TR_AZ if lang in ("tr", "az") else (_lib.LOCALE_LT if lang == "lt" else _lib.LOCALE_ROOT)
+
+
+class DeviceCaseMap(_Owner):
+    """The preprocessors on the GPU (ldgpu_preprocess; include/ldgpu.h
+    PREPROCESS): lower-casing and the symbol / space cleanup over UTF-16 units."""
+
+    def __init__(self, device: Optional[int] = None, variant: str = "product"):
+        self.lib = _lib.load(variant=variant)
+        self.ctx = _lib.context(device, variant=variant)
+        lower, special = case_tables()
+        h = ctypes.c_void_p()
+        self._check(self.lib.ldgpu_casemap_create(self.ctx, _ptr(lower), _ptr(special), ctypes.byref(h)))
+        self.h = h.value
+
+    @staticmethod
+    def pack_units(texts: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+        """Java strings: UTF-16 code units (u16) and offsets in units."""
+        enc = [t.encode("utf-16-le", "surrogatepass") for t in texts]
+        lens = np.fromiter((len(e) // 2 for e in enc), dtype=np.int64, count=len(enc))
+        off = np.zeros(len(enc) + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        units = np.frombuffer(b"".join(enc) + b"\0\0", dtype=np.uint16)
+        return np.ascontiguousarray(units), off
+
+    def run(self, units: np.ndarray, offsets: np.ndarray, locale: Optional[np.ndarray], flags: int
+            ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(output units or bytes, output offsets, host flags) of ldgpu_preprocess."""
+        n = len(offsets) - 1
+        units = np.ascontiguousarray(units, dtype=np.uint16)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        if locale is not None:
+            locale = np.ascontiguousarray(locale, dtype=np.uint8)
+        cap = max(int(offsets[-1] - offsets[0]) if n else 0, 1)
+        out = np.zeros(cap + 4, dtype=np.uint8 if flags & _lib.PRE_LOW_BYTES else np.uint16)
+        out_off = np.zeros(n + 1, dtype=np.int64)
+        host = np.zeros(max(n, 1), dtype=np.uint8)
+        self._check(self.lib.ldgpu_preprocess(self.h, _ptr(units), _ptr(offsets), n, _ptr(locale), flags,
+                                              _ptr(out), _ptr(out_off), _ptr(host)))
+        return out, out_off, host[:n]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ldgpu_casemap_destroy(ctypes.c_void_p(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -98,3 +98,16 @@ def test_language_enumeration():
     assert Language(0).name == "ab" and str(Language(181)) == "zu"
     with pytest.raises(KeyError, match="No value found for 'xx'"):
         Language.withName("xx")
+
+
+def test_case_tables_for_the_device():
+    """The 1:1 lower-case table and the host-only units handed to
+    ldgpu_casemap_create (include/ldgpu.h PREPROCESS)."""
+    import numpy as np
+    from languagedetection.runtime import case_tables, locale_class
+    lower, special = case_tables()
+    bits = np.unpackbits(special, bitorder="little").astype(bool)
+    assert lower[ord("A")] == ord("a") and lower[ord("a")] == ord("a") and lower[0xC4] == 0xE4
+    assert lower[ord("I")] == ord("i")                     # root locale; tr/az is the device's rule
+    assert bits[0x130] and bits[0x3A3] and bits[0xD801] and not bits[ord("A")] and not bits[0xD800]
+    assert [locale_class(t) for t in ("tr", "az-Latn", "lt", "en", "?", "TR")] == [1, 1, 2, 0, 0, 1]
