@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--langs", type=int, default=None)
     ap.add_argument("--grams", type=str, default=None)
     ap.add_argument("--profile-size", type=int, default=None)
-    ap.add_argument("--pool", type=int, default=250_000, help="distinct generated docs, tiled to --docs")
+    ap.add_argument("--pool", type=int, default=None,
+                    help="distinct docs generated on the host and tiled to --docs (default: every document "
+                         "distinct, drawn on the GPU)")
     ap.add_argument("--train-docs", type=int, default=None, help="training docs per language for the table")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -669,16 +671,28 @@ def main():
         else:
             model = DeviceModel.from_masks(*packed, args.langs, grams, device=local)
 
-    # this rank's documents: a generated pool tiled to --docs, resident in HBM
-    pool = min(args.pool, args.docs)
-    pdata, poff, plang = synth.generate(ls, pool, args.doc_min, args.doc_max,
-                                        seed=synth.SEED_BASE + args.config + 1000 * rank)
-    data, off, _ = synth.tile(pdata, poff, plang, args.docs)
+    # this rank's documents, resident in HBM: every one distinct, drawn on the
+    # GPU (synth.generate_device), or (--pool) a host-generated pool tiled
+    if args.pool is None:
+        pool = args.docs
+        d_bytes, d_off, d_plang = synth.generate_device(ls, args.docs, args.doc_min, args.doc_max,
+                                                        seed=synth.SEED_BASE + args.config + 1000 * rank, device=dev,
+                                                        chunk_docs=1 << 20)
+        off = d_off.cpu().numpy()
+        n_bytes = int(off[-1])
+        data = d_bytes[:n_bytes].cpu().numpy()
+        plang = d_plang.cpu().numpy()
+        del d_plang
+    else:
+        pool = min(args.pool, args.docs)
+        pdata, poff, plang = synth.generate(ls, pool, args.doc_min, args.doc_max,
+                                            seed=synth.SEED_BASE + args.config + 1000 * rank)
+        data, off, _ = synth.tile(pdata, poff, plang, args.docs)
+        n_bytes = int(off[-1])
+        d_bytes = torch.empty(((n_bytes + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
+        d_bytes[:n_bytes].copy_(torch.from_numpy(data))
+        d_off = torch.from_numpy(off).to(dev)
     n_docs = len(off) - 1
-    n_bytes = int(off[-1])
-    d_bytes = torch.empty(((n_bytes + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
-    d_bytes[:n_bytes].copy_(torch.from_numpy(data))
-    d_off = torch.from_numpy(off).to(dev)
     d_lab = torch.empty(n_docs, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -710,7 +724,7 @@ def main():
         elapsed = float(t.item())
 
     # labels sanity (synthetic docs carry their generating language)
-    acc = float((d_lab[:pool].cpu().numpy() == plang[:n_docs][:pool]).mean()) if (table or packed) else None
+    acc = float((d_lab[:pool].cpu().numpy() == plang[:pool]).mean()) if (table or packed) else None
 
     info = model.info()
     doc_b = n_bytes / max(n_docs, 1)                      # mean document bytes
@@ -808,7 +822,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (Markov-chain text per language, SURVEY.md §8d generator; table FIT on the GPU)",
+        "data": ("synthetic (Markov-chain text per language, SURVEY.md §8d generator; table FIT on the GPU; "
+                 + ("every document distinct, drawn on the GPU)" if args.pool is None
+                    else f"a pool of {pool} documents tiled)")),
         "config": {"workload": f"config{args.config}: score {n_docs} x {doc_desc} docs per GPU, {args.langs} "
                                f"languages, grams {args.grams}, profile size {args.profile_size}",
                    "docs_per_gpu": n_docs, "doc_bytes": round(doc_b, 2), "languages": args.langs,

@@ -1589,9 +1589,15 @@ __device__ __forceinline__ void group_load(const ScoreParams& p, int64_t s0, int
 // scores documents p.doc_idx[i], i = w, w + waves, ... < *p.n_docs_dev (count
 // written by the device), each in place from global memory, its label stored
 // to labels[doc_idx[i]]; workgroups with no document exit before staging.
+#ifndef LDGPU_LATE_OFFSETS
+#define LDGPU_LATE_OFFSETS 1
+#endif
 template <int S, int MODE, int BL, bool PACK = false, bool WIDE = false, bool IND = false>
 __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 4) void score_kernel(const ScoreParams p) {
     constexpr bool FLDS = BL == 0;
+    // the kernels at the register cap (packs, global-memory blooms) load the
+    // next group's offsets after the group's documents, not before
+    constexpr bool kLateOffsets = LDGPU_LATE_OFFSETS && (PACK || BL != 0);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1681,7 +1687,8 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
         // bytes and offsets of the next group (hidden behind this group's work)
         if (g1 < dend) group_dma(p, send & ~(int64_t)15, par ? buf0 : buf1);
         const int64_t n1 = min(g1 + (int64_t)G, dend);
-        const int64_t offn = p.offsets[min(g1 + (int64_t)min((int)fresh_lane(), G), n1)];
+        int64_t offn = 0;
+        if constexpr (!kLateOffsets) offn = p.offsets[min(g1 + (int64_t)min((int)fresh_lane(), G), n1)];
         // the previous group's labels: one coalesced store
         {
             const uint32_t l = fresh_lane();
@@ -1734,6 +1741,10 @@ __global__ __launch_bounds__(kScoreWaves * 64, kScoreMinWgPerCu * kScoreWaves / 
             }
         }
         __builtin_amdgcn_wave_barrier();
+        // (kLateOffsets: the next group's offsets loaded only now -- held in
+        // registers across the group's documents they were spilled to
+        // scratch, one 512-B store + reload per group: config 4's writes)
+        if constexpr (kLateOffsets) offn = p.offsets[min(g1 + (int64_t)min((int)fresh_lane(), G), n1)];
         prev_g0 = g0;
         prev_cnt = cnt;
         offv = offn;

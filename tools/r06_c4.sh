@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r06c4; mkdir -p $OUT
-LIBS="${LIBS:-n4base n4k}" CFGS="--config 4" ROUNDS=${ROUNDS:-2} STEPS=10 tools/ab.sh || exit 1
+[ -n "${SKIP_AB:-}" ] || LIBS="${LIBS:-n4base n4k}" CFGS="--config 4" ROUNDS=${ROUNDS:-2} STEPS=10 tools/ab.sh || exit 1
 for lib in ${LIBS:-n4base n4k}; do
   LDGPU_LIB=$PWD/spark-languagedetector_amd/lib/libldgpu_$lib.so timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE \
     --kernel-include-regex score_kernel --output-format csv -d $PWD/$OUT/w_$lib -o run -- python3 bench.py --config 4 \
