@@ -414,7 +414,7 @@ def is_count_kernel(name, L, grams):
     radix sort when the count is FIT v5's (FIT v4 sorts nothing; any other
     sort of a profiled run is an export's: sort_pairs_u64 in counts_pull)."""
     base = name.split("(")[0].split("<")[0]
-    return base in COUNT_KERNELS or (base.startswith("rocprim") and fit_sort_path(L, grams))
+    return base in COUNT_KERNELS or (base == "rocprim_radix_sort" and fit_sort_path(L, grams))
 
 
 def count_traffic(prof, L, grams):

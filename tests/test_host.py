@@ -173,3 +173,32 @@ def test_detect_cache_reuses_only_unchanged_maps():
     f = freeze_table(t)
     assert isinstance(f, FrozenTable) and freeze_table(f) is f
     assert _unchanged(f, _snapshot(f)) and dict(f) == {b"ab": (1.0, 0.0), b"cd": (0.0, 2.0)}
+
+
+def test_round_bench_lines_follow_from_committed_profiles():
+    """Every round-6 bench line's roofline.traffic is what bench.py computes
+    from the committed PMC file of its workload (profiles/pmc_traffic*.json),
+    FIT lines charged with the count's own kernels only; config 5's frac is
+    priced on the bytes its design moves (<= 1)."""
+    import glob
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    lines = sorted(glob.glob(os.path.join(ROOT, "profiles", "r06_bench*.json")))
+    assert len(lines) >= 5
+    for f in lines:
+        d = json.load(open(f))
+        r = d["roofline"]
+        if r.get("workload_key"):
+            want = (bench.traffic_from_profiles(r["workload_key"]) or {}).get("traffic_bytes_per_launch")
+        else:
+            wl = d["config"]
+            L = int(re.search(r"(\d+) languages", wl["workload"]).group(1))
+            G = [int(x) for x in re.search(r"grams ([\d,]+),", wl["workload"]).group(1).split(",")]
+            want = bench.count_traffic(
+                bench.traffic_from_profiles(f"fit:bytes={wl['corpus_bytes_per_gpu']}:L={L}:G={','.join(map(str, G))}"),
+                L, G)
+        assert want and r["traffic"] == want, (f, r["traffic"], want)
+        assert 0 < r["frac"] <= 1, (f, r["frac"])
+        assert d["build"]["match"], f

@@ -55,10 +55,10 @@ d = {"workload_key": f"fit:bytes={cfg['corpus_bytes_per_gpu']}:L={L}:G={m.group(
      "calibration": calibration, "count_only": True}
 traffic = count_traffic(d, L, grams)
 d.update({"traffic_bytes_per_launch": traffic, "traffic_raw_bytes_per_count": round(fetch + write),
-     "windows_per_count": windows, "bytes_per_window_corrected": round(traffic / windows, 2),
-     "bytes_per_window_raw": round((fetch + write) / windows, 2),
-     "count_ms": line["roofline"]["count_ms"],
-     "memory_side_GBps": round(traffic / (line["roofline"]["count_ms"] * 1e-3) / 1e9, 1)}
+          "windows_per_count": windows, "bytes_per_window_corrected": round(traffic / windows, 2),
+          "bytes_per_window_raw": round((fetch + write) / windows, 2),
+          "count_ms": line["roofline"]["count_ms"],
+          "memory_side_GBps": round(traffic / (line["roofline"]["count_ms"] * 1e-3) / 1e9, 1)})
 json.dump(d, open(os.path.join(out, sys.argv[2] if len(sys.argv) > 2 else "pmc_traffic_fit.json"), "w"), indent=1)
 print(json.dumps({k: d[k] for k in d if k != "per_kernel_raw_bytes_per_count"}, indent=1))
 for k, v in sorted(raw.items(), key=lambda kv: -sum(kv[1].values())):

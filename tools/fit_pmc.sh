@@ -3,7 +3,8 @@
 # section): FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes (no
 # tracing) over `bench.py --mode fit --steps 1 --warmup 0 --count-only` (two
 # counts: the timed one and the statistics one, no top-K table), summed per
-# kernel over the ldgpu kernels and the radix sorts (rocprim: FIT v5's), then
+# kernel over the ldgpu kernels and the radix sorts (rocprim: FIT v5's; other
+# rocprim kernels -- torch's, drawing the corpus -- apart), then
 # tools/fit_pmc.py calibrates the raw counters on kernels whose bytes are
 # known exactly (FIT v4: part2 reads and writes every record once; FIT v5:
 # sort_emit writes one 8-B key per corpus byte, sort_runs reads the keys).
@@ -27,7 +28,9 @@ for r in csv.DictReader(open(sys.argv[1])):
     if r["Counter_Name"] != sys.argv[2]:
         continue
     if "rocprim" in k and "ldgpu" not in k:
-        k = "rocprim_radix_sort"
+        # the radix sorts (FIT v5's own); any other rocprim kernel (torch's
+        # boolean indexing while the corpus is drawn) is kept apart
+        k = "rocprim_radix_sort" if "radix_sort" in k else "rocprim_other"
     elif "ldgpu" in k:
         k = k.split("(ldgpu")[0].replace("ldgpu::(anonymous namespace)::", "").replace("void ", "")
     else:
