@@ -186,7 +186,7 @@ def test_round_bench_lines_follow_from_committed_profiles():
     sys.path.insert(0, ROOT)
     import bench
     lines = sorted(glob.glob(os.path.join(ROOT, "profiles", "r06_bench*.json")))
-    assert len(lines) >= 5
+    assert len(lines) >= 6
     for f in lines:
         d = json.load(open(f))
         r = d["roofline"]
@@ -199,6 +199,6 @@ def test_round_bench_lines_follow_from_committed_profiles():
             want = bench.count_traffic(
                 bench.traffic_from_profiles(f"fit:bytes={wl['corpus_bytes_per_gpu']}:L={L}:G={','.join(map(str, G))}"),
                 L, G)
-        assert want and r["traffic"] == want, (f, r["traffic"], want)
+        assert r["traffic"] == want, (f, r["traffic"], want)   # (None: no PMC profile, no claim)
         assert 0 < r["frac"] <= 1, (f, r["frac"])
         assert d["build"]["match"], f
