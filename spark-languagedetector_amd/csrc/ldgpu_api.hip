@@ -1849,6 +1849,9 @@ int score_launch(ldgpu_model* m, const uint8_t* d_bytes, int64_t n_bytes, const 
     }
     gram_lists(m, p, mode);
     if (mode != 3 && mode != 4) p.direct_words = 0;  // the ordered replay reads no direct tables
+    // count mode, labels only: a fast-path document (<= 256 B, so far below
+    // count_argmax_len) takes the count argmax (score kernel kFmArgmax)
+    if (mode == 3 && p.count_argmax_len >= 256 && !d_scores && !d_best) p.fast_mask |= 1u << 17;
     HIP_TRY(launch_score(p, m->slices, mode, m->lds_filter, score_grid(m, n_docs), st));
     if (classes) return class_replay(m, p, st);
     return LDGPU_OK;
@@ -3179,7 +3182,20 @@ int count_launch_sorted(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes
         for (int j = 0; j < d.n && d.len[j] <= r; ++j) ++k;
         tails_of[r] = tails_of[r - 1] + k;
     }
+    // positions per batch: at most kSortBatch, and at most what half of the
+    // device memory left (plus the scratch this context already holds) takes
+    // at ~36 B per position -- the keys and the sort's second buffer (8 B
+    // each), a length's run entries (20 B), the sort's scratch -- so a fit
+    // that fits a smaller or shared device runs in more, smaller batches
     int64_t batch = kSortBatch;
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const double held = (double)(x->f_rec.cap + x->f_rec2.cap + x->f_okl.cap + x->f_stmp.cap);
+            const int64_t fit = (int64_t)(0.5 * ((double)free_b + held) / 36.0);
+            batch = std::max<int64_t>(1ll << 24, std::min<int64_t>(batch, fit));
+        }
+    }
     if (const char* b = diag_env("LDGPU_FIT_SORT_BATCH")) batch = std::max(1ll, atoll(b));
     const bool trace = diag_env("LDGPU_FIT_TRACE") != nullptr;
     auto now_ms = [] {
