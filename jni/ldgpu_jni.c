@@ -447,3 +447,49 @@ JNIEXPORT jint JNICALL FN(countsMerge)(JNIEnv* env, jobject self, jlong counts, 
     jclear();
     return ldgpu_counts_merge((ldgpu_counts*)(intptr_t)counts, (ldgpu_comm*)(intptr_t)comm);
 }
+
+/* The device preprocessors (ldgpu_casemap_create / ldgpu_preprocess).  The
+ * case map is the JVM's own: lower = Character.toLowerCase of every unit
+ * (65536 u16), special = the units whose String.toLowerCase is not 1:1
+ * (8192 bytes, one bit each) -- built once by the caller, so the device
+ * lower-cases exactly as the executor's JVM does. */
+JNIEXPORT jint JNICALL FN(casemapCreate)(JNIEnv* env, jobject self, jlong ctx, jobject lower, jobject special,
+                                         jlongArray out) {
+    (void)self;
+    jclear();
+    CHECK(need(env, lower, 2 * 65536, "lower"));
+    CHECK(need(env, special, 65536 / 8, "special"));
+    ldgpu_casemap* m = NULL;
+    const int rc = ldgpu_casemap_create((ldgpu_ctx*)(intptr_t)ctx, (const uint16_t*)addr(env, lower),
+                                        (const uint8_t*)addr(env, special), &m);
+    return put_handle(env, out, m, rc);
+}
+
+JNIEXPORT jint JNICALL FN(casemapDestroy)(JNIEnv* env, jobject self, jlong map) {
+    (void)env;
+    (void)self;
+    jclear();
+    return ldgpu_casemap_destroy((ldgpu_casemap*)(intptr_t)map);
+}
+
+/* units: UTF-16 code units up to offsets[nDocs]; out: the worst case (every
+ * unit kept) of offsets[nDocs] - offsets[0] units, or bytes with
+ * LDGPU_PRE_LOW_BYTES; outOffsets nDocs + 1 longs; host and locale (nullable)
+ * nDocs bytes. */
+JNIEXPORT jint JNICALL FN(preprocess)(JNIEnv* env, jobject self, jlong map, jobject units, jobject offsets,
+                                      jlong n_docs, jobject locale, jint flags, jobject out, jobject out_offsets,
+                                      jobject host) {
+    (void)self;
+    jclear();
+    int64_t nu = 0;
+    CHECK(need_offsets(env, offsets, n_docs, "offsets", &nu));
+    CHECK(need(env, units, bytes_of(2, nu, 1), "units"));
+    const int64_t first = ((const int64_t*)addr(env, offsets))[0];
+    CHECK(need(env, out, bytes_of((flags & LDGPU_PRE_LOW_BYTES) ? 1 : 2, nu - first, 1), "out"));
+    CHECK(need(env, out_offsets, bytes_of(8, n_docs + 1, 1), "outOffsets"));
+    CHECK(need(env, host, n_docs, "host"));
+    if (locale) CHECK(need(env, locale, n_docs, "locale"));
+    return ldgpu_preprocess((ldgpu_casemap*)(intptr_t)map, (const uint16_t*)addr(env, units),
+                            (const int64_t*)addr(env, offsets), n_docs, (const uint8_t*)addr(env, locale), flags,
+                            addr(env, out), (int64_t*)addr(env, out_offsets), (uint8_t*)addr(env, host));
+}

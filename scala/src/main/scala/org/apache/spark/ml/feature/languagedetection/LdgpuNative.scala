@@ -69,6 +69,21 @@ object LdgpuNative {
   @native def commCreateRccl(ctx: Long, id: Array[Byte], rank: Int, world: Int, out: Array[Long]): Int
   @native def commDestroy(comm: Long): Int
   @native def countsMerge(counts: Long, comm: Long): Int
+  // the preprocessors on the device (include/ldgpu.h PREPROCESS)
+  /** lower: 65536 u16, Character.toLowerCase of every unit; special: 8192 bytes, bit u = unit u goes to the host */
+  @native def casemapCreate(ctx: Long, lower: ByteBuffer, special: ByteBuffer, out: Array[Long]): Int
+  @native def casemapDestroy(map: Long): Int
+  /** units: UTF-16 code units, offsets in units; out: offsets(nDocs) - offsets(0) units (bytes with PreLowBytes);
+    * outOffsets: nDocs + 1 longs; host, locale (nullable): nDocs bytes */
+  @native def preprocess(map: Long, units: ByteBuffer, offsets: ByteBuffer, nDocs: Long, locale: ByteBuffer,
+                         flags: Int, out: ByteBuffer, outOffsets: ByteBuffer, host: ByteBuffer): Int
+
+  val PreLower = 1
+  val PreClean = 2
+  val PreLowBytes = 4
+  val LocaleRoot = 0
+  val LocaleTrAz = 1
+  val LocaleLt = 2
 
   /** The reference's exception for each failure class: a wrong-length row
     * hit (BLAS.axpy's require) and n <= 0 (sliding's require) are

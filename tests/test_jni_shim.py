@@ -121,6 +121,47 @@ def test_count_add_and_table_exports_need_handles(jh):
     assert s.call("fitTableExport", 0, s.buf(kb), s.buf(ko), s.buf(rows), 2, 6, 4) == EINVAL
 
 
+def test_preprocess_buffers_are_checked(jh):
+    """casemapCreate needs the whole case map (65536 units + 8192 bitmap
+    bytes); preprocess needs units up to offsets[n], an output buffer for the
+    worst case (every unit kept: units, or bytes with LOW_BYTES), n + 1 output
+    offsets and n host flags -- all checked before the library is reached."""
+    s = Shim(jh)
+    lower = np.arange(65536, dtype=np.uint16)
+    special = np.zeros(8192, np.uint8)
+    h = np.zeros(1, np.int64)
+    assert s.call("casemapCreate", 0, s.buf(lower, 2 * 65536 - 2), s.buf(special), s.arr(h)) == EINVAL
+    assert "lower holds" in s.err()
+    assert s.call("casemapCreate", 0, s.buf(lower), s.buf(special, 8191), s.arr(h)) == EINVAL
+    assert "special" in s.err()
+    units = np.frombuffer("Hello World, Straße".encode("utf-16-le"), np.uint16).copy()
+    off = np.array([0, 5, 11, len(units)], np.int64)
+    n = 3
+    out = np.zeros(len(units), np.uint16)
+    oo = np.zeros(n + 1, np.int64)
+    host = np.zeros(n, np.uint8)
+    args = lambda u, o, ob, oob, hb, flags=_lib.PRE_LOWER: (
+        "preprocess", 0, u, o, n, None, flags, ob, oob, hb)
+    assert s.call(*args(s.buf(units, 2 * len(units) - 1), s.buf(off), s.buf(out), s.buf(oo), s.buf(host))) == EINVAL
+    assert "units holds" in s.err()
+    assert s.call(*args(s.buf(units), s.buf(off), s.buf(out, 2 * len(units) - 2), s.buf(oo), s.buf(host))) == EINVAL
+    assert "out holds" in s.err()
+    # bytes output: half the buffer is enough, less is not
+    assert s.call(*args(s.buf(units), s.buf(off), s.buf(out, len(units) - 1), s.buf(oo), s.buf(host),
+                        _lib.PRE_LOWER | _lib.PRE_LOW_BYTES)) == EINVAL
+    assert s.call(*args(s.buf(units), s.buf(off), s.buf(out), s.buf(oo, 8 * n), s.buf(host))) == EINVAL
+    assert "outOffsets" in s.err()
+    assert s.call(*args(s.buf(units), s.buf(off), s.buf(out), s.buf(oo), s.buf(host, n - 1))) == EINVAL
+    assert "host" in s.err()
+    loc = np.zeros(n - 1, np.uint8)
+    assert s.call("preprocess", 0, s.buf(units), s.buf(off), n, s.buf(loc), _lib.PRE_LOWER, s.buf(out), s.buf(oo),
+                  s.buf(host)) == EINVAL
+    assert "locale" in s.err()
+    # right-sized buffers reach the library, which refuses the null map
+    assert s.call(*args(s.buf(units), s.buf(off), s.buf(out), s.buf(oo), s.buf(host))) == EINVAL
+    assert "casemap" in s.err()
+
+
 @pytest.mark.gpu
 def test_shim_on_device_handles(jh):
     """Real handles: the scores buffer and count rows are sized by the
@@ -175,3 +216,30 @@ def test_shim_on_device_handles(jh):
     assert {bytes(tk[tko[i]:tko[i + 1]]): list(rows[i]) for i in range(rows_n)} == c.fit_table(10)
     m.close()
     c.close()
+
+
+@pytest.mark.gpu
+def test_shim_preprocess_on_the_device(jh):
+    """A case map made through the shim lower-cases and cleans exactly as
+    DeviceCaseMap (the Python binding of the same ABI) does."""
+    from languagedetection.runtime import DeviceCaseMap, case_tables
+    s = Shim(jh)
+    lower, special = case_tables()
+    ctx = _lib.context(None)
+    h = np.zeros(1, np.int64)
+    assert s.call("casemapCreate", ctx, s.buf(lower), s.buf(special), s.arr(h)) == 0
+    texts = ["Hello  World!", "ISTANBUL (İ)", "Straße #1", "ΟΔΟΣ", ""]
+    loc = np.array([0, 1, 0, 0, 0], np.uint8)
+    dm = DeviceCaseMap()
+    units, off = dm.pack_units(texts)
+    for flags in (_lib.PRE_LOWER, _lib.PRE_LOWER | _lib.PRE_CLEAN, _lib.PRE_CLEAN | _lib.PRE_LOW_BYTES):
+        ob = np.zeros(len(units) + 4, np.uint8 if flags & _lib.PRE_LOW_BYTES else np.uint16)
+        oo = np.zeros(len(texts) + 1, np.int64)
+        host = np.zeros(len(texts), np.uint8)
+        assert s.call("preprocess", int(h[0]), s.buf(units), s.buf(off), len(texts), s.buf(loc), flags, s.buf(ob),
+                      s.buf(oo), s.buf(host)) == 0, s.err()
+        e_out, e_oo, e_host = dm.run(units, off, loc, flags)
+        assert np.array_equal(oo, e_oo) and np.array_equal(host, e_host)
+        assert np.array_equal(ob[:oo[-1]], e_out[:e_oo[-1]])
+    assert s.call("casemapDestroy", int(h[0])) == 0
+    dm.close()
