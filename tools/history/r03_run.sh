@@ -2,7 +2,7 @@
 # Round-3 GPU pass: selected gpu tests (-k PATTERN, "all" = every gpu test),
 # then any number of bench runs given as quoted argument strings; each step
 # under its own time limit, stopping at the first fault / abort / timeout.
-#   tools/r03_run.sh TAG PATTERN ["bench args" ...]
+#   tools/history/r03_run.sh TAG PATTERN ["bench args" ...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; PAT=$2; shift 2

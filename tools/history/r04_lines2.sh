@@ -12,5 +12,5 @@ for c in "fit:--mode fit --steps 3 --warmup 1" "c4:--config 4" "c5:--config 5 --
   tail -c 200 $O/$t.log; echo
 done
 LDGPU_LIB=spark-languagedetector_amd/lib/libldgpu_diag.so LDGPU_FIT_TRACE=1 timeout -k 10 300 python3 -u bench.py --mode fit --steps 1 --warmup 1 --no-cpu-baseline --json-out $O/fit_trace.json > $O/fit_trace.log 2>&1 || { tail -5 $O/fit_trace.log; exit 1; }
-tools/r04_prof.sh fitL200b "--mode fit --langs 200 --grams 1,2,3,4,5,6,7 --profile-size 50000 --fit-bytes 1000000000 --steps 1 --warmup 0 --cpu-seconds 20" > /dev/null 2>&1 || exit 1
+tools/history/r04_prof.sh fitL200b "--mode fit --langs 200 --grams 1,2,3,4,5,6,7 --profile-size 50000 --fit-bytes 1000000000 --steps 1 --warmup 0 --cpu-seconds 20" > /dev/null 2>&1 || exit 1
 echo done

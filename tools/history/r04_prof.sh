@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel-trace profile of one bench run: rocprofv3 --kernel-trace --stats,
 # the kernel stats CSV copied to gpurun_out/TAG/kernel_stats.csv.
-#   tools/r04_prof.sh TAG "bench args"
+#   tools/history/r04_prof.sh TAG "bench args"
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; ARGS=$2
