@@ -34,7 +34,11 @@ struct CountParams {
     // counts == null): the reference's reduceGrams rows (LanguageDetector.
     // scala:57-65) -- one (gram, language) -> count pair per row, not a dense
     // row of L counters per gram.  keys[cap] holds the grams with kcnt[cap],
-    // the number of languages each occurs in (its pairs: k of computeProbabilities);
+    // the number of languages each occurs in (its pairs: k of
+    // computeProbabilities) MINUS ONE, mod 2^32 (gram_k): the thread that
+    // creates a gram and its first pair -- most grams' only one -- adds
+    // nothing, every other new pair adds 1, a creator whose pair is not new
+    // subtracts 1 (kcnt_delta);
     // the pair table pkeys[pcap] / pcounts[pcap] is keyed (gram slot + 1) << 12 | lang.
     uint32_t* kcnt;
     uint64_t* pkeys;

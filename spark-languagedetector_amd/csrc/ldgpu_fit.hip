@@ -72,6 +72,51 @@ __device__ __forceinline__ unsigned long long block_compact(bool occ, C* out_n, 
     return o;
 }
 
+// block_compact for chunks of several items per thread (kScanIpt items,
+// kScanThreads apart): bit j of sm flags this thread's item j.  The block's
+// flagged items of one chunk get consecutive output positions from ONE global
+// atomic, in (item, wave, lane) order -- so each item's writes stay coalesced
+// across the wave, as with block_compact; rel[j] + base is item j's index.
+// Each chunk costs the block three barriers and the round trip of its atomic
+// on the single counter, so the scans over ~1G positions (FIT v5 runs, the
+// top-K's pair and gram scans) take kScanIpt items per thread per chunk.
+constexpr int kScanIpt = 8;
+static_assert(kScanIpt * (kScanThreads / 64) == 128, "block_place scans 2 counters per lane");
+
+template <typename C = unsigned long long>
+__device__ __forceinline__ void block_place(uint32_t sm, C* out_n, unsigned int* wcnt, unsigned long long* bbase,
+                                            uint32_t (&rel)[kScanIpt], unsigned long long& base) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < kScanIpt; ++j) {
+        const uint64_t m = __ballot((sm >> j) & 1u);
+        if (lane == 0) wcnt[j * (kScanThreads / 64) + wave] = (unsigned int)__popcll(m);
+        rel[j] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    __syncthreads();
+    if (wave == 0) {  // exclusive scan of the 128 counters, two per lane
+        const uint32_t a = wcnt[2 * lane], b = wcnt[2 * lane + 1], t = a + b;
+        uint32_t incl = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        wcnt[2 * lane] = incl - t;
+        wcnt[2 * lane + 1] = incl - t + a;
+        const uint32_t tot = __shfl(incl, 63);
+        if (lane == 0) *bbase = tot ? (unsigned long long)atomicAdd(out_n, (C)tot) : 0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScanIpt; ++j) rel[j] += wcnt[j * (kScanThreads / 64) + wave];
+    base = *bbase;
+    __syncthreads();  // wcnt / bbase are reused by the next chunk
+}
+
+// grid of a scan placing kScanIpt items per thread per chunk
+unsigned scan_grid_ipt(uint64_t n) { return scan_grid((n + kScanIpt - 1) / kScanIpt); }
+
 // FIT v4 derive: flag of the prefix aggregates a level adds to T1 (never a
 // key bit: klen <= 15 in bits 56..59; pair keys use <= 57 bits)
 constexpr uint64_t kDerived = 1ull << 62;
@@ -164,11 +209,26 @@ __device__ __forceinline__ int64_t pair_find_or_insert(const CountParams& p, uin
     return pair_find_or_insert_at<false>(p, pk, fit_hash(pk) >> p.pshift, 0ull, new_pair);
 }
 
+// kcnt (ldgpu_fit.h) of one add: +1 for a new pair, -1 for a new gram (its
+// creator's pair is counted by the encoding) -- 0, no atomic, for the usual
+// new gram with its new pair
+__device__ __forceinline__ void kcnt_delta(const CountParams& p, int64_t g, bool new_gram, bool new_pair) {
+    const int d = (int)new_pair - (int)new_gram;
+    if (g >= 0 && d) atomicAdd(&p.kcnt[g], (uint32_t)d);
+}
+
+// the language count k of the gram at occupied slot g
+__device__ __forceinline__ int gram_k(const CountParams& p, uint64_t g) { return (int)(p.kcnt[g] + 1u); }
+
 // c of (key, lang) into the sparse table: the gram's slot (its language
 // count up when the pair is new), then the pair's counter.  An add that reaches a
 // probe limit in either table goes to the overflow list as (key, lang, c) --
 // re-adding it finds the gram if it was placed.  A zero count adds nothing
 // (a reduceGrams row has count >= 1).  Returns new gram | new pair << 32.
+// UNIQ: no other thread of the launch adds this (key, lang) (FIT v5's run
+// entries: one per (gram, language) per launch), so a pair this thread
+// claimed takes its count by a plain store, not an atomic add.
+template <bool UNIQ = false>
 __device__ __forceinline__ uint64_t sparse_add_q(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
     if (!c) return 0;
     bool new_gram = false, new_pair = false;
@@ -177,9 +237,10 @@ __device__ __forceinline__ uint64_t sparse_add_q(const CountParams& p, uint64_t 
     if (g >= 0) {
         s = pair_find_or_insert(p, ((uint64_t)(g + 1) << kPairLangBits) | (uint64_t)lang, new_pair);
         if (s >= 0) {
-            atomicAdd(pcnt_at(p, s), c);
-            if (new_pair) atomicAdd(&p.kcnt[g], 1u);
+            if (UNIQ && new_pair) *pcnt_at(p, s) = c;
+            else atomicAdd(pcnt_at(p, s), c);
         }
+        kcnt_delta(p, g, new_gram, new_pair);
     }
     if (s < 0) {
         const unsigned int at = atomicAdd(p.ovf_n, 1u);
@@ -227,8 +288,9 @@ __device__ __forceinline__ bool add_count_q(const CountParams& p, uint64_t key, 
 
 // an add into T (sparse) or a dense table without the counter updates: new
 // keys | new pairs << 32 (t_flush adds them up)
+template <bool UNIQ = false>
 __device__ __forceinline__ uint64_t t_add_q(const CountParams& p, uint64_t key, int lang, unsigned long long c) {
-    if (p.pkeys) return sparse_add_q(p, key, lang, c);
+    if (p.pkeys) return sparse_add_q<UNIQ>(p, key, lang, c);
     return add_count_q(p, key, lang, c) ? 1ull : 0ull;
 }
 
@@ -726,16 +788,30 @@ __global__ void cand_mark_kernel(int64_t n, const uint32_t* lang_sorted, const u
 __global__ __launch_bounds__(kScanThreads) void gram_rows_kernel(const CountParams p, uint64_t cap, uint64_t* out_keys,
                                                                  int32_t* out_k, uint32_t* rowof,
                                                                  unsigned long long* out_n) {
-    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned int wcnt[kScanIpt * (kScanThreads / 64)];
     __shared__ unsigned long long bbase;
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < cap; c0 += (uint64_t)gridDim.x * kScanThreads) {
-        const uint64_t i = c0 + threadIdx.x;
-        const bool occ = i < cap && p.keys[i] != kEmpty;
-        const unsigned long long o = block_compact(occ, out_n, wcnt, &bbase);
-        if (!occ) continue;
-        out_keys[o] = p.keys[i];
-        out_k[o] = (int32_t)p.kcnt[i];
-        rowof[i] = (uint32_t)o;
+    constexpr uint64_t kChunk = (uint64_t)kScanIpt * kScanThreads;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < cap; c0 += (uint64_t)gridDim.x * kChunk) {
+        uint64_t key[kScanIpt];
+        uint32_t om = 0;
+#pragma unroll
+        for (int j = 0; j < kScanIpt; ++j) {
+            const uint64_t i = c0 + (uint64_t)j * kScanThreads + threadIdx.x;
+            key[j] = i < cap ? p.keys[i] : kEmpty;
+            if (key[j] != kEmpty) om |= 1u << j;
+        }
+        uint32_t rel[kScanIpt];
+        unsigned long long base;
+        block_place(om, out_n, wcnt, &bbase, rel, base);
+#pragma unroll
+        for (int j = 0; j < kScanIpt; ++j) {
+            if (!((om >> j) & 1u)) continue;
+            const uint64_t i = c0 + (uint64_t)j * kScanThreads + threadIdx.x;
+            const unsigned long long o = base + rel[j];
+            out_keys[o] = key[j];
+            out_k[o] = (int32_t)gram_k(p, i);
+            rowof[i] = (uint32_t)o;
+        }
     }
 }
 
@@ -758,7 +834,7 @@ __global__ __launch_bounds__(kScanThreads) void pair_hist_kernel(const CountPara
         const uint64_t pk = *pkey_at(p, i);
         if (pk == kEmpty) continue;
         const uint32_t l = pair_lang(pk);
-        const int k = (int)p.kcnt[pair_slot(pk)];
+        const int k = gram_k(p, pair_slot(pk));
         if (k <= kl) atomicAdd(&lh[l * kw + k], 1u);
         else atomicAdd(&hist[l * (L + 1) + k], 1u);
     }
@@ -781,34 +857,57 @@ __global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountPa
                                                                    uint8_t* chosen, int32_t* cand_lang,
                                                                    uint64_t* cand_key, uint32_t* cand_idx,
                                                                    unsigned int* cand_n, int L, unsigned int* lenhist) {
-    __shared__ unsigned int wcnt[kScanThreads / 64];
+    __shared__ unsigned int wcnt[kScanIpt * (kScanThreads / 64)];
     __shared__ unsigned long long bbase;
     extern __shared__ unsigned int lh[];
     if (lenhist) {
         for (int i = threadIdx.x; i < 16 * L; i += blockDim.x) lh[i] = 0u;
         __syncthreads();
     }
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kScanThreads; c0 < pcap; c0 += (uint64_t)gridDim.x * kScanThreads) {
-        const uint64_t i = c0 + threadIdx.x;
-        const uint64_t pk = i < pcap ? *pkey_at(p, i) : kEmpty;
-        bool cand = false;
-        uint32_t l = 0, j = 0;
-        if (pk != kEmpty) {
-            l = pair_lang(pk);
-            const uint64_t g = pair_slot(pk);
-            j = rowof[g];
-            const int k = (int)p.kcnt[g];
-            const int ksl = kstar[l];
-            if (k < ksl) chosen[j] = 1;
-            cand = k == ksl && need[l] > 0;
+    constexpr uint64_t kChunk = (uint64_t)kScanIpt * kScanThreads;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < pcap; c0 += (uint64_t)gridDim.x * kChunk) {
+        // kScanIpt pairs per thread: their random gram-slot reads in flight together
+        uint64_t pk[kScanIpt];
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) {
+            const uint64_t i = c0 + (uint64_t)q * kScanThreads + threadIdx.x;
+            pk[q] = i < pcap ? *pkey_at(p, i) : kEmpty;
         }
-        const unsigned long long at = block_compact<unsigned int>(cand, cand_n, wcnt, &bbase);
-        if (!cand) continue;
-        const uint64_t sk = sort_key(keys[j]);
-        cand_lang[at] = (int32_t)l;
-        cand_key[at] = sk;
-        cand_idx[at] = j;
-        if (lenhist) atomicAdd(&lh[16 * l + (int)(sk >> 56)], 1u);
+        uint32_t j[kScanIpt];
+        int k[kScanIpt];
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) {
+            j[q] = 0;
+            k[q] = 0;
+            if (pk[q] != kEmpty) {
+                const uint64_t g = pair_slot(pk[q]);
+                j[q] = rowof[g];
+                k[q] = gram_k(p, g);
+            }
+        }
+        uint32_t cm = 0;
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) {
+            if (pk[q] == kEmpty) continue;
+            const uint32_t l = pair_lang(pk[q]);
+            const int ksl = kstar[l];
+            if (k[q] < ksl) chosen[j[q]] = 1;
+            if (k[q] == ksl && need[l] > 0) cm |= 1u << q;
+        }
+        uint32_t rel[kScanIpt];
+        unsigned long long base;
+        block_place<unsigned int>(cm, cand_n, wcnt, &bbase, rel, base);
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) {
+            if (!((cm >> q) & 1u)) continue;
+            const unsigned long long at = base + rel[q];
+            const uint32_t l = pair_lang(pk[q]);
+            const uint64_t sk = sort_key(keys[j[q]]);
+            cand_lang[at] = (int32_t)l;
+            cand_key[at] = sk;
+            cand_idx[at] = j[q];
+            if (lenhist) atomicAdd(&lh[16 * l + (int)(sk >> 56)], 1u);
+        }
     }
     if (lenhist) {
         __syncthreads();
@@ -994,7 +1093,7 @@ __global__ void gather_u64_kernel(int64_t n, const uint32_t* idx, const uint64_t
 
 hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint32_t* rowof,
                             unsigned long long* out_n, hipStream_t stream) {
-    hipLaunchKernelGGL(gram_rows_kernel, dim3(scan_grid(cap)), dim3(kScanThreads), 0, stream, p, cap, out_keys, out_k,
+    hipLaunchKernelGGL(gram_rows_kernel, dim3(scan_grid_ipt(cap)), dim3(kScanThreads), 0, stream, p, cap, out_keys, out_k,
                        rowof, out_n);
     return hipGetLastError();
 }
@@ -1017,7 +1116,7 @@ hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_
                               unsigned int* lenhist, hipStream_t stream) {
     if (pcap == 0) return hipSuccess;
     const size_t lds = lenhist ? (size_t)16 * L * 4 : 0;
-    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid(pcap)), dim3(kScanThreads), lds, stream, p, pcap, rowof,
+    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid_ipt(pcap)), dim3(kScanThreads), lds, stream, p, pcap, rowof,
                        keys, kstar, need, chosen, cand_lang, cand_key, cand_idx, cand_n, L, lenhist);
     return hipGetLastError();
 }
@@ -2390,10 +2489,8 @@ __global__ __launch_bounds__(256) void derive_pairs_level_kernel(const CountPara
                     int64_t sp = -1;
                     if (g[u] >= 0) {
                         sp = pair_find_or_insert_at<true>(to, pp[u], pa[u], pv[u], np);
-                        if (sp >= 0) {
-                            atomicAdd(pcnt_at(to, sp), cm);
-                            if (np) atomicAdd(&to.kcnt[g[u]], 1u);
-                        }
+                        if (sp >= 0) atomicAdd(pcnt_at(to, sp), cm);
+                        kcnt_delta(to, g[u], ng[u], np);
                     }
                     if (sp < 0) {  // a probe limit: (key, lang, c) to the overflow list (sparse_add_q)
                         const unsigned int at = atomicAdd(to.ovf_n, 1u);
@@ -2566,54 +2663,106 @@ __global__ __launch_bounds__(256) void sort_emit_kernel(const SortFitParams p, c
 }
 
 // Runs of gram length n: position i starts one when its n-byte prefix (with
-// the language) differs from position i - 1's; its length is found by a
-// galloping search (1, 2, 4, ... positions ahead, then bisection), so the
-// long runs of short grams cost O(log run) loads and the ~1-position runs of
-// long grams one load of the next key.  Compaction: one global atomic per
-// block-chunk.
+// the language) differs from position i - 1's; the run ends at the next
+// start.  A chunk of kScanIpt x kScanThreads positions keeps its starts as a
+// bitmap in LDS, so most runs end within a few map words (the ~1-position
+// runs of long grams, the short runs of middle lengths); a run that leaves
+// the words searched is found by a galloping search from there (1, 2, 4, ...
+// positions ahead, then bisection): O(log run) loads for the long runs of
+// short grams.  Compaction: one global atomic per chunk (block_place).
 __global__ __launch_bounds__(kScanThreads) void sort_runs_kernel(const uint64_t* keys, int64_t R, int N, int n,
                                                                  uint32_t mult, uint64_t* out_key, int32_t* out_lang,
                                                                  unsigned long long* out_cnt,
                                                                  unsigned long long* out_n) {
-    __shared__ unsigned int wcnt[kScanThreads / 64];
+    constexpr int64_t kChunk = (int64_t)kScanIpt * kScanThreads;
+    constexpr int kMapWords = (int)(kChunk / 32);
+    constexpr int kScanWords = 8;  // map words searched for the next start before galloping
+    __shared__ unsigned int wcnt[kScanIpt * (kScanThreads / 64)];
     __shared__ unsigned long long bbase;
+    // the chunk's run starts, one bit per position (relative position
+    // j * kScanThreads + thread), double-buffered: a wave still reading chunk
+    // k's map has passed no barrier of chunk k + 1, which writes the other one
+    __shared__ uint32_t smap[2][kMapWords];
     const int shift = 8 * (N - n);
-    for (int64_t c0 = (int64_t)blockIdx.x * kScanThreads; c0 < R; c0 += (int64_t)gridDim.x * kScanThreads) {
-        const int64_t i = c0 + threadIdx.x;
-        uint64_t pk = 0;
-        bool start = false;
-        if (i < R) {
-            pk = keys[i] >> shift;
-            start = i == 0 || (keys[i - 1] >> shift) != pk;
-        }
-        const unsigned long long o = block_compact(start, out_n, wcnt, &bbase);
-        if (!start) continue;
-        int64_t lo = i, hi = R;
-        for (int64_t step = 1; lo + step < R; step <<= 1) {
-            if ((keys[lo + step] >> shift) != pk) {
-                hi = lo + step;
-                break;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int par = 0;
+    for (int64_t c0 = (int64_t)blockIdx.x * kChunk; c0 < R; c0 += (int64_t)gridDim.x * kChunk, par ^= 1) {
+        // kScanIpt positions per thread, kScanThreads apart (coalesced)
+        uint64_t pk[kScanIpt];
+        uint32_t sm = 0;
+#pragma unroll
+        for (int j = 0; j < kScanIpt; ++j) {
+            const int64_t i = c0 + (int64_t)j * kScanThreads + threadIdx.x;
+            pk[j] = 0;
+            if (i < R) {
+                pk[j] = keys[i] >> shift;
+                if (i == 0 || (keys[i - 1] >> shift) != pk[j]) sm |= 1u << j;
             }
-            lo += step;
         }
-        while (hi - lo > 1) {
-            const int64_t mid = lo + ((hi - lo) >> 1);
-            if ((keys[mid] >> shift) == pk) lo = mid;
-            else hi = mid;
+        uint32_t* const map = smap[par];
+#pragma unroll
+        for (int j = 0; j < kScanIpt; ++j) {
+            const uint64_t m = __ballot((sm >> j) & 1u);
+            if (lane < 2) map[(j * kScanThreads + wave * 64) / 32 + lane] = (uint32_t)(m >> (32 * lane));
         }
-        out_key[o] = __builtin_bswap64((pk & byte_mask(n)) << (64 - 8 * n)) | ((uint64_t)n << 56);
-        out_lang[o] = (int32_t)(pk >> (8 * n));
-        out_cnt[o] = (unsigned long long)(hi - i) * mult;
+        uint32_t rel[kScanIpt];
+        unsigned long long base;
+        block_place(sm, out_n, wcnt, &bbase, rel, base);  // (its barriers publish the map)
+        const int64_t cend = c0 + kChunk < R ? c0 + kChunk : R;
+#pragma unroll
+        for (int j = 0; j < kScanIpt; ++j) {
+            if (!((sm >> j) & 1u)) continue;
+            const int r = j * kScanThreads + (int)threadIdx.x;
+            const int64_t i = c0 + r;
+            const unsigned long long o = base + rel[j];
+            // the run ends at the next start: in this chunk's map (a few
+            // words), else by galloping from the last position known to
+            // continue the run (1, 2, 4, ... ahead, then bisection)
+            int64_t hi = -1;
+            int w = r >> 5;
+            uint32_t bits = (r & 31) == 31 ? 0u : map[w] & (~0u << ((r & 31) + 1));
+            for (int k = 0;; ++k) {
+                if (bits) {
+                    hi = c0 + 32 * w + __builtin_ctz(bits);
+                    break;
+                }
+                if (++w == kMapWords || k == kScanWords) break;
+                bits = map[w];
+            }
+            if (hi < 0) {
+                // positions (i, c0 + 32 w) continue the run (no start among them)
+                int64_t lo = (c0 + 32 * (int64_t)w < cend ? c0 + 32 * (int64_t)w : cend) - 1;
+                hi = R;
+                for (int64_t step = 1; lo + step < R; step <<= 1) {
+                    if ((keys[lo + step] >> shift) != pk[j]) {
+                        hi = lo + step;
+                        break;
+                    }
+                    lo += step;
+                }
+                while (hi - lo > 1) {
+                    const int64_t mid = lo + ((hi - lo) >> 1);
+                    if ((keys[mid] >> shift) == pk[j]) lo = mid;
+                    else hi = mid;
+                }
+            }
+            out_key[o] = __builtin_bswap64((pk[j] & byte_mask(n)) << (64 - 8 * n)) | ((uint64_t)n << 56);
+            out_lang[o] = (int32_t)(pk[j] >> (8 * n));
+            out_cnt[o] = (unsigned long long)(hi - i) * mult;
+        }
     }
 }
 
+#ifndef LDGPU_RUNS_UNIQ
+#define LDGPU_RUNS_UNIQ 1
+#endif
 // (key, language, count) entries into T, grid-stride; the new-key counters
 // once per thread (t_flush)
 __global__ __launch_bounds__(256) void runs_add_kernel(const CountParams p, const uint64_t* keys, const int32_t* lang,
                                                        const unsigned long long* cnt, int64_t n) {
     uint64_t n_new = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        n_new += t_add_q(p, keys[i], lang[i], cnt[i]);
+        n_new += t_add_q<LDGPU_RUNS_UNIQ>(p, keys[i], lang[i], cnt[i]);
     t_flush(p, n_new);
 }
 
@@ -2639,7 +2788,7 @@ hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, int n, uint3
                             int32_t* out_lang, unsigned long long* out_cnt, unsigned long long* out_n,
                             hipStream_t stream) {
     if (R <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sort_runs_kernel, dim3(scan_grid((uint64_t)R)), dim3(kScanThreads), 0, stream, keys, R, N, n,
+    hipLaunchKernelGGL(sort_runs_kernel, dim3(scan_grid_ipt((uint64_t)R)), dim3(kScanThreads), 0, stream, keys, R, N, n,
                        mult, out_key, out_lang, out_cnt, out_n);
     return hipGetLastError();
 }
