@@ -3201,8 +3201,8 @@ int count_launch_sorted(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes
     auto now_ms = [] {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
-    HIP_TRY(x->f_on.ensure(64));
-    unsigned long long* d_n = (unsigned long long*)x->f_on.p;
+    HIP_TRY(x->f_on.ensure(sizeof(unsigned long long) * (kMaxGram + 2)));
+    unsigned long long* d_n = (unsigned long long*)x->f_on.p;  // [0]: entries written, [1..7]: runs per length
     for (int64_t d0 = 0; d0 < n_docs;) {
         const double t0 = trace ? now_ms() : 0.0;
         int64_t d1 = d0, R = 0, tails = 0;
@@ -3250,29 +3250,52 @@ int count_launch_sorted(ldgpu_counts* c, const uint8_t* d_bytes, int64_t n_bytes
             const uint64_t* sorted = in_alt ? alt : keys;
             if (trace) HIP_TRY(hipStreamSynchronize(st));
             const double t2 = trace ? now_ms() : 0.0;
-            // one gram length's run entries: key, count, language (20 B)
+            // run entries (key, count, language: 20 B), room for R of them:
+            // the runs of every gram length, counted in one pass, then
+            // written by passes over groups of lengths whose entries fit
+            // (each length has at most R runs), inserted into T per pass
             const size_t cap = (size_t)std::max<int64_t>(R, 1);
             HIP_TRY(x->f_okl.ensure(cap * (2 * sizeof(uint64_t) + sizeof(int32_t)) + 64));
             uint64_t* rk = (uint64_t*)x->f_okl.p;
             unsigned long long* rcnt = (unsigned long long*)(rk + cap);
             int32_t* rl = (int32_t*)(rcnt + cap);
             double t_runs = 0.0, t_ins = 0.0;
-            for (int n = N; n >= 1 && R > 0; --n) {
-                if (!mult[n]) continue;
+            unsigned long long runs[kMaxGram + 1] = {};
+            if (R > 0) {
+                const double ta = trace ? now_ms() : 0.0;
+                HIP_TRY(hipMemsetAsync(d_n, 0, sizeof(unsigned long long) * (kMaxGram + 2), st));
+                HIP_TRY(launch_runs_count(sorted, R, N, d_n + 1, st));
+                HIP_TRY(hipMemcpyAsync(runs, d_n + 1, sizeof runs, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                if (trace) t_runs += now_ms() - ta;
+            }
+            for (int n = N; n >= 1 && R > 0;) {
+                RunLens lens{};
+                unsigned long long want = 0;
+                for (; n >= 1; --n) {
+                    if (!mult[n]) continue;
+                    if (runs[n] > (unsigned long long)R)
+                        return fail(LDGPU_EDEVICE, "FIT runs: %llu of length %d from %lld keys", runs[n], n, (long long)R);
+                    if (want + runs[n] > (unsigned long long)R) break;
+                    want += runs[n];
+                    lens.mask |= 1u << n;
+                    lens.mult[n] = mult[n];
+                }
+                if (!lens.mask) continue;
                 const double ta = trace ? now_ms() : 0.0;
                 HIP_TRY(hipMemsetAsync(d_n, 0, sizeof(unsigned long long), st));
-                HIP_TRY(launch_sort_runs(sorted, R, N, n, mult[n], rk, rl, rcnt, d_n, st));
+                HIP_TRY(launch_sort_runs(sorted, R, N, lens, rk, rl, rcnt, d_n, st));
                 unsigned long long rn = 0;
                 HIP_TRY(hipMemcpyAsync(&rn, d_n, sizeof rn, hipMemcpyDeviceToHost, st));
                 HIP_TRY(hipStreamSynchronize(st));
-                if (rn > (unsigned long long)R)
-                    return fail(LDGPU_EDEVICE, "FIT runs: %llu entries from %lld keys", rn, (long long)R);
+                if (rn != want)
+                    return fail(LDGPU_EDEVICE, "FIT runs: %llu entries, %llu counted (lengths 0x%x)", rn, want, lens.mask);
                 const double tb2 = trace ? now_ms() : 0.0;
                 if (int rc = insert_runs(c, rk, rl, rcnt, (int64_t)rn)) return rc;
                 if (trace) {
                     t_runs += tb2 - ta;
                     t_ins += now_ms() - tb2;
-                    fprintf(stderr, "fit v5 length %d: %llu runs\n", n, rn);
+                    fprintf(stderr, "fit v5 lengths 0x%x: %llu runs\n", lens.mask, rn);
                 }
             }
             if (trace)

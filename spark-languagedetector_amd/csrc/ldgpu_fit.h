@@ -289,10 +289,21 @@ hipError_t launch_sort_emit(const SortFitParams& p, const CountParams& to, hipSt
 // sorted keys are in alt
 hipError_t sort_keys_u64(int64_t n, uint64_t* keys, uint64_t* alt, int bits, void* tmp, size_t* tmp_bytes,
                          bool* in_alt, hipStream_t stream);
-// the runs of gram length n in sorted keys[0, R): one entry per distinct
-// (language, n-byte prefix) -- packed key, language, run length x mult --
-// appended at out_n (block-level compaction)
-hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, int n, uint32_t mult, uint64_t* out_key,
+// the gram lengths of one runs pass (bit n of mask) and their multiplicities
+// in gramLengths
+struct RunLens {
+    uint32_t mask;
+    uint32_t mult[kMaxGram + 1];
+};
+// runs[n] (n = 1..N) += the runs of gram length n in sorted keys[0, R) (one
+// pass for every length: a run of length n starts where a key's common prefix
+// with the previous key, language included, is shorter than n bytes)
+hipError_t launch_runs_count(const uint64_t* keys, int64_t R, int N, unsigned long long* runs, hipStream_t stream);
+// the runs of the gram lengths in lens in sorted keys[0, R), read once for
+// all of them: one entry per distinct (language, n-byte prefix) -- packed
+// key, language, run length x mult -- appended at out_n (block-level
+// compaction)
+hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, const RunLens& lens, uint64_t* out_key,
                             int32_t* out_lang, unsigned long long* out_cnt, unsigned long long* out_n,
                             hipStream_t stream);
 // n (key, language, count) entries into T (sparse or dense), grid-stride:

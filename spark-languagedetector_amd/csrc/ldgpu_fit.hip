@@ -2662,93 +2662,136 @@ __global__ __launch_bounds__(256) void sort_emit_kernel(const SortFitParams p, c
     t_flush(to, n_new);
 }
 
-// Runs of gram length n: position i starts one when its n-byte prefix (with
-// the language) differs from position i - 1's; the run ends at the next
-// start.  A chunk of kScanIpt x kScanThreads positions keeps its starts as a
-// bitmap in LDS, so most runs end within a few map words (the ~1-position
-// runs of long grams, the short runs of middle lengths); a run that leaves
-// the words searched is found by a galloping search from there (1, 2, 4, ...
-// positions ahead, then bisection): O(log run) loads for the long runs of
-// short grams.  Compaction: one global atomic per chunk (block_place).
-__global__ __launch_bounds__(kScanThreads) void sort_runs_kernel(const uint64_t* keys, int64_t R, int N, int n,
-                                                                 uint32_t mult, uint64_t* out_key, int32_t* out_lang,
-                                                                 unsigned long long* out_cnt,
+// the common prefix of sorted keys a (at i) and b (at i - 1) in gram bytes:
+// 0 when the language differs, N when the keys are equal.  Position i starts a
+// run of every gram length n > common_prefix.
+__device__ __forceinline__ int common_prefix(uint64_t a, uint64_t b, int N) {
+    const uint64_t x = a ^ b;
+    if (x >> (8 * N)) return 0;
+    if (!x) return N;
+    return (__builtin_clzll(x) - (64 - 8 * N)) >> 3;
+}
+
+__global__ __launch_bounds__(256) void runs_count_kernel(const uint64_t* keys, int64_t R, int N,
+                                                         unsigned long long* runs) {
+    __shared__ unsigned long long h[kMaxGram + 1];
+    if (threadIdx.x <= kMaxGram) h[threadIdx.x] = 0ull;
+    __syncthreads();
+    uint32_t c[kMaxGram + 1] = {};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (int64_t)gridDim.x * blockDim.x) {
+        const int cp = i == 0 ? 0 : common_prefix(keys[i], keys[i - 1], N);
+#pragma unroll
+        for (int n = 1; n <= kMaxGram; ++n) c[n] += cp < n ? 1u : 0u;
+    }
+#pragma unroll
+    for (int n = 1; n <= kMaxGram; ++n) {
+        uint32_t v = c[n];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&h[n], (unsigned long long)v);
+    }
+    __syncthreads();
+    if (threadIdx.x >= 1 && threadIdx.x <= kMaxGram && threadIdx.x <= N && h[threadIdx.x])
+        atomicAdd(&runs[threadIdx.x], h[threadIdx.x]);
+}
+
+// Runs of the gram lengths in lens: position i starts one of length n when
+// its common prefix with position i - 1 (language included) is shorter than
+// n bytes; the run ends at the next start.  The keys of a chunk of
+// kScanIpt x kScanThreads positions are read once for every length of the
+// pass.  Per length, the chunk keeps its starts as a bitmap in LDS, so most
+// runs end within a few map words (the ~1-position runs of long grams, the
+// short runs of middle lengths); a run that leaves the words searched is
+// found by a galloping search from there (1, 2, 4, ... positions ahead, then
+// bisection): O(log run) loads for the long runs of short grams.
+// Compaction: one global atomic per chunk and length (block_place).
+__global__ __launch_bounds__(kScanThreads) void sort_runs_kernel(const uint64_t* keys, int64_t R, int N,
+                                                                 const RunLens lens, uint64_t* out_key,
+                                                                 int32_t* out_lang, unsigned long long* out_cnt,
                                                                  unsigned long long* out_n) {
     constexpr int64_t kChunk = (int64_t)kScanIpt * kScanThreads;
     constexpr int kMapWords = (int)(kChunk / 32);
     constexpr int kScanWords = 8;  // map words searched for the next start before galloping
     __shared__ unsigned int wcnt[kScanIpt * (kScanThreads / 64)];
     __shared__ unsigned long long bbase;
-    // the chunk's run starts, one bit per position (relative position
-    // j * kScanThreads + thread), double-buffered: a wave still reading chunk
-    // k's map has passed no barrier of chunk k + 1, which writes the other one
+    // one length's starts in the chunk, one bit per position (relative
+    // position j * kScanThreads + thread), double-buffered: a wave still
+    // reading one (chunk, length) step's map has passed no barrier of the next
+    // step, which writes the other one
     __shared__ uint32_t smap[2][kMapWords];
-    const int shift = 8 * (N - n);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int par = 0;
-    for (int64_t c0 = (int64_t)blockIdx.x * kChunk; c0 < R; c0 += (int64_t)gridDim.x * kChunk, par ^= 1) {
+    for (int64_t c0 = (int64_t)blockIdx.x * kChunk; c0 < R; c0 += (int64_t)gridDim.x * kChunk) {
         // kScanIpt positions per thread, kScanThreads apart (coalesced)
-        uint64_t pk[kScanIpt];
-        uint32_t sm = 0;
+        uint64_t key[kScanIpt];
+        int cp[kScanIpt];
 #pragma unroll
         for (int j = 0; j < kScanIpt; ++j) {
             const int64_t i = c0 + (int64_t)j * kScanThreads + threadIdx.x;
-            pk[j] = 0;
+            key[j] = 0;
+            cp[j] = N;  // past R: no start
             if (i < R) {
-                pk[j] = keys[i] >> shift;
-                if (i == 0 || (keys[i - 1] >> shift) != pk[j]) sm |= 1u << j;
+                key[j] = keys[i];
+                cp[j] = i == 0 ? 0 : common_prefix(key[j], keys[i - 1], N);
             }
         }
-        uint32_t* const map = smap[par];
-#pragma unroll
-        for (int j = 0; j < kScanIpt; ++j) {
-            const uint64_t m = __ballot((sm >> j) & 1u);
-            if (lane < 2) map[(j * kScanThreads + wave * 64) / 32 + lane] = (uint32_t)(m >> (32 * lane));
-        }
-        uint32_t rel[kScanIpt];
-        unsigned long long base;
-        block_place(sm, out_n, wcnt, &bbase, rel, base);  // (its barriers publish the map)
         const int64_t cend = c0 + kChunk < R ? c0 + kChunk : R;
+        for (int n = N; n >= 1; --n) {
+            if (!((lens.mask >> n) & 1u)) continue;
+            const int shift = 8 * (N - n);
+            const uint32_t mult = lens.mult[n];
+            uint32_t sm = 0;
 #pragma unroll
-        for (int j = 0; j < kScanIpt; ++j) {
-            if (!((sm >> j) & 1u)) continue;
-            const int r = j * kScanThreads + (int)threadIdx.x;
-            const int64_t i = c0 + r;
-            const unsigned long long o = base + rel[j];
-            // the run ends at the next start: in this chunk's map (a few
-            // words), else by galloping from the last position known to
-            // continue the run (1, 2, 4, ... ahead, then bisection)
-            int64_t hi = -1;
-            int w = r >> 5;
-            uint32_t bits = (r & 31) == 31 ? 0u : map[w] & (~0u << ((r & 31) + 1));
-            for (int k = 0;; ++k) {
-                if (bits) {
-                    hi = c0 + 32 * w + __builtin_ctz(bits);
-                    break;
-                }
-                if (++w == kMapWords || k == kScanWords) break;
-                bits = map[w];
+            for (int j = 0; j < kScanIpt; ++j) sm |= cp[j] < n ? 1u << j : 0u;
+            uint32_t* const map = smap[par];
+            par ^= 1;
+#pragma unroll
+            for (int j = 0; j < kScanIpt; ++j) {
+                const uint64_t m = __ballot((sm >> j) & 1u);
+                if (lane < 2) map[(j * kScanThreads + wave * 64) / 32 + lane] = (uint32_t)(m >> (32 * lane));
             }
-            if (hi < 0) {
-                // positions (i, c0 + 32 w) continue the run (no start among them)
-                int64_t lo = (c0 + 32 * (int64_t)w < cend ? c0 + 32 * (int64_t)w : cend) - 1;
-                hi = R;
-                for (int64_t step = 1; lo + step < R; step <<= 1) {
-                    if ((keys[lo + step] >> shift) != pk[j]) {
-                        hi = lo + step;
+            uint32_t rel[kScanIpt];
+            unsigned long long base;
+            block_place(sm, out_n, wcnt, &bbase, rel, base);  // (its barriers publish the map)
+#pragma unroll
+            for (int j = 0; j < kScanIpt; ++j) {
+                if (!((sm >> j) & 1u)) continue;
+                const int r = j * kScanThreads + (int)threadIdx.x;
+                const int64_t i = c0 + r;
+                const uint64_t pk = key[j] >> shift;
+                const unsigned long long o = base + rel[j];
+                int64_t hi = -1;
+                int w = r >> 5;
+                uint32_t bits = (r & 31) == 31 ? 0u : map[w] & (~0u << ((r & 31) + 1));
+                for (int k = 0;; ++k) {
+                    if (bits) {
+                        hi = c0 + 32 * w + __builtin_ctz(bits);
                         break;
                     }
-                    lo += step;
+                    if (++w == kMapWords || k == kScanWords) break;
+                    bits = map[w];
                 }
-                while (hi - lo > 1) {
-                    const int64_t mid = lo + ((hi - lo) >> 1);
-                    if ((keys[mid] >> shift) == pk[j]) lo = mid;
-                    else hi = mid;
+                if (hi < 0) {
+                    // positions (i, c0 + 32 w) continue the run (no start among them)
+                    int64_t lo = (c0 + 32 * (int64_t)w < cend ? c0 + 32 * (int64_t)w : cend) - 1;
+                    hi = R;
+                    for (int64_t step = 1; lo + step < R; step <<= 1) {
+                        if ((keys[lo + step] >> shift) != pk) {
+                            hi = lo + step;
+                            break;
+                        }
+                        lo += step;
+                    }
+                    while (hi - lo > 1) {
+                        const int64_t mid = lo + ((hi - lo) >> 1);
+                        if ((keys[mid] >> shift) == pk) lo = mid;
+                        else hi = mid;
+                    }
                 }
+                out_key[o] = __builtin_bswap64((pk & byte_mask(n)) << (64 - 8 * n)) | ((uint64_t)n << 56);
+                out_lang[o] = (int32_t)(pk >> (8 * n));
+                out_cnt[o] = (unsigned long long)(hi - i) * mult;
             }
-            out_key[o] = __builtin_bswap64((pk[j] & byte_mask(n)) << (64 - 8 * n)) | ((uint64_t)n << 56);
-            out_lang[o] = (int32_t)(pk[j] >> (8 * n));
-            out_cnt[o] = (unsigned long long)(hi - i) * mult;
         }
     }
 }
@@ -2784,12 +2827,19 @@ hipError_t sort_keys_u64(int64_t n, uint64_t* keys, uint64_t* alt, int bits, voi
     return e;
 }
 
-hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, int n, uint32_t mult, uint64_t* out_key,
+hipError_t launch_runs_count(const uint64_t* keys, int64_t R, int N, unsigned long long* runs, hipStream_t stream) {
+    if (R <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>(4096, (R + 255) / 256);
+    hipLaunchKernelGGL(runs_count_kernel, dim3(g), dim3(256), 0, stream, keys, R, N, runs);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_runs(const uint64_t* keys, int64_t R, int N, const RunLens& lens, uint64_t* out_key,
                             int32_t* out_lang, unsigned long long* out_cnt, unsigned long long* out_n,
                             hipStream_t stream) {
     if (R <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sort_runs_kernel, dim3(scan_grid_ipt((uint64_t)R)), dim3(kScanThreads), 0, stream, keys, R, N, n,
-                       mult, out_key, out_lang, out_cnt, out_n);
+    hipLaunchKernelGGL(sort_runs_kernel, dim3(scan_grid_ipt((uint64_t)R)), dim3(kScanThreads), 0, stream, keys, R, N,
+                       lens, out_key, out_lang, out_cnt, out_n);
     return hipGetLastError();
 }
 
