@@ -5120,7 +5120,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
     // leaving the others waiting in the next all-gather.
     auto agree = [&](int rc) { return cm ? comm_agree(cm, rc, "fit table") : rc; };
     uint64_t* d_keys = nullptr;
-    uint32_t* d_rowof = nullptr;
+    uint64_t* d_rk = nullptr;  // per gram slot: row | k << 32
     int32_t* d_k = nullptr;
     unsigned long long* d_n = nullptr;
     unsigned int* d_hist = nullptr;
@@ -5131,15 +5131,15 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         if (n > (int64_t)0xffffffffll) return fail(LDGPU_EUNSUPPORTED, "fit table: %lld grams", (long long)n);
         HIP_TRY(db.alloc(&d_keys, n));
         HIP_TRY(db.alloc(&d_k, n));
-        HIP_TRY(db.alloc(&d_rowof, c->cap));
+        HIP_TRY(db.alloc(&d_rk, c->cap));
         HIP_TRY(db.alloc(&d_n, 2));
         HIP_TRY(db.alloc(&d_hist, (size_t)L * (L + 1)));
         mark("table: scratch");
         HIP_TRY(hipMemsetAsync(d_n, 0, 2 * sizeof(unsigned long long), st));
         HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(unsigned int) * L * (L + 1), st));
-        HIP_TRY(launch_gram_rows(cp, c->cap, d_keys, d_k, d_rowof, d_n, st));
+        HIP_TRY(launch_gram_rows(cp, c->cap, d_keys, d_k, d_rk, d_n, st));
         mark("table: gram rows");
-        HIP_TRY(launch_pair_hist(cp, c->pcap, L, d_hist, c->ctx->cus, st));
+        HIP_TRY(launch_pair_hist(cp, c->pcap, L, d_rk, d_hist, c->ctx->cus, st));
         mark("table: pair histogram");
         unsigned long long got = 0;
         HIP_TRY(hipMemcpyAsync(hist.data(), d_hist, sizeof(unsigned int) * hist.size(), hipMemcpyDeviceToHost, st));
@@ -5189,7 +5189,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
             uint64_t* d_masks;
             HIP_TRY(db.alloc(&d_masks, (size_t)n * S));
             HIP_TRY(hipMemsetAsync(d_masks, 0, sizeof(uint64_t) * n * S, st));
-            HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, nullptr, S, d_masks, st));
+            HIP_TRY(launch_pair_masks(cp, c->pcap, d_rk, nullptr, S, d_masks, st));
             HIP_TRY(hipMemcpyAsync(hk.data(), d_keys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(hm.data(), d_masks, sizeof(uint64_t) * n * S, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -5303,7 +5303,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         HIP_TRY(hipMemcpyAsync(d_need, need.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemsetAsync(d_cn, 0, 2 * sizeof(unsigned int), st));
         HIP_TRY(hipMemsetAsync(d_chosen, 0, (size_t)n, st));
-        HIP_TRY(launch_pair_select(cp, c->pcap, d_rowof, d_keys, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn, L,
+        HIP_TRY(launch_pair_select(cp, c->pcap, d_rk, d_keys, d_kstar, d_need, d_chosen, d_cl, d_ck, d_ci, d_cn, L,
                                    d_lh, st));
         std::vector<unsigned int> lh(split ? (size_t)16 * L : 0);
         HIP_TRY(hipMemcpyAsync(&cn, d_cn, sizeof cn, hipMemcpyDeviceToHost, st));
@@ -5446,7 +5446,7 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         mark("table: gather rows");
         HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
         HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
-        HIP_TRY(launch_pair_masks(cp, c->pcap, d_rowof, d_outrow, S, d_om, st));
+        HIP_TRY(launch_pair_masks(cp, c->pcap, d_rk, d_outrow, S, d_om, st));
         mark("table: masks");
         if (multi && m) {
             ok.resize(m);

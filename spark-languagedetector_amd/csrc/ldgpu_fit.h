@@ -354,16 +354,18 @@ hipError_t launch_long_rehash(const LongCountParams& from, const LongCountParams
 
 // ---- top-K over the sparse table's pairs (computeProbabilities +
 // filterTopGrams, LanguageDetector.scala:75-132): the grams compacted
-// (out_keys[o], out_k[o] = k, rowof[slot] = o); the (language, k) histogram,
+// (out_keys[o], out_k[o] = k, rk[slot] = o | k << 32); the (language, k) histogram,
 // the selection and the chosen rows' presence masks all from the pairs
-hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint32_t* rowof,
+// rk[g] = row | k << 32 of every occupied gram slot g (its compacted row and
+// its language count: one 8-B gather per pair in the pair scans below)
+hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint64_t* rk,
                             unsigned long long* out_n, hipStream_t stream);
-hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, unsigned int* hist, int cus,
+hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, const uint64_t* rk, unsigned int* hist, int cus,
                             hipStream_t stream);
 // chosen[j] = 1 when the gram is below its language's threshold class; the
 // threshold-class pairs (need[l] > 0) appended as candidates (lang, sort key, j);
 // lenhist (nullable, [L][16]) += the candidates per (language, key length)
-hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
+hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint64_t* rk, const uint64_t* keys,
                               const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
                               uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, int L,
                               unsigned int* lenhist, hipStream_t stream);
@@ -385,9 +387,9 @@ hipError_t launch_sort_keys_of(int64_t n, const uint64_t* keys, uint64_t* sk, un
 hipError_t launch_rows_permute(int64_t n, int S, const unsigned long long* idx, const uint64_t* keys, const int32_t* ks,
                                const uint64_t* masks, uint64_t* out_keys, int32_t* out_k, uint64_t* out_masks,
                                hipStream_t stream);
-// presence masks: masks[row][l / 64] |= bit l for every pair, row = outrow[rowof[g]]
-// (outrow null: rowof[g]); masks zeroed by the caller
-hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow, int S,
+// presence masks: masks[row][l / 64] |= bit l for every pair, row = outrow[(uint32_t)rk[g]]
+// (outrow null: the row itself); masks zeroed by the caller
+hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint64_t* rk, const uint32_t* outrow, int S,
                              uint64_t* masks, hipStream_t stream);
 
 // threshold-class ties: per language the need[l] smallest (length, bytes)

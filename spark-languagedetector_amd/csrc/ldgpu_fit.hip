@@ -786,7 +786,7 @@ __global__ void cand_mark_kernel(int64_t n, const uint32_t* lang_sorted, const u
 
 // ---- top-K over the sparse table's pairs
 __global__ __launch_bounds__(kScanThreads) void gram_rows_kernel(const CountParams p, uint64_t cap, uint64_t* out_keys,
-                                                                 int32_t* out_k, uint32_t* rowof,
+                                                                 int32_t* out_k, uint64_t* rk,
                                                                  unsigned long long* out_n) {
     __shared__ unsigned int wcnt[kScanIpt * (kScanThreads / 64)];
     __shared__ unsigned long long bbase;
@@ -808,9 +808,10 @@ __global__ __launch_bounds__(kScanThreads) void gram_rows_kernel(const CountPara
             if (!((om >> j) & 1u)) continue;
             const uint64_t i = c0 + (uint64_t)j * kScanThreads + threadIdx.x;
             const unsigned long long o = base + rel[j];
+            const uint32_t k = (uint32_t)gram_k(p, i);
             out_keys[o] = key[j];
-            out_k[o] = (int32_t)gram_k(p, i);
-            rowof[i] = (uint32_t)o;
+            out_k[o] = (int32_t)k;
+            rk[i] = o | ((uint64_t)k << 32);
         }
     }
 }
@@ -818,25 +819,36 @@ __global__ __launch_bounds__(kScanThreads) void gram_rows_kernel(const CountPara
 __device__ __forceinline__ uint32_t pair_lang(uint64_t pk) { return (uint32_t)(pk & ((1ull << kPairLangBits) - 1ull)); }
 __device__ __forceinline__ uint64_t pair_slot(uint64_t pk) { return (pk >> kPairLangBits) - 1ull; }
 
-// (language, k) histogram of the pairs, k = the gram's language count (kcnt
-// at its slot: one random read per pair).  Classes k <= kl count in LDS
+// (language, k) histogram of the pairs, k = the gram's language count (rk
+// at its slot: one random 8-B read per pair, kScanIpt in flight per thread).  Classes k <= kl count in LDS
 // ([L][kl + 1], kl = L when it fits), the rest -- rare: most grams are in
 // few languages -- in global memory; each block flushes its nonzero LDS
 // counters once.  (Global atomics on the ~L hot counters of k = 1: 152 ms on
 // config 5's 1.39G pairs.)
 __global__ __launch_bounds__(kScanThreads) void pair_hist_kernel(const CountParams p, uint64_t pcap, int L, int kl,
-                                                                 unsigned int* hist) {
+                                                                 const uint64_t* rk, unsigned int* hist) {
     extern __shared__ unsigned int lh[];
     const int kw = kl + 1;
     for (int i = threadIdx.x; i < L * kw; i += blockDim.x) lh[i] = 0u;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pcap; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t pk = *pkey_at(p, i);
-        if (pk == kEmpty) continue;
-        const uint32_t l = pair_lang(pk);
-        const int k = gram_k(p, pair_slot(pk));
-        if (k <= kl) atomicAdd(&lh[l * kw + k], 1u);
-        else atomicAdd(&hist[l * (L + 1) + k], 1u);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < pcap; i0 += kScanIpt * stride) {
+        uint64_t pk[kScanIpt];
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) {
+            const uint64_t i = i0 + q * stride;
+            pk[q] = i < pcap ? *pkey_at(p, i) : kEmpty;
+        }
+        int k[kScanIpt];
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) k[q] = pk[q] != kEmpty ? (int)(rk[pair_slot(pk[q])] >> 32) : 0;
+#pragma unroll
+        for (int q = 0; q < kScanIpt; ++q) {
+            if (pk[q] == kEmpty) continue;
+            const uint32_t l = pair_lang(pk[q]);
+            if (k[q] <= kl) atomicAdd(&lh[l * kw + k[q]], 1u);
+            else atomicAdd(&hist[l * (L + 1) + k[q]], 1u);
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < L * kw; i += blockDim.x) {
@@ -852,7 +864,7 @@ __global__ __launch_bounds__(kScanThreads) void pair_hist_kernel(const CountPara
 // lenhist (nullable): the candidates per (language, key length) ([L][16],
 // in LDS, flushed once per block) -- the threshold class's length split
 __global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountParams p, uint64_t pcap,
-                                                                   const uint32_t* rowof, const uint64_t* keys,
+                                                                   const uint64_t* rk, const uint64_t* keys,
                                                                    const int32_t* kstar, const int32_t* need,
                                                                    uint8_t* chosen, int32_t* cand_lang,
                                                                    uint64_t* cand_key, uint32_t* cand_idx,
@@ -880,9 +892,9 @@ __global__ __launch_bounds__(kScanThreads) void pair_select_kernel(const CountPa
             j[q] = 0;
             k[q] = 0;
             if (pk[q] != kEmpty) {
-                const uint64_t g = pair_slot(pk[q]);
-                j[q] = rowof[g];
-                k[q] = gram_k(p, g);
+                const uint64_t v = rk[pair_slot(pk[q])];
+                j[q] = (uint32_t)v;
+                k[q] = (int)(v >> 32);
             }
         }
         uint32_t cm = 0;
@@ -969,14 +981,14 @@ __global__ __launch_bounds__(kScanThreads) void gather_rows_kernel(int64_t n, co
     }
 }
 
-__global__ void pair_masks_kernel(const CountParams p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow,
+__global__ void pair_masks_kernel(const CountParams p, uint64_t pcap, const uint64_t* rk, const uint32_t* outrow,
                                   int S, uint64_t* masks) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= pcap) return;
     const uint64_t pk = *pkey_at(p, i);
     if (pk == kEmpty) return;
     const uint32_t l = pair_lang(pk);
-    uint32_t r = rowof[pair_slot(pk)];
+    uint32_t r = (uint32_t)rk[pair_slot(pk)];
     if (outrow) r = outrow[r];
     if (r == 0xffffffffu) return;
     atomicOr(reinterpret_cast<unsigned long long*>(&masks[(size_t)r * S + (l >> 6)]), 1ull << (l & 63));
@@ -1091,14 +1103,14 @@ __global__ void gather_u64_kernel(int64_t n, const uint32_t* idx, const uint64_t
 
 }  // namespace
 
-hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint32_t* rowof,
+hipError_t launch_gram_rows(const CountParams& p, uint64_t cap, uint64_t* out_keys, int32_t* out_k, uint64_t* rk,
                             unsigned long long* out_n, hipStream_t stream) {
     hipLaunchKernelGGL(gram_rows_kernel, dim3(scan_grid_ipt(cap)), dim3(kScanThreads), 0, stream, p, cap, out_keys, out_k,
-                       rowof, out_n);
+                       rk, out_n);
     return hipGetLastError();
 }
 
-hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, unsigned int* hist, int cus,
+hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, const uint64_t* rk, unsigned int* hist, int cus,
                             hipStream_t stream) {
     if (pcap == 0) return hipSuccess;
     // LDS classes: every k when L (L + 1) counters fit 48 KiB, else as many
@@ -1106,17 +1118,17 @@ hipError_t launch_pair_hist(const CountParams& p, uint64_t pcap, int L, unsigned
     const int kl = std::max(1, std::min(L, (int)(12288 / L) - 1));
     const size_t lds = (size_t)L * (kl + 1) * 4;
     const unsigned g = (unsigned)std::min<uint64_t>((uint64_t)cus * 2, (pcap + kScanThreads - 1) / kScanThreads);
-    hipLaunchKernelGGL(pair_hist_kernel, dim3(std::max(1u, g)), dim3(kScanThreads), lds, stream, p, pcap, L, kl, hist);
+    hipLaunchKernelGGL(pair_hist_kernel, dim3(std::max(1u, g)), dim3(kScanThreads), lds, stream, p, pcap, L, kl, rk, hist);
     return hipGetLastError();
 }
 
-hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint64_t* keys,
+hipError_t launch_pair_select(const CountParams& p, uint64_t pcap, const uint64_t* rk, const uint64_t* keys,
                               const int32_t* kstar, const int32_t* need, uint8_t* chosen, int32_t* cand_lang,
                               uint64_t* cand_key, uint32_t* cand_idx, unsigned int* cand_n, int L,
                               unsigned int* lenhist, hipStream_t stream) {
     if (pcap == 0) return hipSuccess;
     const size_t lds = lenhist ? (size_t)16 * L * 4 : 0;
-    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid_ipt(pcap)), dim3(kScanThreads), lds, stream, p, pcap, rowof,
+    hipLaunchKernelGGL(pair_select_kernel, dim3(scan_grid_ipt(pcap)), dim3(kScanThreads), lds, stream, p, pcap, rk,
                        keys, kstar, need, chosen, cand_lang, cand_key, cand_idx, cand_n, L, lenhist);
     return hipGetLastError();
 }
@@ -1155,10 +1167,10 @@ hipError_t launch_rows_permute(int64_t n, int S, const unsigned long long* idx, 
     return hipGetLastError();
 }
 
-hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint32_t* rowof, const uint32_t* outrow, int S,
+hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint64_t* rk, const uint32_t* outrow, int S,
                              uint64_t* masks, hipStream_t stream) {
     if (pcap == 0) return hipSuccess;
-    hipLaunchKernelGGL(pair_masks_kernel, dim3(grid_of((int64_t)pcap, 256)), dim3(256), 0, stream, p, pcap, rowof,
+    hipLaunchKernelGGL(pair_masks_kernel, dim3(grid_of((int64_t)pcap, 256)), dim3(256), 0, stream, p, pcap, rk,
                        outrow, S, masks);
     return hipGetLastError();
 }
