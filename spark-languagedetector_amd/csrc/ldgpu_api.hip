@@ -5446,7 +5446,8 @@ int fit_table_device(ldgpu_counts* c, int32_t K, int64_t* n_rows, int64_t* key_b
         mark("table: gather rows");
         HIP_TRY(db.alloc(&d_om, (size_t)std::max<unsigned long long>(m, 1) * S));
         HIP_TRY(hipMemsetAsync(d_om, 0, sizeof(uint64_t) * std::max<unsigned long long>(m, 1) * S, st));
-        HIP_TRY(launch_pair_masks(cp, c->pcap, d_rk, d_outrow, S, d_om, st));
+        HIP_TRY(launch_rows_final(cp, c->cap, d_outrow, d_rk, st));  // (rk's rows are not read after this)
+        HIP_TRY(launch_pair_masks(cp, c->pcap, d_rk, nullptr, S, d_om, st));
         mark("table: masks");
         if (multi && m) {
             ok.resize(m);

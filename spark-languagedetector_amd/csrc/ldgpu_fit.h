@@ -387,6 +387,10 @@ hipError_t launch_sort_keys_of(int64_t n, const uint64_t* keys, uint64_t* sk, un
 hipError_t launch_rows_permute(int64_t n, int S, const unsigned long long* idx, const uint64_t* keys, const int32_t* ks,
                                const uint64_t* masks, uint64_t* out_keys, int32_t* out_k, uint64_t* out_masks,
                                hipStream_t stream);
+// rk[g]'s row replaced by outrow[row] for every occupied gram slot (then
+// launch_pair_masks with outrow null)
+hipError_t launch_rows_final(const CountParams& p, uint64_t cap, const uint32_t* outrow, uint64_t* rk,
+                             hipStream_t stream);
 // presence masks: masks[row][l / 64] |= bit l for every pair, row = outrow[(uint32_t)rk[g]]
 // (outrow null: the row itself); masks zeroed by the caller
 hipError_t launch_pair_masks(const CountParams& p, uint64_t pcap, const uint64_t* rk, const uint32_t* outrow, int S,

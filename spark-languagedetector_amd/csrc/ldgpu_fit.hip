@@ -981,6 +981,16 @@ __global__ __launch_bounds__(kScanThreads) void gather_rows_kernel(int64_t n, co
     }
 }
 
+// rk[g]'s row -> outrow[row] (0xffffffff: not chosen) for every occupied gram
+// slot: rows follow slot order, so the outrow reads are near-sequential here,
+// and the pair scan after it gathers one word per pair instead of two
+__global__ void rows_final_kernel(const CountParams p, uint64_t cap, const uint32_t* outrow, uint64_t* rk) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= cap || p.keys[g] == kEmpty) return;
+    const uint64_t v = rk[g];
+    rk[g] = (v & ~0xffffffffull) | outrow[(uint32_t)v];
+}
+
 __global__ void pair_masks_kernel(const CountParams p, uint64_t pcap, const uint64_t* rk, const uint32_t* outrow,
                                   int S, uint64_t* masks) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1164,6 +1174,13 @@ hipError_t launch_rows_permute(int64_t n, int S, const unsigned long long* idx, 
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(rows_permute_kernel, dim3(grid_of(n, 256)), dim3(256), 0, stream, n, S, idx, keys, ks, masks,
                        out_keys, out_k, out_masks);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_final(const CountParams& p, uint64_t cap, const uint32_t* outrow, uint64_t* rk,
+                             hipStream_t stream) {
+    if (cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(rows_final_kernel, dim3(grid_of((int64_t)cap, 256)), dim3(256), 0, stream, p, cap, outrow, rk);
     return hipGetLastError();
 }
 
