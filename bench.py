@@ -390,7 +390,7 @@ def traffic_from_profiles(workload_key):
 COUNT_KERNELS = ("emit_kernel", "fit_offsets_kernel", "part2_kernel", "reduce_kernel", "merge_kernel",
                  "derive_level_kernel", "derive_pairs_level_kernel", "derive_pairs2_level_kernel", "len_hist_kernel",
                  "partial_kernel", "rehash_kernel", "wide_rehash_kernel", "sparse_rehash_kernel", "pair_rehash_kernel",
-                 "counts_add_kernel", "sort_emit_kernel", "sort_runs_kernel", "runs_add_kernel")
+                 "counts_add_kernel", "sort_emit_kernel", "runs_count_kernel", "sort_runs_kernel", "runs_add_kernel")
 
 
 def fit_sort_path(L, grams):
@@ -405,7 +405,7 @@ def fit_sort_path(L, grams):
 
 def fit_count_kernels(L, grams):
     if fit_sort_path(L, grams):
-        return "count (FIT v5: sort_emit + radix sort + sort_runs per length + runs_add into T)"
+        return "count (FIT v5: sort_emit + radix sort + runs_count + sort_runs per length group + runs_add into T)"
     return "count (FIT v4: emit + part2 + reduce + merge + derive)"
 
 
@@ -551,6 +551,7 @@ def fit_main(args, world, rank, local, dev, backend):
         "phases_s": {k: round(float(np.mean([p[0].get(k, 0.0) for p in parts])), 4)
                      for k in ("create_s", "count_s", "merge_s", "table_s", "close_s", "total_s")},
         "count_s_per_step": [round(float(p[0].get("count_s", 0.0)), 4) for p in parts],
+        "table_s_per_step": [round(float(p[0].get("table_s", 0.0)), 4) for p in parts],
         "count_windows_per_s": round(windows / count_s, 1),
         "count_ms_per_gib": round(count_s * 1e3 * (1 << 30) / n_bytes, 2),
         "windows_counted_exactly_once": windows_ok,

@@ -4,8 +4,8 @@
 known bytes, per count and per window:
   FIT v4: part2 reads and writes each record once (8 B per corpus byte, K = 1);
   FIT v5: sort_emit writes one 8-B sort key per corpus byte (write factor),
-          sort_runs reads the sorted keys once per gram length (8 B per full
-          window; its galloping reads stay within the lines it reads).
+          runs_count reads the sorted keys once (8 B per key; round 5:
+          sort_runs, once per gram length).
     python tools/fit_pmc.py OUTDIR [OUTNAME]"""
 import json
 import os
@@ -33,13 +33,19 @@ else:
     grams = [int(g) for g in re.search(r"grams ([\d,]+),", cfg["workload"]).group(1).split(",")]
     n_len = len({g for g in grams if g <= 7})
     em = next(v for k, v in raw.items() if k.startswith("sort_emit_kernel"))
-    rn = next(v for k, v in raw.items() if k.startswith("sort_runs_kernel"))
-    keys_read = 8 * cfg["windows_per_gpu"] / max(1, len(grams)) * n_len  # ~8 B per full window per length pass
+    rc = next((v for k, v in raw.items() if k.startswith("runs_count_kernel")), None)
     wf = rec_bytes / em["WRITE_SIZE"]
-    rf = keys_read / rn["FETCH_SIZE"]
-    calibration = ("FIT v5: write factor = sort_emit's 8 B per corpus byte / its raw WRITE_SIZE; read factor = "
-                   "sort_runs' 8 B per key per gram-length pass / its raw FETCH_SIZE; applied to every kernel "
-                   "(the random probes of runs_add into T and the radix sort's scatter: approximate)")
+    if rc:  # round 6: one pass counts every length's runs, reading each sorted key once
+        rf = 8 * cfg["windows_per_gpu"] / max(1, len(grams)) / rc["FETCH_SIZE"]
+        calibration = ("FIT v5: write factor = sort_emit's 8 B per corpus byte / its raw WRITE_SIZE; read factor = "
+                       "runs_count's 8 B per sorted key (one pass) / its raw FETCH_SIZE; applied to every kernel "
+                       "(the random probes of runs_add into T and the radix sort's scatter: approximate)")
+    else:  # round 5: sort_runs read the keys once per gram length
+        rn = next(v for k, v in raw.items() if k.startswith("sort_runs_kernel"))
+        rf = 8 * cfg["windows_per_gpu"] / max(1, len(grams)) * n_len / rn["FETCH_SIZE"]
+        calibration = ("FIT v5: write factor = sort_emit's 8 B per corpus byte / its raw WRITE_SIZE; read factor = "
+                       "sort_runs' 8 B per key per gram-length pass / its raw FETCH_SIZE; applied to every kernel "
+                       "(the random probes of runs_add into T and the radix sort's scatter: approximate)")
 m = re.search(r"(\d+) languages, grams ([\d,]+), profile", cfg["workload"])
 L, grams = int(m.group(1)), [int(g) for g in m.group(2).split(",")]
 # only the count's own kernels (bench.is_count_kernel): a FIT v4 count sorts
