@@ -280,6 +280,7 @@ struct ldgpu_ctx {
     std::mutex cache_mu;
     std::vector<std::pair<size_t, void*>> cache;
     size_t cache_bytes = 0;
+    size_t cache_max = 96ull << 30;  // half the device's memory (ldgpu_ctx_create)
     // FIT: T1 keys per corpus byte of the last count call on this context --
     // sizes the next call's T1 (of any count table: an executor fits
     // partition after partition of like text), so it is not grown by
@@ -289,8 +290,14 @@ struct ldgpu_ctx {
 };
 
 namespace {
-constexpr size_t kCacheMaxBytes = 96ull << 30;
-constexpr size_t kCacheMaxBlocks = 64;
+// The block cache keeps freed device blocks for the next call of the same
+// shape, up to half the device's memory: a config-5-sized fit frees ~90 GB per
+// call (T, the top-K scratch), and a 96 GB cap evicted blocks the next fit
+// then re-allocated -- 3.5 s of hipMalloc in one table phase of eight -- and
+// up to 256 blocks (at 64, the big blocks a larger byte cap keeps pushed out
+// the small top-K scratch blocks of config 3's fits instead).  An allocation
+// that fails frees the whole cache and retries (cache_alloc).
+constexpr size_t kCacheMaxBlocks = 256;
 
 hipError_t cache_alloc(ldgpu_ctx* c, void** p, size_t bytes) {
     {
@@ -321,7 +328,7 @@ void cache_free(ldgpu_ctx* c, void* p, size_t bytes) {
     std::lock_guard<std::mutex> g(c->cache_mu);
     c->cache.emplace_back(bytes, p);
     c->cache_bytes += bytes;
-    while (!c->cache.empty() && (c->cache_bytes > kCacheMaxBytes || c->cache.size() > kCacheMaxBlocks)) {
+    while (!c->cache.empty() && (c->cache_bytes > c->cache_max || c->cache.size() > kCacheMaxBlocks)) {
         (void)hipFree(c->cache.front().second);
         c->cache_bytes -= c->cache.front().first;
         c->cache.erase(c->cache.begin());
@@ -403,6 +410,7 @@ extern "C" int ldgpu_ctx_create(int32_t device, ldgpu_ctx** out) {
     auto* c = new ldgpu_ctx();
     c->device = device;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->cache_max = std::max<size_t>(c->cache_max, prop.totalGlobalMem / 2);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         (void)ldgpu_ctx_destroy(c);
